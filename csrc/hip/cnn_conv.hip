@@ -1,0 +1,395 @@
+// Genetic-CNN convolution kernels for MI355X (gfx950), NHWC bf16, channels
+// padded to a multiple of 8 so one 16-byte access = 8 channels.
+//
+// conv_fwd  (K1 + K2 of SURVEY.md §2.4): implicit GEMM on
+//   v_mfma_f32_16x16x32_bf16. One workgroup = 4 waves = TH full output rows
+//   (<= 64 pixels) of one image of one fold, all output channels of a
+//   64-channel block. The input patch (TH+KH-1 rows x W+KW-1 cols x Cin) is
+//   staged ONCE into LDS, with the Genetic-CNN DAG's N-ary Add fused into the
+//   staging (sum of up to 4 producer tensors, fp32 then bf16), an optional
+//   ReLU-mask multiply (dgrad: dz = dy * (y > 0)) and an optional batch gather
+//   (first layer reads dataset images through the epoch's index table, so no
+//   separate gather kernel and no host->device batch copy).
+//   MFMA operands: A = weights [co][k] (16-B global loads, L2-resident),
+//   B = patch pixels (ds_read_b128). Epilogue: bias + ReLU, 8-byte stores of
+//   4 consecutive channels, optional accumulate into up to 4 outputs (DAG
+//   gradient fan-out without an add kernel).
+//   The same kernel is the data-gradient (K2): stride-1 'same' dgrad is a
+//   'same' conv of dz with the flipped, transposed weights W'.
+//
+// conv_wgrad (K3): dW[co][kh][kw][ci] = sum_pix dz[pix][co] * x[pix+(kh,kw)][ci]
+//   as a split-K GEMM: each workgroup owns a 64(co) x 64(kh,kw,ci) block and
+//   a pixel range; per 32-pixel K-step the dz tile and the im2col tile are
+//   staged TRANSPOSED into LDS so both MFMA operands are ds_read_b128 rows.
+//   Partial sums go to a [S][G][Coutp][K] fp32 workspace that the Adam kernel
+//   reduces in a fixed order (deterministic, no float atomics).
+//
+// pool2x2 fwd/bwd (K4): vectorised 8-channel max-pool and its scatter.
+
+#include <algorithm>
+
+#include "common.h"
+
+struct ConvArgs {
+  const uint16_t* in[4];     // summed inputs [G][B][H][W][Cinp]
+  const uint16_t* mask;      // optional: staged value *= (mask > 0), same shape as in
+  const int64_t* gather;     // optional: image table [steps][G][B]; in[0] is then the dataset
+  const StepState* st;       // cur_step for the gather table
+  uint16_t* out[4];          // [G][B][H][W][Coutp]
+  const uint16_t* w;         // [G][Coutp][KH][KW][Cinp] bf16
+  const float* bias;         // [G][Coutp] or null
+  int n_in, n_out, acc_flags, relu;
+  int G, B, H, W, Cinp, Coutp, KH, KW, TH;
+};
+
+__global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint4* patch = reinterpret_cast<uint4*>(smem);
+  const int tid = threadIdx.x;
+  const int nth = (a.H + a.TH - 1) / a.TH;
+  const int b = blockIdx.x / nth;
+  const int h0 = (blockIdx.x % nth) * a.TH;
+  const int g = blockIdx.y;
+  const int co_blk = blockIdx.z * 64;
+  const int ph = a.KH >> 1, pw = a.KW >> 1;
+  const int PH = a.TH + a.KH - 1, PW = a.W + a.KW - 1;
+  const int ncb = a.Cinp >> 3;
+  const long img = (long)a.H * a.W * a.Cinp;
+
+  // ---- stage the summed / masked input patch -------------------------------
+  const uint16_t* src[4];
+  for (int k = 0; k < a.n_in; ++k) src[k] = a.in[k] + ((long)g * a.B + b) * img;
+  if (a.gather) {
+    const long id = a.gather[((long)a.st->cur_step * a.G + g) * a.B + b];
+    src[0] = a.in[0] + id * img;
+  }
+  const uint16_t* msrc = a.mask ? a.mask + ((long)g * a.B + b) * img : nullptr;
+  const int total = PH * PW * ncb;
+  for (int i = tid; i < total; i += 256) {
+    const int cb = i % ncb;
+    const int pix = i / ncb;
+    const int pc = pix % PW, pr = pix / PW;
+    const int hh = h0 - ph + pr, ww = pc - pw;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) {
+      const long off = ((long)hh * a.W + ww) * a.Cinp + cb * 8;
+      if (a.n_in == 1 && !msrc) {
+        v = *reinterpret_cast<const uint4*>(src[0] + off);
+      } else {
+        float acc[8], t[8];
+        unpack8(*reinterpret_cast<const uint4*>(src[0] + off), acc);
+        for (int k = 1; k < a.n_in; ++k) {
+          unpack8(*reinterpret_cast<const uint4*>(src[k] + off), t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] += t[j];
+        }
+        if (msrc) {
+          unpack8(*reinterpret_cast<const uint4*>(msrc + off), t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[j] = t[j] > 0.f ? acc[j] : 0.f;
+        }
+        v = pack8(acc);
+      }
+    }
+    patch[i] = v;
+  }
+  __syncthreads();
+
+  // ---- MFMA main loop -------------------------------------------------------
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int pl = wave * 16 + l16;                 // pixel within the tile
+  const int npx = a.TH * a.W;
+  const int py = pl / a.W, px = pl % a.W;
+  const bool pvalid = (pl < npx) && (h0 + py < a.H);
+  const int nchunks = a.KH * a.KW * ncb;
+  const int Kdim = a.KH * a.KW * a.Cinp;
+  const uint16_t* wg = a.w + (long)g * a.Coutp * Kdim;
+  const int nco = min(64, a.Coutp - co_blk);
+  const int NT = (nco + 15) >> 4;
+  f32x4_t acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  for (int ks = 0; ks < nchunks; ks += 4) {
+    const int c = ks + kq;
+    uint4 bf = make_uint4(0, 0, 0, 0);
+    const bool cval = c < nchunks;
+    if (cval && pvalid) {
+      const int cb = c % ncb, kk = c / ncb;
+      const int kw = kk % a.KW, kh = kk / a.KW;
+      bf = patch[((py + kh) * PW + (px + kw)) * ncb + cb];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t < NT) {
+        const int co = co_blk + t * 16 + l16;
+        uint4 af = make_uint4(0, 0, 0, 0);
+        if (cval && co < a.Coutp) af = *reinterpret_cast<const uint4*>(wg + (long)co * Kdim + c * 8);
+        acc[t] = mfma16(af, bf, acc[t]);
+      }
+    }
+  }
+
+  // ---- epilogue: bias + relu, 4 channels per lane ---------------------------
+  if (!pvalid) return;
+  const long obase = ((((long)g * a.B + b) * a.H + (h0 + py)) * a.W + px) * a.Coutp;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t >= NT) continue;
+    const int co0 = co_blk + t * 16 + kq * 4;
+    if (co0 >= a.Coutp) continue;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float x = acc[t][i];
+      if (a.bias) x += a.bias[(long)g * a.Coutp + co0 + i];
+      if (a.relu) x = fmaxf(x, 0.f);
+      v[i] = x;
+    }
+    for (int k = 0; k < a.n_out; ++k) {
+      uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
+      if ((a.acc_flags >> k) & 1) {
+        const uint2 old = *dst;
+        float o[4] = {__uint_as_float(old.x << 16), __uint_as_float(old.x & 0xffff0000u),
+                      __uint_as_float(old.y << 16), __uint_as_float(old.y & 0xffff0000u)};
+        float s[4] = {v[0] + o[0], v[1] + o[1], v[2] + o[2], v[3] + o[3]};
+        *dst = pack4(s);
+      } else {
+        *dst = pack4(v);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient (split-K, deterministic partials)
+// ---------------------------------------------------------------------------
+
+struct WgradArgs {
+  const uint16_t* in[4];     // summed inputs of the layer [G][B][H][W][Cinp]
+  const int64_t* gather;     // optional dataset gather (first layer)
+  const StepState* st;
+  const uint16_t* dy;        // grad of the layer output [G][B][H][W][Coutp]
+  const uint16_t* ymask;     // layer output (ReLU mask), same shape as dy
+  float* part_w;             // [S][G][Coutp][Kdim]
+  float* part_b;             // [S][G][Coutp]
+  int n_in;
+  int G, B, H, W, Cinp, Coutp, KH, KW, S, pps;  // pps = pixels per split (multiple of 32)
+};
+
+#define WG_LD 40   // LDS row stride (elements) of the transposed tiles: 32 pixels + 8 pad
+
+__global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 64 * WG_LD];
+  uint16_t* dzT = lds;                 // [64 co][WG_LD]
+  uint16_t* colT = lds + 64 * WG_LD;   // [64 col][WG_LD]
+  const int tid = threadIdx.x;
+  const int nb = blockIdx.x;           // column block (64 cols of kh,kw,ci)
+  const int s = blockIdx.y;            // split
+  const int mblocks = (a.Coutp + 63) / 64;
+  const int g = blockIdx.z / mblocks;
+  const int co_blk = (blockIdx.z % mblocks) * 64;
+  const int Kdim = a.KH * a.KW * a.Cinp;
+  const int ncb = a.Cinp >> 3;
+  const int ph = a.KH >> 1, pw = a.KW >> 1;
+  const long HW = (long)a.H * a.W;
+  const long npix = (long)a.B * HW;
+  const long p_begin = (long)s * a.pps;
+  const long p_end = (p_begin + a.pps < npix) ? p_begin + a.pps : npix;
+
+  // staging roles: pixel = tid >> 3 (0..31), chunk = tid & 7
+  const int sp = tid >> 3, sj = tid & 7;
+  const int co_st = co_blk + sj * 8;                    // dz chunk channels
+  const int col_st = nb * 64 + sj * 8;                  // im2col chunk column
+  int c_kh = 0, c_kw = 0, c_cb = 0;
+  const bool col_ok = col_st < Kdim;
+  if (col_ok) {
+    const int c8 = col_st >> 3;
+    c_cb = c8 % ncb;
+    const int kk = c8 / ncb;
+    c_kw = kk % a.KW; c_kh = kk / a.KW;
+  }
+  const int wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  f32x4_t acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  const bool do_bias = (nb == 0) && (a.part_b != nullptr);
+
+  for (long p0 = p_begin; p0 < p_end; p0 += 32) {
+    const long p = p0 + sp;
+    float dz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float xs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (p < p_end) {
+      const long bimg = p / HW;
+      const int rem = (int)(p % HW);
+      const int hh = rem / a.W, ww = rem % a.W;
+      if (co_st < a.Coutp) {
+        const long off = (((long)g * a.B + bimg) * HW + rem) * a.Coutp + co_st;
+        float m[8];
+        unpack8(*reinterpret_cast<const uint4*>(a.dy + off), dz);
+        unpack8(*reinterpret_cast<const uint4*>(a.ymask + off), m);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dz[j] = m[j] > 0.f ? dz[j] : 0.f;
+      }
+      const int ih = hh + c_kh - ph, iw = ww + c_kw - pw;
+      if (col_ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
+        const long pix_off = ((long)ih * a.W + iw) * a.Cinp + c_cb * 8;
+        float t[8];
+        for (int k = 0; k < a.n_in; ++k) {
+          const uint16_t* base;
+          if (k == 0 && a.gather) {
+            const long id = a.gather[((long)a.st->cur_step * a.G + g) * a.B + bimg];
+            base = a.in[0] + id * HW * a.Cinp;
+          } else {
+            base = a.in[k] + ((long)g * a.B + bimg) * HW * a.Cinp;
+          }
+          unpack8(*reinterpret_cast<const uint4*>(base + pix_off), t);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xs[j] += t[j];
+        }
+      }
+    }
+    __syncthreads();   // previous K-step's reads are done
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dzT[(sj * 8 + j) * WG_LD + sp] = f2bf(dz[j]);
+      colT[(sj * 8 + j) * WG_LD + sp] = f2bf(xs[j]);
+    }
+    __syncthreads();
+    if (do_bias && tid < 64) {
+      float t = 0.f;
+      for (int q = 0; q < 32; ++q) t += bf2f(dzT[tid * WG_LD + q]);
+      bsum += t;
+    }
+    const uint4 bfrag = *reinterpret_cast<const uint4*>(&colT[(wave * 16 + l16) * WG_LD + kq * 8]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint4 afrag = *reinterpret_cast<const uint4*>(&dzT[(t * 16 + l16) * WG_LD + kq * 8]);
+      acc[t] = mfma16(afrag, bfrag, acc[t]);
+    }
+  }
+
+  // D[row = co][col]: lane holds rows kq*4+i of tile t, column l16 of wave's 16 columns
+  const int col = nb * 64 + wave * 16 + l16;
+  if (col < Kdim) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = co_blk + t * 16 + kq * 4 + i;
+        if (co < a.Coutp) a.part_w[(((long)s * a.G + g) * a.Coutp + co) * Kdim + col] = acc[t][i];
+      }
+    }
+  }
+  if (do_bias && tid < 64 && co_blk + tid < a.Coutp)
+    a.part_b[((long)s * a.G + g) * a.Coutp + co_blk + tid] = bsum;
+}
+
+// ---------------------------------------------------------------------------
+// 2x2/2 max-pool (floor) and its backward scatter
+// ---------------------------------------------------------------------------
+
+__global__ void pool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int NB, int H, int W,
+                                int Cp) {
+  const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
+  const long total = (long)NB * Ho * Wo * ncb;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cb = (int)(i % ncb);
+    long r = i / ncb;
+    const int wo = (int)(r % Wo); r /= Wo;
+    const int ho = (int)(r % Ho);
+    const long n = r / Ho;
+    const uint16_t* base = x + ((n * H + 2 * ho) * W + 2 * wo) * Cp + cb * 8;
+    float m[8], t[8];
+    unpack8(*reinterpret_cast<const uint4*>(base), m);
+    const long offs[3] = {(long)Cp, (long)W * Cp, (long)W * Cp + Cp};
+    for (int q = 0; q < 3; ++q) {
+      unpack8(*reinterpret_cast<const uint4*>(base + offs[q]), t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], t[j]);
+    }
+    *reinterpret_cast<uint4*>(y + ((n * Ho + ho) * Wo + wo) * Cp + cb * 8) = pack8(m);
+  }
+}
+
+// dx[pixel] = dy[pool cell] if pixel is the cell's first maximum else 0
+__global__ void pool_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
+                                uint16_t* __restrict__ dx, int NB, int H, int W, int Cp) {
+  const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
+  const long total = (long)NB * H * W * ncb;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    const int cb = (int)(i % ncb);
+    long r = i / ncb;
+    const int w = (int)(r % W); r /= W;
+    const int h = (int)(r % H);
+    const long n = r / H;
+    float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int ho = h >> 1, wo = w >> 1;
+    if (ho < Ho && wo < Wo) {
+      const uint16_t* base = x + ((n * H + 2 * ho) * W + 2 * wo) * Cp + cb * 8;
+      float v[4][8];
+      unpack8(*reinterpret_cast<const uint4*>(base), v[0]);
+      unpack8(*reinterpret_cast<const uint4*>(base + Cp), v[1]);
+      unpack8(*reinterpret_cast<const uint4*>(base + (long)W * Cp), v[2]);
+      unpack8(*reinterpret_cast<const uint4*>(base + (long)W * Cp + Cp), v[3]);
+      float g[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + ((n * Ho + ho) * Wo + wo) * Cp + cb * 8), g);
+      const int me = (h & 1) * 2 + (w & 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        int arg = 0;
+        float m = v[0][j];
+        for (int q = 1; q < 4; ++q) if (v[q][j] > m) { m = v[q][j]; arg = q; }
+        out[j] = (arg == me) ? g[j] : 0.f;
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + ((n * H + h) * W + w) * Cp + cb * 8) = pack8(out);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launchers (C ABI; stream = the caller's current hipStream_t)
+// ---------------------------------------------------------------------------
+
+extern "C" {
+
+int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
+  if (a->Cinp % 8 || a->Coutp % 8 || a->n_in < 1 || a->n_in > 4 || a->n_out < 1 || a->n_out > 4) return -1;
+  if (a->TH * a->W > 64 || a->TH < 1) return -2;
+  const int nth = (a->H + a->TH - 1) / a->TH;
+  const size_t lds = (size_t)(a->TH + a->KH - 1) * (a->W + a->KW - 1) * a->Cinp * 2;
+  if (lds > 160 * 1024) return -3;
+  dim3 grid(a->B * nth, a->G, (a->Coutp + 63) / 64);
+  hipLaunchKernelGGL(conv_fwd_kernel, grid, dim3(256), lds, stream, *a);
+  return (int)hipGetLastError();
+}
+
+int gt_conv_wgrad(const WgradArgs* a, hipStream_t stream) {
+  if (a->Cinp % 8 || a->Coutp % 8 || a->pps % 32 || a->n_in < 1 || a->n_in > 4) return -1;
+  const int Kdim = a->KH * a->KW * a->Cinp;
+  dim3 grid((Kdim + 63) / 64, a->S, a->G * ((a->Coutp + 63) / 64));
+  hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+int gt_pool_fwd(const uint16_t* x, uint16_t* y, int NB, int H, int W, int Cp, hipStream_t stream) {
+  const long total = (long)NB * (H / 2) * (W / 2) * (Cp / 8);
+  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x, y, NB, H, W, Cp);
+  return (int)hipGetLastError();
+}
+
+int gt_pool_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, int NB, int H, int W, int Cp,
+                hipStream_t stream) {
+  const long total = (long)NB * H * W * (Cp / 8);
+  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(blocks), dim3(256), 0, stream, x, dy, dx, NB, H, W, Cp);
+  return (int)hipGetLastError();
+}
+
+size_t gt_sizeof_conv_args() { return sizeof(ConvArgs); }
+size_t gt_sizeof_wgrad_args() { return sizeof(WgradArgs); }
+
+}  // extern "C"

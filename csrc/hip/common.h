@@ -1,0 +1,75 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+#define GT_WAVE 64
+
+// Step state shared by every kernel of one captured train step (int32 words):
+//  [0] step_ctr (index into the epoch's batch table, ++ per step)
+//  [1] cur_step (step_ctr snapshot for this step)
+//  [2] t        (Adam step, float bits)
+//  [3] lr       (float bits)
+//  [4] lr_t     (bias-corrected step size, float bits)
+//  [5] global_step (never reset; keys the dropout stream)
+struct StepState {
+  int step_ctr, cur_step;
+  float t, lr, lr_t;
+  int global_step, pad0, pad1;
+};
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN
+  u += 0x7fffu + ((u >> 16) & 1u);                      // round to nearest even
+  return (uint16_t)(u >> 16);
+}
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+  v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
+  v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  return v;
+}
+
+__device__ __forceinline__ uint2 pack4(const float* f) {
+  uint2 v;
+  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
+  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+  return v;
+}
+
+__device__ __forceinline__ bf16x8_t as_frag(const uint4& v) { return __builtin_bit_cast(bf16x8_t, v); }
+
+__device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(b), c, 0, 0, 0);
+}
+
+// Counter-based hash -> uniform in [0,1): keyed dropout (deterministic per
+// (seed, fold, step, row, col), independent of launch geometry).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t hash4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t h = mix32(a ^ 0x9e3779b9U);
+  h = mix32(h ^ b);
+  h = mix32(h ^ (c * 0x85ebca6bU));
+  return mix32(h ^ (d * 0xc2b2ae35U));
+}

@@ -1,0 +1,132 @@
+"""``GeneticCnnModel`` -- reference-compatible fitness model for Genetic-CNN.
+
+API parity with gentun/models/keras_models.py:19-143 (constructor signature,
+``build_model``, static ``build_dag``, ``reset_weights``, ``plot``,
+``cross_validate``); the Keras/TF graph is replaced by a decoded
+:class:`~gentun_amd.models.genome.Plan` executed by the fold-batched engine
+(:mod:`gentun_amd.models.cnn_engine`) -- HIP kernels on MI355X.
+"""
+
+import torch
+
+from ..utils.data import labels_from_onehot, stratified_kfold
+from .generic_models import GentunModel
+from .genome import decode_stage, make_plan
+from . import cnn_engine as _eng
+
+
+def _pick_device(device):
+    if device is not None:
+        return torch.device(device)
+    if torch.cuda.is_available():
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+class GeneticCnnModel(GentunModel):
+
+    def __init__(self, x_train, y_train, genes, nodes, input_shape, kernels_per_layer, kernel_sizes, dense_units,
+                 dropout_probability, classes, nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
+                 loss="bce_compat", dtype="bf16", seed=0, backend=None, device=None, fold_parallel=True):
+        super(GeneticCnnModel, self).__init__(x_train, y_train)
+        self.genes = dict(genes)
+        self.name = '-'.join(self.genes[k] for k in sorted(self.genes))
+        # Reference type rules (keras_models.py:30-38), relaxed per SURVEY.md Q7:
+        # int epochs may come with an int OR float learning rate.
+        if isinstance(epochs, (list, tuple)) != isinstance(learning_rate, (list, tuple)):
+            raise ValueError("epochs and learning_rate must both be scalars or both be tuples")
+        if isinstance(epochs, list) or isinstance(learning_rate, list):
+            raise ValueError("epochs and learning_rate must be tuples (lists are rejected like the reference)")
+        if not isinstance(epochs, tuple):
+            epochs, learning_rate = (int(epochs),), (float(learning_rate),)
+        if len(epochs) != len(learning_rate):
+            raise ValueError("epochs and learning_rate tuples must have the same length")
+        self.nodes = tuple(nodes)
+        self.input_shape = tuple(input_shape)
+        self.kernels_per_layer = tuple(kernels_per_layer)
+        self.kernel_sizes = tuple(tuple(k) for k in kernel_sizes)
+        self.dense_units = dense_units
+        self.dropout_probability = dropout_probability
+        self.classes = classes
+        self.nfold = nfold
+        self.epochs = epochs
+        self.learning_rate = learning_rate
+        self.batch_size = batch_size
+        self.device = _pick_device(device)
+        self.backend = backend or _eng.default_backend(self.device)
+        self.cfg = _eng.TrainConfig(epochs=epochs, learning_rate=learning_rate, batch_size=batch_size,
+                                    dropout=dropout_probability, loss=loss, dtype=dtype, seed=seed)
+        self.fold_parallel = fold_parallel
+        self.model = self.build_model(self.genes, self.nodes, self.input_shape, self.kernels_per_layer,
+                                      self.kernel_sizes, self.dense_units, self.dropout_probability, self.classes)
+        self.fold_scores = []
+        self.fold_metrics = None
+
+    # ------------------------------------------------------------ structure
+    def build_model(self, genes, nodes, input_shape, kernels_per_layer, kernel_sizes, dense_units,
+                    dropout_probability, classes):
+        """Decode genes into an executable plan (keras_models.py:97-118)."""
+        return make_plan(genes, nodes, input_shape, kernels_per_layer, kernel_sizes, dense_units, classes)
+
+    @staticmethod
+    def build_dag(x, nodes, connections, kernels):
+        """Symbolic DAG of one stage (keras_models.py:46-95): returns the
+        list of ``(node, input_expr)`` and the output expression, with
+        ``x`` as the stage-input name. Raises IndexError on all-zero bits."""
+        preds, _succs, active, outputs = decode_stage(connections, nodes)
+        names = {}
+        body = []
+        for i in range(nodes):
+            if not active[i]:
+                continue
+            src = x if not preds[i] else " + ".join(names[p] for p in preds[i])
+            names[i] = "n{}".format(i)
+            body.append((names[i], "relu(conv3x3x{}({}))".format(kernels, src)))
+        return body, " + ".join(names[i] for i in outputs)
+
+    def reset_weights(self):
+        """Weights are re-initialised per fold inside the engine (Glorot
+        kernels, zero biases); kept for API compatibility."""
+        return None
+
+    def plot(self, path=None):
+        """Write the decoded topology as text (Keras' plot_model needs
+        graphviz; keras_models.py:41-44)."""
+        path = path or "{}.txt".format(self.name)
+        with open(path, "w") as f:
+            f.write(self.model.describe() + "\n")
+        return path
+
+    # ------------------------------------------------------------ training
+    def make_folds(self):
+        labels = labels_from_onehot(self.y_train)
+        return stratified_kfold(labels, self.nfold, seed=self.cfg.seed)
+
+    def make_jobs(self, stream=None, fold_ids=None):
+        folds = self.make_folds()
+        ids = list(range(self.nfold)) if fold_ids is None else list(fold_ids)
+        groups = [ids] if self.fold_parallel else [[i] for i in ids]
+        return [_eng.make_job(self.backend, self.model, self.x_train, self.y_train, [folds[i] for i in grp],
+                              self.cfg, self.device, fold_ids=grp, stream=stream) for grp in groups]
+
+    def primary_metric(self):
+        return "binary_accuracy" if self.cfg.loss == "bce_compat" else "categorical_accuracy"
+
+    def collect(self, results):
+        """Merge per-job results (in fold order) into fitness."""
+        merged = {"val_loss": [], "binary_accuracy": [], "categorical_accuracy": []}
+        for res in results:
+            for k in merged:
+                merged[k].extend(res[k])
+        self.fold_metrics = merged
+        self.fold_scores = list(merged[self.primary_metric()])
+        return sum(self.fold_scores) / len(self.fold_scores)
+
+    def cross_validate(self):
+        """Mean validation metric over ``nfold`` folds (keras_models.py:127-143)."""
+        jobs = self.make_jobs()
+        results = []
+        for job in jobs:
+            job.launch()
+            results.append(job.finish())
+        return self.collect(results)

@@ -1,0 +1,469 @@
+"""Fold-batched Genetic-CNN training engine (device side).
+
+One *job* = one candidate architecture trained on ``G`` cross-validation
+folds AT ONCE: every parameter carries a leading fold dimension and every
+kernel launch processes all folds (SURVEY.md §2.4 "fold-batch", §7.3 hard
+part 1). The whole train step (gather -> fwd -> loss -> bwd -> Adam) is
+captured once per architecture into a HIP graph and replayed
+``epochs x steps`` times; per-epoch shuffles, learning-rate stages and Adam
+resets are enqueued asynchronously on the job's own stream, so the host
+can enqueue several candidates on different streams and the GPU runs them
+concurrently (hard part 1: a single tiny candidate cannot fill 256 CUs).
+
+Training protocol (reference: gentun/models/keras_models.py:120-143, Keras
+2.2 semantics -- SURVEY.md §2.2):
+
+* per fold: fresh Glorot-uniform kernels, zero biases (the reference resets
+  kernels only and lets biases carry over between *sequential* folds; with
+  folds trained concurrently every fold starts from zero biases -- the
+  ``reset="all"`` variant of SURVEY.md Q6);
+* per ``(epochs_i, lr_i)`` stage a NEW Adam (m, v, t reset), beta1 0.9,
+  beta2 0.999, eps 1e-7, Keras bias-corrected step size;
+* loss ``bce_compat`` = binary cross-entropy on the softmax output with
+  probabilities clipped to [1e-7, 1-1e-7], metric ``binary_accuracy``
+  (Keras' resolution of 'accuracy' for that loss), or ``ce`` = categorical
+  cross-entropy with categorical accuracy;
+* dropout is inverted dropout on the dense layer;
+* each epoch visits every training sample once in a fresh random order;
+  an epoch is ``ceil(n_train / B)`` full batches and the last batch wraps
+  around to the start of the permutation (Keras would run one short
+  batch; fixed shapes keep the step graph-capturable).
+
+Backends: ``hip`` (MI355X kernels, :mod:`gentun_amd.models.cnn_hip`) and
+``torch`` (autograd oracle / comparator path (a) of SURVEY.md §6).
+"""
+
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..utils import rng as _rng
+from .genome import ConvSpec, PoolSpec
+
+ADAM_B1, ADAM_B2, ADAM_EPS = 0.9, 0.999, 1e-7
+CLIP_EPS = 1e-7
+
+
+class TrainConfig(object):
+    def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
+                 dtype="bf16", seed=0, use_graph=True, eval_batch=1000):
+        if isinstance(epochs, int):
+            epochs = (epochs,)
+        if isinstance(learning_rate, (int, float)):
+            learning_rate = (float(learning_rate),)
+        epochs, learning_rate = tuple(epochs), tuple(float(x) for x in learning_rate)
+        if len(epochs) != len(learning_rate):
+            raise ValueError("epochs and learning_rate must have the same length")
+        if loss not in ("bce_compat", "ce"):
+            raise ValueError("loss must be 'bce_compat' or 'ce'")
+        if dtype not in ("bf16", "fp32"):
+            raise ValueError("dtype must be 'bf16' or 'fp32'")
+        self.epochs = epochs
+        self.learning_rate = learning_rate
+        self.batch_size = int(batch_size)
+        self.dropout = float(dropout)
+        self.loss = loss
+        self.dtype = dtype
+        self.seed = seed
+        self.use_graph = use_graph
+        self.eval_batch = int(eval_batch)
+
+    def total_epochs(self):
+        return sum(self.epochs)
+
+
+# ---------------------------------------------------------------------------
+# Device-resident dataset cache (no per-batch H2D)
+# ---------------------------------------------------------------------------
+
+class DeviceData(object):
+    def __init__(self, x, y, device, layout):
+        x = np.asarray(x)
+        y = np.asarray(y)
+        self.n = x.shape[0]
+        self.hwc = tuple(x.shape[1:])
+        self.classes = y.shape[1] if y.ndim == 2 else int(y.max()) + 1
+        lab = np.argmax(y, 1) if y.ndim == 2 else y.astype(np.int64)
+        self.labels_np = lab.astype(np.int64)
+        self.device = device
+        self.layout = layout
+        xt = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32))
+        if layout == "nchw":
+            self.x = xt.permute(0, 3, 1, 2).contiguous().to(device)
+        elif layout == "nhwc8":
+            # channels padded to a multiple of 8 so one 16-byte load = 8 channels
+            c = xt.shape[-1]
+            cp = (c + 7) // 8 * 8
+            pad = torch.zeros(xt.shape[:-1] + (cp,), dtype=torch.float32)
+            pad[..., :c] = xt
+            self.x = pad.to(device=device, dtype=torch.bfloat16).contiguous()
+        else:
+            raise ValueError(layout)
+        self.labels = torch.from_numpy(self.labels_np).to(device)
+        self.onehot = F.one_hot(self.labels, self.classes).float()
+
+
+_DATA_CACHE = []
+
+
+def device_data(x, y, device, layout):
+    for ent in _DATA_CACHE:
+        if ent[0] is x and ent[1] is y and ent[2] == str(device) and ent[3] == layout:
+            return ent[4]
+    dd = DeviceData(x, y, device, layout)
+    _DATA_CACHE.append((x, y, str(device), layout, dd))
+    while len(_DATA_CACHE) > 3:
+        _DATA_CACHE.pop(0)
+    return dd
+
+
+# ---------------------------------------------------------------------------
+# Shared job driver
+# ---------------------------------------------------------------------------
+
+class FoldJob(object):
+    """Train one architecture on ``len(folds)`` folds concurrently.
+
+    ``launch()`` only ENQUEUES work on ``self.stream``; ``finish()`` waits and
+    returns per-fold metrics. Subclasses supply the executor.
+    """
+
+    layout = "nchw"
+
+    def __init__(self, plan, x, y, folds, cfg, device, fold_ids=None, stream=None):
+        self.plan = plan
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.folds = folds
+        self.G = len(folds)
+        self.fold_ids = list(range(self.G)) if fold_ids is None else list(fold_ids)
+        self.data = device_data(x, y, self.device, self.layout)
+        self.stream = stream if stream is not None else torch.cuda.current_stream(self.device) \
+            if self.device.type == "cuda" else None
+        self.B = cfg.batch_size
+        ntr = [len(tr) for tr, _ in folds]
+        nva = [len(va) for _, va in folds]
+        self.ntrain = ntr
+        self.nval = nva
+        self.steps_per_epoch = int(math.ceil(max(ntr) / self.B))
+        gkey = _rng.stable_hash("cnn", cfg.seed, sorted(plan.genes.items()))
+        self.base_seed = gkey & 0x7FFFFFFFFFFF
+        # device index tables
+        maxn = max(ntr)
+        tm = np.zeros((self.G, maxn), np.int64)
+        for g, (tr, _) in enumerate(folds):
+            tm[g, :len(tr)] = tr
+        self.train_mat = torch.from_numpy(tm).to(self.device)
+        self.ntrain_t = torch.tensor(ntr, dtype=torch.int64, device=self.device)
+        maxv = max(nva)
+        vm = np.zeros((self.G, maxv), np.int64)
+        vmask = np.zeros((self.G, maxv), np.float32)
+        for g, (_, va) in enumerate(folds):
+            vm[g, :len(va)] = va
+            vmask[g, :len(va)] = 1.0
+        self.val_mat = torch.from_numpy(vm).to(self.device)
+        self.val_mask = torch.from_numpy(vmask).to(self.device)
+        # One generator per fold, keyed by the fold id: a fold's data order is
+        # the same whether it is trained alone or batched with other folds.
+        self.shuffle_gens = []
+        for fid in self.fold_ids:
+            gen = torch.Generator(device=self.device)
+            gen.manual_seed(_rng.stable_hash(self.base_seed, "shuffle", fid) & 0x7FFFFFFF)
+            self.shuffle_gens.append(gen)
+        self.epoch_idx = torch.zeros((self.steps_per_epoch, self.G, self.B), dtype=torch.int64,
+                                     device=self.device)
+        self.step_ctr = torch.zeros((1,), dtype=torch.int64, device=self.device)
+        self.result = None
+
+    # -- shuffling -----------------------------------------------------------
+    def _new_epoch_order(self):
+        G, maxn = self.train_mat.shape
+        keys = torch.stack([torch.rand((maxn,), generator=gen, device=self.device) for gen in self.shuffle_gens])
+        valid = torch.arange(maxn, device=self.device)[None, :] < self.ntrain_t[:, None]
+        keys = torch.where(valid, keys, torch.full_like(keys, 2.0))
+        order = torch.argsort(keys, dim=1)
+        perm = torch.gather(self.train_mat, 1, order)
+        pos = torch.arange(self.steps_per_epoch * self.B, device=self.device)[None, :] % self.ntrain_t[:, None]
+        idx = torch.gather(perm, 1, pos).view(G, self.steps_per_epoch, self.B)
+        self.epoch_idx.copy_(idx.permute(1, 0, 2))
+        self.step_ctr.zero_()
+
+    def _fold_seed(self, g):
+        return _rng.stable_hash(self.base_seed, "init", self.fold_ids[g]) & 0x7FFFFFFFFFFF
+
+    # -- to implement ----------------------------------------------------------
+    def init_params(self):
+        raise NotImplementedError
+
+    def reset_optimizer(self, lr):
+        raise NotImplementedError
+
+    def train_step(self):
+        """One optimizer step for all folds; must be graph-capturable and read
+        its batch from ``epoch_idx[step_ctr]`` then increment ``step_ctr``."""
+        raise NotImplementedError
+
+    def evaluate(self):
+        """Return device tensors (loss_sum[G], bin_correct[G], cat_correct[G])."""
+        raise NotImplementedError
+
+    def snapshot(self):
+        raise NotImplementedError
+
+    def restore(self, snap):
+        raise NotImplementedError
+
+    # -- driver --------------------------------------------------------------
+    def _capture(self):
+        snap = self.snapshot()
+        self._new_epoch_order()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self.train_step()
+        # Raw capture API: ``torch.cuda.graph`` would device-synchronize on
+        # entry and serialise the candidates running on other streams.
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.stream(side):
+            graph.capture_begin(capture_error_mode="thread_local")
+            try:
+                self.train_step()
+            finally:
+                graph.capture_end()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self.restore(snap)
+        return graph
+
+    def launch(self):
+        use_graph = self.cfg.use_graph and self.device.type == "cuda" and getattr(self, "capture_ok", True)
+        ctx = torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
+        with ctx:
+            self.init_params()
+            graph = self._capture() if use_graph else None
+            for epochs, lr in zip(self.cfg.epochs, self.cfg.learning_rate):
+                self.reset_optimizer(lr)
+                for _ in range(epochs):
+                    self._new_epoch_order()
+                    for _ in range(self.steps_per_epoch):
+                        if graph is not None:
+                            graph.replay()
+                        else:
+                            self.train_step()
+            self._graph = graph
+            self._eval = self.evaluate()
+            if self.stream is not None:
+                self._done = torch.cuda.Event()
+                self._done.record(self.stream)
+        return self
+
+    def finish(self):
+        if getattr(self, "_done", None) is not None:
+            self._done.synchronize()
+        loss, binc, catc = (t.detach().float().cpu().numpy() for t in self._eval)
+        nval = np.asarray(self.nval, np.float64)
+        self.result = {
+            "val_loss": (loss / nval).tolist(),
+            "binary_accuracy": (binc / (nval * self.data.classes)).tolist(),
+            "categorical_accuracy": (catc / nval).tolist(),
+        }
+        self._graph = None
+        return self.result
+
+
+class _nullctx(object):
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def loss_and_metrics(logits, onehot, mode):
+    """Shared oracle of the fused softmax+loss kernel (K9)."""
+    p = torch.softmax(logits.float(), dim=-1)
+    if mode == "bce_compat":
+        pc = p.clamp(CLIP_EPS, 1.0 - CLIP_EPS)
+        per = -(onehot * torch.log(pc) + (1.0 - onehot) * torch.log(1.0 - pc)).mean(-1)
+    else:
+        per = -(onehot * torch.log(p.clamp_min(1e-30))).sum(-1)
+    binc = (torch.round(p) == onehot).float().sum(-1)
+    catc = (p.argmax(-1) == onehot.argmax(-1)).float()
+    return per, binc, catc
+
+
+# ---------------------------------------------------------------------------
+# torch (autograd) oracle executor
+# ---------------------------------------------------------------------------
+
+class TorchFoldJob(FoldJob):
+    """Stock PyTorch-ROCm ops (MIOpen grouped convs, batched GEMMs, autograd).
+
+    Folds are batched as conv groups: activations live as ``[B, G*C, H, W]``.
+    Used as the numerics oracle for the HIP path and as comparator (a).
+    """
+
+    layout = "nchw"
+
+    def __init__(self, *a, **kw):
+        super(TorchFoldJob, self).__init__(*a, **kw)
+        plan, G = self.plan, self.G
+        shapes = []
+        for st in plan.convs():
+            shapes.append((st.name + ".w", (G, st.cout, st.cin, st.k[0], st.k[1]), "glorot",
+                           (st.cin * st.k[0] * st.k[1], st.cout * st.k[0] * st.k[1])))
+            shapes.append((st.name + ".b", (G, st.cout), "zero", None))
+        shapes.append(("dense1.w", (G, plan.flatten, plan.dense_units), "glorot", (plan.flatten, plan.dense_units)))
+        shapes.append(("dense1.b", (G, plan.dense_units), "zero", None))
+        shapes.append(("dense2.w", (G, plan.dense_units, plan.classes), "glorot", (plan.dense_units, plan.classes)))
+        shapes.append(("dense2.b", (G, plan.classes), "zero", None))
+        self.shapes = shapes
+        total = sum(int(np.prod(s)) for _, s, _, _ in shapes)
+        self.flat = torch.zeros(total, device=self.device, requires_grad=True)
+        self.m = torch.zeros(total, device=self.device)
+        self.v = torch.zeros(total, device=self.device)
+        self.t = torch.zeros((), device=self.device)
+        self.lr = torch.zeros((), device=self.device)
+        self.flat.grad = torch.zeros_like(self.flat)
+        # MIOpen's algorithm search is not graph-capture safe: the stock-ops
+        # comparator runs eagerly unless explicitly asked to capture.
+        import os
+        self.capture_ok = os.environ.get("GENTUN_TORCH_GRAPH") == "1"
+        self.amp = (self.cfg.dtype == "bf16") and self.device.type == "cuda"
+        self.drop_gen = None
+
+    def init_params(self):
+        with torch.no_grad():
+            self.flat.zero_()
+            off = 0
+            for name, shape, kind, fans in self.shapes:
+                n = int(np.prod(shape))
+                if kind == "glorot":
+                    limit = math.sqrt(6.0 / (fans[0] + fans[1]))
+                    per = n // self.G
+                    for g in range(self.G):
+                        gen = torch.Generator(device=self.device)
+                        gen.manual_seed(_rng.stable_hash(self._fold_seed(g), name) & 0x7FFFFFFF)
+                        vals = torch.rand(per, generator=gen, device=self.device) * (2 * limit) - limit
+                        self.flat[off + g * per: off + (g + 1) * per].copy_(vals)
+                off += n
+
+    def reset_optimizer(self, lr):
+        self.m.zero_()
+        self.v.zero_()
+        self.t.zero_()
+        self.lr.fill_(lr)
+
+    def snapshot(self):
+        return (self.flat.detach().clone(), self.m.clone(), self.v.clone(), self.t.clone())
+
+    def restore(self, snap):
+        with torch.no_grad():
+            self.flat.copy_(snap[0])
+            self.m.copy_(snap[1])
+            self.v.copy_(snap[2])
+            self.t.copy_(snap[3])
+
+    def _views(self):
+        # Views are rebuilt per call so their autograd nodes live on the
+        # stream that runs the step (graph-capture friendly).
+        out, off = {}, 0
+        for name, shape, _, _ in self.shapes:
+            n = int(np.prod(shape))
+            out[name] = self.flat[off:off + n].view(shape)
+            off += n
+        return out
+
+    def _forward(self, xb, train):
+        """xb: [B, G*C, H, W] -> logits [G, B, classes]."""
+        G, plan, P = self.G, self.plan, self._views()
+        acts = {"input": xb}
+        for st in plan.steps:
+            if isinstance(st, ConvSpec):
+                inp = acts[st.inputs[0]]
+                for extra in st.inputs[1:]:
+                    inp = inp + acts[extra]
+                w = P[st.name + ".w"].reshape(G * st.cout, st.cin, st.k[0], st.k[1])
+                b = P[st.name + ".b"].reshape(G * st.cout)
+                acts[st.name] = F.relu(F.conv2d(inp, w, b, padding=(st.k[0] // 2, st.k[1] // 2), groups=G))
+            else:
+                src = acts[st.srcs[0]]
+                acts[st.name] = F.max_pool2d(src, 2, 2)
+        last = acts[plan.steps[-1].name]
+        Bn = last.shape[0]
+        feat = last.reshape(Bn, G, -1).permute(1, 0, 2)                     # [G, B, F]
+        h = torch.baddbmm(P["dense1.b"][:, None, :], feat, P["dense1.w"])
+        h = F.relu(h)
+        if train and self.cfg.dropout > 0:
+            h = F.dropout(h, self.cfg.dropout, training=True)
+        return torch.baddbmm(P["dense2.b"][:, None, :], h, P["dense2.w"])
+
+    def _gather(self, idx):
+        """idx [G, B] -> [B, G*C, H, W]."""
+        G, Bn = idx.shape
+        xb = self.data.x.index_select(0, idx.reshape(-1))                   # [G*B, C, H, W]
+        C, H, W = xb.shape[1:]
+        return xb.view(G, Bn, C, H, W).permute(1, 0, 2, 3, 4).reshape(Bn, G * C, H, W)
+
+    def train_step(self):
+        idx = self.epoch_idx.index_select(0, self.step_ctr).view(self.G, self.B)
+        self.step_ctr.add_(1)
+        xb = self._gather(idx)
+        yb = self.data.onehot.index_select(0, idx.reshape(-1)).view(self.G, self.B, -1)
+        self.flat.grad.zero_()
+        if self.amp:
+            with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+                logits = self._forward(xb, True)
+        else:
+            logits = self._forward(xb, True)
+        per, _, _ = loss_and_metrics(logits, yb, self.cfg.loss)
+        per.mean(-1).sum().backward()
+        with torch.no_grad():
+            g = self.flat.grad
+            self.t.add_(1.0)
+            step = self.lr * torch.sqrt(1.0 - ADAM_B2 ** self.t) / (1.0 - ADAM_B1 ** self.t)
+            self.m.mul_(ADAM_B1).add_(g, alpha=1.0 - ADAM_B1)
+            self.v.mul_(ADAM_B2).addcmul_(g, g, value=1.0 - ADAM_B2)
+            self.flat.sub_(step * self.m / (self.v.sqrt() + ADAM_EPS))
+
+    def evaluate(self):
+        G = self.G
+        loss = torch.zeros(G, device=self.device)
+        binc = torch.zeros(G, device=self.device)
+        catc = torch.zeros(G, device=self.device)
+        maxv = self.val_mat.shape[1]
+        eb = self.cfg.eval_batch
+        with torch.no_grad():
+            for s in range(0, maxv, eb):
+                idx = self.val_mat[:, s:s + eb]
+                mask = self.val_mask[:, s:s + eb]
+                xb = self._gather(idx)
+                yb = self.data.onehot.index_select(0, idx.reshape(-1)).view(G, idx.shape[1], -1)
+                if self.amp:
+                    with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
+                        logits = self._forward(xb, False)
+                else:
+                    logits = self._forward(xb, False)
+                per, b, c = loss_and_metrics(logits, yb, self.cfg.loss)
+                loss += (per * mask).sum(-1)
+                binc += (b * mask).sum(-1)
+                catc += (c * mask).sum(-1)
+        return loss, binc, catc
+
+
+def make_job(backend, plan, x, y, folds, cfg, device, fold_ids=None, stream=None):
+    if backend == "torch":
+        return TorchFoldJob(plan, x, y, folds, cfg, device, fold_ids=fold_ids, stream=stream)
+    if backend == "hip":
+        from .cnn_hip import HipFoldJob
+        return HipFoldJob(plan, x, y, folds, cfg, device, fold_ids=fold_ids, stream=stream)
+    raise ValueError("unknown backend {!r}".format(backend))
+
+
+def default_backend(device):
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        return "torch"
+    return "hip"

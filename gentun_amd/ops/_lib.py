@@ -1,0 +1,79 @@
+"""Loader for the in-tree native libraries (built by ``tools/build_native.py``).
+
+The libraries are plain shared objects with a C ABI, loaded with ctypes:
+the HIP kernels take raw device pointers plus the ``hipStream_t`` of the
+caller's current torch stream, so they are captured into HIP graphs exactly
+like torch's own launches. If a library is missing it is built on first use
+(hipcc cross-compiles without a GPU); on a GPU box a missing or unloadable
+HIP library is a hard error -- there is no silent fallback.
+"""
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+NATIVE_DIR = os.path.join(os.path.dirname(_HERE), "_native")
+_LOCK = threading.Lock()
+_LIBS = {}
+
+
+def _path(name):
+    return os.path.join(NATIVE_DIR, name)
+
+
+def _ensure_built(name):
+    import sys
+    root = os.path.dirname(os.path.dirname(_HERE))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    from tools import build_native
+    return build_native.build_target(name)
+
+
+def load(name):
+    with _LOCK:
+        lib = _LIBS.get(name)
+        if lib is not None:
+            return lib
+        path = _path(name)
+        if os.environ.get("GENTUN_NO_AUTOBUILD") != "1":
+            try:
+                _ensure_built(name)
+            except Exception as exc:  # noqa: BLE001
+                if not os.path.exists(path):
+                    raise RuntimeError("native library {} missing and build failed: {}".format(name, exc))
+        if not os.path.exists(path):
+            raise RuntimeError("native library {} not found at {}".format(name, path))
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        _LIBS[name] = lib
+        return lib
+
+
+def gbdt():
+    lib = load("libgentun_gbdt.so")
+    if not getattr(lib, "_typed", False):
+        c = ctypes
+        lib.gbdt_cv.restype = c.c_int
+        lib.gbdt_cv.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p,
+                                c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_ulonglong, c.c_int,
+                                c.c_void_p]
+        lib.gbdt_quantize.restype = c.c_int
+        lib.gbdt_quantize.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
+        lib._typed = True
+    return lib
+
+
+def hip():
+    """The gfx950 kernel library (raises if it cannot be loaded)."""
+    return load("libgentun_hip.so")
+
+
+def load_all(require_gpu=False):
+    out = {"gbdt": gbdt()}
+    try:
+        out["hip"] = hip()
+    except Exception:
+        if require_gpu:
+            raise
+    return out

@@ -1,0 +1,437 @@
+"""Master/evaluator protocol over collectives (RCCL on MI355X).
+
+Reference: ``DistributedPopulation`` / ``DistributedGridPopulation``
+(gentun/master.py:82-145) fan jobs out as JSON over RabbitMQ, one connection
++ one thread per job, and ``GentunWorker`` (gentun/worker.py:13-66) consumes
+them. Here every rank is a persistent evaluator
+(one per GPU) and rank 0 also runs the GA:
+
+per generation (collectives X2/X3 of SURVEY.md §2.6)
+  1. rank 0 broadcasts ``int64[4]`` = (command, generation, P, nfold),
+     the species' ``additional_parameters`` as a JSON blob (X1), and the
+     genome table ``float64[U, 3 + width]`` = (candidate slot, owner rank,
+     fold mask, encoded genes) for the ``U`` work units;
+  2. every rank evaluates the units it owns (several concurrently on its GPU,
+     :class:`~gentun_amd.parallel.evaluators.LocalBatchEvaluator`);
+  3. one ``all_gather`` of ``float64[U, 3 + nfold]`` = (status, fitness,
+     wall_s, fold scores) -- < 2 KB, latency-bound on xGMI;
+  4. rank 0 merges fold groups per candidate, re-evaluates failed units
+     locally once (worst fitness if that fails too) and breeds.
+
+Failure handling: collective timeout from
+``init_process_group(timeout=...)``; per-unit status codes; fault injection
+via ``GENTUN_FAULT="rank:generation:kind"`` (kind = ``raise``).
+"""
+
+import json
+import os
+import time
+import warnings
+
+import numpy as np
+
+from ..populations import Population, GridPopulation
+from .comm import LocalComm, from_env
+from .evaluators import LocalBatchEvaluator
+from .scheduler import lpt_assign, make_units
+
+CMD_STOP, CMD_EVAL, CMD_SYNC = 0, 1, 2
+ST_NONE, ST_OK, ST_ERR = 0.0, 1.0, 2.0
+
+
+# ---------------------------------------------------------------------------
+# genome codec
+# ---------------------------------------------------------------------------
+
+class GenomeCodec(object):
+    """Encode genes as a float64 row (bits -> 0/1, numbers as-is)."""
+
+    def __init__(self, genome):
+        self.names = sorted(genome)
+        self.genome = genome
+        self.kind = []
+        self.width = 0
+        for n in self.names:
+            spec = genome[n]
+            if isinstance(spec, int) and not isinstance(spec, bool):      # bit string of `spec` bits
+                self.kind.append(("bits", spec))
+                self.width += spec
+            else:
+                is_int = isinstance(spec[0], int) and not isinstance(spec[0], bool)
+                self.kind.append(("int" if is_int else "float", 1))
+                self.width += 1
+
+    def encode(self, genes):
+        row = np.zeros(self.width, np.float64)
+        o = 0
+        for n, (kind, w) in zip(self.names, self.kind):
+            v = genes[n]
+            if kind == "bits":
+                row[o:o + w] = [1.0 if c == '1' else 0.0 for c in v]
+            else:
+                row[o] = float(v)
+            o += w
+        return row
+
+    def decode(self, row):
+        genes, o = {}, 0
+        for n, (kind, w) in zip(self.names, self.kind):
+            if kind == "bits":
+                genes[n] = ''.join('1' if x > 0.5 else '0' for x in row[o:o + w])
+            elif kind == "int":
+                genes[n] = int(round(row[o]))
+            else:
+                genes[n] = float(row[o])
+            o += w
+        return genes
+
+
+def _jsonable(d):
+    out = {}
+    for k, v in d.items():
+        out[k] = list(v) if isinstance(v, tuple) else v
+    return out
+
+
+def _tuplify(v):
+    if isinstance(v, list):
+        return tuple(_tuplify(x) for x in v)
+    return v
+
+
+def _fault_hook(rank, generation):
+    spec = os.environ.get("GENTUN_FAULT")
+    if not spec:
+        return
+    try:
+        r, g, kind = spec.split(":")
+    except ValueError:
+        return
+    if int(r) == rank and int(g) == generation and kind == "raise":
+        raise RuntimeError("injected fault on rank {} generation {}".format(rank, generation))
+
+
+class _Unit(object):
+    """A (candidate, fold-group) work unit materialised on one rank."""
+
+    def __init__(self, slot, ind, fold_ids):
+        self.slot = slot
+        self.ind = ind
+        self.fold_ids = fold_ids
+
+
+def evaluate_units(units, evaluator, nfold, rank, generation):
+    """Evaluate this rank's units; returns ``{unit_index: row}``."""
+    rows = {}
+    cnn_units, other_units = [], []
+    for ui, u in units:
+        (cnn_units if hasattr(u.ind, "build_fitness_model") else other_units).append((ui, u))
+    for ui, u in other_units:
+        t0 = time.perf_counter()
+        try:
+            _fault_hook(rank, generation)
+            u.ind.evaluate_fitness()
+            scores = u.ind.fold_scores or []
+            rows[ui] = _row(ST_OK, u.ind.fitness, time.perf_counter() - t0, scores, nfold, u.fold_ids)
+        except Exception as exc:     # noqa: BLE001 -- reported as a status code
+            warnings.warn("evaluation failed on rank {}: {}".format(rank, exc))
+            rows[ui] = _row(ST_ERR, np.nan, time.perf_counter() - t0, [], nfold, u.fold_ids)
+    if cnn_units:
+        try:
+            _fault_hook(rank, generation)
+            rows.update(_evaluate_cnn_units(cnn_units, evaluator, nfold))
+        except Exception as exc:     # noqa: BLE001
+            warnings.warn("CNN evaluation failed on rank {}: {}".format(rank, exc))
+            for ui, u in cnn_units:
+                rows[ui] = _row(ST_ERR, np.nan, 0.0, [], nfold, u.fold_ids)
+    return rows
+
+
+def _evaluate_cnn_units(cnn_units, evaluator, nfold):
+    """Launch every unit's fold-batched job on the evaluator's streams."""
+    streams = evaluator.streams() if hasattr(evaluator, "streams") else [None]
+    device = getattr(evaluator, "device", None)
+    order = sorted(range(len(cnn_units)), key=lambda k: -cnn_units[k][1].ind.cost() * len(cnn_units[k][1].fold_ids))
+    rows, window = {}, []
+
+    def retire(entry):
+        ui, u, model, jobs, t0 = entry
+        res = [job.finish() for job in jobs]
+        merged = {"binary_accuracy": [], "categorical_accuracy": [], "val_loss": []}
+        for r in res:
+            for k in merged:
+                merged[k].extend(r[k])
+        scores = merged[model.primary_metric()]
+        rows[ui] = _row(ST_OK, float(np.mean(scores)), time.perf_counter() - t0, scores, nfold, u.fold_ids)
+
+    for k, idx in enumerate(order):
+        ui, u = cnn_units[idx]
+        if len(window) >= len(streams):
+            retire(window.pop(0))
+        model = u.ind.build_fitness_model(device=device)
+        jobs = model.make_jobs(stream=streams[k % len(streams)], fold_ids=u.fold_ids)
+        t0 = time.perf_counter()
+        for job in jobs:
+            job.launch()
+        window.append((ui, u, model, jobs, t0))
+    for entry in window:
+        retire(entry)
+    return rows
+
+
+def _row(status, fitness, wall, scores, nfold, fold_ids):
+    row = np.full(3 + nfold, np.nan, np.float64)
+    row[0], row[1], row[2] = status, fitness, wall
+    for j, f in enumerate(fold_ids[:len(scores)]):
+        row[3 + f] = scores[j]
+    return row
+
+
+# ---------------------------------------------------------------------------
+# master side
+# ---------------------------------------------------------------------------
+
+class DistributedPopulation(Population):
+    """Population whose pending individuals are evaluated by all ranks.
+
+    Signature-compatible with gentun/master.py:88-90. ``host``/``port`` map
+    to ``MASTER_ADDR``/``MASTER_PORT`` when the process group still has to be
+    created; ``user``/``password``/``rabbit_queue`` have no meaning without a
+    broker and are accepted for compatibility.
+    """
+
+    def __init__(self, species, x_train=None, y_train=None, individual_list=None, size=None,
+                 crossover_rate=0.5, mutation_rate=0.015, maximize=True, additional_parameters=None,
+                 host='localhost', port=5672, user='guest', password='guest', rabbit_queue='rpc_queue',
+                 comm=None, evaluator=None, split_folds=True):
+        self.comm = comm if comm is not None else _comm_from_args(host, port)
+        if evaluator is None:
+            evaluator = LocalBatchEvaluator()
+        self.local_evaluator = evaluator
+        self.split_folds = split_folds
+        self.credentials = {'host': host, 'port': port, 'user': user, 'password': password,
+                            'rabbit_queue': rabbit_queue}
+        self.generation_counter = 0
+        self.last_dispatch = None
+        super(DistributedPopulation, self).__init__(
+            species, x_train, y_train, individual_list, size, crossover_rate, mutation_rate, maximize,
+            additional_parameters, evaluator=None)
+
+    def empty_like(self, individual_list=None):
+        pop = DistributedPopulation.__new__(DistributedPopulation)
+        pop.comm = self.comm
+        pop.local_evaluator = self.local_evaluator
+        pop.split_folds = self.split_folds
+        pop.credentials = dict(self.credentials)
+        pop.generation_counter = self.generation_counter
+        pop.last_dispatch = None
+        Population.__init__(pop, self.species, self.x_train, self.y_train,
+                            individual_list=[] if individual_list is None else individual_list,
+                            crossover_rate=self.crossover_rate, mutation_rate=self.mutation_rate,
+                            maximize=self.maximize, additional_parameters=self.additional_parameters)
+        return pop
+
+    def get_fittest(self):
+        self.evaluate_in_parallel()
+        return Population.get_fittest(self)
+
+    def evaluate_pending(self):
+        return self.evaluate_in_parallel()
+
+    def evaluate_in_parallel(self):
+        """Dispatch pending individuals to every rank and collect fitness."""
+        todo = self.pending()
+        if not todo:
+            return 0
+        self.generation_counter += 1
+        comm = self.comm
+        nfold = int(getattr(todo[0], "nfold", 1) or 1)
+        codec = GenomeCodec(todo[0].get_genome())
+        costs = [float(ind.cost()) if hasattr(ind, "cost") else 1.0 for ind in todo]
+        splittable = self.split_folds and hasattr(todo[0], "build_fitness_model")
+        units, ucost = make_units(costs, nfold, comm.world_size, splittable)
+        owner = lpt_assign(ucost, comm.world_size)
+        table = np.zeros((len(units), 3 + codec.width), np.float64)
+        for k, (slot, fids) in enumerate(units):
+            table[k, 0] = slot
+            table[k, 1] = owner[k]
+            table[k, 2] = sum(1 << f for f in fids)
+            table[k, 3:] = codec.encode(todo[slot].get_genes())
+        extra = _jsonable(todo[0].get_additional_parameters())
+        blob = np.frombuffer(json.dumps({"species": self.species.__name__, "extra": extra}).encode(), np.uint8)
+        t0 = time.perf_counter()
+        comm.broadcast_array(np.array([CMD_EVAL, self.generation_counter, len(todo), nfold], np.int64))
+        comm.broadcast_array(blob)
+        comm.broadcast_array(table)
+        mine = [(k, _Unit(slot, todo[slot] if len(fids) == nfold else _clone(todo[slot]), fids))
+                for k, (slot, fids) in enumerate(units) if owner[k] == comm.rank]
+        rows = evaluate_units(mine, self.local_evaluator, nfold, comm.rank, self.generation_counter)
+        local = np.zeros((len(units), 3 + nfold), np.float64)
+        for k, row in rows.items():
+            local[k] = row
+        gathered = comm.all_gather_array(local)
+        merged = _merge(gathered, units, len(todo), nfold)
+        retried = 0
+        for slot, ind in enumerate(todo):
+            status, fitness, scores = merged[slot]
+            if status != ST_OK:
+                retried += 1
+                try:
+                    ind.set_fitness(None)
+                    ind.evaluate_fitness()
+                except Exception as exc:   # noqa: BLE001
+                    warnings.warn("re-evaluation of slot {} failed: {}".format(slot, exc))
+                    ind.set_fitness(float("-inf") if self.maximize else float("inf"))
+            else:
+                ind.set_fitness(fitness)
+                ind.fold_scores = scores
+        self.last_dispatch = {"units": len(units), "candidates": len(todo), "retried": retried,
+                              "wall_s": time.perf_counter() - t0,
+                              "per_rank_units": [int(sum(1 for o in owner if o == r)) for r in range(comm.world_size)]}
+        return len(todo)
+
+    def sync_ranks(self):
+        """Device-synchronise every rank and barrier (bench timing fence)."""
+        if self.comm.world_size > 1:
+            self.comm.broadcast_array(np.array([CMD_SYNC, self.generation_counter, 0, 0], np.int64))
+        _device_sync(self.local_evaluator)
+        self.comm.barrier()
+
+    def shutdown(self):
+        """Release the evaluator ranks (they return from ``work()``)."""
+        if self.comm.world_size > 1:
+            self.comm.broadcast_array(np.array([CMD_STOP, self.generation_counter, 0, 0], np.int64))
+
+
+def _clone(ind):
+    twin = ind.copy()
+    twin.set_fitness(None)
+    return twin
+
+
+def _merge(gathered, units, ncand, nfold):
+    """Combine per-rank result tables into ``(status, fitness, fold_scores)`` per candidate."""
+    per = [{"status": ST_OK, "scores": [np.nan] * nfold, "fit": [], "n": 0} for _ in range(ncand)]
+    have = [False] * len(units)
+    rows = [None] * len(units)
+    for table in gathered:
+        for k in range(len(units)):
+            if table[k, 0] != ST_NONE and not have[k]:
+                have[k] = True
+                rows[k] = table[k]
+    for k, (slot, fids) in enumerate(units):
+        row = rows[k]
+        p = per[slot]
+        if row is None or row[0] != ST_OK:
+            p["status"] = ST_ERR
+            continue
+        p["fit"].append((row[1], len(fids)))
+        for f in fids:
+            p["scores"][f] = float(row[3 + f])
+    out = []
+    for p in per:
+        if p["status"] != ST_OK or not p["fit"]:
+            out.append((ST_ERR, None, None))
+            continue
+        scores = [s for s in p["scores"] if not np.isnan(s)]
+        if scores and len(scores) == sum(n for _, n in p["fit"]):
+            fit = float(np.mean(scores))
+        else:
+            tot = sum(n for _, n in p["fit"])
+            fit = float(sum(f * n for f, n in p["fit"]) / tot)
+        out.append((ST_OK, fit, p["scores"] if scores else None))
+    return out
+
+
+class DistributedGridPopulation(DistributedPopulation, GridPopulation):
+    """Grid-initialised distributed population (gentun/master.py:132-145)."""
+
+    def __init__(self, species, x_train=None, y_train=None, individual_list=None, genes_grid=None,
+                 crossover_rate=0.5, mutation_rate=0.015, maximize=True, additional_parameters=None,
+                 host='localhost', port=5672, user='guest', password='guest', rabbit_queue='rpc_queue',
+                 comm=None, evaluator=None, split_folds=True):
+        if individual_list is None and genes_grid is not None:
+            grid = GridPopulation(species, x_train, y_train, genes_grid=genes_grid, crossover_rate=crossover_rate,
+                                  mutation_rate=mutation_rate, maximize=maximize,
+                                  additional_parameters=additional_parameters)
+            individual_list = grid.individuals
+        DistributedPopulation.__init__(self, species, x_train, y_train, individual_list, None, crossover_rate,
+                                       mutation_rate, maximize, additional_parameters, host, port, user,
+                                       password, rabbit_queue, comm, evaluator, split_folds)
+
+
+# ---------------------------------------------------------------------------
+# evaluator ranks
+# ---------------------------------------------------------------------------
+
+class GentunWorker(object):
+    """Evaluator rank (gentun/worker.py:13-66): serve generations broadcast by
+    rank 0 until it broadcasts STOP."""
+
+    def __init__(self, individual, x_train, y_train, host='localhost', port=5672, user='guest',
+                 password='guest', rabbit_queue='rpc_queue', comm=None, evaluator=None):
+        self.individual = individual
+        self.x_train = x_train
+        self.y_train = y_train
+        self.comm = comm if comm is not None else _comm_from_args(host, port)
+        self.evaluator = evaluator if evaluator is not None else LocalBatchEvaluator()
+        self.served = 0
+
+    def serve_one(self):
+        """Handle one broadcast; returns False on STOP."""
+        comm = self.comm
+        hdr = comm.broadcast_array(None)
+        cmd, generation, _ncand, nfold = (int(v) for v in hdr)
+        if cmd == CMD_STOP:
+            return False
+        if cmd == CMD_SYNC:
+            _device_sync(self.evaluator)
+            comm.barrier()
+            return True
+        blob = comm.broadcast_array(None)
+        meta = json.loads(bytes(blob.astype(np.uint8)).decode())
+        table = comm.broadcast_array(None)
+        extra = {k: _tuplify(v) for k, v in meta["extra"].items()}
+        mine = []
+        codec = None
+        for k in range(table.shape[0]):
+            if int(table[k, 1]) != comm.rank:
+                continue
+            if codec is None:
+                codec = GenomeCodec(self.individual(None, None, **extra).get_genome())
+            genes = codec.decode(table[k, 3:])
+            fids = [f for f in range(nfold) if (int(table[k, 2]) >> f) & 1]
+            ind = self.individual(self.x_train, self.y_train, genes=genes, **extra)
+            mine.append((k, _Unit(int(table[k, 0]), ind, fids)))
+        rows = evaluate_units(mine, self.evaluator, nfold, comm.rank, generation)
+        local = np.zeros((table.shape[0], 3 + nfold), np.float64)
+        for k, row in rows.items():
+            local[k] = row
+        comm.all_gather_array(local)
+        self.served += len(mine)
+        return True
+
+    def work(self):
+        print(" [x] Evaluator rank {} of {} awaiting generations".format(self.comm.rank, self.comm.world_size))
+        try:
+            while self.serve_one():
+                pass
+        except KeyboardInterrupt:
+            print()
+        print("Good bye!")
+
+
+def _comm_from_args(host, port):
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return LocalComm()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1" if host == "localhost" else str(host))
+    if port != 5672:
+        os.environ.setdefault("MASTER_PORT", str(port))
+    return from_env()
+
+
+def _device_sync(evaluator):
+    dev = getattr(evaluator, "device", None)
+    if dev is not None and getattr(dev, "type", "") == "cuda":
+        import torch
+        torch.cuda.synchronize(dev)

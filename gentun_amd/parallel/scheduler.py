@@ -1,0 +1,58 @@
+"""Static work assignment for a generation (SURVEY.md §5.8, §7.3 hard part 3).
+
+The reference load-balances dynamically through a RabbitMQ pull queue with
+``prefetch_count=1`` (gentun/worker.py:59-63). Here every rank receives the
+whole genome table, so an assignment computed on rank 0 from a cost model
+(forward FLOPs per sample, :meth:`Plan.forward_flops`) is broadcast with it.
+
+Work units are ``(candidate, fold-group)``. A candidate's folds stay
+together (one fold-batched launch) unless there are fewer candidates than
+ranks, in which case candidates are split into fold groups so every GPU gets
+work. Units are placed Longest-Processing-Time-first on the least-loaded
+rank; ties break on rank id, so the result is deterministic.
+"""
+
+import heapq
+
+
+def lpt_assign(costs, world_size):
+    """Return ``owner[i]`` for each unit cost (LPT greedy)."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    heap = [(0.0, r) for r in range(world_size)]
+    heapq.heapify(heap)
+    owner = [0] * len(costs)
+    for i in order:
+        load, r = heapq.heappop(heap)
+        owner[i] = r
+        heapq.heappush(heap, (load + costs[i], r))
+    return owner
+
+
+def make_units(costs, nfold, world_size, split_folds=True):
+    """Units ``(candidate, fold_ids)`` with their costs.
+
+    Splits candidates into fold groups only while that helps fill the ranks:
+    the number of groups per candidate is ``min(nfold, ceil(world/ncand))``.
+    """
+    n = len(costs)
+    if n == 0:
+        return [], []
+    groups = 1
+    if split_folds and nfold > 1 and n < world_size:
+        groups = min(nfold, -(-world_size // n))
+    units, ucost = [], []
+    for i, c in enumerate(costs):
+        folds = list(range(nfold))
+        size = -(-nfold // groups)
+        for g0 in range(0, nfold, size):
+            fid = folds[g0:g0 + size]
+            units.append((i, fid))
+            ucost.append(c * len(fid) / float(nfold))
+    return units, ucost
+
+
+def makespan(costs, owner, world_size):
+    loads = [0.0] * world_size
+    for c, r in zip(costs, owner):
+        loads[r] += c
+    return max(loads) if loads else 0.0

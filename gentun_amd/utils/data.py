@@ -1,0 +1,150 @@
+"""Datasets and cross-validation splits.
+
+* ``make_cifar_like``  -- synthetic CIFAR-10-shaped data (32x32x3, 10
+  classes) with *learnable* class structure (class templates + nuisance
+  transforms + noise), the protocol fixed in BASELINE.md (there is no
+  network, so real CIFAR-10 cannot be fetched).
+* ``make_mnist_like``  -- same idea at 28x28x1 (reference driver config,
+  tests/test_mnist.py:17-34, whose MNIST download is dead).
+* ``load_iris_xy`` / ``load_wine_quality`` -- tabular fixtures for the GBDT
+  species (BASELINE cfg 1; reference tests/test_wine-quality.py:15-19).
+* ``stratified_kfold`` / ``kfold`` -- deterministic fold builders (the
+  reference uses an unseeded ``StratifiedKFold(shuffle=True)``,
+  gentun/models/keras_models.py:132; xgboost's ``cv`` uses seed 0).
+"""
+
+import os
+
+import numpy as np
+
+
+def _smooth_field(rng, h, w, c, scale):
+    """Low-frequency random pattern in [-1, 1] (sum of a few 2-D cosines)."""
+    yy, xx = np.meshgrid(np.linspace(0, 1, h, dtype=np.float32), np.linspace(0, 1, w, dtype=np.float32),
+                         indexing="ij")
+    out = np.zeros((h, w, c), np.float32)
+    for ch in range(c):
+        for _ in range(4):
+            fy, fx = rng.uniform(0.5, scale, size=2)
+            ph = rng.uniform(0, 2 * np.pi, size=2)
+            out[:, :, ch] += np.cos(2 * np.pi * fy * yy + ph[0]) * np.cos(2 * np.pi * fx * xx + ph[1])
+    out /= np.abs(out).max() + 1e-6
+    return out
+
+
+def make_image_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, noise=0.35, shift=3,
+                              dtype=np.float32):
+    """Synthetic image classification set: x in [0,1] NHWC, y one-hot.
+
+    Each class owns a smooth template; a sample is its template, randomly
+    translated by up to ``shift`` pixels, contrast/brightness jittered,
+    mixed with a second class's template at low weight and with Gaussian
+    noise. A small CNN reaches well above chance but not 100 %, so the GA
+    has signal to optimise.
+    """
+    rng = np.random.default_rng(seed)
+    h, w, c = shape
+    templates = np.stack([_smooth_field(rng, h + 2 * shift, w + 2 * shift, c, 4.0) for _ in range(classes)])
+    labels = np.arange(n) % classes
+    rng.shuffle(labels)
+    x = np.empty((n, h, w, c), np.float32)
+    dy = rng.integers(0, 2 * shift + 1, size=n)
+    dx = rng.integers(0, 2 * shift + 1, size=n)
+    amp = rng.uniform(0.5, 1.0, size=n).astype(np.float32)
+    bright = rng.uniform(-0.1, 0.1, size=n).astype(np.float32)
+    other = rng.integers(0, classes, size=n)
+    mix = rng.uniform(0.0, 0.45, size=n).astype(np.float32)
+    for i in range(n):
+        t = templates[labels[i], dy[i]:dy[i] + h, dx[i]:dx[i] + w]
+        o = templates[other[i], dy[i]:dy[i] + h, dx[i]:dx[i] + w]
+        x[i] = 0.5 + 0.25 * amp[i] * (t + mix[i] * o) + bright[i]
+    x += noise * 0.25 * rng.standard_normal(size=x.shape).astype(np.float32)
+    np.clip(x, 0.0, 1.0, out=x)
+    y = np.zeros((n, classes), np.float32)
+    y[np.arange(n), labels] = 1.0
+    return x.astype(dtype), y
+
+
+def make_cifar_like(n=10000, seed=0):
+    return make_image_classification(n=n, shape=(32, 32, 3), classes=10, seed=seed)
+
+
+def make_mnist_like(n=10000, seed=0):
+    return make_image_classification(n=n, shape=(28, 28, 1), classes=10, seed=seed)
+
+
+def load_iris_xy():
+    """Iris (150x4, 3 classes) from scikit-learn's bundled copy."""
+    from sklearn.datasets import load_iris
+    d = load_iris()
+    return d.data.astype(np.float64), d.target.astype(np.float64)
+
+
+def load_wine_quality(path=None):
+    """White wine quality (4,898 x 11 -> quality). ``path`` defaults to the
+    reference fixture (tests/data/winequality-white.csv, ';'-separated)."""
+    import pandas as pd
+    if path is None:
+        path = os.environ.get("GENTUN_WINE_CSV", "/root/reference/tests/data/winequality-white.csv")
+    df = pd.read_csv(path, sep=";")
+    y = df.pop("quality").to_numpy(np.float64)
+    return df.to_numpy(np.float64), y
+
+
+def make_regression(n=100000, f=32, seed=0, noise=0.1):
+    """Synthetic tabular regression with non-linear structure (GBDT bench)."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((n, f)).astype(np.float32)
+    y = (np.sin(x[:, 0]) + 0.5 * x[:, 1] * x[:, 2] + np.where(x[:, 3] > 0, 1.0, -0.5)
+         + 0.25 * x[:, 4] ** 2 + noise * rng.standard_normal(n)).astype(np.float32)
+    return x, y
+
+
+# ---------------------------------------------------------------------------
+# Cross-validation splits
+# ---------------------------------------------------------------------------
+
+def labels_from_onehot(y):
+    y = np.asarray(y)
+    if y.ndim == 2:
+        return np.argmax(y, axis=1)
+    return y.astype(np.int64)
+
+
+def stratified_kfold(labels, nfold, seed=0):
+    """Deterministic stratified shuffled k-fold.
+
+    Returns a list of ``(train_idx, val_idx)`` int64 arrays. Per class the
+    sample indices are shuffled with ``seed`` and dealt to folds in turn, so
+    fold sizes differ by at most one per class (sklearn semantics).
+    """
+    labels = np.asarray(labels)
+    n = labels.shape[0]
+    rng = np.random.default_rng(seed)
+    fold_of = np.empty(n, np.int64)
+    offset = 0
+    for cls in np.unique(labels):
+        idx = np.flatnonzero(labels == cls)
+        rng.shuffle(idx)
+        fold_of[idx] = (np.arange(idx.size) + offset) % nfold
+        offset += idx.size
+    out = []
+    for k in range(nfold):
+        val = np.flatnonzero(fold_of == k)
+        train = np.flatnonzero(fold_of != k)
+        out.append((train, val))
+    return out
+
+
+def kfold(n, nfold, seed=0, shuffle=True):
+    """Plain k-fold (xgboost ``cv`` default: shuffled, not stratified)."""
+    idx = np.arange(n)
+    if shuffle:
+        np.random.default_rng(seed).shuffle(idx)
+    parts = np.array_split(idx, nfold)
+    out = []
+    for k in range(nfold):
+        val = np.sort(parts[k])
+        train = np.sort(np.concatenate([parts[j] for j in range(nfold) if j != k]))
+        out.append((train, val))
+    return out
