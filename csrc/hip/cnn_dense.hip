@@ -1,0 +1,441 @@
+// Genetic-CNN head + optimizer kernels for MI355X (gfx950).
+//
+// step_begin   : advances the captured step's device state (batch row, Adam t,
+//                bias-corrected lr_t) -- keeps the whole step graph-replayable.
+// dense_fwd    : K7  h = dropout(relu(x W1 + b1)) on v_mfma_f32_16x16x32_bf16,
+//                A = W1^T bf16 copy [u][f], B = x [b][f]; 4 consecutive units per
+//                lane in the epilogue -> 8-byte stores; dropout keyed by
+//                hash(seed, fold, global step, row, unit) (deterministic).
+// head         : K9  logits = h W2 + b2, softmax, loss gradient (bce_compat =
+//                Keras softmax + binary_crossentropy with eps clipping, or ce),
+//                dh -> dH = dh * scale * (h > 0), dW2, db2, db1 -- one
+//                workgroup per fold, everything through LDS.
+// dense_dgrad  : K8  dX = dH W1^T on MFMA (A = W1 rows fp32->bf16, B = dH).
+// dense_wgrad_adam : K8+K10 fused: dW1 = X^T dH (K = batch, VALU) immediately
+//                applied by Adam to the fp32 master/m/v, plus the transposed
+//                bf16 copy for the next forward -- the gradient of the largest
+//                tensor (90 % of all parameters) never touches HBM.
+// adam_segments: K10 multi-tensor Adam over every other parameter; reduces
+//                the conv wgrad split-K partials in fixed order, writes bf16
+//                copies (and the flipped/transposed dgrad copy of conv weights).
+// eval_head    : per-sample loss / binary-accuracy / categorical-accuracy.
+
+#include <algorithm>
+
+#include "common.h"
+
+#define ADAM_B1 0.9f
+#define ADAM_B2 0.999f
+#define ADAM_EPS 1e-7f
+#define CLIP_EPS 1e-7f
+
+__global__ void step_begin_kernel(StepState* s) {
+  s->cur_step = s->step_ctr;
+  s->step_ctr += 1;
+  s->global_step += 1;
+  const float t = s->t + 1.0f;
+  s->t = t;
+  s->lr_t = s->lr * sqrtf(1.0f - powf(ADAM_B2, t)) / (1.0f - powf(ADAM_B1, t));
+}
+
+// ---------------------------------------------------------------------------
+struct DenseFwdArgs {
+  const uint16_t* x;       // [G][B][Fp] (pooled features, NHWC flatten)
+  const uint16_t* wt;      // [G][Up][Fp] bf16 (transposed copy of W1)
+  const float* bias;       // [G][Up]
+  uint16_t* out;           // [G][B][Up]
+  const StepState* st;
+  const int* fold_ids;     // [G]
+  int G, B, Fp, Up;
+  float drop_p;
+  int train;
+  unsigned seed;
+};
+
+// grid (Up/64, ceil(B/32), G); wave w: units [64*bx + 16w, +16) x rows [32*by, +32)
+__global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  const int g = blockIdx.z;
+  const int u_t = blockIdx.x * 64 + wave * 16;
+  const int b0 = blockIdx.y * 32;
+  const int nchunks = a.Fp >> 3;
+  const uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
+  const uint16_t* x = a.x + (long)g * a.B * a.Fp;
+  f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  const int urow = u_t + l16;
+  const int br0 = b0 + l16, br1 = b0 + 16 + l16;
+  for (int ks = 0; ks < nchunks; ks += 4) {
+    const int c = ks + kq;
+    uint4 af = make_uint4(0, 0, 0, 0), bf0 = make_uint4(0, 0, 0, 0), bf1 = make_uint4(0, 0, 0, 0);
+    if (c < nchunks) {
+      if (urow < a.Up) af = *reinterpret_cast<const uint4*>(wt + (long)urow * a.Fp + c * 8);
+      if (br0 < a.B) bf0 = *reinterpret_cast<const uint4*>(x + (long)br0 * a.Fp + c * 8);
+      if (br1 < a.B) bf1 = *reinterpret_cast<const uint4*>(x + (long)br1 * a.Fp + c * 8);
+    }
+    acc[0] = mfma16(af, bf0, acc[0]);
+    acc[1] = mfma16(af, bf1, acc[1]);
+  }
+  // D[row = unit][col = batch row]
+  const int u0 = u_t + kq * 4;
+  if (u0 >= a.Up) return;
+  const float keep_scale = 1.0f / (1.0f - a.drop_p);
+  const uint32_t thr = (uint32_t)(a.drop_p * 4294967296.0);
+  const int gstep = a.st ? a.st->global_step : 0;
+  const uint32_t fid = a.fold_ids ? (uint32_t)a.fold_ids[g] : (uint32_t)g;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = b0 + h * 16 + l16;
+    if (row >= a.B) continue;
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float z = acc[h][i] + a.bias[(long)g * a.Up + u0 + i];
+      z = fmaxf(z, 0.f);
+      if (a.train && a.drop_p > 0.f) {
+        const uint32_t r = hash4(a.seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)row, (uint32_t)(u0 + i));
+        z = (r >= thr) ? z * keep_scale : 0.f;
+      }
+      v[i] = z;
+    }
+    *reinterpret_cast<uint2*>(a.out + ((long)g * a.B + row) * a.Up + u0) = pack4(v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+struct HeadArgs {
+  const uint16_t* h;       // [G][B][Up] (post-dropout activations)
+  const float* w2;         // [G][Up][C] fp32 master
+  const float* b2;         // [G][C]
+  const int64_t* labels;   // [N]
+  const int64_t* gather;   // [steps][G][B] sample ids
+  const StepState* st;
+  float* dH;               // [G][B][Up] fp32 (pre-activation grad)
+  float* gw2;              // [G][Up][C]
+  float* gb2;              // [G][C]
+  float* gb1;              // [G][Up]
+  float* eval_out;         // eval mode: [G][B][3] (loss, binary-correct, categorical-correct)
+  int G, B, Up, C;
+  int loss_ce;             // 0 = bce_compat, 1 = ce
+  float drop_scale;        // 1/(1-p)
+  int eval;
+};
+
+#define HEAD_MAXB 64
+#define HEAD_MAXC 16
+
+__global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int g = blockIdx.x, tid = threadIdx.x;
+  const int B = a.B, Up = a.Up, C = a.C;
+  float* w2s = reinterpret_cast<float*>(smem);              // [Up][C]
+  float* logit = w2s + (long)Up * C;                         // [B][C]
+  float* dz = logit + B * C;                                  // [B][C]
+  uint16_t* hs = reinterpret_cast<uint16_t*>(dz + B * C);     // [B][Up]
+  const float* w2 = a.w2 + (long)g * Up * C;
+  for (int i = tid; i < Up * C; i += 256) w2s[i] = w2[i];
+  const uint16_t* hg = a.h + (long)g * B * Up;
+  for (int i = tid; i < (B * Up) / 8; i += 256)
+    reinterpret_cast<uint4*>(hs)[i] = reinterpret_cast<const uint4*>(hg)[i];
+  __syncthreads();
+  for (int o = tid; o < B * C; o += 256) {
+    const int b = o / C, c = o % C;
+    float s = a.b2[(long)g * C + c];
+    for (int u = 0; u < Up; ++u) s += bf2f(hs[b * Up + u]) * w2s[u * C + c];
+    logit[o] = s;
+  }
+  __syncthreads();
+  if (tid < B) {
+    const int b = tid;
+    const int step = a.st ? a.st->cur_step : 0;
+    const long sid = a.gather[((long)step * a.G + g) * B + b];
+    const int y = (int)a.labels[sid];
+    float p[HEAD_MAXC];
+    float mx = -INFINITY;
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, logit[b * C + c]);
+    float z = 0.f;
+    for (int c = 0; c < C; ++c) { p[c] = expf(logit[b * C + c] - mx); z += p[c]; }
+    int arg = 0;
+    float loss = 0.f, binc = 0.f;
+    for (int c = 0; c < C; ++c) {
+      p[c] /= z;
+      if (p[c] > p[arg]) arg = c;
+      const float yc = (c == y) ? 1.f : 0.f;
+      binc += (rintf(p[c]) == yc) ? 1.f : 0.f;
+      if (!a.loss_ce) {
+        const float pc = fminf(fmaxf(p[c], CLIP_EPS), 1.f - CLIP_EPS);
+        loss += -(yc * logf(pc) + (1.f - yc) * logf(1.f - pc)) / C;
+      }
+    }
+    if (a.loss_ce) loss = -logf(fmaxf(p[y], 1e-30f));
+    if (a.eval) {
+      float* e = a.eval_out + ((long)g * B + b) * 3;
+      e[0] = loss; e[1] = binc; e[2] = (arg == y) ? 1.f : 0.f;
+    } else {
+      const float inv_b = 1.0f / B;
+      if (a.loss_ce) {
+        for (int c = 0; c < C; ++c) dz[b * C + c] = (p[c] - ((c == y) ? 1.f : 0.f)) * inv_b;
+      } else {
+        // dL/dp_c = (pc - y)/(pc(1-pc)) / C inside the clip range, 0 where clipped
+        float dp[HEAD_MAXC], s = 0.f;
+        for (int c = 0; c < C; ++c) {
+          const float yc = (c == y) ? 1.f : 0.f;
+          const bool inside = p[c] >= CLIP_EPS && p[c] <= 1.f - CLIP_EPS;
+          const float pc = fminf(fmaxf(p[c], CLIP_EPS), 1.f - CLIP_EPS);
+          dp[c] = inside ? (pc - yc) / (pc * (1.f - pc)) / C : 0.f;
+          s += p[c] * dp[c];
+        }
+        for (int c = 0; c < C; ++c) dz[b * C + c] = p[c] * (dp[c] - s) * inv_b;
+      }
+    }
+  }
+  if (a.eval) return;
+  __syncthreads();
+  // dH[b][u] = (sum_c dz[b][c] W2[u][c]) * scale * (h > 0);  gb1[u] = sum_b dH
+  float* dHg = a.dH + (long)g * B * Up;
+  for (int u = tid; u < Up; u += 256) {
+    float sb = 0.f;
+    for (int b = 0; b < B; ++b) {
+      float s = 0.f;
+      for (int c = 0; c < C; ++c) s += dz[b * C + c] * w2s[u * C + c];
+      const float hv = bf2f(hs[b * Up + u]);
+      const float d = hv > 0.f ? s * a.drop_scale : 0.f;
+      dHg[(long)b * Up + u] = d;
+      sb += d;
+    }
+    a.gb1[(long)g * Up + u] = sb;
+  }
+  // gw2[u][c] = sum_b h[b][u] dz[b][c]
+  for (int o = tid; o < Up * C; o += 256) {
+    const int u = o / C, c = o % C;
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += bf2f(hs[b * Up + u]) * dz[b * C + c];
+    a.gw2[(long)g * Up * C + o] = s;
+  }
+  if (tid < C) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += dz[b * C + tid];
+    a.gb2[(long)g * C + tid] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+struct DenseDgradArgs {
+  const float* dH;     // [G][B][Up]
+  const float* w1;     // [G][Fp][Up] fp32 master
+  uint16_t* dx;        // [G][B][Fp]
+  int G, B, Fp, Up;
+};
+
+// grid (Fp/64, ceil(B/32), G): D[row = f][col = b], K = units
+__global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  const int g = blockIdx.z;
+  const int f_t = blockIdx.x * 64 + wave * 16;
+  const int b0 = blockIdx.y * 32;
+  const float* w1 = a.w1 + (long)g * a.Fp * a.Up;
+  const float* dH = a.dH + (long)g * a.B * a.Up;
+  const int frow = f_t + l16;
+  const int br0 = b0 + l16, br1 = b0 + 16 + l16;
+  f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  const int nchunks = a.Up >> 3;
+  for (int ks = 0; ks < nchunks; ks += 4) {
+    const int c = ks + kq;
+    float fa[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (c < nchunks) {
+      if (frow < a.Fp) {
+        const float4* p = reinterpret_cast<const float4*>(w1 + (long)frow * a.Up + c * 8);
+        const float4 q0 = p[0], q1 = p[1];
+        fa[0] = q0.x; fa[1] = q0.y; fa[2] = q0.z; fa[3] = q0.w; fa[4] = q1.x; fa[5] = q1.y; fa[6] = q1.z; fa[7] = q1.w;
+      }
+      if (br0 < a.B) {
+        const float4* p = reinterpret_cast<const float4*>(dH + (long)br0 * a.Up + c * 8);
+        const float4 q0 = p[0], q1 = p[1];
+        f0[0] = q0.x; f0[1] = q0.y; f0[2] = q0.z; f0[3] = q0.w; f0[4] = q1.x; f0[5] = q1.y; f0[6] = q1.z; f0[7] = q1.w;
+      }
+      if (br1 < a.B) {
+        const float4* p = reinterpret_cast<const float4*>(dH + (long)br1 * a.Up + c * 8);
+        const float4 q0 = p[0], q1 = p[1];
+        f1[0] = q0.x; f1[1] = q0.y; f1[2] = q0.z; f1[3] = q0.w; f1[4] = q1.x; f1[5] = q1.y; f1[6] = q1.z; f1[7] = q1.w;
+      }
+    }
+    const uint4 af = pack8(fa), b0f = pack8(f0), b1f = pack8(f1);
+    acc[0] = mfma16(af, b0f, acc[0]);
+    acc[1] = mfma16(af, b1f, acc[1]);
+  }
+  const int fo = f_t + kq * 4;
+  if (fo >= a.Fp) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = b0 + h * 16 + l16;
+    if (row >= a.B) continue;
+    float v[4] = {acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+    *reinterpret_cast<uint2*>(a.dx + ((long)g * a.B + row) * a.Fp + fo) = pack4(v);
+  }
+}
+
+// ---------------------------------------------------------------------------
+struct DenseWgradAdamArgs {
+  const uint16_t* x;   // [G][B][Fp]
+  const float* dH;     // [G][B][Up]
+  float* p; float* m; float* v;   // [G][Fp][Up]
+  uint16_t* wt;        // [G][Up][Fp] bf16 copy (transposed)
+  const StepState* st;
+  int G, B, Fp, Up;
+};
+
+// grid (Fp/16, G), 256 threads. Thread: unit quad q (4 units), rows fr, fr+2, ..., fr+14.
+__global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* xs = reinterpret_cast<float*>(smem);                       // [B][16]
+  uint16_t* tt = reinterpret_cast<uint16_t*>(xs + a.B * 16);        // [Up][16] transposed bf16 tile
+  const int g = blockIdx.y, f0 = blockIdx.x * 16, tid = threadIdx.x;
+  const uint16_t* x = a.x + (long)g * a.B * a.Fp;
+  for (int i = tid; i < a.B * 16; i += 256) {
+    const int b = i >> 4, j = i & 15;
+    xs[i] = (f0 + j < a.Fp) ? bf2f(x[(long)b * a.Fp + f0 + j]) : 0.f;
+  }
+  __syncthreads();
+  const float lr_t = a.st->lr_t;
+  const float* dH = a.dH + (long)g * a.B * a.Up;
+  const int nq = a.Up >> 2;
+  const int fr = tid >> 7;
+  for (int q = tid & 127; q < nq; q += 128) {
+    const int u0 = q * 4;
+    float acc[8][4];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0.f;
+    for (int b = 0; b < a.B; ++b) {
+      const float4 d = *reinterpret_cast<const float4*>(dH + (long)b * a.Up + u0);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float xv = xs[b * 16 + fr + 2 * r];
+        acc[r][0] += xv * d.x; acc[r][1] += xv * d.y; acc[r][2] += xv * d.z; acc[r][3] += xv * d.w;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int f = f0 + fr + 2 * r;
+      if (f >= a.Fp) continue;
+      const long off = ((long)g * a.Fp + f) * a.Up + u0;
+      float4 pp = *reinterpret_cast<float4*>(a.p + off);
+      float4 mm = *reinterpret_cast<float4*>(a.m + off);
+      float4 vv = *reinterpret_cast<float4*>(a.v + off);
+      float* P = &pp.x; float* M = &mm.x; float* V = &vv.x;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gr = acc[r][i];
+        M[i] = ADAM_B1 * M[i] + (1.f - ADAM_B1) * gr;
+        V[i] = ADAM_B2 * V[i] + (1.f - ADAM_B2) * gr * gr;
+        P[i] -= lr_t * M[i] / (sqrtf(V[i]) + ADAM_EPS);
+        tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
+      }
+      *reinterpret_cast<float4*>(a.p + off) = pp;
+      *reinterpret_cast<float4*>(a.m + off) = mm;
+      *reinterpret_cast<float4*>(a.v + off) = vv;
+    }
+  }
+  __syncthreads();
+  // transposed bf16 copy: wt[u][f0 .. f0+15] (32 contiguous bytes per unit)
+  uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
+  for (int i = tid; i < a.Up * 2; i += 256) {
+    const int u = i >> 1, half = i & 1;
+    if (f0 + half * 8 + 8 <= a.Fp) {
+      *reinterpret_cast<uint4*>(wt + (long)u * a.Fp + f0 + half * 8) =
+          *reinterpret_cast<const uint4*>(&tt[u * 16 + half * 8]);
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (f0 + half * 8 + j < a.Fp) wt[(long)u * a.Fp + f0 + half * 8 + j] = tt[u * 16 + half * 8 + j];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+struct AdamSeg {
+  float* p; float* m; float* v;
+  const float* g;        // gradient (or S split-K partials, stride gstride)
+  uint16_t* bf;          // optional bf16 copy (same layout)
+  uint16_t* bfT;         // optional flipped/transposed conv copy [G][Ci][KH][KW][Co]
+  long n, gstride;
+  int S, tG, tCo, tKH, tKW, tCi, pad;
+};
+
+struct AdamArgs {
+  const AdamSeg* segs;
+  const int2* blocks;    // per block: (segment, element offset)
+  const StepState* st;
+};
+
+__global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
+  const int2 blk = a.blocks[blockIdx.x];
+  const AdamSeg sg = a.segs[blk.x];
+  const long i = (long)blk.y + threadIdx.x;
+  if (i >= sg.n) return;
+  float gr = 0.f;
+  for (int s = 0; s < sg.S; ++s) gr += sg.g[(long)s * sg.gstride + i];
+  const float lr_t = a.st->lr_t;
+  float m = ADAM_B1 * sg.m[i] + (1.f - ADAM_B1) * gr;
+  float v = ADAM_B2 * sg.v[i] + (1.f - ADAM_B2) * gr * gr;
+  float p = sg.p[i] - lr_t * m / (sqrtf(v) + ADAM_EPS);
+  sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
+  const uint16_t pb = f2bf(p);
+  if (sg.bf) sg.bf[i] = pb;
+  if (sg.bfT) {
+    long r = i;
+    const int ci = (int)(r % sg.tCi); r /= sg.tCi;
+    const int kw = (int)(r % sg.tKW); r /= sg.tKW;
+    const int kh = (int)(r % sg.tKH); r /= sg.tKH;
+    const int co = (int)(r % sg.tCo);
+    const long gg = r / sg.tCo;
+    const long o = ((((gg * sg.tCi + ci) * sg.tKH + (sg.tKH - 1 - kh)) * sg.tKW) + (sg.tKW - 1 - kw)) * sg.tCo + co;
+    sg.bfT[o] = pb;
+  }
+}
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int gt_step_begin(StepState* s, hipStream_t stream) {
+  hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, stream, s);
+  return (int)hipGetLastError();
+}
+
+int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
+  if (a->Fp % 8 || a->Up % 64) return -1;
+  dim3 grid(a->Up / 64, (a->B + 31) / 32, a->G);
+  hipLaunchKernelGGL(dense_fwd_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+int gt_head(const HeadArgs* a, hipStream_t stream) {
+  if (a->B > HEAD_MAXB || a->C > HEAD_MAXC || (a->B * a->Up) % 8) return -1;
+  const size_t lds = sizeof(float) * ((size_t)a->Up * a->C + 2 * a->B * a->C) + 2 * (size_t)a->B * a->Up;
+  if (lds > 160 * 1024) return -2;
+  hipLaunchKernelGGL(head_kernel, dim3(a->G), dim3(256), lds, stream, *a);
+  return (int)hipGetLastError();
+}
+
+int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
+  if (a->Fp % 64 && a->Fp % 8) return -1;
+  if (a->Up % 8) return -1;
+  dim3 grid((a->Fp + 63) / 64, (a->B + 31) / 32, a->G);
+  hipLaunchKernelGGL(dense_dgrad_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+int gt_dense_wgrad_adam(const DenseWgradAdamArgs* a, hipStream_t stream) {
+  if (a->Up % 4) return -1;
+  const size_t lds = sizeof(float) * (size_t)a->B * 16 + 2 * (size_t)a->Up * 16;
+  if (lds > 160 * 1024) return -2;
+  dim3 grid((a->Fp + 15) / 16, a->G);
+  hipLaunchKernelGGL(dense_wgrad_adam_kernel, grid, dim3(256), lds, stream, *a);
+  return (int)hipGetLastError();
+}
+
+int gt_adam_segments(const AdamArgs* a, int nblocks, hipStream_t stream) {
+  hipLaunchKernelGGL(adam_segments_kernel, dim3(nblocks), dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
+size_t gt_sizeof_adam_seg() { return sizeof(AdamSeg); }
+
+}  // extern "C"

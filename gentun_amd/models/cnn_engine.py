@@ -218,7 +218,9 @@ class FoldJob(object):
     # -- driver --------------------------------------------------------------
     def _capture(self):
         snap = self.snapshot()
-        self._new_epoch_order()
+        # warm-up steps read the (still all-zero, i.e. valid) batch table; the
+        # shuffle streams are NOT advanced so graph and eager runs are identical
+        self.step_ctr.zero_()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):

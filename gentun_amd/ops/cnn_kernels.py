@@ -1,0 +1,96 @@
+"""ctypes bindings of the Genetic-CNN HIP kernels (csrc/hip/cnn_*.hip).
+
+Every launcher takes raw device pointers and the caller's current
+``hipStream_t`` (``torch.cuda.current_stream().cuda_stream``), so launches
+interleave with torch's own and are captured by HIP graphs.
+"""
+
+import ctypes as C
+
+from . import _lib
+
+P = C.c_void_p
+I = C.c_int
+
+
+class ConvArgs(C.Structure):
+    _fields_ = [("inp", P * 4), ("mask", P), ("gather", P), ("st", P), ("out", P * 4), ("w", P), ("bias", P),
+                ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
+                ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
+                ("TH", I)]
+
+
+class WgradArgs(C.Structure):
+    _fields_ = [("inp", P * 4), ("gather", P), ("st", P), ("dy", P), ("ymask", P), ("part_w", P),
+                ("part_b", P), ("n_in", I), ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I),
+                ("KH", I), ("KW", I), ("S", I), ("pps", I)]
+
+
+class DenseFwdArgs(C.Structure):
+    _fields_ = [("x", P), ("wt", P), ("bias", P), ("out", P), ("st", P), ("fold_ids", P),
+                ("G", I), ("B", I), ("Fp", I), ("Up", I), ("drop_p", C.c_float), ("train", I),
+                ("seed", C.c_uint)]
+
+
+class HeadArgs(C.Structure):
+    _fields_ = [("h", P), ("w2", P), ("b2", P), ("labels", P), ("gather", P), ("st", P), ("dH", P),
+                ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P),
+                ("G", I), ("B", I), ("Up", I), ("C", I), ("loss_ce", I), ("drop_scale", C.c_float), ("eval", I)]
+
+
+class DenseDgradArgs(C.Structure):
+    _fields_ = [("dH", P), ("w1", P), ("dx", P), ("G", I), ("B", I), ("Fp", I), ("Up", I)]
+
+
+class DenseWgradAdamArgs(C.Structure):
+    _fields_ = [("x", P), ("dH", P), ("p", P), ("m", P), ("v", P), ("wt", P), ("st", P),
+                ("G", I), ("B", I), ("Fp", I), ("Up", I)]
+
+
+class AdamSeg(C.Structure):
+    _fields_ = [("p", P), ("m", P), ("v", P), ("g", P), ("bf", P), ("bfT", P), ("n", C.c_long),
+                ("gstride", C.c_long), ("S", I), ("tG", I), ("tCo", I), ("tKH", I), ("tKW", I), ("tCi", I),
+                ("pad", I)]
+
+
+class AdamArgs(C.Structure):
+    _fields_ = [("segs", P), ("blocks", P), ("st", P)]
+
+
+_TYPED = {}
+
+
+def lib():
+    L = _lib.hip()
+    if not _TYPED.get(id(L)):
+        for name, argt in (("gt_conv_fwd", C.POINTER(ConvArgs)), ("gt_conv_wgrad", C.POINTER(WgradArgs)),
+                           ("gt_dense_fwd", C.POINTER(DenseFwdArgs)), ("gt_head", C.POINTER(HeadArgs)),
+                           ("gt_dense_dgrad", C.POINTER(DenseDgradArgs)),
+                           ("gt_dense_wgrad_adam", C.POINTER(DenseWgradAdamArgs))):
+            fn = getattr(L, name)
+            fn.argtypes = [argt, P]
+            fn.restype = I
+        L.gt_adam_segments.argtypes = [C.POINTER(AdamArgs), I, P]
+        L.gt_adam_segments.restype = I
+        L.gt_step_begin.argtypes = [P, P]
+        L.gt_step_begin.restype = I
+        L.gt_pool_fwd.argtypes = [P, P, I, I, I, I, P]
+        L.gt_pool_fwd.restype = I
+        L.gt_pool_bwd.argtypes = [P, P, P, I, I, I, I, P]
+        L.gt_pool_bwd.restype = I
+        for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg"):
+            getattr(L, name).restype = C.c_size_t
+        assert L.gt_sizeof_conv_args() == C.sizeof(ConvArgs), "ConvArgs ABI mismatch"
+        assert L.gt_sizeof_wgrad_args() == C.sizeof(WgradArgs), "WgradArgs ABI mismatch"
+        assert L.gt_sizeof_adam_seg() == C.sizeof(AdamSeg), "AdamSeg ABI mismatch"
+        _TYPED[id(L)] = True
+    return L
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError("HIP kernel launch {} failed with code {}".format(what, rc))
+
+
+def ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)

@@ -1,0 +1,348 @@
+"""Numerics of every Genetic-CNN HIP kernel against a plain PyTorch fp32
+reference of the same op (inputs rounded to bf16 first, so only the
+kernel's accumulation/rounding differs)."""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0) if torch.cuda.is_available() else None
+
+
+def K():
+    from gentun_amd.ops import cnn_kernels
+    cnn_kernels.lib()
+    return cnn_kernels
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def nhwc_pad(x_nchw, cp):
+    n, c, h, w = x_nchw.shape
+    out = torch.zeros((n, h, w, cp), dtype=x_nchw.dtype, device=x_nchw.device)
+    out[..., :c] = x_nchw.permute(0, 2, 3, 1)
+    return out
+
+
+def conv_ref(xs_nchw, w_oihw, bias, relu):
+    x = sum(xs_nchw)
+    y = F.conv2d(x, w_oihw, bias, padding=(w_oihw.shape[2] // 2, w_oihw.shape[3] // 2))
+    return F.relu(y) if relu else y
+
+
+def pack_w(w_oihw, coutp, cinp):
+    co, ci, kh, kw = w_oihw.shape
+    out = torch.zeros((coutp, kh, kw, cinp), dtype=w_oihw.dtype, device=w_oihw.device)
+    out[:co, :, :, :ci] = w_oihw.permute(0, 2, 3, 1)
+    return out
+
+
+@pytest.mark.parametrize("H,W,cin,cout,k,nin", [(32, 32, 3, 20, 5, 1), (32, 32, 20, 20, 3, 3), (16, 16, 20, 50, 5, 1),
+                                               (16, 16, 50, 50, 3, 2), (8, 8, 64, 128, 3, 1), (7, 7, 50, 50, 3, 4),
+                                               (28, 28, 1, 20, 5, 1)])
+def test_conv_fwd(H, W, cin, cout, k, nin):
+    Km = K()
+    torch.manual_seed(0)
+    G, B = 2, 3
+    cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
+    xs = [bf(torch.randn(G, B, cin, H, W, device=DEV)).float() for _ in range(nin)]
+    w = bf(torch.randn(G, cout, cin, k, k, device=DEV) * 0.2).float()
+    b = torch.randn(G, cout, device=DEV) * 0.1
+    x_in = [torch.stack([nhwc_pad(x[g], cinp) for g in range(G)]).to(torch.bfloat16).contiguous() for x in xs]
+    wp = torch.stack([pack_w(w[g], coutp, cinp) for g in range(G)]).to(torch.bfloat16).contiguous()
+    bp = torch.zeros(G, coutp, device=DEV)
+    bp[:, :cout] = b
+    out = torch.zeros(G, B, H, W, coutp, dtype=torch.bfloat16, device=DEV)
+    a = Km.ConvArgs()
+    for i, t in enumerate(x_in):
+        a.inp[i] = t.data_ptr()
+    a.out[0] = out.data_ptr()
+    a.n_in, a.n_out, a.acc_flags, a.relu = nin, 1, 0, 1
+    a.w, a.bias = wp.data_ptr(), bp.data_ptr()
+    a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
+    a.TH = max(1, min(H, 64 // W))
+    Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv")
+    torch.cuda.synchronize()
+    for g in range(G):
+        # the fused Add is rounded to bf16 before the MFMA: mirror that
+        xsum = bf(sum(x[g] for x in xs)).float()
+        ref = conv_ref([xsum], w[g], b[g], True)
+        got = out[g, ..., :cout].float().permute(0, 3, 1, 2)
+        tol = 2e-2 * ref.abs().max().item() + 1e-2
+        assert (got - ref).abs().max().item() < tol
+        if coutp > cout:
+            assert out[g, ..., cout:].abs().max().item() == 0
+
+
+def test_conv_dgrad_mask_and_accumulate():
+    """dgrad = conv of (dy * (y>0)) with flipped/transposed weights, fanned out
+    into two outputs, one accumulating."""
+    Km = K()
+    torch.manual_seed(1)
+    G, B, H, W, cin, cout, k = 2, 2, 16, 16, 20, 50, 3
+    cinp, coutp = 24, 56
+    x = bf(torch.randn(G, B, cin, H, W, device=DEV)).float()
+    w = bf(torch.randn(G, cout, cin, k, k, device=DEV) * 0.2).float()
+    y = torch.stack([F.relu(F.conv2d(x[g], w[g], padding=1)) for g in range(G)])
+    dy = bf(torch.randn_like(y)).float()
+    y = bf(y).float()
+    ref = torch.stack([torch.nn.grad.conv2d_input(x[g].shape, w[g], dy[g] * (y[g] > 0), padding=1) for g in range(G)])
+    wp = torch.stack([pack_w(w[g], coutp, cinp) for g in range(G)]).float()
+    wT = wp.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous().to(torch.bfloat16)
+    dy_p = torch.stack([nhwc_pad(dy[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
+    y_p = torch.stack([nhwc_pad(y[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
+    out0 = torch.zeros(G, B, H, W, cinp, dtype=torch.bfloat16, device=DEV)
+    prev = bf(torch.randn(G, B, H, W, cinp, device=DEV))
+    prev[..., cin:] = 0
+    out1 = prev.clone()
+    a = Km.ConvArgs()
+    a.inp[0] = dy_p.data_ptr()
+    a.mask = y_p.data_ptr()
+    a.out[0], a.out[1] = out0.data_ptr(), out1.data_ptr()
+    a.n_in, a.n_out, a.acc_flags, a.relu = 1, 2, 2, 0
+    a.w, a.bias = wT.data_ptr(), 0
+    a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.TH = G, B, H, W, coutp, cinp, k, k, 4
+    Km.check(Km.lib().gt_conv_fwd(a, stream()), "dgrad")
+    torch.cuda.synchronize()
+    got0 = out0[..., :cin].float().permute(0, 1, 4, 2, 3)
+    tol = 2e-2 * ref.abs().max().item()
+    assert (got0 - ref).abs().max().item() < tol
+    got1 = out1[..., :cin].float().permute(0, 1, 4, 2, 3)
+    ref1 = ref + prev[..., :cin].float().permute(0, 1, 4, 2, 3)
+    assert (got1 - ref1).abs().max().item() < tol + 2e-2 * ref1.abs().max().item()
+
+
+@pytest.mark.parametrize("H,W,cin,cout,k,nin,first", [(32, 32, 3, 20, 5, 1, True), (16, 16, 50, 50, 3, 2, False),
+                                                      (32, 32, 20, 20, 3, 1, False), (8, 8, 64, 128, 3, 1, False)])
+def test_conv_wgrad(H, W, cin, cout, k, nin, first):
+    Km = K()
+    torch.manual_seed(2)
+    G, B = 2, 4
+    cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
+    xs = [bf(torch.randn(G, B, cin, H, W, device=DEV)).float() for _ in range(nin)]
+    y = bf(torch.randn(G, B, cout, H, W, device=DEV)).float()
+    dy = bf(torch.randn(G, B, cout, H, W, device=DEV)).float()
+    xsum = bf(sum(xs)).float()
+    dz = dy * (y > 0)
+    ref = torch.stack([torch.nn.grad.conv2d_weight(xsum[g], (cout, cin, k, k), dz[g], padding=k // 2)
+                       for g in range(G)])
+    refb = dz.sum((1, 3, 4))
+    x_in = [torch.stack([nhwc_pad(x[g], cinp) for g in range(G)]).to(torch.bfloat16).contiguous() for x in xs]
+    gather = None
+    if first:
+        # dataset of 3*G*B images, gathered through a [1][G][B] table
+        data = torch.zeros(3 * G * B, H, W, cinp, dtype=torch.bfloat16, device=DEV)
+        perm = torch.randperm(3 * G * B, device=DEV)[:G * B]
+        data[perm] = x_in[0].view(G * B, H, W, cinp)
+        gather = perm.view(1, G, B).to(torch.int64).contiguous()
+        x_in = [data]
+    dy_p = torch.stack([nhwc_pad(dy[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
+    y_p = torch.stack([nhwc_pad(y[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
+    Kdim = k * k * cinp
+    npix = B * H * W
+    pps = max(32, ((npix // 4) + 31) // 32 * 32)
+    S = -(-npix // pps)
+    pw = torch.zeros(S, G, coutp, Kdim, device=DEV)
+    pb = torch.zeros(S, G, coutp, device=DEV)
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    a = Km.WgradArgs()
+    for i, t in enumerate(x_in):
+        a.inp[i] = t.data_ptr()
+    a.n_in = len(x_in)
+    a.gather = gather.data_ptr() if gather is not None else 0
+    a.st = st.data_ptr()
+    a.dy, a.ymask, a.part_w, a.part_b = dy_p.data_ptr(), y_p.data_ptr(), pw.data_ptr(), pb.data_ptr()
+    a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.S, a.pps = G, B, H, W, cinp, coutp, k, k, S, pps
+    Km.check(Km.lib().gt_conv_wgrad(a, stream()), "wgrad")
+    torch.cuda.synchronize()
+    got = pw.sum(0).view(G, coutp, k, k, cinp)[:, :cout, :, :, :cin].permute(0, 1, 4, 2, 3)
+    tol = 1e-2 * ref.abs().max().item() + 1e-3
+    assert (got - ref).abs().max().item() < tol
+    gotb = pb.sum(0)[:, :cout]
+    assert (gotb - refb).abs().max().item() < 1e-2 * refb.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("H,W", [(32, 32), (7, 7), (14, 14)])
+def test_pool_fwd_bwd(H, W):
+    Km = K()
+    torch.manual_seed(3)
+    N, C, cp = 6, 20, 24
+    x = bf(torch.randn(N, C, H, W, device=DEV)).float()
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 2, 2)
+    dy = bf(torch.randn_like(y)).float()
+    y.backward(dy)
+    xp = nhwc_pad(x, cp).to(torch.bfloat16).contiguous()
+    yp = torch.zeros(N, H // 2, W // 2, cp, dtype=torch.bfloat16, device=DEV)
+    Km.check(Km.lib().gt_pool_fwd(xp.data_ptr(), yp.data_ptr(), N, H, W, cp, stream()), "pool")
+    dyp = nhwc_pad(dy, cp).to(torch.bfloat16).contiguous()
+    dxp = torch.full((N, H, W, cp), 7.0, dtype=torch.bfloat16, device=DEV)
+    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), dyp.data_ptr(), dxp.data_ptr(), N, H, W, cp, stream()), "poolb")
+    torch.cuda.synchronize()
+    assert torch.equal(yp[..., :C].float().permute(0, 3, 1, 2), y.detach())
+    assert torch.allclose(dxp[..., :C].float().permute(0, 3, 1, 2), xr.grad, atol=1e-6)
+
+
+def test_dense_fwd_dgrad():
+    Km = K()
+    torch.manual_seed(4)
+    G, B, Fp, Up = 3, 32, 3584, 512
+    x = bf(torch.randn(G, B, Fp, device=DEV)).float()
+    w1 = (torch.randn(G, Fp, Up, device=DEV) * 0.02)
+    b1 = torch.randn(G, Up, device=DEV) * 0.1
+    w1b = bf(w1).float()
+    ref = F.relu(torch.baddbmm(b1[:, None], x, w1b))
+    wt = w1b.transpose(1, 2).contiguous().to(torch.bfloat16)
+    xb = x.to(torch.bfloat16).contiguous()
+    out = torch.zeros(G, B, Up, dtype=torch.bfloat16, device=DEV)
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    a = Km.DenseFwdArgs()
+    a.x, a.wt, a.bias, a.out, a.st, a.fold_ids = xb.data_ptr(), wt.data_ptr(), b1.data_ptr(), out.data_ptr(), \
+        st.data_ptr(), 0
+    a.G, a.B, a.Fp, a.Up, a.drop_p, a.train, a.seed = G, B, Fp, Up, 0.5, 0, 1
+    Km.check(Km.lib().gt_dense_fwd(a, stream()), "dense")
+    # dropout statistics in train mode
+    out2 = torch.zeros_like(out)
+    a.out, a.train = out2.data_ptr(), 1
+    Km.check(Km.lib().gt_dense_fwd(a, stream()), "dense-train")
+    dH = torch.randn(G, B, Up, device=DEV)
+    dx = torch.zeros(G, B, Fp, dtype=torch.bfloat16, device=DEV)
+    d = Km.DenseDgradArgs()
+    d.dH, d.w1, d.dx, d.G, d.B, d.Fp, d.Up = dH.data_ptr(), w1.data_ptr(), dx.data_ptr(), G, B, Fp, Up
+    Km.check(Km.lib().gt_dense_dgrad(d, stream()), "dgrad")
+    torch.cuda.synchronize()
+    assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
+    kept = (out2.float() != 0)
+    pos = (ref > 0)
+    frac = (kept & pos).sum().item() / max(1, pos.sum().item())
+    assert 0.4 < frac < 0.6
+    both = kept & pos
+    assert torch.allclose(out2.float()[both], 2 * out.float()[both], rtol=2e-2, atol=1e-2)
+    refdx = torch.bmm(bf(dH).float(), bf(w1).float().transpose(1, 2))
+    assert (dx.float() - refdx).abs().max().item() < 2e-2 * refdx.abs().max().item()
+
+
+def _adam_ref(p, m, v, g, lr, t):
+    m = 0.9 * m + 0.1 * g
+    v = 0.999 * v + 0.001 * g * g
+    lr_t = lr * math.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+    return p - lr_t * m / (v.sqrt() + 1e-7), m, v
+
+
+def test_dense_wgrad_adam_and_step_begin():
+    Km = K()
+    torch.manual_seed(5)
+    G, B, Fp, Up = 2, 32, 400, 512
+    x = bf(torch.randn(G, B, Fp, device=DEV)).float()
+    dH = torch.randn(G, B, Up, device=DEV)
+    p = torch.randn(G, Fp, Up, device=DEV)
+    m = torch.randn(G, Fp, Up, device=DEV) * 0.01
+    v = torch.rand(G, Fp, Up, device=DEV) * 0.01
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    stf = st.view(torch.float32)
+    stf[2] = 4.0   # t before this step
+    stf[3] = 1e-3
+    Km.check(Km.lib().gt_step_begin(st.data_ptr(), stream()), "step_begin")
+    g = torch.bmm(x.transpose(1, 2), dH)
+    rp, rm, rv = _adam_ref(p.clone(), m.clone(), v.clone(), g, 1e-3, 5)
+    wt = torch.zeros(G, Up, Fp, dtype=torch.bfloat16, device=DEV)
+    a = Km.DenseWgradAdamArgs()
+    xb = x.to(torch.bfloat16).contiguous()
+    a.x, a.dH, a.p, a.m, a.v, a.wt, a.st = xb.data_ptr(), dH.data_ptr(), p.data_ptr(), m.data_ptr(), v.data_ptr(), \
+        wt.data_ptr(), st.data_ptr()
+    a.G, a.B, a.Fp, a.Up = G, B, Fp, Up
+    Km.check(Km.lib().gt_dense_wgrad_adam(a, stream()), "wgrad_adam")
+    torch.cuda.synchronize()
+    assert st[1].item() == 0 and st[0].item() == 1 and abs(stf[2].item() - 5.0) < 1e-6
+    assert torch.allclose(m, rm, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(v, rv, rtol=1e-4, atol=1e-6)
+    assert torch.allclose(p, rp, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(wt.float(), bf(rp).transpose(1, 2).float(), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("loss", ["bce_compat", "ce"])
+def test_head(loss):
+    Km = K()
+    from gentun_amd.models.cnn_engine import loss_and_metrics
+    torch.manual_seed(6)
+    G, B, Up, C, N = 2, 32, 512, 10, 100
+    h = bf(F.relu(torch.randn(G, B, Up, device=DEV))).float()
+    w2 = torch.randn(G, Up, C, device=DEV) * 0.05
+    b2 = torch.randn(G, C, device=DEV) * 0.1
+    labels = torch.randint(0, C, (N,), device=DEV)
+    gather = torch.randint(0, N, (1, G, B), device=DEV)
+    y = F.one_hot(labels[gather[0]], C).float()
+    hr = h.clone().requires_grad_(True)
+    w2r = w2.clone().requires_grad_(True)
+    b2r = b2.clone().requires_grad_(True)
+    logits = torch.baddbmm(b2r[:, None], hr, w2r)
+    per, binc, catc = loss_and_metrics(logits, y, loss)
+    per.mean(-1).sum().backward()
+    dH = torch.zeros(G, B, Up, device=DEV)
+    gw2, gb2, gb1 = torch.zeros_like(w2), torch.zeros_like(b2), torch.zeros(G, Up, device=DEV)
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    hb = h.to(torch.bfloat16).contiguous()
+    a = Km.HeadArgs()
+    a.h, a.w2, a.b2, a.labels, a.gather, a.st = hb.data_ptr(), w2.data_ptr(), b2.data_ptr(), labels.data_ptr(), \
+        gather.data_ptr(), st.data_ptr()
+    a.dH, a.gw2, a.gb2, a.gb1, a.eval_out = dH.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), gb1.data_ptr(), 0
+    a.G, a.B, a.Up, a.C, a.loss_ce, a.drop_scale, a.eval = G, B, Up, C, int(loss == "ce"), 2.0, 0
+    Km.check(Km.lib().gt_head(a, stream()), "head")
+    ev = torch.zeros(G, B, 3, device=DEV)
+    a.eval, a.eval_out = 1, ev.data_ptr()
+    Km.check(Km.lib().gt_head(a, stream()), "head-eval")
+    torch.cuda.synchronize()
+    refdH = hr.grad * 2.0 * (h > 0)
+    assert torch.allclose(dH, refdH, rtol=1e-3, atol=1e-6)
+    assert torch.allclose(gw2, w2r.grad, rtol=1e-3, atol=1e-6)
+    assert torch.allclose(gb2, b2r.grad, rtol=1e-3, atol=1e-6)
+    assert torch.allclose(gb1, refdH.sum(1), rtol=1e-3, atol=1e-5)
+    assert torch.allclose(ev[..., 0], per.detach(), rtol=1e-4, atol=1e-6)
+    assert torch.equal(ev[..., 1], binc)
+    assert torch.equal(ev[..., 2], catc)
+
+
+def test_adam_segments_with_partials_and_transpose():
+    Km = K()
+    import ctypes
+    torch.manual_seed(7)
+    G, co, kh, kw, ci, S = 2, 16, 3, 3, 8, 3
+    n = G * co * kh * kw * ci
+    p = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    parts = torch.randn(S, n, device=DEV)
+    bfc = torch.zeros(n, dtype=torch.bfloat16, device=DEV)
+    bfT = torch.zeros(n, dtype=torch.bfloat16, device=DEV)
+    sg = Km.AdamSeg()
+    sg.p, sg.m, sg.v, sg.g, sg.bf, sg.bfT = p.data_ptr(), m.data_ptr(), v.data_ptr(), parts.data_ptr(), \
+        bfc.data_ptr(), bfT.data_ptr()
+    sg.n, sg.gstride, sg.S = n, n, S
+    sg.tG, sg.tCo, sg.tKH, sg.tKW, sg.tCi = G, co, kh, kw, ci
+    raw = bytes(memoryview((Km.AdamSeg * 1)(sg)).cast("B"))
+    segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(DEV)
+    blocks = torch.tensor([[0, o] for o in range(0, n, 256)], dtype=torch.int32, device=DEV)
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    st.view(torch.float32)[3] = 1e-2
+    Km.check(Km.lib().gt_step_begin(st.data_ptr(), stream()), "sb")
+    a = Km.AdamArgs()
+    a.segs, a.blocks, a.st = segs.data_ptr(), blocks.data_ptr(), st.data_ptr()
+    rp, rm, rv = _adam_ref(p.clone(), m.clone(), v.clone(), parts.sum(0), 1e-2, 1)
+    Km.check(Km.lib().gt_adam_segments(ctypes.byref(a), blocks.shape[0], stream()), "adam")
+    torch.cuda.synchronize()
+    assert torch.allclose(p, rp, rtol=1e-5, atol=1e-6)
+    assert torch.equal(bfc, rp.to(torch.bfloat16))
+    W = rp.view(G, co, kh, kw, ci)
+    WT = W.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous().to(torch.bfloat16).view(-1)
+    assert torch.equal(bfT, WT)
