@@ -178,30 +178,88 @@ struct WgradArgs {
   int G, B, H, W, Cinp, Coutp, KH, KW, S, pps;  // pps = pixels per split (multiple of 32)
 };
 
-#define WG_LD 40   // LDS row stride (elements) of the transposed tiles: 32 pixels + 8 pad
+#define WG_LD 72   // LDS row stride (elements) of the [32 pixel][64] tiles (144 B: 16-B aligned rows)
+#define WG_TILE (32 * WG_LD)
+
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+
+// Two ds_read_b64_tr_b16 give a lane the 8 k-values (pixels 8g..8g+7 of the
+// K-step) of column (col0 + lane&15) of a row-major [pixel][col] LDS tile:
+// exactly the 16x16x32 MFMA operand layout (k = 8*(lane>>4) + j).
+__device__ __forceinline__ uint4 tr_frag(const uint16_t* tile, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  typedef __attribute__((address_space(3))) short4_t lds_s4;
+  const uint16_t* r0 = tile + (8 * g + q) * WG_LD + col0 + 4 * p;
+  const uint16_t* r1 = r0 + 4 * WG_LD;
+  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(r0));
+  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(r1));
+  uint4 v;
+  v.x = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
+  v.y = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
+  v.z = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
+  v.w = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
+  return v;
+}
+
+__device__ __forceinline__ void wgrad_load(const WgradArgs& a, long p, long p_end, int g, int co_st, bool col_ok,
+                                           int c_kh, int c_kw, int c_cb, uint4& dzv, uint4& xsv, float* bsum) {
+  const long HW = (long)a.H * a.W;
+  float dz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float xs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (p < p_end) {
+    const long bimg = p / HW;
+    const int rem = (int)(p % HW);
+    const int hh = rem / a.W, ww = rem % a.W;
+    if (co_st < a.Coutp) {
+      const long off = (((long)g * a.B + bimg) * HW + rem) * a.Coutp + co_st;
+      float m[8];
+      unpack8(*reinterpret_cast<const uint4*>(a.dy + off), dz);
+      unpack8(*reinterpret_cast<const uint4*>(a.ymask + off), m);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { dz[j] = m[j] > 0.f ? dz[j] : 0.f; bsum[j] += dz[j]; }
+    }
+    const int ih = hh + c_kh - (a.KH >> 1), iw = ww + c_kw - (a.KW >> 1);
+    if (col_ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
+      const long pix_off = ((long)ih * a.W + iw) * a.Cinp + c_cb * 8;
+      if (a.n_in == 1) {
+        const uint16_t* base = a.gather
+            ? a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + bimg] * HW * a.Cinp
+            : a.in[0] + ((long)g * a.B + bimg) * HW * a.Cinp;
+        xsv = *reinterpret_cast<const uint4*>(base + pix_off);
+        dzv = pack8(dz);
+        return;
+      }
+      float t[8];
+      for (int k = 0; k < a.n_in; ++k) {
+        const uint16_t* base = a.in[k] + ((long)g * a.B + bimg) * HW * a.Cinp;
+        unpack8(*reinterpret_cast<const uint4*>(base + pix_off), t);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xs[j] += t[j];
+      }
+    }
+  }
+  dzv = pack8(dz);
+  xsv = pack8(xs);
+}
 
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 64 * WG_LD];
-  uint16_t* dzT = lds;                 // [64 co][WG_LD]
-  uint16_t* colT = lds + 64 * WG_LD;   // [64 col][WG_LD]
+  __shared__ __attribute__((aligned(16))) uint16_t lds[4 * WG_TILE];   // 2 buffers x (dz, im2col)
+  __shared__ float bred[32][65];
   const int tid = threadIdx.x;
-  const int nb = blockIdx.x;           // column block (64 cols of kh,kw,ci)
-  const int s = blockIdx.y;            // split
+  const int nb = blockIdx.x;
+  const int s = blockIdx.y;
   const int mblocks = (a.Coutp + 63) / 64;
   const int g = blockIdx.z / mblocks;
   const int co_blk = (blockIdx.z % mblocks) * 64;
   const int Kdim = a.KH * a.KW * a.Cinp;
   const int ncb = a.Cinp >> 3;
-  const int ph = a.KH >> 1, pw = a.KW >> 1;
-  const long HW = (long)a.H * a.W;
-  const long npix = (long)a.B * HW;
+  const long npix = (long)a.B * a.H * a.W;
   const long p_begin = (long)s * a.pps;
   const long p_end = (p_begin + a.pps < npix) ? p_begin + a.pps : npix;
 
-  // staging roles: pixel = tid >> 3 (0..31), chunk = tid & 7
   const int sp = tid >> 3, sj = tid & 7;
-  const int co_st = co_blk + sj * 8;                    // dz chunk channels
-  const int col_st = nb * 64 + sj * 8;                  // im2col chunk column
+  const int co_st = co_blk + sj * 8;
+  const int col_st = nb * 64 + sj * 8;
   int c_kh = 0, c_kw = 0, c_cb = 0;
   const bool col_ok = col_st < Kdim;
   if (col_ok) {
@@ -211,71 +269,49 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
     c_kw = kk % a.KW; c_kh = kk / a.KW;
   }
   const int wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  const int MT = (min(64, a.Coutp - co_blk) + 15) >> 4;
+  const bool wave_live = nb * 64 + wave * 16 < Kdim;
   f32x4_t acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float bsum = 0.f;
+  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const bool do_bias = (nb == 0) && (a.part_b != nullptr);
 
+  uint4 dzv, xsv;
+  wgrad_load(a, p_begin + sp, p_end, g, co_st, col_ok, c_kh, c_kw, c_cb, dzv, xsv, bsum);
+  *reinterpret_cast<uint4*>(&lds[sp * WG_LD + sj * 8]) = dzv;
+  *reinterpret_cast<uint4*>(&lds[WG_TILE + sp * WG_LD + sj * 8]) = xsv;
+  __syncthreads();
+  int buf = 0;
   for (long p0 = p_begin; p0 < p_end; p0 += 32) {
-    const long p = p0 + sp;
-    float dz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float xs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (p < p_end) {
-      const long bimg = p / HW;
-      const int rem = (int)(p % HW);
-      const int hh = rem / a.W, ww = rem % a.W;
-      if (co_st < a.Coutp) {
-        const long off = (((long)g * a.B + bimg) * HW + rem) * a.Coutp + co_st;
-        float m[8];
-        unpack8(*reinterpret_cast<const uint4*>(a.dy + off), dz);
-        unpack8(*reinterpret_cast<const uint4*>(a.ymask + off), m);
+    const bool more = p0 + 32 < p_end;
+    if (more) wgrad_load(a, p0 + 32 + sp, p_end, g, co_st, col_ok, c_kh, c_kw, c_cb, dzv, xsv, bsum);
+    const uint16_t* dzT = lds + buf * 2 * WG_TILE;
+    const uint16_t* colT = dzT + WG_TILE;
+    if (wave_live) {
+      const uint4 bfrag = tr_frag(colT, wave * 16, lane);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dz[j] = m[j] > 0.f ? dz[j] : 0.f;
-      }
-      const int ih = hh + c_kh - ph, iw = ww + c_kw - pw;
-      if (col_ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
-        const long pix_off = ((long)ih * a.W + iw) * a.Cinp + c_cb * 8;
-        float t[8];
-        for (int k = 0; k < a.n_in; ++k) {
-          const uint16_t* base;
-          if (k == 0 && a.gather) {
-            const long id = a.gather[((long)a.st->cur_step * a.G + g) * a.B + bimg];
-            base = a.in[0] + id * HW * a.Cinp;
-          } else {
-            base = a.in[k] + ((long)g * a.B + bimg) * HW * a.Cinp;
-          }
-          unpack8(*reinterpret_cast<const uint4*>(base + pix_off), t);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) xs[j] += t[j];
+      for (int t = 0; t < 4; ++t) {
+        if (t < MT) {
+          const uint4 afrag = tr_frag(dzT, t * 16, lane);
+          acc[t] = mfma16(afrag, bfrag, acc[t]);
         }
       }
     }
-    __syncthreads();   // previous K-step's reads are done
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      dzT[(sj * 8 + j) * WG_LD + sp] = f2bf(dz[j]);
-      colT[(sj * 8 + j) * WG_LD + sp] = f2bf(xs[j]);
+    if (more) {
+      uint16_t* nd = lds + (buf ^ 1) * 2 * WG_TILE;
+      *reinterpret_cast<uint4*>(&nd[sp * WG_LD + sj * 8]) = dzv;
+      *reinterpret_cast<uint4*>(&nd[WG_TILE + sp * WG_LD + sj * 8]) = xsv;
     }
     __syncthreads();
-    if (do_bias && tid < 64) {
-      float t = 0.f;
-      for (int q = 0; q < 32; ++q) t += bf2f(dzT[tid * WG_LD + q]);
-      bsum += t;
-    }
-    const uint4 bfrag = *reinterpret_cast<const uint4*>(&colT[(wave * 16 + l16) * WG_LD + kq * 8]);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint4 afrag = *reinterpret_cast<const uint4*>(&dzT[(t * 16 + l16) * WG_LD + kq * 8]);
-      acc[t] = mfma16(afrag, bfrag, acc[t]);
-    }
+    buf ^= 1;
   }
 
-  // D[row = co][col]: lane holds rows kq*4+i of tile t, column l16 of wave's 16 columns
   const int col = nb * 64 + wave * 16 + l16;
   if (col < Kdim) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
+      if (t >= MT) continue;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int co = co_blk + t * 16 + kq * 4 + i;
@@ -283,8 +319,16 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
       }
     }
   }
-  if (do_bias && tid < 64 && co_blk + tid < a.Coutp)
-    a.part_b[((long)s * a.G + g) * a.Coutp + co_blk + tid] = bsum;
+  if (do_bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bred[sp][sj * 8 + j] = bsum[j];
+    __syncthreads();
+    if (tid < 64 && co_blk + tid < a.Coutp) {
+      float t = 0.f;
+      for (int q = 0; q < 32; ++q) t += bred[q][tid];
+      a.part_b[((long)s * a.G + g) * a.Coutp + co_blk + tid] = t;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------

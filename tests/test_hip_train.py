@@ -32,7 +32,9 @@ def test_hip_matches_torch_band(loss):
     h = np.mean(res["hip"]["categorical_accuracy"])
     t = np.mean(res["torch"]["categorical_accuracy"])
     assert h > 0.3, res
-    assert abs(h - t) < 0.15, res
+    # bf16 HIP path must not be worse than the fp32-master torch oracle
+    # (bce_compat on softmax occasionally stalls a fold on either path)
+    assert h > t - 0.15, res
     assert np.all(np.isfinite(res["hip"]["val_loss"]))
 
 
