@@ -42,9 +42,11 @@ struct ConvArgs {
   int G, B, H, W, Cinp, Coutp, KH, KW, TH;
 };
 
+#define CF_KB 16                 // weight K-block: 16 chunks of 8 = 128 k
+#define CF_WLD (CF_KB * 8 + 8)    // LDS row stride of a weight block (272 B: conflict-free b128 reads)
+
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint4* patch = reinterpret_cast<uint4*>(smem);
   const int tid = threadIdx.x;
   const int nth = (a.H + a.TH - 1) / a.TH;
   const int b = blockIdx.x / nth;
@@ -55,6 +57,33 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
   const int PH = a.TH + a.KH - 1, PW = a.W + a.KW - 1;
   const int ncb = a.Cinp >> 3;
   const long img = (long)a.H * a.W * a.Cinp;
+  const int total = PH * PW * ncb;
+  const int nchunks = a.KH * a.KW * ncb;
+  const int Kdim = a.KH * a.KW * a.Cinp;
+  // LDS carve: [weight block x2][patch][chunk offset table]
+  uint16_t* wbuf = reinterpret_cast<uint16_t*>(smem);                       // 2 x 64 x CF_WLD
+  uint4* patch = reinterpret_cast<uint4*>(smem + 2 * 64 * CF_WLD * 2);
+  int* coff = reinterpret_cast<int*>(smem + 2 * 64 * CF_WLD * 2 + (size_t)total * 16);
+  const uint16_t* wg = a.w + (long)g * a.Coutp * Kdim;
+
+  // weight-block staging role: row = tid >> 2 (64 rows), 4 chunks per thread
+  const int wr = tid >> 2, wq = (tid & 3) * 4;
+  const bool wrow_ok = co_blk + wr < a.Coutp;
+  const uint16_t* wsrc = wg + (long)(co_blk + wr) * Kdim;
+  uint4 wreg[4];
+  auto load_wblock = [&](int kb) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = kb * CF_KB + wq + j;
+      wreg[j] = (wrow_ok && c < nchunks) ? *reinterpret_cast<const uint4*>(wsrc + c * 8) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_wblock = [&](int buf) {
+    uint16_t* dst = wbuf + buf * 64 * CF_WLD + wr * CF_WLD + wq * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<uint4*>(dst + j * 8) = wreg[j];
+  };
+  load_wblock(0);
 
   // ---- stage the summed / masked input patch -------------------------------
   const uint16_t* src[4];
@@ -64,12 +93,13 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
     src[0] = a.in[0] + id * img;
   }
   const uint16_t* msrc = a.mask ? a.mask + ((long)g * a.B + b) * img : nullptr;
-  const int total = PH * PW * ncb;
+  const FastDiv div_ncb(ncb), div_pw(PW);
   for (int i = tid; i < total; i += 256) {
-    const int cb = i % ncb;
-    const int pix = i / ncb;
-    const int pc = pix % PW, pr = pix / PW;
-    const int hh = h0 - ph + pr, ww = pc - pw;
+    uint32_t pix, cbu, pr, pc;
+    div_ncb.divmod((uint32_t)i, pix, cbu);
+    div_pw.divmod(pix, pr, pc);
+    const int cb = (int)cbu;
+    const int hh = h0 - ph + (int)pr, ww = (int)pc - pw;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) {
       const long off = ((long)hh * a.W + ww) * a.Cinp + cb * 8;
@@ -93,70 +123,101 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
     }
     patch[i] = v;
   }
-  __syncthreads();
-
-  // ---- MFMA main loop -------------------------------------------------------
-  const int wave = tid >> 6, lane = tid & 63;
-  const int kq = lane >> 4, l16 = lane & 15;
-  const int pl = wave * 16 + l16;                 // pixel within the tile
-  const int npx = a.TH * a.W;
-  const int py = pl / a.W, px = pl % a.W;
-  const bool pvalid = (pl < npx) && (h0 + py < a.H);
-  const int nchunks = a.KH * a.KW * ncb;
-  const int Kdim = a.KH * a.KW * a.Cinp;
-  const uint16_t* wg = a.w + (long)g * a.Coutp * Kdim;
-  const int nco = min(64, a.Coutp - co_blk);
-  const int NT = (nco + 15) >> 4;
-  f32x4_t acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  for (int ks = 0; ks < nchunks; ks += 4) {
-    const int c = ks + kq;
-    uint4 bf = make_uint4(0, 0, 0, 0);
-    const bool cval = c < nchunks;
-    if (cval && pvalid) {
-      const int cb = c % ncb, kk = c / ncb;
-      const int kw = kk % a.KW, kh = kk / a.KW;
-      bf = patch[((py + kh) * PW + (px + kw)) * ncb + cb];
-    }
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t < NT) {
-        const int co = co_blk + t * 16 + l16;
-        uint4 af = make_uint4(0, 0, 0, 0);
-        if (cval && co < a.Coutp) af = *reinterpret_cast<const uint4*>(wg + (long)co * Kdim + c * 8);
-        acc[t] = mfma16(af, bf, acc[t]);
+  {
+    const FastDiv div_kw(a.KW);
+    for (int c = tid; c < nchunks + 4; c += 256) {
+      if (c < nchunks) {
+        uint32_t kk, cb, kh, kw;
+        div_ncb.divmod((uint32_t)c, kk, cb);
+        div_kw.divmod(kk, kh, kw);
+        coff[c] = ((int)kh * PW + (int)kw) * ncb + (int)cb;
+      } else {
+        coff[c] = -1;
       }
     }
   }
+  store_wblock(0);
+  __syncthreads();
+
+  // ---- MFMA main loop: each wave = 32 pixels (2 B fragments) x all co tiles --
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int npx = a.TH * a.W;
+  int pbase[2];
+  bool pvalid[2];
+  int pyy[2], pxx[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int pl = wave * 32 + h * 16 + l16;
+    pyy[h] = pl / a.W; pxx[h] = pl % a.W;
+    pvalid[h] = (pl < npx) && (h0 + pyy[h] < a.H);
+    pbase[h] = (pyy[h] * PW + pxx[h]) * ncb;
+  }
+  const int nco = min(64, a.Coutp - co_blk);
+  const int NT = (nco + 15) >> 4;
+  f32x4_t acc[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[h][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bool more = kb + 1 < nkb;
+    if (more) load_wblock(kb + 1);
+    const uint16_t* wcur = wbuf + (kb & 1) * 64 * CF_WLD;
+#pragma unroll
+    for (int kk = 0; kk < CF_KB / 4; ++kk) {
+      const int c = kb * CF_KB + kk * 4 + kq;
+      if (kb * CF_KB + kk * 4 >= nchunks) break;
+      const int co_off = coff[c];
+      uint4 bf0 = make_uint4(0, 0, 0, 0), bf1 = make_uint4(0, 0, 0, 0);
+      if (co_off >= 0) {
+        if (pvalid[0]) bf0 = patch[pbase[0] + co_off];
+        if (pvalid[1]) bf1 = patch[pbase[1] + co_off];
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < NT) {
+          const uint4 af = *reinterpret_cast<const uint4*>(wcur + (t * 16 + l16) * CF_WLD + (kk * 4 + kq) * 8);
+          acc[0][t] = mfma16(af, bf0, acc[0][t]);
+          acc[1][t] = mfma16(af, bf1, acc[1][t]);
+        }
+      }
+    }
+    if (more) store_wblock((kb + 1) & 1);
+    __syncthreads();
+  }
 
   // ---- epilogue: bias + relu, 4 channels per lane ---------------------------
-  if (!pvalid) return;
-  const long obase = ((((long)g * a.B + b) * a.H + (h0 + py)) * a.W + px) * a.Coutp;
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    if (t >= NT) continue;
-    const int co0 = co_blk + t * 16 + kq * 4;
-    if (co0 >= a.Coutp) continue;
-    float v[4];
+  for (int h = 0; h < 2; ++h) {
+    if (!pvalid[h]) continue;
+    const long obase = ((((long)g * a.B + b) * a.H + (h0 + pyy[h])) * a.W + pxx[h]) * a.Coutp;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float x = acc[t][i];
-      if (a.bias) x += a.bias[(long)g * a.Coutp + co0 + i];
-      if (a.relu) x = fmaxf(x, 0.f);
-      v[i] = x;
-    }
-    for (int k = 0; k < a.n_out; ++k) {
-      uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
-      if ((a.acc_flags >> k) & 1) {
-        const uint2 old = *dst;
-        float o[4] = {__uint_as_float(old.x << 16), __uint_as_float(old.x & 0xffff0000u),
-                      __uint_as_float(old.y << 16), __uint_as_float(old.y & 0xffff0000u)};
-        float s[4] = {v[0] + o[0], v[1] + o[1], v[2] + o[2], v[3] + o[3]};
-        *dst = pack4(s);
-      } else {
-        *dst = pack4(v);
+    for (int t = 0; t < 4; ++t) {
+      if (t >= NT) continue;
+      const int co0 = co_blk + t * 16 + kq * 4;
+      if (co0 >= a.Coutp) continue;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float x = acc[h][t][i];
+        if (a.bias) x += a.bias[(long)g * a.Coutp + co0 + i];
+        if (a.relu) x = fmaxf(x, 0.f);
+        v[i] = x;
+      }
+      for (int k = 0; k < a.n_out; ++k) {
+        uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
+        if ((a.acc_flags >> k) & 1) {
+          const uint2 old = *dst;
+          float o[4] = {__uint_as_float(old.x << 16), __uint_as_float(old.x & 0xffff0000u),
+                        __uint_as_float(old.y << 16), __uint_as_float(old.y & 0xffff0000u)};
+          float sum[4] = {v[0] + o[0], v[1] + o[1], v[2] + o[2], v[3] + o[3]};
+          *dst = pack4(sum);
+        } else {
+          *dst = pack4(v);
+        }
       }
     }
   }
@@ -175,11 +236,11 @@ struct WgradArgs {
   float* part_w;             // [S][G][Coutp][Kdim]
   float* part_b;             // [S][G][Coutp]
   int n_in;
-  int G, B, H, W, Cinp, Coutp, KH, KW, S, pps;  // pps = pixels per split (multiple of 32)
+  int G, B, H, W, Cinp, Coutp, KH, KW, S, pps;  // pps = pixels per split (multiple of 64)
 };
 
 #define WG_LD 72   // LDS row stride (elements) of the [32 pixel][64] tiles (144 B: 16-B aligned rows)
-#define WG_TILE (32 * WG_LD)
+#define WG_TILE (64 * WG_LD)   // 64 pixels per K-step
 
 typedef __attribute__((ext_vector_type(4))) short short4_t;
 
@@ -207,9 +268,12 @@ __device__ __forceinline__ void wgrad_load(const WgradArgs& a, long p, long p_en
   float dz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float xs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (p < p_end) {
-    const long bimg = p / HW;
-    const int rem = (int)(p % HW);
-    const int hh = rem / a.W, ww = rem % a.W;
+    uint32_t bq, remu, hq, wq;
+    FastDiv((uint32_t)HW).divmod((uint32_t)p, bq, remu);
+    FastDiv((uint32_t)a.W).divmod(remu, hq, wq);
+    const long bimg = bq;
+    const int rem = (int)remu;
+    const int hh = (int)hq, ww = (int)wq;
     if (co_st < a.Coutp) {
       const long off = (((long)g * a.B + bimg) * HW + rem) * a.Coutp + co_st;
       float m[8];
@@ -277,32 +341,43 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const bool do_bias = (nb == 0) && (a.part_b != nullptr);
 
-  uint4 dzv, xsv;
-  wgrad_load(a, p_begin + sp, p_end, g, co_st, col_ok, c_kh, c_kw, c_cb, dzv, xsv, bsum);
-  *reinterpret_cast<uint4*>(&lds[sp * WG_LD + sj * 8]) = dzv;
-  *reinterpret_cast<uint4*>(&lds[WG_TILE + sp * WG_LD + sj * 8]) = xsv;
+  uint4 dzv[2], xsv[2];
+  auto load_step = [&](long p0) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      wgrad_load(a, p0 + h * 32 + sp, p_end, g, co_st, col_ok, c_kh, c_kw, c_cb, dzv[h], xsv[h], bsum);
+  };
+  auto store_step = [&](int bf) {
+    uint16_t* nd = lds + bf * 2 * WG_TILE;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<uint4*>(&nd[(h * 32 + sp) * WG_LD + sj * 8]) = dzv[h];
+      *reinterpret_cast<uint4*>(&nd[WG_TILE + (h * 32 + sp) * WG_LD + sj * 8]) = xsv[h];
+    }
+  };
+  load_step(p_begin);
+  store_step(0);
   __syncthreads();
   int buf = 0;
-  for (long p0 = p_begin; p0 < p_end; p0 += 32) {
-    const bool more = p0 + 32 < p_end;
-    if (more) wgrad_load(a, p0 + 32 + sp, p_end, g, co_st, col_ok, c_kh, c_kw, c_cb, dzv, xsv, bsum);
+  for (long p0 = p_begin; p0 < p_end; p0 += 64) {
+    const bool more = p0 + 64 < p_end;
+    if (more) load_step(p0 + 64);
     const uint16_t* dzT = lds + buf * 2 * WG_TILE;
     const uint16_t* colT = dzT + WG_TILE;
     if (wave_live) {
-      const uint4 bfrag = tr_frag(colT, wave * 16, lane);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (t < MT) {
-          const uint4 afrag = tr_frag(dzT, t * 16, lane);
-          acc[t] = mfma16(afrag, bfrag, acc[t]);
+      for (int h = 0; h < 2; ++h) {
+        const uint4 bfrag = tr_frag(colT + h * 32 * WG_LD, wave * 16, lane);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (t < MT) {
+            const uint4 afrag = tr_frag(dzT + h * 32 * WG_LD, t * 16, lane);
+            acc[t] = mfma16(afrag, bfrag, acc[t]);
+          }
         }
       }
     }
-    if (more) {
-      uint16_t* nd = lds + (buf ^ 1) * 2 * WG_TILE;
-      *reinterpret_cast<uint4*>(&nd[sp * WG_LD + sj * 8]) = dzv;
-      *reinterpret_cast<uint4*>(&nd[WG_TILE + sp * WG_LD + sj * 8]) = xsv;
-    }
+    if (more) store_step(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
@@ -401,9 +476,10 @@ extern "C" {
 
 int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   if (a->Cinp % 8 || a->Coutp % 8 || a->n_in < 1 || a->n_in > 4 || a->n_out < 1 || a->n_out > 4) return -1;
-  if (a->TH * a->W > 64 || a->TH < 1) return -2;
+  if (a->TH * a->W > 128 || a->TH < 1) return -2;
   const int nth = (a->H + a->TH - 1) / a->TH;
-  const size_t lds = (size_t)(a->TH + a->KH - 1) * (a->W + a->KW - 1) * a->Cinp * 2;
+  const size_t total = (size_t)(a->TH + a->KH - 1) * (a->W + a->KW - 1) * (a->Cinp / 8);
+  const size_t lds = 2 * 64 * CF_WLD * 2 + total * 16 + 4 * ((size_t)a->KH * a->KW * (a->Cinp / 8) + 4);
   if (lds > 160 * 1024) return -3;
   dim3 grid(a->B * nth, a->G, (a->Coutp + 63) / 64);
   hipLaunchKernelGGL(conv_fwd_kernel, grid, dim3(256), lds, stream, *a);
@@ -411,7 +487,7 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
 }
 
 int gt_conv_wgrad(const WgradArgs* a, hipStream_t stream) {
-  if (a->Cinp % 8 || a->Coutp % 8 || a->pps % 32 || a->n_in < 1 || a->n_in > 4) return -1;
+  if (a->Cinp % 8 || a->Coutp % 8 || a->pps % 64 || a->n_in < 1 || a->n_in > 4) return -1;
   const int Kdim = a->KH * a->KW * a->Cinp;
   dim3 grid((Kdim + 63) / 64, a->S, a->G * ((a->Coutp + 63) / 64));
   hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, stream, *a);

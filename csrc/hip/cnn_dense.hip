@@ -52,11 +52,13 @@ struct DenseFwdArgs {
   unsigned seed;
 };
 
-// grid (Up/64, ceil(B/32), G); wave w: units [64*bx + 16w, +16) x rows [32*by, +32)
+// grid (Up/16, ceil(B/32), G): one 16-unit x 32-row tile per workgroup, the
+// K (feature) loop split over the 4 waves and reduced through LDS.
 __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
+  __shared__ f32x4_t red[3][2][64];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
   const int g = blockIdx.z;
-  const int u_t = blockIdx.x * 64 + wave * 16;
+  const int u_t = blockIdx.x * 16;
   const int b0 = blockIdx.y * 32;
   const int nchunks = a.Fp >> 3;
   const uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
@@ -64,17 +66,29 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
   f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   const int urow = u_t + l16;
   const int br0 = b0 + l16, br1 = b0 + 16 + l16;
-  for (int ks = 0; ks < nchunks; ks += 4) {
+  const uint16_t* pa = wt + (long)urow * a.Fp;
+  const uint16_t* pb0 = x + (long)br0 * a.Fp;
+  const uint16_t* pb1 = x + (long)br1 * a.Fp;
+  const bool ua = urow < a.Up, b0ok = br0 < a.B, b1ok = br1 < a.B;
+  for (int ks = wave * 4; ks < nchunks; ks += 16) {
     const int c = ks + kq;
     uint4 af = make_uint4(0, 0, 0, 0), bf0 = make_uint4(0, 0, 0, 0), bf1 = make_uint4(0, 0, 0, 0);
     if (c < nchunks) {
-      if (urow < a.Up) af = *reinterpret_cast<const uint4*>(wt + (long)urow * a.Fp + c * 8);
-      if (br0 < a.B) bf0 = *reinterpret_cast<const uint4*>(x + (long)br0 * a.Fp + c * 8);
-      if (br1 < a.B) bf1 = *reinterpret_cast<const uint4*>(x + (long)br1 * a.Fp + c * 8);
+      if (ua) af = *reinterpret_cast<const uint4*>(pa + c * 8);
+      if (b0ok) bf0 = *reinterpret_cast<const uint4*>(pb0 + c * 8);
+      if (b1ok) bf1 = *reinterpret_cast<const uint4*>(pb1 + c * 8);
     }
     acc[0] = mfma16(af, bf0, acc[0]);
     acc[1] = mfma16(af, bf1, acc[1]);
   }
+  if (wave > 0) {
+    red[wave - 1][0][lane] = acc[0];
+    red[wave - 1][1][lane] = acc[1];
+  }
+  __syncthreads();
+  if (wave > 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w) { acc[0] += red[w][0][lane]; acc[1] += red[w][1][lane]; }
   // D[row = unit][col = batch row]
   const int u0 = u_t + kq * 4;
   if (u0 >= a.Up) return;
@@ -114,6 +128,7 @@ struct HeadArgs {
   float* gb2;              // [G][C]
   float* gb1;              // [G][Up]
   float* eval_out;         // eval mode: [G][B][3] (loss, binary-correct, categorical-correct)
+  float* dz;               // [G][B][C] logits gradient workspace
   int G, B, Up, C;
   int loss_ce;             // 0 = bce_compat, 1 = ce
   float drop_scale;        // 1/(1-p)
@@ -123,97 +138,129 @@ struct HeadArgs {
 #define HEAD_MAXB 64
 #define HEAD_MAXC 16
 
-__global__ void __launch_bounds__(256) head_kernel(HeadArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int g = blockIdx.x, tid = threadIdx.x;
-  const int B = a.B, Up = a.Up, C = a.C;
-  float* w2s = reinterpret_cast<float*>(smem);              // [Up][C]
-  float* logit = w2s + (long)Up * C;                         // [B][C]
-  float* dz = logit + B * C;                                  // [B][C]
-  uint16_t* hs = reinterpret_cast<uint16_t*>(dz + B * C);     // [B][Up]
+// (1) one 64-thread workgroup per (fold, sample): logits -> softmax -> loss
+//     gradient dz (train) or per-sample loss/accuracies (eval).
+__global__ void __launch_bounds__(64) head_fwd_kernel(HeadArgs a) {
+  __shared__ float part[64][HEAD_MAXC + 1];
+  const int g = blockIdx.y, b = blockIdx.x, lane = threadIdx.x;
+  const int Up = a.Up, C = a.C;
+  const uint16_t* h = a.h + ((long)g * a.B + b) * Up;
   const float* w2 = a.w2 + (long)g * Up * C;
-  for (int i = tid; i < Up * C; i += 256) w2s[i] = w2[i];
-  const uint16_t* hg = a.h + (long)g * B * Up;
-  for (int i = tid; i < (B * Up) / 8; i += 256)
-    reinterpret_cast<uint4*>(hs)[i] = reinterpret_cast<const uint4*>(hg)[i];
+  float acc[HEAD_MAXC];
+#pragma unroll
+  for (int c = 0; c < HEAD_MAXC; ++c) acc[c] = 0.f;
+  for (int u = lane; u < Up; u += 64) {
+    const float hv = bf2f(h[u]);
+    if (hv != 0.f) {
+      const float* wr = w2 + (long)u * C;
+#pragma unroll
+      for (int c = 0; c < HEAD_MAXC; ++c) if (c < C) acc[c] += hv * wr[c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < HEAD_MAXC; ++c) part[lane][c] = acc[c];
   __syncthreads();
-  for (int o = tid; o < B * C; o += 256) {
-    const int b = o / C, c = o % C;
-    float s = a.b2[(long)g * C + c];
-    for (int u = 0; u < Up; ++u) s += bf2f(hs[b * Up + u]) * w2s[u * C + c];
-    logit[o] = s;
+  if (lane < C) {
+    float s = a.b2[(long)g * C + lane];
+    for (int l = 0; l < 64; ++l) s += part[l][lane];
+    part[0][HEAD_MAXC] = 0.f;
+    acc[0] = s;
   }
   __syncthreads();
-  if (tid < B) {
-    const int b = tid;
-    const int step = a.st ? a.st->cur_step : 0;
-    const long sid = a.gather[((long)step * a.G + g) * B + b];
-    const int y = (int)a.labels[sid];
-    float p[HEAD_MAXC];
-    float mx = -INFINITY;
-    for (int c = 0; c < C; ++c) mx = fmaxf(mx, logit[b * C + c]);
-    float z = 0.f;
-    for (int c = 0; c < C; ++c) { p[c] = expf(logit[b * C + c] - mx); z += p[c]; }
-    int arg = 0;
-    float loss = 0.f, binc = 0.f;
+  if (lane < C) part[lane][0] = acc[0];   // logits now in part[c][0]
+  __syncthreads();
+  if (lane != 0) return;
+  const int step = a.st ? a.st->cur_step : 0;
+  const long sid = a.gather[((long)step * a.G + g) * a.B + b];
+  const int y = (int)a.labels[sid];
+  float p[HEAD_MAXC];
+  float mx = -INFINITY;
+  for (int c = 0; c < C; ++c) mx = fmaxf(mx, part[c][0]);
+  float z = 0.f;
+  for (int c = 0; c < C; ++c) { p[c] = expf(part[c][0] - mx); z += p[c]; }
+  int arg = 0;
+  float loss = 0.f, binc = 0.f;
+  for (int c = 0; c < C; ++c) {
+    p[c] /= z;
+    if (p[c] > p[arg]) arg = c;
+    const float yc = (c == y) ? 1.f : 0.f;
+    binc += (rintf(p[c]) == yc) ? 1.f : 0.f;
+    if (!a.loss_ce) {
+      const float pc = fminf(fmaxf(p[c], CLIP_EPS), 1.f - CLIP_EPS);
+      loss += -(yc * logf(pc) + (1.f - yc) * logf(1.f - pc)) / C;
+    }
+  }
+  if (a.loss_ce) loss = -logf(fmaxf(p[y], 1e-30f));
+  if (a.eval) {
+    float* e = a.eval_out + ((long)g * a.B + b) * 3;
+    e[0] = loss; e[1] = binc; e[2] = (arg == y) ? 1.f : 0.f;
+    return;
+  }
+  float* dz = a.dz + ((long)g * a.B + b) * C;
+  const float inv_b = 1.0f / a.B;
+  if (a.loss_ce) {
+    for (int c = 0; c < C; ++c) dz[c] = (p[c] - ((c == y) ? 1.f : 0.f)) * inv_b;
+  } else {
+    // dL/dp_c = (pc - y)/(pc(1-pc)) / C inside the clip range, 0 where clipped
+    float dp[HEAD_MAXC], s = 0.f;
     for (int c = 0; c < C; ++c) {
-      p[c] /= z;
-      if (p[c] > p[arg]) arg = c;
       const float yc = (c == y) ? 1.f : 0.f;
-      binc += (rintf(p[c]) == yc) ? 1.f : 0.f;
-      if (!a.loss_ce) {
-        const float pc = fminf(fmaxf(p[c], CLIP_EPS), 1.f - CLIP_EPS);
-        loss += -(yc * logf(pc) + (1.f - yc) * logf(1.f - pc)) / C;
-      }
+      const bool inside = p[c] >= CLIP_EPS && p[c] <= 1.f - CLIP_EPS;
+      const float pc = fminf(fmaxf(p[c], CLIP_EPS), 1.f - CLIP_EPS);
+      dp[c] = inside ? (pc - yc) / (pc * (1.f - pc)) / C : 0.f;
+      s += p[c] * dp[c];
     }
-    if (a.loss_ce) loss = -logf(fmaxf(p[y], 1e-30f));
-    if (a.eval) {
-      float* e = a.eval_out + ((long)g * B + b) * 3;
-      e[0] = loss; e[1] = binc; e[2] = (arg == y) ? 1.f : 0.f;
-    } else {
-      const float inv_b = 1.0f / B;
-      if (a.loss_ce) {
-        for (int c = 0; c < C; ++c) dz[b * C + c] = (p[c] - ((c == y) ? 1.f : 0.f)) * inv_b;
-      } else {
-        // dL/dp_c = (pc - y)/(pc(1-pc)) / C inside the clip range, 0 where clipped
-        float dp[HEAD_MAXC], s = 0.f;
-        for (int c = 0; c < C; ++c) {
-          const float yc = (c == y) ? 1.f : 0.f;
-          const bool inside = p[c] >= CLIP_EPS && p[c] <= 1.f - CLIP_EPS;
-          const float pc = fminf(fmaxf(p[c], CLIP_EPS), 1.f - CLIP_EPS);
-          dp[c] = inside ? (pc - yc) / (pc * (1.f - pc)) / C : 0.f;
-          s += p[c] * dp[c];
-        }
-        for (int c = 0; c < C; ++c) dz[b * C + c] = p[c] * (dp[c] - s) * inv_b;
-      }
-    }
+    for (int c = 0; c < C; ++c) dz[c] = p[c] * (dp[c] - s) * inv_b;
   }
-  if (a.eval) return;
+}
+
+// (2) grid (ceil(Up/64), G): per 64-unit slice, dH = (dz W2^T) * scale * (h > 0),
+//     gb1 = sum_b dH, gW2 = h^T dz; block 0 also gb2 = sum_b dz.
+__global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
+  __shared__ float dzs[HEAD_MAXB * HEAD_MAXC];
+  __shared__ float w2s[64 * HEAD_MAXC];
+  __shared__ float hsl[HEAD_MAXB][65];
+  __shared__ float colsum[4][64];
+  const int g = blockIdx.y, u0 = blockIdx.x * 64, tid = threadIdx.x;
+  const int B = a.B, Up = a.Up, C = a.C;
+  const float* dz = a.dz + (long)g * B * C;
+  for (int i = tid; i < B * C; i += 256) dzs[i] = dz[i];
+  for (int i = tid; i < 64 * C; i += 256) {
+    const int u = u0 + i / C;
+    w2s[i] = (u < Up) ? a.w2[((long)g * Up + u0) * C + i] : 0.f;
+  }
+  for (int i = tid; i < B * 64; i += 256) {
+    const int b = i >> 6, j = i & 63;
+    hsl[b][j] = (u0 + j < Up) ? bf2f(a.h[((long)g * B + b) * Up + u0 + j]) : 0.f;
+  }
   __syncthreads();
-  // dH[b][u] = (sum_c dz[b][c] W2[u][c]) * scale * (h > 0);  gb1[u] = sum_b dH
-  float* dHg = a.dH + (long)g * B * Up;
-  for (int u = tid; u < Up; u += 256) {
+  // dH and gb1: thread = (unit j, row quarter)
+  {
+    const int j = tid & 63, q = tid >> 6;
     float sb = 0.f;
-    for (int b = 0; b < B; ++b) {
+    for (int b = q; b < B; b += 4) {
       float s = 0.f;
-      for (int c = 0; c < C; ++c) s += dz[b * C + c] * w2s[u * C + c];
-      const float hv = bf2f(hs[b * Up + u]);
-      const float d = hv > 0.f ? s * a.drop_scale : 0.f;
-      dHg[(long)b * Up + u] = d;
+      for (int c = 0; c < C; ++c) s += dzs[b * C + c] * w2s[j * C + c];
+      const float d = hsl[b][j] > 0.f ? s * a.drop_scale : 0.f;
+      if (u0 + j < Up) a.dH[((long)g * B + b) * Up + u0 + j] = d;
       sb += d;
     }
-    a.gb1[(long)g * Up + u] = sb;
+    colsum[q][j] = sb;
   }
-  // gw2[u][c] = sum_b h[b][u] dz[b][c]
-  for (int o = tid; o < Up * C; o += 256) {
-    const int u = o / C, c = o % C;
+  // gW2 slice
+  for (int o = tid; o < 64 * C; o += 256) {
+    const int j = o / C, c = o % C;
+    if (u0 + j >= Up) continue;
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += bf2f(hs[b * Up + u]) * dz[b * C + c];
-    a.gw2[(long)g * Up * C + o] = s;
+    for (int b = 0; b < B; ++b) s += hsl[b][j] * dzs[b * C + c];
+    a.gw2[((long)g * Up + u0) * C + o] = s;
   }
-  if (tid < C) {
+  __syncthreads();
+  if (tid < 64 && u0 + tid < Up)
+    a.gb1[(long)g * Up + u0 + tid] = colsum[0][tid] + colsum[1][tid] + colsum[2][tid] + colsum[3][tid];
+  if (blockIdx.x == 0 && tid < C) {
     float s = 0.f;
-    for (int b = 0; b < B; ++b) s += dz[b * C + tid];
+    for (int b = 0; b < B; ++b) s += dzs[b * C + tid];
     a.gb2[(long)g * C + tid] = s;
   }
 }
@@ -401,16 +448,15 @@ int gt_step_begin(StepState* s, hipStream_t stream) {
 
 int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
   if (a->Fp % 8 || a->Up % 64) return -1;
-  dim3 grid(a->Up / 64, (a->B + 31) / 32, a->G);
+  dim3 grid(a->Up / 16, (a->B + 31) / 32, a->G);
   hipLaunchKernelGGL(dense_fwd_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 
 int gt_head(const HeadArgs* a, hipStream_t stream) {
-  if (a->B > HEAD_MAXB || a->C > HEAD_MAXC || (a->B * a->Up) % 8) return -1;
-  const size_t lds = sizeof(float) * ((size_t)a->Up * a->C + 2 * a->B * a->C) + 2 * (size_t)a->B * a->Up;
-  if (lds > 160 * 1024) return -2;
-  hipLaunchKernelGGL(head_kernel, dim3(a->G), dim3(256), lds, stream, *a);
+  if (a->B > HEAD_MAXB || a->C > HEAD_MAXC) return -1;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(a->B, a->G), dim3(64), 0, stream, *a);
+  if (!a->eval) hipLaunchKernelGGL(head_bwd_kernel, dim3((a->Up + 63) / 64, a->G), dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 

@@ -73,3 +73,12 @@ __device__ __forceinline__ uint32_t hash4(uint32_t a, uint32_t b, uint32_t c, ui
   h = mix32(h ^ (c * 0x85ebca6bU));
   return mix32(h ^ (d * 0xc2b2ae35U));
 }
+
+// Exact unsigned division by a runtime divisor d via one mul-hi, valid
+// whenever n * d < 2^32 (all index math here): m = ceil(2^32 / d).
+struct FastDiv {
+  uint32_t d, m;
+  __device__ __forceinline__ explicit FastDiv(uint32_t dd) : d(dd), m(dd > 1 ? 0xFFFFFFFFu / dd + 1u : 0u) {}
+  __device__ __forceinline__ uint32_t div(uint32_t n) const { return d > 1 ? __umulhi(n, m) : n; }
+  __device__ __forceinline__ void divmod(uint32_t n, uint32_t& q, uint32_t& r) const { q = div(n); r = n - q * d; }
+};

@@ -73,12 +73,9 @@ class HipFoldJob(FoldJob):
                 L.cinp, L.coutp = pad8(st.cin), pad8(st.cout)
                 L.KH, L.KW = st.k
                 L.Kdim = L.KH * L.KW * L.cinp
-                L.TH = max(1, min(L.H, 64 // L.W)) if L.W <= 64 else None
-                if L.TH is None:
-                    raise ValueError("image width > 64 not supported by conv_fwd tiles")
+                L.TH = K.conv_tile_rows(L.H, L.W)
                 npix = B * L.H * L.W
-                L.pps = max(32, round_up(-(-npix // 16), 32))
-                L.S = -(-npix // L.pps)
+                L.pps, L.S = K.wgrad_split(npix, L.Kdim, L.coutp, G)
                 self.shapes[st.name] = (L.H, L.W, L.coutp)
                 self.layers.append(L)
             else:
@@ -99,6 +96,7 @@ class HipFoldJob(FoldJob):
             self.grad[name] = torch.zeros((G, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
         self.hdrop = torch.zeros((G, B, self.Up), dtype=torch.bfloat16, device=dev)
         self.dH = torch.zeros((G, B, self.Up), dtype=torch.float32, device=dev)
+        self.dz_head = torch.zeros((G, B, plan.classes), dtype=torch.float32, device=dev)
         # ---- parameters (flat fp32 master + Adam moments) --------------------
         segs = []
         for L in self.layers:
@@ -225,6 +223,7 @@ class HipFoldJob(FoldJob):
         hd.labels, hd.gather, hd.st = self.data.labels.data_ptr(), gather_train, self.state.data_ptr()
         hd.dH, hd.gw2, hd.gb2, hd.gb1 = self.dH.data_ptr(), self.gW2.data_ptr(), self.gb2.data_ptr(), self.gb1.data_ptr()
         hd.eval_out = 0
+        hd.dz = self.dz_head.data_ptr()
         hd.G, hd.B, hd.Up, hd.C = G, B, self.Up, self.classes
         hd.loss_ce = 1 if self.cfg.loss == "ce" else 0
         hd.drop_scale = 1.0 / (1.0 - self.cfg.dropout) if self.cfg.dropout < 1 else 0.0

@@ -34,7 +34,7 @@ class DenseFwdArgs(C.Structure):
 
 class HeadArgs(C.Structure):
     _fields_ = [("h", P), ("w2", P), ("b2", P), ("labels", P), ("gather", P), ("st", P), ("dH", P),
-                ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P),
+                ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P), ("dz", P),
                 ("G", I), ("B", I), ("Up", I), ("C", I), ("loss_ce", I), ("drop_scale", C.c_float), ("eval", I)]
 
 
@@ -94,3 +94,25 @@ def check(rc, what):
 
 def ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+def conv_tile_rows(H, W):
+    """Output rows per conv_fwd workgroup: up to 128 pixels (4 waves x 32)."""
+    if W > 128:
+        raise ValueError("image width > 128 not supported by conv_fwd tiles")
+    return max(1, min(H, 128 // W))
+
+
+def wgrad_split(npix, kdim, coutp, G=None, target_blocks=256):
+    """(pixels per split, splits) for conv_wgrad: ~``target_blocks``
+    workgroups PER FOLD (the split never depends on how many folds share a
+    launch, so a fold's gradient summation order -- and its result -- is the
+    same alone or batched), 64-pixel K-steps, >= 2 K-steps per workgroup."""
+    nb = -(-kdim // 64)
+    mb = -(-coutp // 64)
+    per = max(1, nb * mb)
+    S = max(1, min(target_blocks // per, npix // 128))
+    pps = -(-npix // S)
+    pps = max(64, -(-pps // 64) * 64)
+    S = -(-npix // pps)
+    return pps, S

@@ -71,7 +71,7 @@ def test_conv_fwd(H, W, cin, cout, k, nin):
     a.n_in, a.n_out, a.acc_flags, a.relu = nin, 1, 0, 1
     a.w, a.bias = wp.data_ptr(), bp.data_ptr()
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
-    a.TH = max(1, min(H, 64 // W))
+    a.TH = Km.conv_tile_rows(H, W)
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv")
     torch.cuda.synchronize()
     for g in range(G):
@@ -151,8 +151,7 @@ def test_conv_wgrad(H, W, cin, cout, k, nin, first):
     y_p = torch.stack([nhwc_pad(y[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
     Kdim = k * k * cinp
     npix = B * H * W
-    pps = max(32, ((npix // 4) + 31) // 32 * 32)
-    S = -(-npix // pps)
+    pps, S = Km.wgrad_split(npix, Kdim, coutp, target_blocks=16)
     pw = torch.zeros(S, G, coutp, Kdim, device=DEV)
     pb = torch.zeros(S, G, coutp, device=DEV)
     st = torch.zeros(8, dtype=torch.int32, device=DEV)
@@ -296,7 +295,9 @@ def test_head(loss):
     a = Km.HeadArgs()
     a.h, a.w2, a.b2, a.labels, a.gather, a.st = hb.data_ptr(), w2.data_ptr(), b2.data_ptr(), labels.data_ptr(), \
         gather.data_ptr(), st.data_ptr()
+    dzw = torch.zeros(G, B, C, device=DEV)
     a.dH, a.gw2, a.gb2, a.gb1, a.eval_out = dH.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), gb1.data_ptr(), 0
+    a.dz = dzw.data_ptr()
     a.G, a.B, a.Up, a.C, a.loss_ce, a.drop_scale, a.eval = G, B, Up, C, int(loss == "ce"), 2.0, 0
     Km.check(Km.lib().gt_head(a, stream()), "head")
     ev = torch.zeros(G, B, 3, device=DEV)
