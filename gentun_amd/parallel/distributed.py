@@ -258,7 +258,9 @@ class DistributedPopulation(Population):
             table[k, 2] = sum(1 << f for f in fids)
             table[k, 3:] = codec.encode(todo[slot].get_genes())
         extra = _jsonable(todo[0].get_additional_parameters())
-        blob = np.frombuffer(json.dumps({"species": self.species.__name__, "extra": extra}).encode(), np.uint8)
+        genome = {k: (list(v) if isinstance(v, tuple) else v) for k, v in todo[0].get_genome().items()}
+        blob = np.frombuffer(json.dumps({"species": self.species.__name__, "extra": extra,
+                                         "genome": genome}).encode(), np.uint8)
         t0 = time.perf_counter()
         comm.broadcast_array(np.array([CMD_EVAL, self.generation_counter, len(todo), nfold], np.int64))
         comm.broadcast_array(blob)
@@ -393,12 +395,13 @@ class GentunWorker(object):
         table = comm.broadcast_array(None)
         extra = {k: _tuplify(v) for k, v in meta["extra"].items()}
         mine = []
-        codec = None
+        # genome spec comes with the broadcast: building a throw-away individual
+        # here would draw random genes from the GA stream
+        genome = {k: (tuple(v) if isinstance(v, list) else v) for k, v in meta["genome"].items()}
+        codec = GenomeCodec(genome)
         for k in range(table.shape[0]):
             if int(table[k, 1]) != comm.rank:
                 continue
-            if codec is None:
-                codec = GenomeCodec(self.individual(None, None, **extra).get_genome())
             genes = codec.decode(table[k, 3:])
             fids = [f for f in range(nfold) if (int(table[k, 2]) >> f) & 1]
             ind = self.individual(self.x_train, self.y_train, genes=genes, **extra)

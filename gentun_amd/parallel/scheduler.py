@@ -41,11 +41,13 @@ def make_units(costs, nfold, world_size, split_folds=True):
     if split_folds and nfold > 1 and n < world_size:
         groups = min(nfold, -(-world_size // n))
     units, ucost = [], []
+    base, extra = divmod(nfold, groups)
     for i, c in enumerate(costs):
-        folds = list(range(nfold))
-        size = -(-nfold // groups)
-        for g0 in range(0, nfold, size):
-            fid = folds[g0:g0 + size]
+        f0 = 0
+        for k in range(groups):
+            size = base + (1 if k < extra else 0)
+            fid = list(range(f0, f0 + size))
+            f0 += size
             units.append((i, fid))
             ucost.append(c * len(fid) / float(nfold))
     return units, ucost

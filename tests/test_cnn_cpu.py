@@ -1,0 +1,92 @@
+"""Genetic-CNN fitness on the CPU (torch oracle path): fold-batched training,
+Keras-compatible loss/metric semantics and the fitness plumbing."""
+
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from gentun_amd import GeneticCnnIndividual, Population, RussianRouletteGA
+from gentun_amd.models import cnn_engine as E
+from gentun_amd.models.genome import make_plan
+from gentun_amd.utils import rng
+from gentun_amd.utils.data import make_image_classification, stratified_kfold
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _data(n=300):
+    return make_image_classification(n=n, shape=(16, 16, 1), classes=4, seed=0, noise=0.3)
+
+
+def test_loss_semantics_match_keras_definitions():
+    logits = torch.tensor([[[2.0, 0.0, -1.0, 0.5]]])
+    y = torch.tensor([[[1.0, 0.0, 0.0, 0.0]]])
+    p = torch.softmax(logits, -1)
+    per, binc, catc = E.loss_and_metrics(logits, y, "bce_compat")
+    ref = -(y * torch.log(p) + (1 - y) * torch.log(1 - p)).mean(-1)
+    assert torch.allclose(per, ref)
+    assert binc.item() == 4.0 and catc.item() == 1.0     # binary_accuracy counts all 4 outputs
+    per, _, _ = E.loss_and_metrics(logits, y, "ce")
+    assert torch.allclose(per, -torch.log(p[..., 0]))
+    # chance-level binary accuracy is 1 - 1/C, not 1/C
+    per, binc, catc = E.loss_and_metrics(torch.zeros(1, 1, 10), torch.eye(10)[None, :1], "bce_compat")
+    assert binc.item() == 9.0 and catc.item() == 1.0
+
+
+def test_fold_batched_torch_training_learns():
+    x, y = _data(900)
+    folds = stratified_kfold(np.argmax(y, 1), 3, seed=0)
+    plan = make_plan({'S_1': '000', 'S_2': '0000000000'}, (3, 5), (16, 16, 1), (8, 16), ((3, 3), (3, 3)), 64, 4)
+    cfg = E.TrainConfig(epochs=(8,), learning_rate=(1e-3,), batch_size=16, dtype="fp32", loss="ce")
+    res = E.make_job("torch", plan, x, y, folds, cfg, "cpu").launch().finish()
+    assert np.mean(res["categorical_accuracy"]) > 0.4 and max(res["categorical_accuracy"]) > 0.5  # chance 0.25
+    assert len(res["binary_accuracy"]) == 3
+
+
+def test_fold_results_independent_of_grouping():
+    x, y = _data(200)
+    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
+    plan = make_plan({'S_1': '100', 'S_2': '0000000000'}, (3, 5), (16, 16, 1), (8, 16), ((3, 3), (3, 3)), 32, 4)
+    # dropout off: the torch oracle draws dropout masks from torch's global RNG
+    # (the HIP path keys them by fold id; tests/test_hip_train.py checks that)
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=16, dtype="fp32", loss="ce", dropout=0.0)
+    together = E.make_job("torch", plan, x, y, folds, cfg, "cpu", fold_ids=[0, 1]).launch().finish()
+    alone = E.make_job("torch", plan, x, y, [folds[1]], cfg, "cpu", fold_ids=[1]).launch().finish()
+    assert abs(together["val_loss"][1] - alone["val_loss"][0]) < 1e-4
+
+
+def test_individual_fitness_and_small_search():
+    x, y = _data(160)
+    rng.seed(3)
+    extra = dict(nodes=(3, 3), input_shape=(16, 16, 1), kernels_per_layer=(4, 8), kernel_sizes=((3, 3), (3, 3)),
+                 dense_units=16, classes=4, nfold=2, epochs=(1,), learning_rate=(1e-3,), batch_size=16,
+                 backend="torch", device="cpu", dtype="fp32")
+    ind = GeneticCnnIndividual(x, y, **extra)
+    f = ind.get_fitness()
+    assert 0.0 <= f <= 1.0 and len(ind.fold_scores) == 2
+    pop = Population(GeneticCnnIndividual, x, y, size=4, crossover_rate=0.3, mutation_rate=0.1,
+                     additional_parameters=extra)
+    ga = RussianRouletteGA(pop, verbose=False)
+    best = ga.run(2)
+    assert best.get_fitness() == max(h["best_fitness"] for h in ga.history)
+
+
+def test_bench_contract_cpu():
+    """bench.py prints exactly one JSON line with the driver's keys."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
+                          "--per-gpu", "1", "--epochs", "1", "--lr", "1e-3", "--samples", "120", "--nfold", "2",
+                          "--backend", "torch"], capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1
+    rec = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config"):
+        assert key in rec
+    assert rec["n_gpus"] == 1 and rec["value"] > 0 and rec["higher_is_better"] is True

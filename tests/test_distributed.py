@@ -1,0 +1,168 @@
+"""Distributed evaluation: master + evaluator ranks
+over collectives. Ranks are threads on a ThreadComm test double and real
+processes on the ``gloo`` backend (CPU stand-in for RCCL)."""
+
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from fake_species import BitIndividual, NumIndividual
+from gentun_amd import GeneticAlgorithm, Population, RussianRouletteGA, XgboostIndividual
+from gentun_amd.parallel import GenomeCodec, ThreadComm, lpt_assign, make_units
+from gentun_amd.parallel.distributed import DistributedGridPopulation, DistributedPopulation, GentunWorker
+from gentun_amd.parallel.evaluators import SequentialEvaluator
+from gentun_amd.utils import rng
+
+
+def test_codec_roundtrip():
+    ind = XgboostIndividual(None, None)
+    c = GenomeCodec(ind.get_genome())
+    genes = ind.get_genes()
+    back = c.decode(c.encode(genes))
+    assert back == genes and all(type(back[k]) is type(genes[k]) for k in genes)
+    from gentun_amd import GeneticCnnIndividual
+    cnn = GeneticCnnIndividual(None, None, genes={'S_1': '101', 'S_2': '0110011001'})
+    c = GenomeCodec(cnn.get_genome())
+    assert c.width == 13 and c.decode(c.encode(cnn.get_genes())) == cnn.get_genes()
+
+
+def test_scheduler():
+    owner = lpt_assign([5, 4, 3, 3, 3], 2)
+    loads = [sum(c for c, o in zip([5, 4, 3, 3, 3], owner) if o == r) for r in range(2)]
+    assert sorted(loads) == [8, 10]
+    assert lpt_assign([1, 1, 1], 2) == lpt_assign([1, 1, 1], 2)    # deterministic
+    units, costs = make_units([10.0, 20.0], 5, 8)
+    assert len(units) == 2 * 4 and sorted(len(f) for _, f in units) == [1, 1, 1, 1, 1, 1, 2, 2]
+    assert sorted(f for _, fids in units if _ == 0 for f in fids) == [0, 1, 2, 3, 4]
+    units, _ = make_units([1.0] * 10, 5, 8)
+    assert all(len(f) == 5 for _, f in units)                        # enough candidates: no split
+
+
+def _ga_run(pop, cls, gens):
+    ga = cls(pop, verbose=False) if cls is RussianRouletteGA else cls(pop, verbose=False)
+    ga.run(gens)
+    return [(h["best_fitness"], h["evals"], tuple(sorted(h["best_genes"].items()))) for h in ga.history]
+
+
+def _threaded(world, species, cls, gens, seed, size=12, fault=None, maximize=True):
+    comms = ThreadComm.group(world)
+    out = {}
+
+    def worker(r):
+        GentunWorker(species, None, None, comm=comms[r], evaluator=SequentialEvaluator()).work()
+
+    threads = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(1, world)]
+    for t in threads:
+        t.start()
+    old = os.environ.get("GENTUN_FAULT")
+    if fault:
+        os.environ["GENTUN_FAULT"] = fault
+    try:
+        rng.seed(seed)
+        pop = DistributedPopulation(species, None, None, size=size, comm=comms[0],
+                                    evaluator=SequentialEvaluator(), maximize=maximize)
+        out["hist"] = _ga_run(pop, cls, gens)
+        out["pop"] = pop
+        pop.shutdown()
+    finally:
+        if fault:
+            if old is None:
+                os.environ.pop("GENTUN_FAULT", None)
+            else:
+                os.environ["GENTUN_FAULT"] = old
+    for t in threads:
+        t.join(timeout=30)
+        assert not t.is_alive()
+    return out
+
+
+def _local(species, cls, gens, seed, size=12, maximize=True):
+    rng.seed(seed)
+    pop = Population(species, None, None, size=size, maximize=maximize)
+    return _ga_run(pop, cls, gens)
+
+
+@pytest.mark.parametrize("cls", [GeneticAlgorithm, RussianRouletteGA])
+def test_threaded_ranks_match_local_run(cls):
+    for world in (2, 3):
+        assert _threaded(world, BitIndividual, cls, 4, seed=21)["hist"] == _local(BitIndividual, cls, 4, seed=21)
+    got = _threaded(3, NumIndividual, GeneticAlgorithm, 3, seed=5, maximize=False)["hist"]
+    assert got == _local(NumIndividual, GeneticAlgorithm, 3, seed=5, maximize=False)
+
+
+def test_fault_injection_is_recovered():
+    res = _threaded(3, BitIndividual, GeneticAlgorithm, 3, seed=8, fault="1:2:raise")
+    assert res["hist"] == _local(BitIndividual, GeneticAlgorithm, 3, seed=8)
+
+
+def test_next_generation_keeps_communicator():
+    comms = ThreadComm.group(1)
+    rng.seed(2)
+    pop = DistributedPopulation(BitIndividual, None, None, size=6, comm=comms[0], evaluator=SequentialEvaluator())
+    ga = GeneticAlgorithm(pop, verbose=False)
+    ga.run(2)
+    assert isinstance(ga.population, DistributedPopulation) and ga.population.comm is comms[0]   # Q1 fixed
+
+
+def test_distributed_grid_population():
+    comms = ThreadComm.group(1)
+    pop = DistributedGridPopulation(XgboostIndividual, None, None, genes_grid={'eta': [0.1, 0.2, 0.3]},
+                                    comm=comms[0])
+    assert pop.get_size() == 3 and isinstance(pop, DistributedPopulation)
+
+
+# ---------------------------------------------------------------------------
+# real processes over torch.distributed (gloo)
+# ---------------------------------------------------------------------------
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _proc(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from fake_species import BitIndividual as Bit
+    from gentun_amd.parallel import DistComm
+    from gentun_amd.parallel.distributed import DistributedPopulation as DP, GentunWorker as GW
+    from gentun_amd.parallel.evaluators import SequentialEvaluator as SE
+    from gentun_amd import RussianRouletteGA as RR
+    from gentun_amd.utils import rng as r
+    comm = DistComm(backend="gloo", timeout_s=60)
+    if rank == 0:
+        r.seed(77)
+        pop = DP(Bit, None, None, size=10, comm=comm, evaluator=SE())
+        ga = RR(pop, verbose=False)
+        ga.run(4)
+        pop = ga.population
+        pop.sync_ranks()
+        pop.shutdown()
+        q.put([(h["best_fitness"], h["evals"], tuple(sorted(h["best_genes"].items()))) for h in ga.history])
+    else:
+        GW(Bit, None, None, comm=comm, evaluator=SE()).work()
+    comm.destroy()
+
+
+def test_gloo_processes_match_local_run():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 2
+    procs = [ctx.Process(target=_proc, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    hist = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert hist == _local(BitIndividual, RussianRouletteGA, 4, seed=77, size=10)
