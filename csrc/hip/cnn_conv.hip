@@ -36,6 +36,7 @@ struct ConvArgs {
   const int64_t* gather;     // optional: image table [steps][G][B]; in[0] is then the dataset
   const StepState* st;       // cur_step for the gather table
   uint16_t* out[4];          // [G][B][H][W][Coutp]
+  const uint16_t* out_mask[4];  // optional per output: final value *= (out_mask > 0) (dz of a ReLU layer)
   const uint16_t* w;         // [G][Coutp][KH][KW][Cinp] bf16
   const float* bias;         // [G][Coutp] or null
   int n_in, n_out, acc_flags, relu;
@@ -60,28 +61,35 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
   const int total = PH * PW * ncb;
   const int nchunks = a.KH * a.KW * ncb;
   const int Kdim = a.KH * a.KW * a.Cinp;
-  // LDS carve: [weight block x2][patch][chunk offset table]
-  uint16_t* wbuf = reinterpret_cast<uint16_t*>(smem);                       // 2 x 64 x CF_WLD
-  uint4* patch = reinterpret_cast<uint4*>(smem + 2 * 64 * CF_WLD * 2);
-  int* coff = reinterpret_cast<int*>(smem + 2 * 64 * CF_WLD * 2 + (size_t)total * 16);
+  // LDS carve: [weight blocks: nbuf x wrows x CF_WLD][patch][chunk offset table].
+  // Only as many weight rows / buffers as this layer needs (occupancy).
+  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
+  const int nbuf = nkb > 1 ? 2 : 1;
+  const int wrows = ((min(64, a.Coutp) + 15) >> 4) << 4;
+  const size_t wbytes = (size_t)nbuf * wrows * CF_WLD * 2;
+  uint16_t* wbuf = reinterpret_cast<uint16_t*>(smem);
+  uint4* patch = reinterpret_cast<uint4*>(smem + wbytes);
+  int* coff = reinterpret_cast<int*>(smem + wbytes + (size_t)total * 16);
   const uint16_t* wg = a.w + (long)g * a.Coutp * Kdim;
 
-  // weight-block staging role: row = tid >> 2 (64 rows), 4 chunks per thread
-  const int wr = tid >> 2, wq = (tid & 3) * 4;
+  // weight-block staging role: row = tid >> 2 (up to 64 rows), 8 chunks per thread
+  const int wr = tid >> 2, wq = (tid & 3) * (CF_KB / 4);
+  const bool wrow_live = wr < wrows;
   const bool wrow_ok = co_blk + wr < a.Coutp;
   const uint16_t* wsrc = wg + (long)(co_blk + wr) * Kdim;
-  uint4 wreg[4];
+  uint4 wreg[CF_KB / 4];
   auto load_wblock = [&](int kb) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < CF_KB / 4; ++j) {
       const int c = kb * CF_KB + wq + j;
       wreg[j] = (wrow_ok && c < nchunks) ? *reinterpret_cast<const uint4*>(wsrc + c * 8) : make_uint4(0, 0, 0, 0);
     }
   };
   auto store_wblock = [&](int buf) {
-    uint16_t* dst = wbuf + buf * 64 * CF_WLD + wr * CF_WLD + wq * 8;
+    if (!wrow_live) return;
+    uint16_t* dst = wbuf + buf * wrows * CF_WLD + wr * CF_WLD + wq * 8;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) *reinterpret_cast<uint4*>(dst + j * 8) = wreg[j];
+    for (int j = 0; j < CF_KB / 4; ++j) *reinterpret_cast<uint4*>(dst + j * 8) = wreg[j];
   };
   load_wblock(0);
 
@@ -161,11 +169,10 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[h][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
   for (int kb = 0; kb < nkb; ++kb) {
     const bool more = kb + 1 < nkb;
     if (more) load_wblock(kb + 1);
-    const uint16_t* wcur = wbuf + (kb & 1) * 64 * CF_WLD;
+    const uint16_t* wcur = wbuf + (kb & 1) * wrows * CF_WLD;
 #pragma unroll
     for (int kk = 0; kk < CF_KB / 4; ++kk) {
       const int c = kb * CF_KB + kk * 4 + kq;
@@ -209,15 +216,20 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
       }
       for (int k = 0; k < a.n_out; ++k) {
         uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
+        float sum[4] = {v[0], v[1], v[2], v[3]};
         if ((a.acc_flags >> k) & 1) {
           const uint2 old = *dst;
-          float o[4] = {__uint_as_float(old.x << 16), __uint_as_float(old.x & 0xffff0000u),
-                        __uint_as_float(old.y << 16), __uint_as_float(old.y & 0xffff0000u)};
-          float sum[4] = {v[0] + o[0], v[1] + o[1], v[2] + o[2], v[3] + o[3]};
-          *dst = pack4(sum);
-        } else {
-          *dst = pack4(v);
+          sum[0] += __uint_as_float(old.x << 16); sum[1] += __uint_as_float(old.x & 0xffff0000u);
+          sum[2] += __uint_as_float(old.y << 16); sum[3] += __uint_as_float(old.y & 0xffff0000u);
         }
+        if (a.out_mask[k]) {
+          const uint2 m = *reinterpret_cast<const uint2*>(a.out_mask[k] + obase + co0);
+          // bf16 > 0  <=>  sign bit clear and not +0
+          const uint32_t mw[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sum[i] = (mw[i] != 0u && mw[i] < 0x8000u) ? sum[i] : 0.f;
+        }
+        *dst = pack4(sum);
       }
     }
   }
@@ -231,8 +243,7 @@ struct WgradArgs {
   const uint16_t* in[4];     // summed inputs of the layer [G][B][H][W][Cinp]
   const int64_t* gather;     // optional dataset gather (first layer)
   const StepState* st;
-  const uint16_t* dy;        // grad of the layer output [G][B][H][W][Coutp]
-  const uint16_t* ymask;     // layer output (ReLU mask), same shape as dy
+  const uint16_t* dz;        // ReLU-masked grad of the layer output [G][B][H][W][Coutp]
   float* part_w;             // [S][G][Coutp][Kdim]
   float* part_b;             // [S][G][Coutp]
   int n_in;
@@ -252,63 +263,26 @@ __device__ __forceinline__ uint4 tr_frag(const uint16_t* tile, int col0, int lan
   typedef __attribute__((address_space(3))) short4_t lds_s4;
   const uint16_t* r0 = tile + (8 * g + q) * WG_LD + col0 + 4 * p;
   const uint16_t* r1 = r0 + 4 * WG_LD;
-  short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(r0));
-  short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(r1));
-  uint4 v;
-  v.x = (uint32_t)(uint16_t)lo[0] | ((uint32_t)(uint16_t)lo[1] << 16);
-  v.y = (uint32_t)(uint16_t)lo[2] | ((uint32_t)(uint16_t)lo[3] << 16);
-  v.z = (uint32_t)(uint16_t)hi[0] | ((uint32_t)(uint16_t)hi[1] << 16);
-  v.w = (uint32_t)(uint16_t)hi[2] | ((uint32_t)(uint16_t)hi[3] << 16);
-  return v;
+  const short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(r0));
+  const short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(r1));
+  typedef __attribute__((ext_vector_type(8))) short short8_t;
+  const short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(uint4, v);
 }
 
-__device__ __forceinline__ void wgrad_load(const WgradArgs& a, long p, long p_end, int g, int co_st, bool col_ok,
-                                           int c_kh, int c_kw, int c_cb, uint4& dzv, uint4& xsv, float* bsum) {
-  const long HW = (long)a.H * a.W;
-  float dz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float xs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (p < p_end) {
-    uint32_t bq, remu, hq, wq;
-    FastDiv((uint32_t)HW).divmod((uint32_t)p, bq, remu);
-    FastDiv((uint32_t)a.W).divmod(remu, hq, wq);
-    const long bimg = bq;
-    const int rem = (int)remu;
-    const int hh = (int)hq, ww = (int)wq;
-    if (co_st < a.Coutp) {
-      const long off = (((long)g * a.B + bimg) * HW + rem) * a.Coutp + co_st;
-      float m[8];
-      unpack8(*reinterpret_cast<const uint4*>(a.dy + off), dz);
-      unpack8(*reinterpret_cast<const uint4*>(a.ymask + off), m);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) { dz[j] = m[j] > 0.f ? dz[j] : 0.f; bsum[j] += dz[j]; }
-    }
-    const int ih = hh + c_kh - (a.KH >> 1), iw = ww + c_kw - (a.KW >> 1);
-    if (col_ok && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
-      const long pix_off = ((long)ih * a.W + iw) * a.Cinp + c_cb * 8;
-      if (a.n_in == 1) {
-        const uint16_t* base = a.gather
-            ? a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + bimg] * HW * a.Cinp
-            : a.in[0] + ((long)g * a.B + bimg) * HW * a.Cinp;
-        xsv = *reinterpret_cast<const uint4*>(base + pix_off);
-        dzv = pack8(dz);
-        return;
-      }
-      float t[8];
-      for (int k = 0; k < a.n_in; ++k) {
-        const uint16_t* base = a.in[k] + ((long)g * a.B + bimg) * HW * a.Cinp;
-        unpack8(*reinterpret_cast<const uint4*>(base + pix_off), t);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xs[j] += t[j];
-      }
-    }
-  }
-  dzv = pack8(dz);
-  xsv = pack8(xs);
-}
+// Coalesced staging of one 64-pixel K-step (pixels p0 .. p0+63 of one fold,
+// consecutive in memory because the fold's images are contiguous):
+//   dz tile  [64 px][64 co] : slot i -> (pixel i / ncc, co chunk i % ncc): a wave
+//                             reads one contiguous run of dy / ymask bytes;
+//   im2col   [64 px][64 col]: slot i -> (col chunk i / 64 (wave-uniform), pixel
+//                             i % 64 = lane): a wave reads 64 consecutive
+//                             pixels at one (kh, kw, cb) shift.
+struct WgSlots {
+  uint4 dz[2], xs[2];
+};
 
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[4 * WG_TILE];   // 2 buffers x (dz, im2col)
-  __shared__ float bred[32][65];
   const int tid = threadIdx.x;
   const int nb = blockIdx.x;
   const int s = blockIdx.y;
@@ -317,44 +291,105 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   const int co_blk = (blockIdx.z % mblocks) * 64;
   const int Kdim = a.KH * a.KW * a.Cinp;
   const int ncb = a.Cinp >> 3;
-  const long npix = (long)a.B * a.H * a.W;
+  const long HW = (long)a.H * a.W;
+  const long npix = (long)a.B * HW;
   const long p_begin = (long)s * a.pps;
   const long p_end = (p_begin + a.pps < npix) ? p_begin + a.pps : npix;
-
-  const int sp = tid >> 3, sj = tid & 7;
-  const int co_st = co_blk + sj * 8;
-  const int col_st = nb * 64 + sj * 8;
-  int c_kh = 0, c_kw = 0, c_cb = 0;
-  const bool col_ok = col_st < Kdim;
-  if (col_ok) {
-    const int c8 = col_st >> 3;
-    c_cb = c8 % ncb;
-    const int kk = c8 / ncb;
-    c_kw = kk % a.KW; c_kh = kk / a.KW;
-  }
+  const int ncc = min(8, (a.Coutp - co_blk) >> 3);          // dz chunks per pixel in this co block
+  const int ndz = 64 * ncc;                                   // dz slots per K-step (<= 512)
   const int wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  const FastDiv div_ncc(ncc), div_hw((uint32_t)HW), div_w(a.W), div_ncb(ncb), div_kw(a.KW);
+
+  // im2col roles: this thread stages column chunks (wave, wave + 4) of the block
+  // column chunk Kdim/8 is the bias chunk: a column of ones, so dW and db come
+  // out of the same MFMAs (db[co] = sum_pix dz[pix][co] * 1)
+  int c_kh[2], c_kw[2], c_cb[2];
+  bool c_ok[2], c_one[2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int col = nb * 64 + (wave + 4 * r) * 8;
+    c_ok[r] = col < Kdim;
+    c_one[r] = (col == Kdim) && (a.part_b != nullptr);
+    uint32_t kk = 0, cb = 0, kh = 0, kw = 0;
+    if (c_ok[r]) { div_ncb.divmod((uint32_t)(col >> 3), kk, cb); div_kw.divmod(kk, kh, kw); }
+    c_kh[r] = (int)kh - (a.KH >> 1); c_kw[r] = (int)kw - (a.KW >> 1); c_cb[r] = (int)cb;
+  }
+  const uint16_t* fold_in[4];
+  for (int k = 0; k < a.n_in; ++k) fold_in[k] = a.in[k] + (long)g * a.B * HW * a.Cinp;
+  const long fold_out = (long)g * npix * a.Coutp;
+
   const int MT = (min(64, a.Coutp - co_blk) + 15) >> 4;
-  const bool wave_live = nb * 64 + wave * 16 < Kdim;
+  const bool wave_live = nb * 64 + wave * 16 <= Kdim;
   f32x4_t acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float bsum[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bool do_bias = (nb == 0) && (a.part_b != nullptr);
 
-  uint4 dzv[2], xsv[2];
+  WgSlots sl;
   auto load_step = [&](long p0) {
+    // dz (masked by the layer's own ReLU output)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
-      wgrad_load(a, p0 + h * 32 + sp, p_end, g, co_st, col_ok, c_kh, c_kw, c_cb, dzv[h], xsv[h], bsum);
-  };
-  auto store_step = [&](int bf) {
-    uint16_t* nd = lds + bf * 2 * WG_TILE;
+    for (int r = 0; r < 2; ++r) {
+      const int i = tid + 256 * r;
+      sl.dz[r] = make_uint4(0, 0, 0, 0);
+      if (i < ndz) {
+        uint32_t px, cc;
+        div_ncc.divmod((uint32_t)i, px, cc);
+        const long p = p0 + px;
+        if (p < p_end) sl.dz[r] = *reinterpret_cast<const uint4*>(a.dz + fold_out + p * a.Coutp + co_blk + cc * 8);
+      }
+    }
+    // im2col: lane = pixel
+    const long p = p0 + lane;
+    uint32_t bq = 0, rem = 0, hq = 0, wq = 0;
+    if (p < p_end) { div_hw.divmod((uint32_t)p, bq, rem); div_w.divmod(rem, hq, wq); }
+    const uint16_t* gimg = nullptr;
+    if (a.gather && p < p_end)
+      gimg = a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + bq] * HW * a.Cinp;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      *reinterpret_cast<uint4*>(&nd[(h * 32 + sp) * WG_LD + sj * 8]) = dzv[h];
-      *reinterpret_cast<uint4*>(&nd[WG_TILE + (h * 32 + sp) * WG_LD + sj * 8]) = xsv[h];
+    for (int r = 0; r < 2; ++r) {
+      sl.xs[r] = make_uint4(0, 0, 0, 0);
+      if (c_one[r] && p < p_end) sl.xs[r].x = 0x3f80u;          // bf16 1.0 in element 0
+      const int ih = (int)hq + c_kh[r], iw = (int)wq + c_kw[r];
+      if (p < p_end && c_ok[r] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
+        const long pix_off = ((long)ih * a.W + iw) * a.Cinp + c_cb[r] * 8;
+        if (gimg) {
+          sl.xs[r] = *reinterpret_cast<const uint4*>(gimg + pix_off);
+        } else if (a.n_in == 1) {
+          sl.xs[r] = *reinterpret_cast<const uint4*>(fold_in[0] + (long)bq * HW * a.Cinp + pix_off);
+        } else {
+          float xsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t[8];
+          for (int k = 0; k < a.n_in; ++k) {
+            unpack8(*reinterpret_cast<const uint4*>(fold_in[k] + (long)bq * HW * a.Cinp + pix_off), t);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xsum[j] += t[j];
+          }
+          sl.xs[r] = pack8(xsum);
+        }
+      }
     }
   };
+  auto store_step = [&](int bf) {
+    uint16_t* dzT = lds + bf * 2 * WG_TILE;
+    uint16_t* colT = dzT + WG_TILE;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int i = tid + 256 * r;
+      if (i < ndz) {
+        uint32_t px, cc;
+        div_ncc.divmod((uint32_t)i, px, cc);
+        *reinterpret_cast<uint4*>(&dzT[px * WG_LD + cc * 8]) = sl.dz[r];
+      }
+      *reinterpret_cast<uint4*>(&colT[lane * WG_LD + (wave + 4 * r) * 8]) = sl.xs[r];
+    }
+  };
+  // dz columns beyond this block's channels must read as zero
+  if (ncc < 8) {
+    for (int i = tid; i < 2 * 64 * (8 - ncc); i += 256) {
+      const int bf = i / (64 * (8 - ncc)), rem = i % (64 * (8 - ncc));
+      const int px = rem / (8 - ncc), cc = ncc + rem % (8 - ncc);
+      *reinterpret_cast<uint4*>(&lds[bf * 2 * WG_TILE + px * WG_LD + cc * 8]) = make_uint4(0, 0, 0, 0);
+    }
+  }
   load_step(p_begin);
   store_step(0);
   __syncthreads();
@@ -393,15 +428,15 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
         if (co < a.Coutp) a.part_w[(((long)s * a.G + g) * a.Coutp + co) * Kdim + col] = acc[t][i];
       }
     }
-  }
-  if (do_bias) {
+  } else if (col == Kdim && a.part_b) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) bred[sp][sj * 8 + j] = bsum[j];
-    __syncthreads();
-    if (tid < 64 && co_blk + tid < a.Coutp) {
-      float t = 0.f;
-      for (int q = 0; q < 32; ++q) t += bred[q][tid];
-      a.part_b[((long)s * a.G + g) * a.Coutp + co_blk + tid] = t;
+    for (int t = 0; t < 4; ++t) {
+      if (t >= MT) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = co_blk + t * 16 + kq * 4 + i;
+        if (co < a.Coutp) a.part_b[((long)s * a.G + g) * a.Coutp + co] = acc[t][i];
+      }
     }
   }
 }
@@ -435,7 +470,7 @@ __global__ void pool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __rest
 
 // dx[pixel] = dy[pool cell] if pixel is the cell's first maximum else 0
 __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                                uint16_t* __restrict__ dx, int NB, int H, int W, int Cp) {
+                                uint16_t* __restrict__ dx, int NB, int H, int W, int Cp, int relu_mask) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
   const long total = (long)NB * H * W * ncb;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -461,7 +496,7 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* 
         int arg = 0;
         float m = v[0][j];
         for (int q = 1; q < 4; ++q) if (v[q][j] > m) { m = v[q][j]; arg = q; }
-        out[j] = (arg == me) ? g[j] : 0.f;
+        out[j] = (arg == me && (!relu_mask || m > 0.f)) ? g[j] : 0.f;
       }
     }
     *reinterpret_cast<uint4*>(dx + ((n * H + h) * W + w) * Cp + cb * 8) = pack8(out);
@@ -479,7 +514,10 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   if (a->TH * a->W > 128 || a->TH < 1) return -2;
   const int nth = (a->H + a->TH - 1) / a->TH;
   const size_t total = (size_t)(a->TH + a->KH - 1) * (a->W + a->KW - 1) * (a->Cinp / 8);
-  const size_t lds = 2 * 64 * CF_WLD * 2 + total * 16 + 4 * ((size_t)a->KH * a->KW * (a->Cinp / 8) + 4);
+  const int nchunks = a->KH * a->KW * (a->Cinp / 8);
+  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
+  const int wrows = ((std::min(64, a->Coutp) + 15) / 16) * 16;
+  const size_t lds = (size_t)(nkb > 1 ? 2 : 1) * wrows * CF_WLD * 2 + total * 16 + 4 * ((size_t)nchunks + 4);
   if (lds > 160 * 1024) return -3;
   dim3 grid(a->B * nth, a->G, (a->Coutp + 63) / 64);
   hipLaunchKernelGGL(conv_fwd_kernel, grid, dim3(256), lds, stream, *a);
@@ -489,7 +527,7 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
 int gt_conv_wgrad(const WgradArgs* a, hipStream_t stream) {
   if (a->Cinp % 8 || a->Coutp % 8 || a->pps % 64 || a->n_in < 1 || a->n_in > 4) return -1;
   const int Kdim = a->KH * a->KW * a->Cinp;
-  dim3 grid((Kdim + 63) / 64, a->S, a->G * ((a->Coutp + 63) / 64));
+  dim3 grid((Kdim + (a->part_b ? 8 : 0) + 63) / 64, a->S, a->G * ((a->Coutp + 63) / 64));
   hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
@@ -501,11 +539,12 @@ int gt_pool_fwd(const uint16_t* x, uint16_t* y, int NB, int H, int W, int Cp, hi
   return (int)hipGetLastError();
 }
 
-int gt_pool_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, int NB, int H, int W, int Cp,
+int gt_pool_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, int NB, int H, int W, int Cp, int relu_mask,
                 hipStream_t stream) {
   const long total = (long)NB * H * W * (Cp / 8);
   const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(pool_bwd_kernel, dim3(blocks), dim3(256), 0, stream, x, dy, dx, NB, H, W, Cp);
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(blocks), dim3(256), 0, stream, x, dy, dx, NB, H, W, Cp,
+                     relu_mask);
   return (int)hipGetLastError();
 }
 

@@ -124,7 +124,7 @@ class HipFoldJob(FoldJob):
         for L in self.layers:
             L.w_bf = torch.zeros((G, L.coutp, L.KH, L.KW, L.cinp), dtype=torch.bfloat16, device=dev)
             L.wT_bf = torch.zeros((G, L.cinp, L.KH, L.KW, L.coutp), dtype=torch.bfloat16, device=dev)
-            L.part_w = torch.zeros((L.S, G, L.coutp, L.Kdim), dtype=torch.float32, device=dev)
+            L.part_w = torch.zeros((L.S, G, L.coutp, L.Kdim), dtype=torch.float32, device=dev)  # split-K partials
             L.part_b = torch.zeros((L.S, G, L.coutp), dtype=torch.float32, device=dev)
         self.w1t_bf = torch.zeros((G, self.Up, self.Fp), dtype=torch.bfloat16, device=dev)
         self.gW2 = torch.zeros((G, self.Up, self.classes), dtype=torch.float32, device=dev)
@@ -240,7 +240,15 @@ class HipFoldJob(FoldJob):
         dw.wt, dw.st = self.w1t_bf.data_ptr(), self.state.data_ptr()
         dw.G, dw.B, dw.Fp, dw.Up = G, B, self.Fp, self.Up
         self.dense_wgrad_args = dw
-        # backward
+        # backward: the LAST writer of a ReLU layer's gradient (its first consumer
+        # in forward order) applies the ReLU mask, so every later reader (wgrad,
+        # dgrad) consumes dz = dy * (y > 0) directly
+        first_consumer = {}
+        for st in self.plan.steps:
+            srcs = st.inputs if isinstance(st, ConvSpec) else st.srcs
+            for n in srcs:
+                first_consumer.setdefault(n, st.name)
+        relu_out = {st.name for st in self.plan.steps if isinstance(st, ConvSpec)}
         self.bwd_ops = []
         written = set()
         for st in reversed(self.plan.steps):
@@ -254,7 +262,7 @@ class HipFoldJob(FoldJob):
                 wa.n_in = len(ins)
                 wa.gather = gather_train if first else 0
                 wa.st = self.state.data_ptr()
-                wa.dy, wa.ymask = self.grad[st.name].data_ptr(), self.act[st.name].data_ptr()
+                wa.dz = self.grad[st.name].data_ptr()
                 wa.part_w, wa.part_b = L.part_w.data_ptr(), L.part_b.data_ptr()
                 wa.G, wa.B, wa.H, wa.W = G, B, L.H, L.W
                 wa.Cinp, wa.Coutp, wa.KH, wa.KW, wa.S, wa.pps = L.cinp, L.coutp, L.KH, L.KW, L.S, L.pps
@@ -266,8 +274,10 @@ class HipFoldJob(FoldJob):
                         if n in written:
                             flags |= 1 << i
                         written.add(n)
-                    a = self._conv_args(L, [self.grad[st.name]], outs, flags, L.wT_bf, None, 0,
-                                        mask=self.act[st.name])
+                    a = self._conv_args(L, [self.grad[st.name]], outs, flags, L.wT_bf, None, 0)
+                    for i, n in enumerate(st.inputs):
+                        if n in relu_out and first_consumer[n] == st.name:
+                            a.out_mask[i] = self.act[n].data_ptr()
                     a.Cinp, a.Coutp, a.KH, a.KW, a.TH = L.coutp, L.cinp, L.KH, L.KW, L.TH
                     self.bwd_ops.append(("conv", a, L))
             else:
@@ -277,7 +287,7 @@ class HipFoldJob(FoldJob):
                 written.add(src)
                 hh, ww, cc = self.shapes[src]
                 self.bwd_ops.append(("pool_bwd", (self.act[src], self.grad[st.name], self.grad[src],
-                                                  G * B, hh, ww, cc), None))
+                                                  G * B, hh, ww, cc, int(src in relu_out)), None))
         aa = K.AdamArgs()
         aa.segs, aa.blocks, aa.st = self.adam_segs.data_ptr(), self.adam_blocks.data_ptr(), self.state.data_ptr()
         self.adam_args = aa
@@ -359,8 +369,9 @@ class HipFoldJob(FoldJob):
             elif kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
             else:
-                x, dy, dx, nb, hh, ww, cc = a
-                K.check(L.gt_pool_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), nb, hh, ww, cc, s), "pool_bwd")
+                x, dy, dx, nb, hh, ww, cc, rm = a
+                K.check(L.gt_pool_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), nb, hh, ww, cc, rm, s),
+                        "pool_bwd")
         K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
 
     def evaluate(self):

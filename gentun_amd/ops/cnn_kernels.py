@@ -14,14 +14,15 @@ I = C.c_int
 
 
 class ConvArgs(C.Structure):
-    _fields_ = [("inp", P * 4), ("mask", P), ("gather", P), ("st", P), ("out", P * 4), ("w", P), ("bias", P),
+    _fields_ = [("inp", P * 4), ("mask", P), ("gather", P), ("st", P), ("out", P * 4), ("out_mask", P * 4),
+                ("w", P), ("bias", P),
                 ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
                 ("TH", I)]
 
 
 class WgradArgs(C.Structure):
-    _fields_ = [("inp", P * 4), ("gather", P), ("st", P), ("dy", P), ("ymask", P), ("part_w", P),
+    _fields_ = [("inp", P * 4), ("gather", P), ("st", P), ("dz", P), ("part_w", P),
                 ("part_b", P), ("n_in", I), ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I),
                 ("KH", I), ("KW", I), ("S", I), ("pps", I)]
 
@@ -76,7 +77,7 @@ def lib():
         L.gt_step_begin.restype = I
         L.gt_pool_fwd.argtypes = [P, P, I, I, I, I, P]
         L.gt_pool_fwd.restype = I
-        L.gt_pool_bwd.argtypes = [P, P, P, I, I, I, I, P]
+        L.gt_pool_bwd.argtypes = [P, P, P, I, I, I, I, I, P]
         L.gt_pool_bwd.restype = I
         for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg"):
             getattr(L, name).restype = C.c_size_t
@@ -103,12 +104,17 @@ def conv_tile_rows(H, W):
     return max(1, min(H, 128 // W))
 
 
+def wgrad_blocks(kdim, with_bias=True):
+    """Column blocks of conv_wgrad (the bias rides in an extra ones-chunk)."""
+    return -(-(kdim + (8 if with_bias else 0)) // 64)
+
+
 def wgrad_split(npix, kdim, coutp, G=None, target_blocks=256):
     """(pixels per split, splits) for conv_wgrad: ~``target_blocks``
     workgroups PER FOLD (the split never depends on how many folds share a
     launch, so a fold's gradient summation order -- and its result -- is the
     same alone or batched), 64-pixel K-steps, >= 2 K-steps per workgroup."""
-    nb = -(-kdim // 64)
+    nb = wgrad_blocks(kdim)
     mb = -(-coutp // 64)
     per = max(1, nb * mb)
     S = max(1, min(target_blocks // per, npix // 128))

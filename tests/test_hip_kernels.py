@@ -110,6 +110,8 @@ def test_conv_dgrad_mask_and_accumulate():
     a.inp[0] = dy_p.data_ptr()
     a.mask = y_p.data_ptr()
     a.out[0], a.out[1] = out0.data_ptr(), out1.data_ptr()
+    pmask = bf(torch.randn(G, B, H, W, cinp, device=DEV))
+    a.out_mask[1] = pmask.data_ptr()        # final writer of out1 applies its ReLU mask
     a.n_in, a.n_out, a.acc_flags, a.relu = 1, 2, 2, 0
     a.w, a.bias = wT.data_ptr(), 0
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.TH = G, B, H, W, coutp, cinp, k, k, 4
@@ -119,7 +121,7 @@ def test_conv_dgrad_mask_and_accumulate():
     tol = 2e-2 * ref.abs().max().item()
     assert (got0 - ref).abs().max().item() < tol
     got1 = out1[..., :cin].float().permute(0, 1, 4, 2, 3)
-    ref1 = ref + prev[..., :cin].float().permute(0, 1, 4, 2, 3)
+    ref1 = (ref + prev[..., :cin].float().permute(0, 1, 4, 2, 3)) * (pmask[..., :cin] > 0).permute(0, 1, 4, 2, 3)
     assert (got1 - ref1).abs().max().item() < tol + 2e-2 * ref1.abs().max().item()
 
 
@@ -147,8 +149,7 @@ def test_conv_wgrad(H, W, cin, cout, k, nin, first):
         data[perm] = x_in[0].view(G * B, H, W, cinp)
         gather = perm.view(1, G, B).to(torch.int64).contiguous()
         x_in = [data]
-    dy_p = torch.stack([nhwc_pad(dy[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
-    y_p = torch.stack([nhwc_pad(y[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
+    dz_p = torch.stack([nhwc_pad(dz[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
     Kdim = k * k * cinp
     npix = B * H * W
     pps, S = Km.wgrad_split(npix, Kdim, coutp, target_blocks=16)
@@ -161,7 +162,7 @@ def test_conv_wgrad(H, W, cin, cout, k, nin, first):
     a.n_in = len(x_in)
     a.gather = gather.data_ptr() if gather is not None else 0
     a.st = st.data_ptr()
-    a.dy, a.ymask, a.part_w, a.part_b = dy_p.data_ptr(), y_p.data_ptr(), pw.data_ptr(), pb.data_ptr()
+    a.dz, a.part_w, a.part_b = dz_p.data_ptr(), pw.data_ptr(), pb.data_ptr()
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.S, a.pps = G, B, H, W, cinp, coutp, k, k, S, pps
     Km.check(Km.lib().gt_conv_wgrad(a, stream()), "wgrad")
     torch.cuda.synchronize()
@@ -187,10 +188,13 @@ def test_pool_fwd_bwd(H, W):
     Km.check(Km.lib().gt_pool_fwd(xp.data_ptr(), yp.data_ptr(), N, H, W, cp, stream()), "pool")
     dyp = nhwc_pad(dy, cp).to(torch.bfloat16).contiguous()
     dxp = torch.full((N, H, W, cp), 7.0, dtype=torch.bfloat16, device=DEV)
-    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), dyp.data_ptr(), dxp.data_ptr(), N, H, W, cp, stream()), "poolb")
+    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), dyp.data_ptr(), dxp.data_ptr(), N, H, W, cp, 0, stream()), "poolb")
+    dxm = torch.full((N, H, W, cp), 7.0, dtype=torch.bfloat16, device=DEV)
+    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), dyp.data_ptr(), dxm.data_ptr(), N, H, W, cp, 1, stream()), "poolm")
     torch.cuda.synchronize()
     assert torch.equal(yp[..., :C].float().permute(0, 3, 1, 2), y.detach())
     assert torch.allclose(dxp[..., :C].float().permute(0, 3, 1, 2), xr.grad, atol=1e-6)
+    assert torch.allclose(dxm[..., :C].float().permute(0, 3, 1, 2), xr.grad * (x > 0), atol=1e-6)
 
 
 def test_dense_fwd_dgrad():

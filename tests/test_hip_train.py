@@ -10,8 +10,8 @@ pytestmark = pytest.mark.gpu
 
 def _setup(n=1200, genes=None):
     from gentun_amd.models.genome import make_plan
-    from gentun_amd.utils.data import make_cifar_like, stratified_kfold
-    x, y = make_cifar_like(n=n, seed=3)
+    from gentun_amd.utils.data import make_image_classification, stratified_kfold
+    x, y = make_image_classification(n=n, shape=(32, 32, 3), classes=10, seed=3, noise=0.35, shift=3)
     folds = stratified_kfold(np.argmax(y, 1), 3, seed=0)
     genes = genes or {'S_1': '101', 'S_2': '0101110011'}
     plan = make_plan(genes, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10)

@@ -40,6 +40,12 @@ shapes = [("s1_in 5x5 3->20", 32, 3, 20, 5, 1), ("s1_n 3x3 20->20", 32, 20, 20, 
           ("s1_n sum3", 32, 20, 20, 3, 3), ("s2_in 5x5 20->50", 16, 20, 50, 5, 1),
           ("s2_n 3x3 50->50", 16, 50, 50, 3, 1), ("deep 3x3 128->128 @8", 8, 128, 128, 3, 1)]
 stream = torch.cuda.current_stream().cuda_stream
+only = os.environ.get("GENTUN_BENCH_ONLY")          # "kernel:shape_index" (PMC runs)
+if only:
+    only_k, only_i = only.split(":")
+    shapes = [shapes[int(only_i)]]
+else:
+    only_k = None
 for name, H, cin, cout, k, nin in shapes:
     W = H
     cinp, coutp = pad8(cin), pad8(cout)
@@ -61,20 +67,20 @@ for name, H, cin, cout, k, nin in shapes:
     a.n_in, a.n_out, a.acc_flags, a.relu = nin, 1, 0, 1
     a.w, a.bias, a.st = w.data_ptr(), bias.data_ptr(), st.data_ptr()
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.TH = G, B, H, W, cinp, coutp, k, k, TH
-    us = timeit(lambda: K.check(L.gt_conv_fwd(a, stream), "fwd"))
+    us = timeit(lambda: K.check(L.gt_conv_fwd(a, stream), "fwd")) if only_k in (None, "conv_fwd") else 0.0
     byt = (nin * G * B * H * W * cinp + G * B * H * W * coutp) * 2
-    print(json.dumps({"kernel": "conv_fwd", "shape": name, "us": round(us, 2), "tflops": round(flops / us / 1e6, 2),
-                      "gbs": round(byt / us / 1e3, 1)}), flush=True)
+    print(json.dumps({"kernel": "conv_fwd", "shape": name, "us": round(us, 2), "tflops": round(flops / max(us, 1e-9) / 1e6, 2),
+                      "gbs": round(byt / max(us, 1e-9) / 1e3, 1)}), flush=True)
     # dgrad
     d = K.ConvArgs()
-    d.inp[0], d.mask, d.out[0] = dy.data_ptr(), y.data_ptr(), dx.data_ptr()
+    d.inp[0], d.mask, d.out[0] = dy.data_ptr(), 0, dx.data_ptr()
     d.n_in, d.n_out, d.acc_flags, d.relu = 1, 1, 0, 0
     d.w, d.bias, d.st = wT.data_ptr(), 0, st.data_ptr()
     d.G, d.B, d.H, d.W, d.Cinp, d.Coutp, d.KH, d.KW, d.TH = G, B, H, W, coutp, cinp, k, k, TH
-    us = timeit(lambda: K.check(L.gt_conv_fwd(d, stream), "dgrad"))
+    us = timeit(lambda: K.check(L.gt_conv_fwd(d, stream), "dgrad")) if only_k in (None, "conv_dgrad") else 0.0
     byt = (2 * G * B * H * W * coutp + G * B * H * W * cinp) * 2
-    print(json.dumps({"kernel": "conv_dgrad", "shape": name, "us": round(us, 2), "tflops": round(flops / us / 1e6, 2),
-                      "gbs": round(byt / us / 1e3, 1)}), flush=True)
+    print(json.dumps({"kernel": "conv_dgrad", "shape": name, "us": round(us, 2), "tflops": round(flops / max(us, 1e-9) / 1e6, 2),
+                      "gbs": round(byt / max(us, 1e-9) / 1e3, 1)}), flush=True)
     # wgrad
     npix = B * H * W
     Kdim = k * k * cinp
@@ -85,9 +91,9 @@ for name, H, cin, cout, k, nin in shapes:
     for i, t in enumerate(xs):
         wa.inp[i] = t.data_ptr()
     wa.n_in, wa.gather, wa.st = nin, 0, st.data_ptr()
-    wa.dy, wa.ymask, wa.part_w, wa.part_b = dy.data_ptr(), y.data_ptr(), pw.data_ptr(), pb.data_ptr()
+    wa.dz, wa.part_w, wa.part_b = dy.data_ptr(), pw.data_ptr(), pb.data_ptr()
     wa.G, wa.B, wa.H, wa.W, wa.Cinp, wa.Coutp, wa.KH, wa.KW, wa.S, wa.pps = G, B, H, W, cinp, coutp, k, k, S, pps
-    us = timeit(lambda: K.check(L.gt_conv_wgrad(wa, stream), "wgrad"))
+    us = timeit(lambda: K.check(L.gt_conv_wgrad(wa, stream), "wgrad")) if only_k in (None, "conv_wgrad") else 0.0
     byt = (nin * G * B * H * W * cinp + 2 * G * B * H * W * coutp) * 2 + S * G * coutp * Kdim * 4
-    print(json.dumps({"kernel": "conv_wgrad", "shape": name, "us": round(us, 2), "tflops": round(flops / us / 1e6, 2),
-                      "gbs": round(byt / us / 1e3, 1), "S": S}), flush=True)
+    print(json.dumps({"kernel": "conv_wgrad", "shape": name, "us": round(us, 2), "tflops": round(flops / max(us, 1e-9) / 1e6, 2),
+                      "gbs": round(byt / max(us, 1e-9) / 1e3, 1), "S": S}), flush=True)
