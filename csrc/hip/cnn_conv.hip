@@ -46,6 +46,7 @@ struct ConvArgs {
 #define CF_KB 16                 // weight K-block: 16 chunks of 8 = 128 k
 #define CF_WLD (CF_KB * 8 + 8)    // LDS row stride of a weight block (272 B: conflict-free b128 reads)
 
+template <int PXG>   // 16-pixel groups per wave (tile = 64 * PXG pixels)
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
@@ -151,21 +152,21 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
   const int wave = tid >> 6, lane = tid & 63;
   const int kq = lane >> 4, l16 = lane & 15;
   const int npx = a.TH * a.W;
-  int pbase[2];
-  bool pvalid[2];
-  int pyy[2], pxx[2];
+  int pbase[PXG];
+  bool pvalid[PXG];
+  int pyy[PXG], pxx[PXG];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int pl = wave * 32 + h * 16 + l16;
+  for (int h = 0; h < PXG; ++h) {
+    const int pl = wave * 16 * PXG + h * 16 + l16;
     pyy[h] = pl / a.W; pxx[h] = pl % a.W;
     pvalid[h] = (pl < npx) && (h0 + pyy[h] < a.H);
     pbase[h] = (pyy[h] * PW + pxx[h]) * ncb;
   }
   const int nco = min(64, a.Coutp - co_blk);
   const int NT = (nco + 15) >> 4;
-  f32x4_t acc[2][4];
+  f32x4_t acc[PXG][4];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < PXG; ++h)
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[h][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
@@ -178,17 +179,16 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
       const int c = kb * CF_KB + kk * 4 + kq;
       if (kb * CF_KB + kk * 4 >= nchunks) break;
       const int co_off = coff[c];
-      uint4 bf0 = make_uint4(0, 0, 0, 0), bf1 = make_uint4(0, 0, 0, 0);
-      if (co_off >= 0) {
-        if (pvalid[0]) bf0 = patch[pbase[0] + co_off];
-        if (pvalid[1]) bf1 = patch[pbase[1] + co_off];
-      }
+      uint4 bfr[PXG];
+#pragma unroll
+      for (int h = 0; h < PXG; ++h)
+        bfr[h] = (co_off >= 0 && pvalid[h]) ? patch[pbase[h] + co_off] : make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (t < NT) {
           const uint4 af = *reinterpret_cast<const uint4*>(wcur + (t * 16 + l16) * CF_WLD + (kk * 4 + kq) * 8);
-          acc[0][t] = mfma16(af, bf0, acc[0][t]);
-          acc[1][t] = mfma16(af, bf1, acc[1][t]);
+#pragma unroll
+          for (int h = 0; h < PXG; ++h) acc[h][t] = mfma16(af, bfr[h], acc[h][t]);
         }
       }
     }
@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
 
   // ---- epilogue: bias + relu, 4 channels per lane ---------------------------
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < PXG; ++h) {
     if (!pvalid[h]) continue;
     const long obase = ((((long)g * a.B + b) * a.H + (h0 + pyy[h])) * a.W + pxx[h]) * a.Coutp;
 #pragma unroll
@@ -511,7 +511,7 @@ extern "C" {
 
 int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   if (a->Cinp % 8 || a->Coutp % 8 || a->n_in < 1 || a->n_in > 4 || a->n_out < 1 || a->n_out > 4) return -1;
-  if (a->TH * a->W > 128 || a->TH < 1) return -2;
+  if (a->TH * a->W > 256 || a->TH < 1) return -2;
   const int nth = (a->H + a->TH - 1) / a->TH;
   const size_t total = (size_t)(a->TH + a->KH - 1) * (a->W + a->KW - 1) * (a->Cinp / 8);
   const int nchunks = a->KH * a->KW * (a->Cinp / 8);
@@ -520,7 +520,10 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   const size_t lds = (size_t)(nkb > 1 ? 2 : 1) * wrows * CF_WLD * 2 + total * 16 + 4 * ((size_t)nchunks + 4);
   if (lds > 160 * 1024) return -3;
   dim3 grid(a->B * nth, a->G, (a->Coutp + 63) / 64);
-  hipLaunchKernelGGL(conv_fwd_kernel, grid, dim3(256), lds, stream, *a);
+  if (a->TH * a->W > 128)
+    hipLaunchKernelGGL(conv_fwd_kernel<4>, grid, dim3(256), lds, stream, *a);
+  else
+    hipLaunchKernelGGL(conv_fwd_kernel<2>, grid, dim3(256), lds, stream, *a);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,170 @@
+"""Command line entry points (the reference has none).
+
+    python -m gentun_amd cnn   [--pop 20 --gens 50 --nodes 3,5 ...]   Genetic-CNN search
+    python -m gentun_amd xgb   [--data iris|wine|PATH.csv --target COL]  GBDT hyper-parameter search
+    python -m gentun_amd info                                            build / device summary
+
+Multi-GPU: launch the same command under ``torchrun --nproc-per-node N``;
+rank 0 runs the GA, every rank is an evaluator (RCCL over xGMI). Runs are
+checkpointed per generation with ``--checkpoint-dir`` and resumed with
+``--resume``.
+"""
+
+import argparse
+import json
+import os
+import sys
+
+
+def _ints(s):
+    return tuple(int(v) for v in s.split(",")) if s else ()
+
+
+def _floats(s):
+    return tuple(float(v) for v in s.split(",")) if s else ()
+
+
+def _common(ap):
+    ap.add_argument("--pop", type=int, default=20)
+    ap.add_argument("--gens", type=int, default=10)
+    ap.add_argument("--algorithm", choices=("roulette", "tournament"), default="roulette")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--checkpoint-dir", default=None)
+    ap.add_argument("--resume", default=None, help="checkpoint file or directory to continue from")
+    ap.add_argument("--events", default=None, help="JSONL event log path")
+    ap.add_argument("--streams", type=int, default=4, help="concurrent candidates per GPU")
+
+
+def _device():
+    import torch
+    if torch.cuda.is_available():
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(lr)
+        return torch.device("cuda", lr)
+    return torch.device("cpu")
+
+
+def _run_search(args, species, x, y, extra, maximize):
+    from . import GeneticAlgorithm, RussianRouletteGA
+    from .metrics import EventLog
+    from .parallel import LocalBatchEvaluator, from_env
+    from .parallel.distributed import DistributedPopulation, GentunWorker
+    from .utils import rng
+    device = _device()
+    comm = from_env(device=device)
+    evaluator = LocalBatchEvaluator(device=device, streams=args.streams)
+    if comm.rank != 0:
+        GentunWorker(species, x, y, comm=comm, evaluator=evaluator).work()
+        return None
+    cls = RussianRouletteGA if args.algorithm == "roulette" else GeneticAlgorithm
+    log = EventLog(args.events) if args.events else None
+    if args.resume:
+        def factory(inds):
+            return DistributedPopulation(species, x, y, individual_list=inds, maximize=maximize,
+                                         additional_parameters=extra, comm=comm, evaluator=evaluator)
+        ga = cls.resume(args.resume, species, x, y, population_factory=factory, checkpoint_dir=args.checkpoint_dir,
+                        event_log=log)
+    else:
+        rng.seed(args.seed)
+        pop = DistributedPopulation(species, x, y, size=args.pop, maximize=maximize, additional_parameters=extra,
+                                    comm=comm, evaluator=evaluator)
+        ga = cls(pop, seed=args.seed, checkpoint_dir=args.checkpoint_dir, event_log=log)
+    best = ga.run(args.gens)
+    ga.population.shutdown()
+    out = {"best_fitness": best.get_fitness(), "best_genes": best.get_genes(),
+           "history": [{k: h[k] for k in ("generation", "best_fitness", "evals", "wall_s", "candidates_per_hour")}
+                       for h in ga.history]}
+    print(json.dumps(out, default=str))
+    return out
+
+
+def cmd_cnn(args):
+    from . import GeneticCnnIndividual
+    from .utils.data import make_image_classification
+    shape = _ints(args.input_shape)
+    x, y = make_image_classification(n=args.samples, shape=shape, classes=args.classes, seed=args.data_seed,
+                                     noise=args.noise)
+    nodes = _ints(args.nodes)
+    kernels = _ints(args.kernels)
+    ks = tuple((k, k) for k in _ints(args.kernel_sizes))
+    extra = dict(nodes=nodes, input_shape=shape, kernels_per_layer=kernels, kernel_sizes=ks,
+                 dense_units=args.dense, dropout_probability=args.dropout, classes=args.classes, nfold=args.nfold,
+                 epochs=_ints(args.epochs), learning_rate=_floats(args.lr), batch_size=args.batch, loss=args.loss,
+                 seed=args.seed)
+    return _run_search(args, GeneticCnnIndividual, x, y, extra, maximize=True)
+
+
+def cmd_xgb(args):
+    from . import XgboostIndividual
+    from .utils import data
+    if args.data == "iris":
+        x, y = data.load_iris_xy()
+    elif args.data == "wine":
+        x, y = data.load_wine_quality()
+    elif args.data == "synthetic":
+        x, y = data.make_regression(n=args.rows, f=args.features)
+    else:
+        import pandas as pd
+        df = pd.read_csv(args.data, sep=None, engine="python")
+        y = df.pop(args.target).to_numpy()
+        x = df.to_numpy()
+    extra = dict(nfold=args.nfold, num_boost_round=args.rounds, early_stopping_rounds=args.early_stopping,
+                 objective=args.objective, eval_metric=args.metric,
+                 device="cuda:{}".format(os.environ.get("LOCAL_RANK", "0")) if args.gpu else None)
+    return _run_search(args, XgboostIndividual, x, y, extra, maximize=False)
+
+
+def cmd_info(_args):
+    import torch
+    from .ops import _lib
+    info = {"torch": torch.__version__, "hip": getattr(torch.version, "hip", None),
+            "gpu": torch.cuda.is_available()}
+    libs = _lib.load_all(require_gpu=False)
+    info["native"] = sorted(libs)
+    if torch.cuda.is_available():
+        info["device"] = torch.cuda.get_device_name(0)
+    print(json.dumps(info))
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="python -m gentun_amd")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    c = sub.add_parser("cnn", help="Genetic-CNN architecture search")
+    _common(c)
+    c.add_argument("--nodes", default="3,5")
+    c.add_argument("--kernels", default="20,50")
+    c.add_argument("--kernel-sizes", default="5,5")
+    c.add_argument("--input-shape", default="32,32,3")
+    c.add_argument("--classes", type=int, default=10)
+    c.add_argument("--samples", type=int, default=10000)
+    c.add_argument("--noise", type=float, default=1.2)
+    c.add_argument("--data-seed", type=int, default=0)
+    c.add_argument("--dense", type=int, default=500)
+    c.add_argument("--dropout", type=float, default=0.5)
+    c.add_argument("--nfold", type=int, default=5)
+    c.add_argument("--epochs", default="20,4,1")
+    c.add_argument("--lr", default="1e-3,1e-4,1e-5")
+    c.add_argument("--batch", type=int, default=32)
+    c.add_argument("--loss", choices=("bce_compat", "ce"), default="bce_compat")
+    c.set_defaults(fn=cmd_cnn)
+    x = sub.add_parser("xgb", help="GBDT (XGBoost-style) hyper-parameter search")
+    _common(x)
+    x.add_argument("--data", default="iris", help="iris | wine | synthetic | path to a CSV")
+    x.add_argument("--target", default="quality")
+    x.add_argument("--rows", type=int, default=100000)
+    x.add_argument("--features", type=int, default=32)
+    x.add_argument("--nfold", type=int, default=5)
+    x.add_argument("--rounds", type=int, default=5000)
+    x.add_argument("--early-stopping", type=int, default=100)
+    x.add_argument("--objective", default="reg:linear")
+    x.add_argument("--metric", default="rmse")
+    x.add_argument("--gpu", action="store_true", help="run the GBDT histograms on the GPU")
+    x.set_defaults(fn=cmd_xgb)
+    i = sub.add_parser("info", help="build / device summary")
+    i.set_defaults(fn=cmd_info)
+    args = ap.parse_args(argv)
+    return args.fn(args)
+
+
+if __name__ == "__main__":
+    sys.exit(0 if main() is not None or True else 1)

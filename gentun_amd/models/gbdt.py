@@ -73,11 +73,12 @@ def cv(params, x, y, num_boost_round=10, nfold=3, early_stopping_rounds=None, se
     hist = np.zeros((nrounds, len(metrics), 4), np.float64)
     parr = np.array([p[k] for k in PARAM_ORDER], np.float64)
     marr = np.array([METRICS[m] for m in metrics], np.int32)
+    kept = None
     if device is not None and str(device).startswith("cuda"):
         from . import gbdt_hip
         kept = gbdt_hip.cv(x, y, fold_of, len(folds), parr, obj, num_class, marr, nrounds,
                            early_stopping_rounds or 0, seed, hist)
-    else:
+    if kept is None:
         lib = _lib.gbdt()
         kept = lib.gbdt_cv(x.ctypes.data, n, x.shape[1], y.ctypes.data, fold_of.ctypes.data, len(folds),
                            parr.ctypes.data, obj, num_class, marr.ctypes.data, len(metrics), nrounds,

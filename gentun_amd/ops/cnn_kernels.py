@@ -97,11 +97,15 @@ def ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
 
 
-def conv_tile_rows(H, W):
-    """Output rows per conv_fwd workgroup: up to 128 pixels (4 waves x 32)."""
-    if W > 128:
-        raise ValueError("image width > 128 not supported by conv_fwd tiles")
-    return max(1, min(H, 128 // W))
+CONV_TILE_PIXELS = 128   # 256-pixel tiles measured slower on every layer (profiles/bench_kernels_tiles.log)
+
+
+def conv_tile_rows(H, W, tile_pixels=None):
+    """Output rows per conv_fwd workgroup: up to 256 pixels (4 waves x 64)."""
+    tp = tile_pixels or CONV_TILE_PIXELS
+    if W > tp:
+        raise ValueError("image width > {} not supported by conv_fwd tiles".format(tp))
+    return max(1, min(H, tp // W))
 
 
 def wgrad_blocks(kdim, with_bias=True):

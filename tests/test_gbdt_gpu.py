@@ -1,0 +1,36 @@
+"""HIP GBDT path (histogram / split / partition / predict kernels) against
+the CPU engine on the same folds."""
+
+import numpy as np
+import pytest
+
+from gentun_amd.models import gbdt
+from gentun_amd.utils.data import load_iris_xy, make_regression
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("params", [
+    {'objective': 'reg:linear', 'eta': 0.3, 'max_depth': 4},
+    {'objective': 'reg:linear', 'eta': 0.1, 'max_depth': 6, 'lambda': 3.0, 'alpha': 0.5, 'gamma': 0.1,
+     'min_child_weight': 5, 'max_delta_step': 2},
+    {'objective': 'reg:linear', 'eta': 0.2, 'max_depth': 5, 'subsample': 0.8, 'colsample_bytree': 0.7,
+     'colsample_bylevel': 0.8},
+])
+def test_hip_matches_cpu_regression(params):
+    x, y = make_regression(n=20000, f=16, seed=4)
+    cpu = gbdt.cv(params, x, y, num_boost_round=40, nfold=3, seed=0)
+    gpu = gbdt.cv(params, x, y, num_boost_round=40, nfold=3, seed=0, device="cuda:0")
+    a, b = np.array(cpu['test-rmse-mean']), np.array(gpu['test-rmse-mean'])
+    assert len(a) == len(b)
+    assert np.max(np.abs(a - b) / a) < 0.02, (a[-5:], b[-5:])
+
+
+def test_hip_binary_logistic_and_early_stopping():
+    x, y = load_iris_xy()
+    yb = (y == 2).astype(np.float64)
+    p = {'objective': 'binary:logistic', 'eval_metric': 'logloss', 'max_depth': 3}
+    cpu = gbdt.cv(p, x, yb, num_boost_round=200, nfold=5, early_stopping_rounds=10)
+    gpu = gbdt.cv(p, x, yb, num_boost_round=200, nfold=5, early_stopping_rounds=10, device="cuda:0")
+    assert abs(cpu['test-logloss-mean'][-1] - gpu['test-logloss-mean'][-1]) < 0.03
+    assert gpu['test-logloss-mean'][-1] == min(gpu['test-logloss-mean'])
