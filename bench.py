@@ -31,7 +31,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--per-gpu", type=int, default=4, help="candidates per GPU per generation")
+    ap.add_argument("--per-gpu", type=int, default=8, help="candidates per GPU per generation")
     ap.add_argument("--streams", type=int, default=4, help="concurrent candidates per GPU")
     ap.add_argument("--backend", default=None, help="hip (default on GPU) or torch")
     ap.add_argument("--epochs", default="20,4,1")

@@ -24,6 +24,7 @@
 
 #include "common.h"
 
+#define HEAD_MAXC_FWD 16
 #define ADAM_B1 0.9f
 #define ADAM_B2 0.999f
 #define ADAM_EPS 1e-7f
@@ -44,12 +45,15 @@ struct DenseFwdArgs {
   const uint16_t* wt;      // [G][Up][Fp] bf16 (transposed copy of W1)
   const float* bias;       // [G][Up]
   uint16_t* out;           // [G][B][Up]
+  const float* w2;         // [G][Up][C] fp32: dense2 weights (fused partial logits)
+  float* plog;             // [G][Up/16][B][C] partial logits of this 16-unit tile (fixed-order sum later)
   const StepState* st;
   const int* fold_ids;     // [G]
   int G, B, Fp, Up;
   float drop_p;
   int train;
   unsigned seed;
+  int C;
 };
 
 // grid (Up/16, ceil(B/32), G): one 16-unit x 32-row tile per workgroup, the
@@ -91,27 +95,48 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
   for (int w = 0; w < 3; ++w) { acc[0] += red[w][0][lane]; acc[1] += red[w][1][lane]; }
   // D[row = unit][col = batch row]
   const int u0 = u_t + kq * 4;
-  if (u0 >= a.Up) return;
+  const bool uok = u0 < a.Up;
   const float keep_scale = 1.0f / (1.0f - a.drop_p);
   const uint32_t thr = (uint32_t)(a.drop_p * 4294967296.0);
   const int gstep = a.st ? a.st->global_step : 0;
   const uint32_t fid = a.fold_ids ? (uint32_t)a.fold_ids[g] : (uint32_t)g;
+  const int C = a.C;
+  const float* w2 = a.w2 + ((long)g * a.Up + u0) * C;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int row = b0 + h * 16 + l16;
-    if (row >= a.B) continue;
-    float v[4];
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (uok && row < a.B) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float z = acc[h][i] + a.bias[(long)g * a.Up + u0 + i];
-      z = fmaxf(z, 0.f);
-      if (a.train && a.drop_p > 0.f) {
-        const uint32_t r = hash4(a.seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)row, (uint32_t)(u0 + i));
-        z = (r >= thr) ? z * keep_scale : 0.f;
+      for (int i = 0; i < 4; ++i) {
+        float z = acc[h][i] + a.bias[(long)g * a.Up + u0 + i];
+        z = fmaxf(z, 0.f);
+        if (a.train && a.drop_p > 0.f) {
+          const uint32_t r = hash4(a.seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)row, (uint32_t)(u0 + i));
+          z = (r >= thr) ? z * keep_scale : 0.f;
+        }
+        v[i] = bf2f(f2bf(z));      // the head sees exactly the stored bf16 activation
       }
-      v[i] = z;
+      *reinterpret_cast<uint2*>(a.out + ((long)g * a.B + row) * a.Up + u0) = pack4(v);
     }
-    *reinterpret_cast<uint2*>(a.out + ((long)g * a.B + row) * a.Up + u0) = pack4(v);
+    if (a.plog == nullptr) continue;
+    // partial logits of this 16-unit tile: 4 units per lane, reduced over the 4 lane groups
+    float pl[HEAD_MAXC_FWD];
+#pragma unroll
+    for (int c = 0; c < HEAD_MAXC_FWD; ++c) {
+      float t = 0.f;
+      if (c < C && uok) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t += v[i] * w2[i * C + c];
+      }
+      t += __shfl_xor(t, 16);
+      t += __shfl_xor(t, 32);
+      pl[c] = t;
+    }
+    if (kq == 0 && row < a.B) {
+      float* dst = a.plog + (((long)g * (a.Up / 16) + blockIdx.x) * a.B + row) * C;
+      for (int c = 0; c < C; ++c) dst[c] = pl[c];
+    }
   }
 }
 
@@ -129,6 +154,7 @@ struct HeadArgs {
   float* gb1;              // [G][Up]
   float* eval_out;         // eval mode: [G][B][3] (loss, binary-correct, categorical-correct)
   float* dz;               // [G][B][C] logits gradient workspace
+  const float* plog;       // [G][Up/16][B][C] partial logits from dense_fwd
   int G, B, Up, C;
   int loss_ce;             // 0 = bce_compat, 1 = ce
   float drop_scale;        // 1/(1-p)
@@ -138,46 +164,27 @@ struct HeadArgs {
 #define HEAD_MAXB 64
 #define HEAD_MAXC 16
 
-// (1) one 64-thread workgroup per (fold, sample): logits -> softmax -> loss
-//     gradient dz (train) or per-sample loss/accuracies (eval).
+// (1) one thread per (fold, sample): logits = b2 + fixed-order sum of the
+//     dense_fwd partial logits, softmax -> loss gradient dz (train) or the
+//     per-sample loss / accuracies (eval).
 __global__ void __launch_bounds__(64) head_fwd_kernel(HeadArgs a) {
-  __shared__ float part[64][HEAD_MAXC + 1];
-  const int g = blockIdx.y, b = blockIdx.x, lane = threadIdx.x;
-  const int Up = a.Up, C = a.C;
-  const uint16_t* h = a.h + ((long)g * a.B + b) * Up;
-  const float* w2 = a.w2 + (long)g * Up * C;
-  float acc[HEAD_MAXC];
-#pragma unroll
-  for (int c = 0; c < HEAD_MAXC; ++c) acc[c] = 0.f;
-  for (int u = lane; u < Up; u += 64) {
-    const float hv = bf2f(h[u]);
-    if (hv != 0.f) {
-      const float* wr = w2 + (long)u * C;
-#pragma unroll
-      for (int c = 0; c < HEAD_MAXC; ++c) if (c < C) acc[c] += hv * wr[c];
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < HEAD_MAXC; ++c) part[lane][c] = acc[c];
-  __syncthreads();
-  if (lane < C) {
-    float s = a.b2[(long)g * C + lane];
-    for (int l = 0; l < 64; ++l) s += part[l][lane];
-    part[0][HEAD_MAXC] = 0.f;
-    acc[0] = s;
-  }
-  __syncthreads();
-  if (lane < C) part[lane][0] = acc[0];   // logits now in part[c][0]
-  __syncthreads();
-  if (lane != 0) return;
+  const int idx = blockIdx.x * 64 + threadIdx.x;
+  if (idx >= a.G * a.B) return;
+  const int g = idx / a.B, b = idx % a.B;
+  const int C = a.C, nt = a.Up / 16;
+  float logit[HEAD_MAXC];
+  for (int c = 0; c < C; ++c) logit[c] = a.b2[(long)g * C + c];
+  const float* pl = a.plog + ((long)g * nt * a.B + b) * C;
+  for (int t = 0; t < nt; ++t)
+    for (int c = 0; c < C; ++c) logit[c] += pl[(long)t * a.B * C + c];
   const int step = a.st ? a.st->cur_step : 0;
   const long sid = a.gather[((long)step * a.G + g) * a.B + b];
   const int y = (int)a.labels[sid];
   float p[HEAD_MAXC];
   float mx = -INFINITY;
-  for (int c = 0; c < C; ++c) mx = fmaxf(mx, part[c][0]);
+  for (int c = 0; c < C; ++c) mx = fmaxf(mx, logit[c]);
   float z = 0.f;
-  for (int c = 0; c < C; ++c) { p[c] = expf(part[c][0] - mx); z += p[c]; }
+  for (int c = 0; c < C; ++c) { p[c] = expf(logit[c] - mx); z += p[c]; }
   int arg = 0;
   float loss = 0.f, binc = 0.f;
   for (int c = 0; c < C; ++c) {
@@ -447,7 +454,7 @@ int gt_step_begin(StepState* s, hipStream_t stream) {
 }
 
 int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
-  if (a->Fp % 8 || a->Up % 64) return -1;
+  if (a->Fp % 8 || a->Up % 64 || a->C > HEAD_MAXC_FWD) return -1;
   dim3 grid(a->Up / 16, (a->B + 31) / 32, a->G);
   hipLaunchKernelGGL(dense_fwd_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
@@ -455,7 +462,8 @@ int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
 
 int gt_head(const HeadArgs* a, hipStream_t stream) {
   if (a->B > HEAD_MAXB || a->C > HEAD_MAXC) return -1;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(a->B, a->G), dim3(64), 0, stream, *a);
+  if (a->Up % 16) return -2;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3((a->G * a->B + 63) / 64), dim3(64), 0, stream, *a);
   if (!a->eval) hipLaunchKernelGGL(head_bwd_kernel, dim3((a->Up + 63) / 64, a->G), dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }

@@ -97,6 +97,7 @@ class HipFoldJob(FoldJob):
         self.hdrop = torch.zeros((G, B, self.Up), dtype=torch.bfloat16, device=dev)
         self.dH = torch.zeros((G, B, self.Up), dtype=torch.float32, device=dev)
         self.dz_head = torch.zeros((G, B, plan.classes), dtype=torch.float32, device=dev)
+        self.plog = torch.zeros((G, self.Up // 16, B, plan.classes), dtype=torch.float32, device=dev)
         # ---- parameters (flat fp32 master + Adam moments) --------------------
         segs = []
         for L in self.layers:
@@ -217,6 +218,7 @@ class HipFoldJob(FoldJob):
         df.st, df.fold_ids = self.state.data_ptr(), self.fold_ids_t.data_ptr()
         df.G, df.B, df.Fp, df.Up = G, B, self.Fp, self.Up
         df.drop_p, df.train, df.seed = self.cfg.dropout, 1, self.drop_seed
+        df.w2, df.plog, df.C = self.views["W2"][0].data_ptr(), self.plog.data_ptr(), self.classes
         self.dense_fwd_args = df
         hd = K.HeadArgs()
         hd.h, hd.w2, hd.b2 = self.hdrop.data_ptr(), self.views["W2"][0].data_ptr(), self.views["b2"][0].data_ptr()
@@ -224,6 +226,7 @@ class HipFoldJob(FoldJob):
         hd.dH, hd.gw2, hd.gb2, hd.gb1 = self.dH.data_ptr(), self.gW2.data_ptr(), self.gb2.data_ptr(), self.gb1.data_ptr()
         hd.eval_out = 0
         hd.dz = self.dz_head.data_ptr()
+        hd.plog = self.plog.data_ptr()
         hd.G, hd.B, hd.Up, hd.C = G, B, self.Up, self.classes
         hd.loss_ce = 1 if self.cfg.loss == "ce" else 0
         hd.drop_scale = 1.0 / (1.0 - self.cfg.dropout) if self.cfg.dropout < 1 else 0.0

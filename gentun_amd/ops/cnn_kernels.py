@@ -28,14 +28,14 @@ class WgradArgs(C.Structure):
 
 
 class DenseFwdArgs(C.Structure):
-    _fields_ = [("x", P), ("wt", P), ("bias", P), ("out", P), ("st", P), ("fold_ids", P),
+    _fields_ = [("x", P), ("wt", P), ("bias", P), ("out", P), ("w2", P), ("plog", P), ("st", P), ("fold_ids", P),
                 ("G", I), ("B", I), ("Fp", I), ("Up", I), ("drop_p", C.c_float), ("train", I),
-                ("seed", C.c_uint)]
+                ("seed", C.c_uint), ("C", I)]
 
 
 class HeadArgs(C.Structure):
     _fields_ = [("h", P), ("w2", P), ("b2", P), ("labels", P), ("gather", P), ("st", P), ("dH", P),
-                ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P), ("dz", P),
+                ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P), ("dz", P), ("plog", P),
                 ("G", I), ("B", I), ("Up", I), ("C", I), ("loss_ce", I), ("drop_scale", C.c_float), ("eval", I)]
 
 

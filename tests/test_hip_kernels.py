@@ -214,7 +214,14 @@ def test_dense_fwd_dgrad():
     a.x, a.wt, a.bias, a.out, a.st, a.fold_ids = xb.data_ptr(), wt.data_ptr(), b1.data_ptr(), out.data_ptr(), \
         st.data_ptr(), 0
     a.G, a.B, a.Fp, a.Up, a.drop_p, a.train, a.seed = G, B, Fp, Up, 0.5, 0, 1
+    Cc = 10
+    w2 = torch.randn(G, Up, Cc, device=DEV) * 0.05
+    plog = torch.zeros(G, Up // 16, B, Cc, device=DEV)
+    a.w2, a.plog, a.C = w2.data_ptr(), plog.data_ptr(), Cc
     Km.check(Km.lib().gt_dense_fwd(a, stream()), "dense")
+    torch.cuda.synchronize()
+    reflog = torch.einsum("gbu,guc->gbc", out.float(), w2)
+    assert torch.allclose(plog.sum(1), reflog, rtol=1e-4, atol=1e-4)
     # dropout statistics in train mode
     out2 = torch.zeros_like(out)
     a.out, a.train = out2.data_ptr(), 1
@@ -302,6 +309,9 @@ def test_head(loss):
     dzw = torch.zeros(G, B, C, device=DEV)
     a.dH, a.gw2, a.gb2, a.gb1, a.eval_out = dH.data_ptr(), gw2.data_ptr(), gb2.data_ptr(), gb1.data_ptr(), 0
     a.dz = dzw.data_ptr()
+    plog = torch.einsum("gbu,guc->gbc", h, w2).unsqueeze(1).contiguous()   # one "tile" holding the full sum
+    plog = torch.cat([plog, torch.zeros(G, Up // 16 - 1, B, C, device=DEV)], 1).contiguous()
+    a.plog = plog.data_ptr()
     a.G, a.B, a.Up, a.C, a.loss_ce, a.drop_scale, a.eval = G, B, Up, C, int(loss == "ce"), 2.0, 0
     Km.check(Km.lib().gt_head(a, stream()), "head")
     ev = torch.zeros(G, B, 3, device=DEV)
