@@ -522,8 +522,10 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   dim3 grid(a->B * nth, a->G, (a->Coutp + 63) / 64);
   if (a->TH * a->W > 128)
     hipLaunchKernelGGL(conv_fwd_kernel<4>, grid, dim3(256), lds, stream, *a);
-  else
+  else if (a->TH * a->W > 64)
     hipLaunchKernelGGL(conv_fwd_kernel<2>, grid, dim3(256), lds, stream, *a);
+  else
+    hipLaunchKernelGGL(conv_fwd_kernel<1>, grid, dim3(256), lds, stream, *a);
   return (int)hipGetLastError();
 }
 

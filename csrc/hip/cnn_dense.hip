@@ -164,19 +164,31 @@ struct HeadArgs {
 #define HEAD_MAXB 64
 #define HEAD_MAXC 16
 
-// (1) one thread per (fold, sample): logits = b2 + fixed-order sum of the
-//     dense_fwd partial logits, softmax -> loss gradient dz (train) or the
-//     per-sample loss / accuracies (eval).
+// (1) one 64-lane wave per (fold, sample): lane t loads the partial logits of
+//     dense_fwd tile t, a shuffle tree sums them (fixed order), lane 0 adds b2
+//     and does softmax -> loss gradient dz (train) or per-sample loss /
+//     accuracies (eval).
 __global__ void __launch_bounds__(64) head_fwd_kernel(HeadArgs a) {
-  const int idx = blockIdx.x * 64 + threadIdx.x;
-  if (idx >= a.G * a.B) return;
+  const int idx = blockIdx.x, lane = threadIdx.x;
   const int g = idx / a.B, b = idx % a.B;
   const int C = a.C, nt = a.Up / 16;
-  float logit[HEAD_MAXC];
-  for (int c = 0; c < C; ++c) logit[c] = a.b2[(long)g * C + c];
+  float acc[HEAD_MAXC];
   const float* pl = a.plog + ((long)g * nt * a.B + b) * C;
-  for (int t = 0; t < nt; ++t)
-    for (int c = 0; c < C; ++c) logit[c] += pl[(long)t * a.B * C + c];
+#pragma unroll
+  for (int c = 0; c < HEAD_MAXC; ++c) acc[c] = 0.f;
+  for (int t = lane; t < nt; t += 64) {
+#pragma unroll
+    for (int c = 0; c < HEAD_MAXC; ++c) if (c < C) acc[c] += pl[(long)t * a.B * C + c];
+  }
+#pragma unroll
+  for (int c = 0; c < HEAD_MAXC; ++c) {
+    if (c >= C) break;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+  }
+  if (lane != 0) return;
+  float logit[HEAD_MAXC];
+  for (int c = 0; c < C; ++c) logit[c] = acc[c] + a.b2[(long)g * C + c];
   const int step = a.st ? a.st->cur_step : 0;
   const long sid = a.gather[((long)step * a.G + g) * a.B + b];
   const int y = (int)a.labels[sid];
@@ -463,7 +475,7 @@ int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
 int gt_head(const HeadArgs* a, hipStream_t stream) {
   if (a->B > HEAD_MAXB || a->C > HEAD_MAXC) return -1;
   if (a->Up % 16) return -2;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3((a->G * a->B + 63) / 64), dim3(64), 0, stream, *a);
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(a->G * a->B), dim3(64), 0, stream, *a);
   if (!a->eval) hipLaunchKernelGGL(head_bwd_kernel, dim3((a->Up + 63) / 64, a->G), dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }

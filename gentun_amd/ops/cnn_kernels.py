@@ -101,7 +101,10 @@ CONV_TILE_PIXELS = 128   # 256-pixel tiles measured slower on every layer (profi
 
 
 def conv_tile_rows(H, W, tile_pixels=None):
-    """Output rows per conv_fwd workgroup: up to 256 pixels (4 waves x 64)."""
+    """Output rows per conv_fwd workgroup (tiles of 64 / 128 / 256 pixels =
+    4 waves x 16 / 32 / 64). 128 is the measured optimum for every layer of the
+    S=(3,5) space (profiles/conv_tiles.json: 64-pixel tiles are 1.3-2.8x
+    slower even when they double the grid)."""
     tp = tile_pixels or CONV_TILE_PIXELS
     if W > tp:
         raise ValueError("image width > {} not supported by conv_fwd tiles".format(tp))
@@ -113,7 +116,7 @@ def wgrad_blocks(kdim, with_bias=True):
     return -(-(kdim + (8 if with_bias else 0)) // 64)
 
 
-def wgrad_split(npix, kdim, coutp, G=None, target_blocks=256):
+def wgrad_split(npix, kdim, coutp, G=None, target_blocks=200):
     """(pixels per split, splits) for conv_wgrad: ~``target_blocks``
     workgroups PER FOLD (the split never depends on how many folds share a
     launch, so a fold's gradient summation order -- and its result -- is the
