@@ -138,7 +138,7 @@ def run(args):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (CIFAR-10-shaped 10k x 32x32x3, learnable class templates; random-init weights)",
+        "data": "synthetic (CIFAR-10-shaped 10k x 32x32x3 coloured stroke glyphs + clutter + noise; random-init weights)",
         "config": {"model": "Genetic-CNN S=(3,5) kernels (20,50) dense 500", "global_batch": 32 * args.nfold,
                    "seq_len": None, "parallelism": "population-dp{}".format(comm.world_size),
                    "candidates_per_step": P, "per_gpu": args.per_gpu, "nfold": args.nfold,

@@ -46,8 +46,12 @@ struct ConvArgs {
 #define CF_KB 16                 // weight K-block: 16 chunks of 8 = 128 k
 #define CF_WLD (CF_KB * 8 + 8)    // LDS row stride of a weight block (272 B: conflict-free b128 reads)
 
+#ifndef CF_WPE
+#define CF_WPE 5   // minimum waves per SIMD the register allocator must allow
+#endif
+
 template <int PXG>   // 16-pixel groups per wave (tile = 64 * PXG pixels)
-__global__ void __launch_bounds__(256) conv_fwd_kernel(ConvArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG == 4 ? 3 : CF_WPE))) conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int nth = (a.H + a.TH - 1) / a.TH;

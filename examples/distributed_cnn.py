@@ -1,0 +1,35 @@
+#!/usr/bin/env python
+"""Distributed Genetic CNN (reference tests/mnist_master.py + mnist_worker.py),
+one evaluator rank per MI355X:
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/distributed_cnn.py
+"""
+import _common
+
+if __name__ == "__main__":
+    import torch
+
+    from gentun import DistributedPopulation, GeneticCnnIndividual, GentunWorker, RussianRouletteGA
+    from gentun_amd import LocalBatchEvaluator
+    from gentun_amd.parallel import from_env
+
+    x_train, y_train = _common.mnist_like()
+    device = None
+    if torch.cuda.is_available():
+        import os
+        device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(device)
+    comm = from_env(device=device)
+    evaluator = LocalBatchEvaluator(device=device, streams=4)
+    if comm.rank == 0:
+        pop = DistributedPopulation(
+            GeneticCnnIndividual, x_train, y_train, size=20, crossover_rate=0.3, mutation_rate=0.1,
+            additional_parameters={
+                'nfold': 5, 'epochs': (20, 4, 1), 'learning_rate': (1e-3, 1e-4, 1e-5), 'batch_size': 32
+            }, maximize=True, comm=comm, evaluator=evaluator
+        )
+        ga = RussianRouletteGA(pop, crossover_probability=0.2, mutation_probability=0.8)
+        ga.run(50)
+        pop.shutdown()
+    else:
+        GentunWorker(GeneticCnnIndividual, x_train, y_train, comm=comm, evaluator=evaluator).work()

@@ -80,9 +80,9 @@ def _run_search(args, species, x, y, extra, maximize):
 
 def cmd_cnn(args):
     from . import GeneticCnnIndividual
-    from .utils.data import make_image_classification
+    from .utils.data import make_glyph_classification
     shape = _ints(args.input_shape)
-    x, y = make_image_classification(n=args.samples, shape=shape, classes=args.classes, seed=args.data_seed,
+    x, y = make_glyph_classification(n=args.samples, shape=shape, classes=args.classes, seed=args.data_seed,
                                      noise=args.noise)
     nodes = _ints(args.nodes)
     kernels = _ints(args.kernels)
@@ -137,7 +137,7 @@ def main(argv=None):
     c.add_argument("--input-shape", default="32,32,3")
     c.add_argument("--classes", type=int, default=10)
     c.add_argument("--samples", type=int, default=10000)
-    c.add_argument("--noise", type=float, default=1.2)
+    c.add_argument("--noise", type=float, default=1.0)
     c.add_argument("--data-seed", type=int, default=0)
     c.add_argument("--dense", type=int, default=500)
     c.add_argument("--dropout", type=float, default=0.5)

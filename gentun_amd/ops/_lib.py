@@ -65,8 +65,18 @@ def gbdt():
 
 
 def hip():
-    """The gfx950 kernel library (raises if it cannot be loaded)."""
+    """The gfx950 kernel library (raises if it cannot be loaded).
+    ``GENTUN_HIP_LIB`` points at an alternative build (kernel tuning runs)."""
+    alt = os.environ.get("GENTUN_HIP_LIB")
+    if alt:
+        global _ALT
+        if _ALT is None:
+            _ALT = ctypes.CDLL(os.path.abspath(alt))
+        return _ALT
     return load("libgentun_hip.so")
+
+
+_ALT = None
 
 
 def load_all(require_gpu=False):

@@ -14,6 +14,7 @@ import torch
 from gentun_amd.ops import cnn_kernels as K
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+TILES = tuple(int(t) for t in os.environ.get("GENTUN_TILES", "128").split(","))
 dev = torch.device("cuda", 0)
 L = K.lib()
 G, B = 5, 32
@@ -67,7 +68,7 @@ for name, H, cin, cout, k, nin in shapes:
     a.n_in, a.n_out, a.acc_flags, a.relu = nin, 1, 0, 1
     a.w, a.bias, a.st = w.data_ptr(), bias.data_ptr(), st.data_ptr()
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.TH = G, B, H, W, cinp, coutp, k, k, TH
-    for tp in (64, 128):
+    for tp in TILES:
         a.TH = K.conv_tile_rows(H, W, tp)
         us = timeit(lambda: K.check(L.gt_conv_fwd(a, stream), "fwd")) if only_k in (None, "conv_fwd") else 0.0
         byt = (nin * G * B * H * W * cinp + G * B * H * W * coutp) * 2
@@ -80,7 +81,7 @@ for name, H, cin, cout, k, nin in shapes:
     d.n_in, d.n_out, d.acc_flags, d.relu = 1, 1, 0, 0
     d.w, d.bias, d.st = wT.data_ptr(), 0, st.data_ptr()
     d.G, d.B, d.H, d.W, d.Cinp, d.Coutp, d.KH, d.KW, d.TH = G, B, H, W, coutp, cinp, k, k, TH
-    for tp in (64, 128):
+    for tp in TILES:
         d.TH = K.conv_tile_rows(H, W, tp)
         us = timeit(lambda: K.check(L.gt_conv_fwd(d, stream), "dgrad")) if only_k in (None, "conv_dgrad") else 0.0
         byt = (2 * G * B * H * W * coutp + G * B * H * W * cinp) * 2

@@ -21,8 +21,8 @@ from gentun_amd.utils.data import make_cifar_like, stratified_kfold
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--noise", type=float, default=1.2)
-    ap.add_argument("--shift", type=int, default=4)
+    ap.add_argument("--noise", type=float, default=1.0)
+    ap.add_argument("--shift", type=int, default=5)
     ap.add_argument("--epochs", default="20,4,1")
     ap.add_argument("--lr", default="1e-3,1e-4,1e-5")
     ap.add_argument("--genes", default="S_1=101,S_2=0101110011")
