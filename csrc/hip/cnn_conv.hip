@@ -240,6 +240,446 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
 }
 
 // ---------------------------------------------------------------------------
+// conv_fwd, LDS-DMA variant (single-input, unmasked layers: most of the DAG)
+// ---------------------------------------------------------------------------
+// The register-staged kernel above is latency-bound: a workgroup walks a chain
+// of dependent global round trips (patch slots, then weight block k+1 behind
+// block k, then bias), and only ~1-5 workgroups per CU exist to hide them.
+// Here every byte reaches LDS through global_load_lds_dwordx4 (no VGPR
+// destination), so the whole patch and the first two weight blocks are in
+// flight at once and the workgroup waits for ONE latency before its MFMAs.
+//   * LDS images are lane-linear (a wave-instruction writes 1 KiB
+//     contiguously); weight rows are 256 B unpadded and XOR-swizzled through
+//     the SOURCE address (chunk c of row r lands at slot c ^ (r & 15)), so the
+//     16 rows an A-fragment read touches hit 16 different bank groups.
+//   * Padding pixels / rows / chunks read a 16-byte zero line.
+//   * Weight blocks > 1 stream through a 2-deep ring with counted vmcnt waits
+//     and raw s_barrier (a __syncthreads() would drain the prefetch).
+
+__device__ __attribute__((aligned(16))) uint4 g_zero16[4];
+
+typedef __attribute__((address_space(1))) const void gvoid_t;
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)lds_wave_base, 16, 0, 0);
+}
+
+// wait until at most n (0..4) LDS-DMA / vector loads of this wave are outstanding
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+// Weight-ring depth: as many 16-chunk blocks as the LDS share of one workgroup
+// allows when the grid needs ceil(nwg / 256) workgroups resident per CU (the
+// s2 / deep layers launch only ~1-2 workgroups per CU, so they can keep every
+// block -- or most of them -- resident and issue all weight DMAs at once).
+__host__ __device__ inline int conv_glds_nbuf(int nkb, int wblk, int fixed_bytes, long nwg) {
+  long per_cu = (nwg + 255) / 256;
+  if (per_cu < 1) per_cu = 1;
+  if (per_cu > 8) per_cu = 8;
+  const long budget = 160L * 1024 / per_cu - 1024 - fixed_bytes;
+  long nb = budget / wblk;
+  if (nb > nkb) nb = nkb;
+  if (nb < 2) nb = nkb < 2 ? nkb : 2;
+  return (int)nb;
+}
+
+__device__ __forceinline__ unsigned long long rt_stamp() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  return t;
+}
+
+// STAMP (diagnostic build only): per workgroup realtime stamps (100 MHz) at
+// entry / operands staged / MFMAs done / exit -> stamps[wg][4].
+template <int PXG, bool STAMP = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG == 4 ? 3 : CF_WPE)))
+conv_fwd_glds_kernel(ConvArgs a, unsigned long long* stamps = nullptr) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const long wg_lin = ((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  if (STAMP && threadIdx.x == 0) stamps[wg_lin * 4 + 0] = rt_stamp();
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int nth = (a.H + a.TH - 1) / a.TH;
+  const int b = blockIdx.x / nth;
+  const int h0 = (blockIdx.x % nth) * a.TH;
+  const int g = blockIdx.y;
+  const int co_blk = blockIdx.z * 64;
+  const int ph = a.KH >> 1, pw = a.KW >> 1;
+  const int PW = a.W + a.KW - 1;
+  const int ncb = a.Cinp >> 3;
+  const long img = (long)a.H * a.W * a.Cinp;
+  const int total = (a.TH + a.KH - 1) * PW * ncb;
+  const int totalr = (total + 255) & ~255;
+  const int nchunks = a.KH * a.KW * ncb;
+  const int Kdim = a.KH * a.KW * a.Cinp;
+  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
+  const int nco = min(64, a.Coutp - co_blk);
+  const int wrows = ((nco + 15) >> 4) << 4;
+  const int wcnt = wrows >> 4;                 // glds per wave per weight block
+  const int wblk = wrows * 256;                // bytes of one block image
+  const int fixed = totalr * 16 + 4 * (nchunks + 4);
+  const int NB = conv_glds_nbuf(nkb, (((min(64, a.Coutp) + 15) >> 4) << 4) * 256, fixed,
+                                (long)gridDim.x * gridDim.y * gridDim.z);
+  const int wstride = (((min(64, a.Coutp) + 15) >> 4) << 4) * 256;   // buffer pitch (host LDS size uses it)
+  char* wbuf = smem;
+  uint4* patch = reinterpret_cast<uint4*>(smem + (size_t)NB * wstride);
+  int* coff = reinterpret_cast<int*>(smem + (size_t)NB * wstride + (size_t)totalr * 16);
+  const uint16_t* wg = a.w + ((long)g * a.Coutp + co_blk) * Kdim;
+  const void* zero = g_zero16;
+
+  auto issue_wblock = [&](int kb, int buf) {
+    for (int q0 = wave * 64; q0 < wrows * 16; q0 += 256) {
+      const int q = q0 + lane, r = q >> 4, c = kb * CF_KB + ((q & 15) ^ (r & 15));
+      const void* src = (r < nco && c < nchunks) ? (const void*)(wg + (long)r * Kdim + c * 8) : zero;
+      glds16(src, wbuf + buf * wstride + q0 * 16);
+    }
+  };
+  // dependent scalar loads first: a plain load issued while DMAs fly makes the
+  // compiler drain them (vmcnt(0)) at its first use
+  const uint16_t* src0 = a.in[0] + ((long)g * a.B + b) * img;
+  if (a.gather) {
+    const long id = a.gather[((long)a.st->cur_step * a.G + g) * a.B + b];
+    src0 = a.in[0] + id * img;
+  }
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int NT = (nco + 15) >> 4;
+  float bias_v[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = co_blk + t * 16 + kq * 4 + i;
+      bias_v[t][i] = (a.bias && t < NT && co < a.Coutp) ? a.bias[(long)g * a.Coutp + co] : 0.f;
+    }
+  issue_wblock(0, 0);
+  {
+    const FastDiv div_ncb(ncb), div_pw(PW);
+    for (int q0 = wave * 64; q0 < total; q0 += 256) {
+      const int q = q0 + lane;
+      uint32_t pix, cbu, pr, pc;
+      div_ncb.divmod((uint32_t)q, pix, cbu);
+      div_pw.divmod(pix, pr, pc);
+      const int hh = h0 - ph + (int)pr, ww = (int)pc - pw;
+      const bool ok = q < total && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+      const void* src = ok ? (const void*)(src0 + ((long)hh * a.W + ww) * a.Cinp + (int)cbu * 8) : zero;
+      glds16(src, reinterpret_cast<char*>(patch) + q0 * 16);
+    }
+  }
+  for (int kb = 1; kb < NB; ++kb) issue_wblock(kb, kb);
+  {
+    const FastDiv div_ncb(ncb), div_kw(a.KW);
+    for (int c = tid; c < nchunks + 4; c += 256) {
+      if (c < nchunks) {
+        uint32_t kk, cb, kh, kw;
+        div_ncb.divmod((uint32_t)c, kk, cb);
+        div_kw.divmod(kk, kh, kw);
+        coff[c] = ((int)kh * PW + (int)kw) * ncb + (int)cb;
+      } else {
+        coff[c] = -1;
+      }
+    }
+  }
+  // Everything staged so far lands before the first MFMA: hipcc waits
+  // vmcnt(0) before any LDS read that may alias an in-flight LDS-DMA anyway.
+  vm_wait(0);
+  raw_barrier();
+  if (STAMP && threadIdx.x == 0) stamps[wg_lin * 4 + 1] = rt_stamp();
+
+  const int npx = a.TH * a.W;
+  int pbase[PXG];
+  bool pvalid[PXG];
+  int pyy[PXG], pxx[PXG];
+#pragma unroll
+  for (int h = 0; h < PXG; ++h) {
+    const int pl = wave * 16 * PXG + h * 16 + l16;
+    pyy[h] = pl / a.W; pxx[h] = pl % a.W;
+    pvalid[h] = (pl < npx) && (h0 + pyy[h] < a.H);
+    pbase[h] = (pyy[h] * PW + pxx[h]) * ncb;
+  }
+  f32x4_t acc[PXG][4];
+#pragma unroll
+  for (int h = 0; h < PXG; ++h)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[h][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  for (int kb = 0; kb < nkb; ++kb) {
+    const char* wcur = wbuf + (kb % NB) * wstride;
+#pragma unroll
+    for (int kk = 0; kk < CF_KB / 4; ++kk) {
+      const int cl = kk * 4 + kq;
+      if (kb * CF_KB + kk * 4 >= nchunks) break;
+      const int co_off = coff[kb * CF_KB + cl];
+      uint4 bfr[PXG];
+#pragma unroll
+      for (int h = 0; h < PXG; ++h)
+        bfr[h] = (co_off >= 0 && pvalid[h]) ? patch[pbase[h] + co_off] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (t < NT) {
+          const uint4 af = *reinterpret_cast<const uint4*>(wcur + (t * 16 + l16) * 256 + ((cl ^ l16) << 4));
+#pragma unroll
+          for (int h = 0; h < PXG; ++h) acc[h][t] = mfma16(af, bfr[h], acc[h][t]);
+        }
+      }
+    }
+    if (kb + NB < nkb) {                   // ring refill (layers whose weights do not fit)
+      raw_barrier();                       // every wave is done with buffer kb % NB
+      issue_wblock(kb + NB, kb % NB);
+      vm_wait(wcnt);                       // block kb+1 landed, kb+NB may fly
+      raw_barrier();
+    }
+  }
+  if (STAMP && threadIdx.x == 0) stamps[wg_lin * 4 + 2] = rt_stamp();
+
+  // ---- epilogue (as the register-staged kernel) ------------------------------
+#pragma unroll
+  for (int h = 0; h < PXG; ++h) {
+    if (!pvalid[h]) continue;
+    const long obase = ((((long)g * a.B + b) * a.H + (h0 + pyy[h])) * a.W + pxx[h]) * a.Coutp;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t >= NT) continue;
+      const int co0 = co_blk + t * 16 + kq * 4;
+      if (co0 >= a.Coutp) continue;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float x = acc[h][t][i] + bias_v[t][i];
+        if (a.relu) x = fmaxf(x, 0.f);
+        v[i] = x;
+      }
+      for (int k = 0; k < a.n_out; ++k) {
+        uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
+        float sum[4] = {v[0], v[1], v[2], v[3]};
+        if ((a.acc_flags >> k) & 1) {
+          const uint2 old = *dst;
+          sum[0] += __uint_as_float(old.x << 16); sum[1] += __uint_as_float(old.x & 0xffff0000u);
+          sum[2] += __uint_as_float(old.y << 16); sum[3] += __uint_as_float(old.y & 0xffff0000u);
+        }
+        if (a.out_mask[k]) {
+          const uint2 m = *reinterpret_cast<const uint2*>(a.out_mask[k] + obase + co0);
+          const uint32_t mw[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sum[i] = (mw[i] != 0u && mw[i] < 0x8000u) ? sum[i] : 0.f;
+        }
+        *dst = pack4(sum);
+      }
+    }
+  }
+  if (STAMP) {
+    __syncthreads();
+    if (threadIdx.x == 0) stamps[wg_lin * 4 + 3] = rt_stamp();
+  }
+}
+
+// ---------------------------------------------------------------------------
+// conv_fwd, persistent LDS-DMA variant (single-input layers whose weights fit)
+// ---------------------------------------------------------------------------
+// Stamps of the one-tile kernels show every workgroup of a launch moving in
+// lock-step through three bursts -- all operands staged (~4 us, the whole
+// grid's loads at once), MFMAs (LDS-bound), stores -- with the memory system
+// idle during the MFMAs and vice versa, and every workgroup re-reading the
+// fold's weights from L2 (more bytes than the patches for 3x3 layers).
+// Here a workgroup keeps ALL of its fold's weight blocks resident, walks a
+// strided list of output tiles, and DMAs tile i+1's patch into the second
+// patch buffer while it runs tile i's MFMAs and stores.
+//   The DMA of the next patch is issued by inline asm: hipcc does not model it,
+//   so it does not put vmcnt(0) in front of every LDS read of the current tile
+//   (which it does for the builtin); the kernel waits for it by hand
+//   (vmcnt(0) + barrier at the end of each tile). A plain load that hipcc does
+//   track can only over-wait (counters retire in order), never under-wait.
+
+__device__ __forceinline__ void glds16_asm(const void* src, const void* lds_wave_base) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(src), "s"(l) : "memory", "m0");
+}
+
+#define CP_MAXT 64   // tiles per workgroup (gather ids cached in LDS)
+
+template <int PXG>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG == 4 ? 3 : CF_WPE)))
+conv_fwd_pers_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int nth = (a.H + a.TH - 1) / a.TH;
+  const int ntile = a.B * nth;
+  const int g = blockIdx.y;
+  const int co_blk = blockIdx.z * 64;
+  const int ph = a.KH >> 1, pw = a.KW >> 1;
+  const int PW = a.W + a.KW - 1;
+  const int ncb = a.Cinp >> 3;
+  const long img = (long)a.H * a.W * a.Cinp;
+  const int total = (a.TH + a.KH - 1) * PW * ncb;
+  const int totalr = (total + 255) & ~255;
+  const int nchunks = a.KH * a.KW * ncb;
+  const int Kdim = a.KH * a.KW * a.Cinp;
+  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
+  const int nco = min(64, a.Coutp - co_blk);
+  const int wrows = ((nco + 15) >> 4) << 4;
+  const int wstride = (((min(64, a.Coutp) + 15) >> 4) << 4) * 256;
+  char* wbuf = smem;
+  char* pbuf = smem + (size_t)nkb * wstride;                          // 2 x totalr x 16 B
+  int* coff = reinterpret_cast<int*>(pbuf + (size_t)2 * totalr * 16);
+  long* gid = reinterpret_cast<long*>(coff + ((nchunks + 4 + 1) & ~1));
+  float* sbias = reinterpret_cast<float*>(gid + CP_MAXT);              // [64]
+  const uint16_t* wg = a.w + ((long)g * a.Coutp + co_blk) * Kdim;
+  const uint16_t* in_fold = a.in[0] + (long)g * a.B * img;
+  const void* zero = g_zero16;
+  const int t0 = blockIdx.x, tstep = gridDim.x;
+  const int my_tiles = t0 < ntile ? (ntile - 1 - t0) / tstep + 1 : 0;
+
+  // gather ids of every tile this workgroup will stage (plain loads, waited below)
+  if (a.gather) {
+    for (int i = tid; i < my_tiles; i += 256) {
+      const int b = (t0 + i * tstep) / nth;
+      gid[i] = a.gather[((long)a.st->cur_step * a.G + g) * a.B + b];
+    }
+  }
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int NT = (nco + 15) >> 4;
+  // bias lives in LDS: an epilogue use of a register loaded from global memory
+  // would make hipcc wait vmcnt(0), i.e. for the next tile's patch DMA
+  if (tid < 64) sbias[tid] = (a.bias && tid < nco) ? a.bias[(long)g * a.Coutp + co_blk + tid] : 0.f;
+  __syncthreads();   // gid / sbias visible (and the plain loads above retired)
+
+  const FastDiv div_ncb(ncb), div_pw(PW);
+  auto issue_patch = [&](int i, int buf) {          // tile t0 + i*tstep -> patch buffer buf
+    const int t = t0 + i * tstep;
+    const int b = t / nth, h0 = (t % nth) * a.TH;
+    const uint16_t* src0 = a.gather ? a.in[0] + gid[i] * img : in_fold + (long)b * img;
+    char* dst = pbuf + (size_t)buf * totalr * 16;
+    for (int q0 = wave * 64; q0 < total; q0 += 256) {
+      const int q = q0 + lane;
+      uint32_t pix, cbu, pr, pc;
+      div_ncb.divmod((uint32_t)q, pix, cbu);
+      div_pw.divmod(pix, pr, pc);
+      const int hh = h0 - ph + (int)pr, ww = (int)pc - pw;
+      const bool ok = q < total && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
+      glds16_asm(ok ? (const void*)(src0 + ((long)hh * a.W + ww) * a.Cinp + (int)cbu * 8) : zero, dst + q0 * 16);
+    }
+  };
+  // all weight blocks (resident for the whole launch)
+  for (int kb = 0; kb < nkb; ++kb) {
+    for (int q0 = wave * 64; q0 < wrows * 16; q0 += 256) {
+      const int q = q0 + lane, r = q >> 4, c = kb * CF_KB + ((q & 15) ^ (r & 15));
+      const void* src = (r < nco && c < nchunks) ? (const void*)(wg + (long)r * Kdim + c * 8) : zero;
+      glds16_asm(src, wbuf + (size_t)kb * wstride + q0 * 16);
+    }
+  }
+  if (my_tiles > 0) issue_patch(0, 0);
+  {
+    const FastDiv div_kw(a.KW);
+    for (int c = tid; c < nchunks + 4; c += 256) {
+      if (c < nchunks) {
+        uint32_t kk, cb, kh, kw;
+        div_ncb.divmod((uint32_t)c, kk, cb);
+        div_kw.divmod(kk, kh, kw);
+        coff[c] = ((int)kh * PW + (int)kw) * ncb + (int)cb;
+      } else {
+        coff[c] = -1;
+      }
+    }
+  }
+  vm_wait(0);
+  raw_barrier();
+
+  const int npx = a.TH * a.W;
+  int pbase[PXG], pyy[PXG], pxx[PXG];
+  bool pin[PXG];
+#pragma unroll
+  for (int h = 0; h < PXG; ++h) {
+    const int pl = wave * 16 * PXG + h * 16 + l16;
+    pyy[h] = pl / a.W; pxx[h] = pl % a.W;
+    pin[h] = pl < npx;
+    pbase[h] = (pyy[h] * PW + pxx[h]) * ncb;
+  }
+
+  for (int i = 0; i < my_tiles; ++i) {
+    if (i + 1 < my_tiles) issue_patch(i + 1, (i + 1) & 1);
+    const int t = t0 + i * tstep;
+    const int b = t / nth, h0 = (t % nth) * a.TH;
+    const uint4* patch = reinterpret_cast<const uint4*>(pbuf + (size_t)(i & 1) * totalr * 16);
+    bool pvalid[PXG];
+#pragma unroll
+    for (int h = 0; h < PXG; ++h) pvalid[h] = pin[h] && (h0 + pyy[h] < a.H);
+    f32x4_t acc[PXG][4];
+#pragma unroll
+    for (int h = 0; h < PXG; ++h)
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) acc[h][tt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    for (int kb = 0; kb < nkb; ++kb) {
+      const char* wcur = wbuf + (size_t)kb * wstride;
+#pragma unroll
+      for (int kk = 0; kk < CF_KB / 4; ++kk) {
+        const int cl = kk * 4 + kq;
+        if (kb * CF_KB + kk * 4 >= nchunks) break;
+        const int co_off = coff[kb * CF_KB + cl];
+        uint4 bfr[PXG];
+#pragma unroll
+        for (int h = 0; h < PXG; ++h)
+          bfr[h] = (co_off >= 0 && pvalid[h]) ? patch[pbase[h] + co_off] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          if (tt < NT) {
+            const uint4 af = *reinterpret_cast<const uint4*>(wcur + (tt * 16 + l16) * 256 + ((cl ^ l16) << 4));
+#pragma unroll
+            for (int h = 0; h < PXG; ++h) acc[h][tt] = mfma16(af, bfr[h], acc[h][tt]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < PXG; ++h) {
+      if (!pvalid[h]) continue;
+      const long obase = ((((long)g * a.B + b) * a.H + (h0 + pyy[h])) * a.W + pxx[h]) * a.Coutp;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        if (tt >= NT) continue;
+        const int co0 = co_blk + tt * 16 + kq * 4;
+        if (co0 >= a.Coutp) continue;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float x = acc[h][tt][j] + sbias[tt * 16 + kq * 4 + j];
+          if (a.relu) x = fmaxf(x, 0.f);
+          v[j] = x;
+        }
+        for (int k = 0; k < a.n_out; ++k) {
+          uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
+          float sum[4] = {v[0], v[1], v[2], v[3]};
+          if ((a.acc_flags >> k) & 1) {
+            const uint2 old = *dst;
+            sum[0] += __uint_as_float(old.x << 16); sum[1] += __uint_as_float(old.x & 0xffff0000u);
+            sum[2] += __uint_as_float(old.y << 16); sum[3] += __uint_as_float(old.y & 0xffff0000u);
+          }
+          if (a.out_mask[k]) {
+            const uint2 m = *reinterpret_cast<const uint2*>(a.out_mask[k] + obase + co0);
+            const uint32_t mw[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) sum[j] = (mw[j] != 0u && mw[j] < 0x8000u) ? sum[j] : 0.f;
+          }
+          *dst = pack4(sum);
+        }
+      }
+    }
+    vm_wait(0);        // next patch landed (this wave's part) ...
+    raw_barrier();     // ... everyone's, and nobody still reads the buffer the next DMA overwrites
+  }
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient (split-K, deterministic partials)
 // ---------------------------------------------------------------------------
 
@@ -513,6 +953,27 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* 
 
 extern "C" {
 
+static int g_conv_mode = 0;   // single-input layers: 1 persistent / one-tile LDS-DMA, 2 one-tile LDS-DMA only, 0 register-staged (fastest measured: profiles/conv_modes.txt)
+static unsigned long long* g_conv_stamps = nullptr;   // diagnostic: stamped LDS-DMA kernel
+static int g_conv_wgs = 512;   // persistent conv: target workgroups per launch
+
+int gt_conv_set_wgs(int n) {
+  const int old = g_conv_wgs;
+  if (n > 0) g_conv_wgs = n;
+  return old;
+}
+
+int gt_conv_set_stamps(void* p) {
+  g_conv_stamps = reinterpret_cast<unsigned long long*>(p);
+  return 0;
+}
+
+int gt_conv_set_mode(int mode) {
+  const int old = g_conv_mode;
+  g_conv_mode = mode;
+  return old;
+}
+
 int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   if (a->Cinp % 8 || a->Coutp % 8 || a->n_in < 1 || a->n_in > 4 || a->n_out < 1 || a->n_out > 4) return -1;
   if (a->TH * a->W > 256 || a->TH < 1) return -2;
@@ -524,6 +985,45 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   const size_t lds = (size_t)(nkb > 1 ? 2 : 1) * wrows * CF_WLD * 2 + total * 16 + 4 * ((size_t)nchunks + 4);
   if (lds > 160 * 1024) return -3;
   dim3 grid(a->B * nth, a->G, (a->Coutp + 63) / 64);
+  if (g_conv_mode == 1 && a->n_in == 1 && !a->mask && !g_conv_stamps) {
+    // persistent kernel when every weight block + 2 patch buffers fit a 2-per-CU share
+    const size_t totalr = (total + 255) / 256 * 256;
+    const size_t lds_p = (size_t)nkb * wrows * 256 + 2 * totalr * 16 + 4 * ((size_t)nchunks + 6) + 8 * CP_MAXT + 256;
+    const int ntile = a->B * nth;
+    const int per_fold = a->G * ((a->Coutp + 63) / 64);
+    int nwg = (g_conv_wgs + per_fold - 1) / per_fold;
+    if (nwg > ntile) nwg = ntile;
+    if (nwg < (ntile + CP_MAXT - 1) / CP_MAXT) nwg = (ntile + CP_MAXT - 1) / CP_MAXT;
+    if (lds_p <= 80 * 1024 && ntile >= 2 * nwg) {
+      dim3 pg(nwg, a->G, (a->Coutp + 63) / 64);
+      if (a->TH * a->W > 64)
+        hipLaunchKernelGGL(conv_fwd_pers_kernel<2>, pg, dim3(256), lds_p, stream, *a);
+      else
+        hipLaunchKernelGGL(conv_fwd_pers_kernel<1>, pg, dim3(256), lds_p, stream, *a);
+      return (int)hipGetLastError();
+    }
+  }
+  if (g_conv_mode >= 1 && a->n_in == 1 && !a->mask) {
+    const size_t totalr = (total + 255) / 256 * 256;
+    const int fixed = (int)(totalr * 16 + 4 * ((size_t)nchunks + 4));
+    const int NB = conv_glds_nbuf(nkb, wrows * 256, fixed, (long)grid.x * grid.y * grid.z);
+    const size_t lds2 = (size_t)NB * wrows * 256 + fixed;
+    if (lds2 > 160 * 1024) return -3;
+    if (g_conv_stamps) {
+      if (a->TH * a->W > 64)
+        hipLaunchKernelGGL((conv_fwd_glds_kernel<2, true>), grid, dim3(256), lds2, stream, *a, g_conv_stamps);
+      else
+        hipLaunchKernelGGL((conv_fwd_glds_kernel<1, true>), grid, dim3(256), lds2, stream, *a, g_conv_stamps);
+      return (int)hipGetLastError();
+    }
+    if (a->TH * a->W > 128)
+      hipLaunchKernelGGL(conv_fwd_glds_kernel<4>, grid, dim3(256), lds2, stream, *a);
+    else if (a->TH * a->W > 64)
+      hipLaunchKernelGGL(conv_fwd_glds_kernel<2>, grid, dim3(256), lds2, stream, *a);
+    else
+      hipLaunchKernelGGL(conv_fwd_glds_kernel<1>, grid, dim3(256), lds2, stream, *a);
+    return (int)hipGetLastError();
+  }
   if (a->TH * a->W > 128)
     hipLaunchKernelGGL(conv_fwd_kernel<4>, grid, dim3(256), lds, stream, *a);
   else if (a->TH * a->W > 64)

@@ -79,6 +79,12 @@ def lib():
         L.gt_pool_fwd.restype = I
         L.gt_pool_bwd.argtypes = [P, P, P, I, I, I, I, I, P]
         L.gt_pool_bwd.restype = I
+        L.gt_conv_set_mode.argtypes = [I]
+        L.gt_conv_set_mode.restype = I
+        L.gt_conv_set_stamps.argtypes = [P]
+        L.gt_conv_set_wgs.argtypes = [I]
+        L.gt_conv_set_wgs.restype = I
+        L.gt_conv_set_stamps.restype = I
         for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg"):
             getattr(L, name).restype = C.c_size_t
         assert L.gt_sizeof_conv_args() == C.sizeof(ConvArgs), "ConvArgs ABI mismatch"

@@ -50,9 +50,15 @@ def pack_w(w_oihw, coutp, cinp):
 
 @pytest.mark.parametrize("H,W,cin,cout,k,nin", [(32, 32, 3, 20, 5, 1), (32, 32, 20, 20, 3, 3), (16, 16, 20, 50, 5, 1),
                                                (16, 16, 50, 50, 3, 2), (8, 8, 64, 128, 3, 1), (7, 7, 50, 50, 3, 4),
-                                               (28, 28, 1, 20, 5, 1)])
-def test_conv_fwd(H, W, cin, cout, k, nin):
+                                               (28, 28, 1, 20, 5, 1), (16, 16, 50, 200, 5, 1)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_conv_fwd(H, W, cin, cout, k, nin, mode):
+    """Single-input layers: mode 1 = persistent LDS-DMA kernel (forced onto
+    this small grid with a tiny workgroup target), 2 = one-tile LDS-DMA
+    kernel, 0 = register-staged kernel (always used for N-ary sums)."""
     Km = K()
+    Km.lib().gt_conv_set_mode(mode)
+    Km.lib().gt_conv_set_wgs(8 if mode == 1 else 512)
     torch.manual_seed(0)
     G, B = 2, 3
     cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
@@ -74,6 +80,8 @@ def test_conv_fwd(H, W, cin, cout, k, nin):
     a.TH = Km.conv_tile_rows(H, W)
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv")
     torch.cuda.synchronize()
+    Km.lib().gt_conv_set_mode(0)
+    Km.lib().gt_conv_set_wgs(512)
     for g in range(G):
         # the fused Add is rounded to bf16 before the MFMA: mirror that
         xsum = bf(sum(x[g] for x in xs)).float()
@@ -85,9 +93,12 @@ def test_conv_fwd(H, W, cin, cout, k, nin):
             assert out[g, ..., cout:].abs().max().item() == 0
 
 
-def test_conv_dgrad_mask_and_accumulate():
+@pytest.mark.parametrize("staged_mask,wgs", [(True, 512), (False, 512), (False, 4)])
+def test_conv_dgrad_mask_and_accumulate(staged_mask, wgs):
     """dgrad = conv of (dy * (y>0)) with flipped/transposed weights, fanned out
-    into two outputs, one accumulating."""
+    into two outputs, one accumulating. ``staged_mask``: the ReLU mask is
+    applied while staging (register kernel); else dy arrives pre-masked (the
+    LDS-DMA kernel's single-input path)."""
     Km = K()
     torch.manual_seed(1)
     G, B, H, W, cin, cout, k = 2, 2, 16, 16, 20, 50, 3
@@ -106,17 +117,23 @@ def test_conv_dgrad_mask_and_accumulate():
     prev = bf(torch.randn(G, B, H, W, cinp, device=DEV))
     prev[..., cin:] = 0
     out1 = prev.clone()
+    if not staged_mask:
+        dy_p = (dy_p.float() * (y_p.float() > 0)).to(torch.bfloat16).contiguous()
     a = Km.ConvArgs()
     a.inp[0] = dy_p.data_ptr()
-    a.mask = y_p.data_ptr()
+    a.mask = y_p.data_ptr() if staged_mask else 0
     a.out[0], a.out[1] = out0.data_ptr(), out1.data_ptr()
     pmask = bf(torch.randn(G, B, H, W, cinp, device=DEV))
     a.out_mask[1] = pmask.data_ptr()        # final writer of out1 applies its ReLU mask
     a.n_in, a.n_out, a.acc_flags, a.relu = 1, 2, 2, 0
     a.w, a.bias = wT.data_ptr(), 0
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.TH = G, B, H, W, coutp, cinp, k, k, 4
+    Km.lib().gt_conv_set_wgs(wgs)
+    Km.lib().gt_conv_set_mode(0 if staged_mask else 1)     # 1: persistent (wgs 4) / one-tile LDS-DMA
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "dgrad")
     torch.cuda.synchronize()
+    Km.lib().gt_conv_set_wgs(512)
+    Km.lib().gt_conv_set_mode(0)
     got0 = out0[..., :cin].float().permute(0, 1, 4, 2, 3)
     tol = 2e-2 * ref.abs().max().item()
     assert (got0 - ref).abs().max().item() < tol
