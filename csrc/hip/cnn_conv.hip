@@ -503,7 +503,9 @@ conv_fwd_glds_kernel(ConvArgs a, unsigned long long* stamps = nullptr) {
 
 __device__ __forceinline__ void glds16_asm(const void* src, const void* lds_wave_base) {
   const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)lds_wave_base);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(src), "s"(l) : "memory", "m0");
+  uint32_t keep;   // m0 is reserved by the compiler: save / restore it around the DMA
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
 }
 
 #define CP_MAXT 64   // tiles per workgroup (gather ids cached in LDS)

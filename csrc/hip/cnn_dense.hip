@@ -182,9 +182,10 @@ __global__ void __launch_bounds__(64) head_fwd_kernel(HeadArgs a) {
   }
 #pragma unroll
   for (int c = 0; c < HEAD_MAXC; ++c) {
-    if (c >= C) break;
+    if (c < C) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+      for (int o = 32; o > 0; o >>= 1) acc[c] += __shfl_xor(acc[c], o);
+    }
   }
   if (lane != 0) return;
   float logit[HEAD_MAXC];
