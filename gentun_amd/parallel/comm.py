@@ -38,12 +38,21 @@ class Communicator(object):
     def barrier(self):
         raise NotImplementedError
 
+    def ticket(self, key):
+        """Atomic fetch-and-increment of a job-wide counter named ``key``
+        (0, 1, 2, ... across all ranks): the work-stealing queue of dynamic
+        scheduling."""
+        raise NotImplementedError
+
     def is_master(self):
         return self.rank == 0
 
 
 class LocalComm(Communicator):
     """world_size == 1."""
+
+    def __init__(self):
+        self._tickets = {}
 
     def broadcast_array(self, arr, src=0):
         return np.array(arr, copy=True)
@@ -53,6 +62,11 @@ class LocalComm(Communicator):
 
     def barrier(self):
         return None
+
+    def ticket(self, key):
+        v = self._tickets.get(key, 0)
+        self._tickets[key] = v + 1
+        return v
 
 
 _DTYPES = [np.float64, np.float32, np.int64, np.int32, np.uint8]
@@ -126,6 +140,12 @@ class DistComm(Communicator):
         else:
             self.dist.barrier()
 
+    def ticket(self, key):
+        # the rendezvous TCPStore of the process group: one round trip to the
+        # store host (rank 0's node), no collective, ranks proceed independently
+        store = self.dist.distributed_c10d._get_default_store()
+        return int(store.add("gentun/" + key, 1)) - 1
+
     def destroy(self):
         if self.dist.is_initialized():
             self.dist.destroy_process_group()
@@ -138,6 +158,7 @@ class _ThreadHub(object):
         self.barrier = threading.Barrier(world_size, timeout=timeout_s)
         self.slots = [None] * world_size
         self.lock = threading.Lock()
+        self.tickets = {}
 
 
 class ThreadComm(Communicator):
@@ -169,6 +190,12 @@ class ThreadComm(Communicator):
 
     def barrier(self):
         self.hub.barrier.wait()
+
+    def ticket(self, key):
+        with self.hub.lock:
+            v = self.hub.tickets.get(key, 0)
+            self.hub.tickets[key] = v + 1
+            return v
 
 
 def from_env(backend=None, timeout_s=None, device=None):

@@ -121,37 +121,104 @@ class _Unit(object):
 
 
 def evaluate_units(units, evaluator, nfold, rank, generation):
-    """Evaluate this rank's units; returns ``{unit_index: row}``."""
+    """Evaluate this rank's units; returns ``{unit_index: row}``.
+
+    ``units`` is a list of ``(unit_index, _Unit)`` (static schedule) or a
+    :class:`UnitClaimer` (dynamic schedule: units are claimed from the job-wide
+    ticket counter one at a time, whenever this rank has a free slot)."""
     rows = {}
-    cnn_units, other_units = [], []
-    for ui, u in units:
-        (cnn_units if hasattr(u.ind, "build_fitness_model") else other_units).append((ui, u))
-    for ui, u in other_units:
+    source = units if isinstance(units, UnitClaimer) else _StaticSource(units)
+    try:
+        _fault_hook(rank, generation)
+    except Exception as exc:     # noqa: BLE001
+        # a failed rank takes no work: dynamic units go to the other ranks,
+        # its static units come back empty and the master re-evaluates them
+        warnings.warn("evaluation failed on rank {}: {}".format(rank, exc))
+        return rows
+    if source.kind() == "cnn":
+        try:
+            rows.update(_evaluate_cnn_units(source, evaluator, nfold))
+        except Exception as exc:     # noqa: BLE001
+            warnings.warn("CNN evaluation failed on rank {}: {}".format(rank, exc))
+            for ui, u in source.taken():
+                if ui not in rows:
+                    rows[ui] = _row(ST_ERR, np.nan, 0.0, [], nfold, u.fold_ids)
+        return rows
+    for ui, u in source:
         t0 = time.perf_counter()
         try:
-            _fault_hook(rank, generation)
             u.ind.evaluate_fitness()
             scores = u.ind.fold_scores or []
             rows[ui] = _row(ST_OK, u.ind.fitness, time.perf_counter() - t0, scores, nfold, u.fold_ids)
         except Exception as exc:     # noqa: BLE001 -- reported as a status code
             warnings.warn("evaluation failed on rank {}: {}".format(rank, exc))
             rows[ui] = _row(ST_ERR, np.nan, time.perf_counter() - t0, [], nfold, u.fold_ids)
-    if cnn_units:
-        try:
-            _fault_hook(rank, generation)
-            rows.update(_evaluate_cnn_units(cnn_units, evaluator, nfold))
-        except Exception as exc:     # noqa: BLE001
-            warnings.warn("CNN evaluation failed on rank {}: {}".format(rank, exc))
-            for ui, u in cnn_units:
-                rows[ui] = _row(ST_ERR, np.nan, 0.0, [], nfold, u.fold_ids)
     return rows
 
 
-def _evaluate_cnn_units(cnn_units, evaluator, nfold):
-    """Launch every unit's fold-batched job on the evaluator's streams."""
+class _StaticSource(object):
+    """Pre-assigned units, most expensive first (so long jobs start early)."""
+
+    def __init__(self, units):
+        self.units = sorted(units, key=lambda e: -_unit_cost(e[1]))
+        self._taken = []
+
+    def kind(self):
+        return "cnn" if self.units and hasattr(self.units[0][1].ind, "build_fitness_model") else "other"
+
+    def __iter__(self):
+        for e in self.units:
+            self._taken.append(e)
+            yield e
+
+    def taken(self):
+        return list(self._taken)
+
+
+class UnitClaimer(object):
+    """Dynamic schedule: iterate units by claiming ``comm.ticket(key)``.
+
+    The master orders the unit table by descending cost, so claiming in
+    ticket order is on-line LPT: every rank takes the most expensive unit
+    nobody has started whenever it has capacity (the pull-queue behaviour of
+    the reference's RabbitMQ workers, gentun/worker.py:59-63, without a
+    broker)."""
+
+    def __init__(self, comm, key, n_units, make_unit, kind):
+        self.comm = comm
+        self.key = key
+        self.n = n_units
+        self.make_unit = make_unit
+        self._kind = kind
+        self._taken = []
+
+    def kind(self):
+        return self._kind
+
+    def __iter__(self):
+        while True:
+            k = self.comm.ticket(self.key)
+            if k >= self.n:
+                return
+            e = (k, self.make_unit(k))
+            self._taken.append(e)
+            yield e
+
+    def taken(self):
+        return list(self._taken)
+
+
+def _unit_cost(u):
+    c = float(u.ind.cost()) if hasattr(u.ind, "cost") else 1.0
+    return c * len(u.fold_ids)
+
+
+def _evaluate_cnn_units(source, evaluator, nfold):
+    """Launch every unit's fold-batched job on the evaluator's streams; at
+    most one unit in flight per stream (a unit is claimed only when a stream
+    frees up, which is what makes dynamic claiming balance the ranks)."""
     streams = evaluator.streams() if hasattr(evaluator, "streams") else [None]
     device = getattr(evaluator, "device", None)
-    order = sorted(range(len(cnn_units)), key=lambda k: -cnn_units[k][1].ind.cost() * len(cnn_units[k][1].fold_ids))
     rows, window = {}, []
 
     def retire(entry):
@@ -164,12 +231,18 @@ def _evaluate_cnn_units(cnn_units, evaluator, nfold):
         scores = merged[model.primary_metric()]
         rows[ui] = _row(ST_OK, float(np.mean(scores)), time.perf_counter() - t0, scores, nfold, u.fold_ids)
 
-    for k, idx in enumerate(order):
-        ui, u = cnn_units[idx]
+    it = iter(source)
+    k = 0
+    while True:
         if len(window) >= len(streams):
             retire(window.pop(0))
+        nxt = next(it, None)
+        if nxt is None:
+            break
+        ui, u = nxt
         model = u.ind.build_fitness_model(device=device)
         jobs = model.make_jobs(stream=streams[k % len(streams)], fold_ids=u.fold_ids)
+        k += 1
         t0 = time.perf_counter()
         for job in jobs:
             job.launch()
@@ -203,12 +276,15 @@ class DistributedPopulation(Population):
     def __init__(self, species, x_train=None, y_train=None, individual_list=None, size=None,
                  crossover_rate=0.5, mutation_rate=0.015, maximize=True, additional_parameters=None,
                  host='localhost', port=5672, user='guest', password='guest', rabbit_queue='rpc_queue',
-                 comm=None, evaluator=None, split_folds=True):
+                 comm=None, evaluator=None, split_folds=True, schedule="dynamic"):
         self.comm = comm if comm is not None else _comm_from_args(host, port)
         if evaluator is None:
             evaluator = LocalBatchEvaluator()
+        if schedule not in ("dynamic", "lpt"):
+            raise ValueError("schedule must be 'dynamic' or 'lpt'")
         self.local_evaluator = evaluator
         self.split_folds = split_folds
+        self.schedule = schedule
         self.credentials = {'host': host, 'port': port, 'user': user, 'password': password,
                             'rabbit_queue': rabbit_queue}
         self.generation_counter = 0
@@ -222,6 +298,7 @@ class DistributedPopulation(Population):
         pop.comm = self.comm
         pop.local_evaluator = self.local_evaluator
         pop.split_folds = self.split_folds
+        pop.schedule = self.schedule
         pop.credentials = dict(self.credentials)
         pop.generation_counter = self.generation_counter
         pop.last_dispatch = None
@@ -250,7 +327,15 @@ class DistributedPopulation(Population):
         costs = [float(ind.cost()) if hasattr(ind, "cost") else 1.0 for ind in todo]
         splittable = self.split_folds and hasattr(todo[0], "build_fitness_model")
         units, ucost = make_units(costs, nfold, comm.world_size, splittable)
-        owner = lpt_assign(ucost, comm.world_size)
+        dynamic = self.schedule == "dynamic" and comm.world_size > 1
+        if dynamic:
+            # table order = claim order: most expensive first (on-line LPT)
+            order = sorted(range(len(units)), key=lambda i: (-ucost[i], i))
+            units = [units[i] for i in order]
+            ucost = [ucost[i] for i in order]
+            owner = [-1] * len(units)
+        else:
+            owner = lpt_assign(ucost, comm.world_size)
         table = np.zeros((len(units), 3 + codec.width), np.float64)
         for k, (slot, fids) in enumerate(units):
             table[k, 0] = slot
@@ -265,8 +350,15 @@ class DistributedPopulation(Population):
         comm.broadcast_array(np.array([CMD_EVAL, self.generation_counter, len(todo), nfold], np.int64))
         comm.broadcast_array(blob)
         comm.broadcast_array(table)
-        mine = [(k, _Unit(slot, todo[slot] if len(fids) == nfold else _clone(todo[slot]), fids))
-                for k, (slot, fids) in enumerate(units) if owner[k] == comm.rank]
+        def make_unit(k):
+            slot, fids = units[k]
+            return _Unit(slot, todo[slot] if len(fids) == nfold else _clone(todo[slot]), fids)
+
+        if dynamic:
+            mine = UnitClaimer(comm, "steal/{}".format(self.generation_counter), len(units), make_unit,
+                               "cnn" if splittable else "other")
+        else:
+            mine = [(k, make_unit(k)) for k in range(len(units)) if owner[k] == comm.rank]
         rows = evaluate_units(mine, self.local_evaluator, nfold, comm.rank, self.generation_counter)
         local = np.zeros((len(units), 3 + nfold), np.float64)
         for k, row in rows.items():
@@ -289,7 +381,8 @@ class DistributedPopulation(Population):
                 ind.fold_scores = scores
         self.last_dispatch = {"units": len(units), "candidates": len(todo), "retried": retried,
                               "wall_s": time.perf_counter() - t0,
-                              "per_rank_units": [int(sum(1 for o in owner if o == r)) for r in range(comm.world_size)]}
+                              "schedule": "dynamic" if dynamic else "lpt",
+                              "per_rank_units": [int(np.sum(g[:, 0] != ST_NONE)) for g in gathered]}
         return len(todo)
 
     def sync_ranks(self):
@@ -394,24 +487,29 @@ class GentunWorker(object):
         meta = json.loads(bytes(blob.astype(np.uint8)).decode())
         table = comm.broadcast_array(None)
         extra = {k: _tuplify(v) for k, v in meta["extra"].items()}
-        mine = []
         # genome spec comes with the broadcast: building a throw-away individual
         # here would draw random genes from the GA stream
         genome = {k: (tuple(v) if isinstance(v, list) else v) for k, v in meta["genome"].items()}
         codec = GenomeCodec(genome)
-        for k in range(table.shape[0]):
-            if int(table[k, 1]) != comm.rank:
-                continue
+
+        def make_unit(k):
             genes = codec.decode(table[k, 3:])
             fids = [f for f in range(nfold) if (int(table[k, 2]) >> f) & 1]
             ind = self.individual(self.x_train, self.y_train, genes=genes, **extra)
-            mine.append((k, _Unit(int(table[k, 0]), ind, fids)))
+            return _Unit(int(table[k, 0]), ind, fids)
+
+        n_units = table.shape[0]
+        if n_units and int(table[0, 1]) < 0:
+            kind = "cnn" if hasattr(self.individual, "build_fitness_model") else "other"
+            mine = UnitClaimer(comm, "steal/{}".format(generation), n_units, make_unit, kind)
+        else:
+            mine = [(k, make_unit(k)) for k in range(n_units) if int(table[k, 1]) == comm.rank]
         rows = evaluate_units(mine, self.evaluator, nfold, comm.rank, generation)
         local = np.zeros((table.shape[0], 3 + nfold), np.float64)
         for k, row in rows.items():
             local[k] = row
         comm.all_gather_array(local)
-        self.served += len(mine)
+        self.served += len(rows)
         return True
 
     def work(self):

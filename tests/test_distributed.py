@@ -48,7 +48,7 @@ def _ga_run(pop, cls, gens):
     return [(h["best_fitness"], h["evals"], tuple(sorted(h["best_genes"].items()))) for h in ga.history]
 
 
-def _threaded(world, species, cls, gens, seed, size=12, fault=None, maximize=True):
+def _threaded(world, species, cls, gens, seed, size=12, fault=None, maximize=True, schedule="dynamic"):
     comms = ThreadComm.group(world)
     out = {}
 
@@ -64,7 +64,7 @@ def _threaded(world, species, cls, gens, seed, size=12, fault=None, maximize=Tru
     try:
         rng.seed(seed)
         pop = DistributedPopulation(species, None, None, size=size, comm=comms[0],
-                                    evaluator=SequentialEvaluator(), maximize=maximize)
+                                    evaluator=SequentialEvaluator(), maximize=maximize, schedule=schedule)
         out["hist"] = _ga_run(pop, cls, gens)
         out["pop"] = pop
         pop.shutdown()
@@ -166,3 +166,67 @@ def test_gloo_processes_match_local_run():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert hist == _local(BitIndividual, RussianRouletteGA, 4, seed=77, size=10)
+
+
+def test_dynamic_and_static_schedules_agree():
+    """Work stealing (ticket counter) and static LPT give the same GA run;
+    every unit is evaluated exactly once."""
+    a = _threaded(3, BitIndividual, GeneticAlgorithm, 3, seed=11, schedule="dynamic")
+    b = _threaded(3, BitIndividual, GeneticAlgorithm, 3, seed=11, schedule="lpt")
+    assert a["hist"] == b["hist"]
+    da, db = a["pop"].last_dispatch, b["pop"].last_dispatch
+    assert da["schedule"] == "dynamic" and db["schedule"] == "lpt"
+    assert sum(da["per_rank_units"]) == da["units"] and sum(db["per_rank_units"]) == db["units"]
+
+
+class _SlowOnRank1(BitIndividual):
+    """Evaluation takes 50 ms on the thread named 'rank1', 1 ms elsewhere."""
+
+    def evaluate_fitness(self):
+        import time
+        time.sleep(0.05 if threading.current_thread().name == "rank1" else 0.001)
+        return super(_SlowOnRank1, self).evaluate_fitness()
+
+
+def test_dynamic_schedule_balances_a_slow_rank():
+    comms = ThreadComm.group(3)
+
+    def worker(r):
+        GentunWorker(_SlowOnRank1, None, None, comm=comms[r], evaluator=SequentialEvaluator()).work()
+
+    threads = [threading.Thread(target=worker, args=(r,), name="rank{}".format(r), daemon=True) for r in (1, 2)]
+    for t in threads:
+        t.start()
+    rng.seed(3)
+    pop = DistributedPopulation(_SlowOnRank1, None, None, size=30, comm=comms[0], evaluator=SequentialEvaluator(),
+                                schedule="dynamic")
+    pop.evaluate_in_parallel()
+    per = pop.last_dispatch["per_rank_units"]
+    pop.shutdown()
+    for t in threads:
+        t.join(timeout=30)
+    assert sum(per) == 30
+    assert per[1] < per[2] and per[1] < per[0]        # the slow rank took fewer units
+    assert all(ind.get_fitness() is not None for ind in pop)
+
+
+def test_ticket_counters():
+    from gentun_amd.parallel.comm import LocalComm
+    c = LocalComm()
+    assert [c.ticket("a"), c.ticket("a"), c.ticket("b")] == [0, 1, 0]
+    comms = ThreadComm.group(4)
+    got = []
+    lock = threading.Lock()
+
+    def take(cm):
+        for _ in range(25):
+            v = cm.ticket("k")
+            with lock:
+                got.append(v)
+
+    ts = [threading.Thread(target=take, args=(cm,)) for cm in comms]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert sorted(got) == list(range(100))
