@@ -36,7 +36,7 @@ __global__ void step_begin_kernel(StepState* s) {
   s->global_step += 1;
   const float t = s->t + 1.0f;
   s->t = t;
-  s->lr_t = s->lr * sqrtf(1.0f - powf(ADAM_B2, t)) / (1.0f - powf(ADAM_B1, t));
+  s->lr_t = s->opt == 1 ? s->lr : s->lr * sqrtf(1.0f - powf(ADAM_B2, t)) / (1.0f - powf(ADAM_B1, t));
 }
 
 // ---------------------------------------------------------------------------
@@ -390,10 +390,7 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
       float* P = &pp.x; float* M = &mm.x; float* V = &vv.x;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float gr = acc[r][i];
-        M[i] = ADAM_B1 * M[i] + (1.f - ADAM_B1) * gr;
-        V[i] = ADAM_B2 * V[i] + (1.f - ADAM_B2) * gr * gr;
-        P[i] -= lr_t * M[i] / (sqrtf(V[i]) + ADAM_EPS);
+        P[i] = opt_update(a.st, P[i], acc[r][i], M[i], V[i], lr_t);
         tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
       }
       *reinterpret_cast<float4*>(a.p + off) = pp;
@@ -440,9 +437,8 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
   float gr = 0.f;
   for (int s = 0; s < sg.S; ++s) gr += sg.g[(long)s * sg.gstride + i];
   const float lr_t = a.st->lr_t;
-  float m = ADAM_B1 * sg.m[i] + (1.f - ADAM_B1) * gr;
-  float v = ADAM_B2 * sg.v[i] + (1.f - ADAM_B2) * gr * gr;
-  float p = sg.p[i] - lr_t * m / (sqrtf(v) + ADAM_EPS);
+  float m = sg.m[i], v = sg.v[i];
+  const float p = opt_update(a.st, sg.p[i], gr, m, v, lr_t);
   sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
   const uint16_t pb = f2bf(p);
   if (sg.bf) sg.bf[i] = pb;

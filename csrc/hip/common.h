@@ -18,8 +18,24 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 struct StepState {
   int step_ctr, cur_step;
   float t, lr, lr_t;
-  int global_step, pad0, pad1;
+  int global_step;
+  int opt;          // 0: Adam (Keras defaults), 1: SGD with momentum (Keras SGD, nesterov=False)
+  float momentum;   // SGD momentum
 };
+
+// One parameter update. Adam: m, v moments, lr_t bias-corrected step.
+// SGD-momentum (Keras 2.2 SGD): m is the velocity, v unused:
+//   m = momentum * m - lr * g ;  p += m
+__device__ __forceinline__ float opt_update(const StepState* st, float p, float g, float& m, float& v,
+                                            float lr_t) {
+  if (st->opt == 1) {
+    m = st->momentum * m - lr_t * g;
+    return p + m;
+  }
+  m = 0.9f * m + (1.f - 0.9f) * g;
+  v = 0.999f * v + (1.f - 0.999f) * g * g;
+  return p - lr_t * m / (sqrtf(v) + 1e-7f);
+}
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 

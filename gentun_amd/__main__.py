@@ -90,7 +90,7 @@ def cmd_cnn(args):
     extra = dict(nodes=nodes, input_shape=shape, kernels_per_layer=kernels, kernel_sizes=ks,
                  dense_units=args.dense, dropout_probability=args.dropout, classes=args.classes, nfold=args.nfold,
                  epochs=_ints(args.epochs), learning_rate=_floats(args.lr), batch_size=args.batch, loss=args.loss,
-                 seed=args.seed)
+                 seed=args.seed, optimizer=args.optimizer, momentum=args.momentum)
     return _run_search(args, GeneticCnnIndividual, x, y, extra, maximize=True)
 
 
@@ -146,6 +146,8 @@ def main(argv=None):
     c.add_argument("--lr", default="1e-3,1e-4,1e-5")
     c.add_argument("--batch", type=int, default=32)
     c.add_argument("--loss", choices=("bce_compat", "ce"), default="bce_compat")
+    c.add_argument("--optimizer", choices=("adam", "sgd"), default="adam")
+    c.add_argument("--momentum", type=float, default=0.9, help="SGD momentum")
     c.set_defaults(fn=cmd_cnn)
     x = sub.add_parser("xgb", help="GBDT (XGBoost-style) hyper-parameter search")
     _common(x)

@@ -262,15 +262,17 @@ class GeneticCnnIndividual(Individual):
     ``loss`` ('bce_compat' = Keras softmax+binary_crossentropy parity, or 'ce'),
     ``dtype`` ('bf16' MFMA with fp32 master weights, or 'fp32'), ``seed``
     (run seed; fitness is a pure function of (genes, seed, fold)),
-    ``backend`` ('hip' -- MI355X kernels, default on GPU -- or 'torch' oracle)
-    and ``device``.
+    ``backend`` ('hip' -- MI355X kernels, default on GPU -- or 'torch' oracle),
+    ``device``, and ``optimizer`` ('adam' = the reference's Keras Adam, or
+    'sgd' = Keras SGD with ``momentum``; both reset at every lr stage).
     """
 
     def __init__(self, x_train, y_train, genome=None, genes=None, crossover_rate=0.3, mutation_rate=0.1,
                  nodes=(3, 5), input_shape=(28, 28, 1), kernels_per_layer=(20, 50),
                  kernel_sizes=((5, 5), (5, 5)), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
-                 loss='bce_compat', dtype='bf16', seed=0, backend=None, device=None):
+                 loss='bce_compat', dtype='bf16', seed=0, backend=None, device=None, optimizer='adam',
+                 momentum=0.9):
         if genome is None:
             genome = {'S_{}'.format(i + 1): k * (k - 1) // 2 for i, k in enumerate(nodes)}
         if genes is None:
@@ -297,6 +299,8 @@ class GeneticCnnIndividual(Individual):
         self.seed = seed
         self.backend = backend
         self.device = device
+        self.optimizer = optimizer
+        self.momentum = momentum
 
     @staticmethod
     def generate_random_genes(genome):
@@ -312,7 +316,8 @@ class GeneticCnnIndividual(Individual):
                                self.kernels_per_layer, self.kernel_sizes, self.dense_units,
                                self.dropout_probability, self.classes, self.nfold, self.epochs,
                                self.learning_rate, self.batch_size, loss=self.loss, dtype=self.dtype,
-                               seed=self.seed, backend=self.backend, device=device or self.device)
+                               seed=self.seed, backend=self.backend, device=device or self.device,
+                               optimizer=self.optimizer, momentum=self.momentum)
 
     def cost(self):
         """Relative training cost (forward FLOPs/sample); LPT scheduling key."""
@@ -343,6 +348,8 @@ class GeneticCnnIndividual(Individual):
             'seed': self.seed,
             'backend': self.backend,
             'device': self.device,
+            'optimizer': self.optimizer,
+            'momentum': self.momentum,
         }
 
     def mutate(self):

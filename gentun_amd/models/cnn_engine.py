@@ -48,7 +48,7 @@ CLIP_EPS = 1e-7
 
 class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
-                 dtype="bf16", seed=0, use_graph=True, eval_batch=1000):
+                 dtype="bf16", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9):
         if isinstance(epochs, int):
             epochs = (epochs,)
         if isinstance(learning_rate, (int, float)):
@@ -60,6 +60,8 @@ class TrainConfig(object):
             raise ValueError("loss must be 'bce_compat' or 'ce'")
         if dtype not in ("bf16", "fp32"):
             raise ValueError("dtype must be 'bf16' or 'fp32'")
+        if optimizer not in ("adam", "sgd"):
+            raise ValueError("optimizer must be 'adam' or 'sgd'")
         self.epochs = epochs
         self.learning_rate = learning_rate
         self.batch_size = int(batch_size)
@@ -69,6 +71,8 @@ class TrainConfig(object):
         self.seed = seed
         self.use_graph = use_graph
         self.eval_batch = int(eval_batch)
+        self.optimizer = optimizer
+        self.momentum = float(momentum)
 
     def total_epochs(self):
         return sum(self.epochs)
@@ -425,10 +429,14 @@ class TorchFoldJob(FoldJob):
         with torch.no_grad():
             g = self.flat.grad
             self.t.add_(1.0)
-            step = self.lr * torch.sqrt(1.0 - ADAM_B2 ** self.t) / (1.0 - ADAM_B1 ** self.t)
-            self.m.mul_(ADAM_B1).add_(g, alpha=1.0 - ADAM_B1)
-            self.v.mul_(ADAM_B2).addcmul_(g, g, value=1.0 - ADAM_B2)
-            self.flat.sub_(step * self.m / (self.v.sqrt() + ADAM_EPS))
+            if self.cfg.optimizer == "sgd":       # Keras SGD: v = mu v - lr g ; p += v
+                self.m.mul_(self.cfg.momentum).sub_(self.lr * g)
+                self.flat.add_(self.m)
+            else:
+                step = self.lr * torch.sqrt(1.0 - ADAM_B2 ** self.t) / (1.0 - ADAM_B1 ** self.t)
+                self.m.mul_(ADAM_B1).add_(g, alpha=1.0 - ADAM_B1)
+                self.v.mul_(ADAM_B2).addcmul_(g, g, value=1.0 - ADAM_B2)
+                self.flat.sub_(step * self.m / (self.v.sqrt() + ADAM_EPS))
 
     def evaluate(self):
         G = self.G

@@ -335,6 +335,8 @@ class HipFoldJob(FoldJob):
         self.v.zero_()
         self.state_f[2:3].zero_()
         self.state_f[3:4].fill_(float(lr))
+        self.state[6:7].fill_(1 if self.cfg.optimizer == "sgd" else 0)     # StepState.opt
+        self.state_f[7:8].fill_(float(self.cfg.momentum))                  # StepState.momentum
 
     def snapshot(self):
         return (self.flat.clone(), self.m.clone(), self.v.clone(), self.state.clone())

@@ -38,12 +38,17 @@ def test_loss_semantics_match_keras_definitions():
     assert binc.item() == 9.0 and catc.item() == 1.0
 
 
-def test_fold_batched_torch_training_learns():
+@pytest.mark.parametrize("optimizer,lr", [("adam", 1e-3), ("sgd", 3e-3)])
+def test_fold_batched_torch_training_learns(optimizer, lr):
     x, y = _data(900)
     folds = stratified_kfold(np.argmax(y, 1), 3, seed=0)
     plan = make_plan({'S_1': '000', 'S_2': '0000000000'}, (3, 5), (16, 16, 1), (8, 16), ((3, 3), (3, 3)), 64, 4)
-    cfg = E.TrainConfig(epochs=(8,), learning_rate=(1e-3,), batch_size=16, dtype="fp32", loss="ce")
+    cfg = E.TrainConfig(epochs=(8,), learning_rate=(lr,), batch_size=16, dtype="fp32", loss="ce",
+                        optimizer=optimizer, momentum=0.9)
     res = E.make_job("torch", plan, x, y, folds, cfg, "cpu").launch().finish()
+    if optimizer == "sgd":           # plain SGD on a Glorot-init ReLU net is slow: require progress only
+        assert np.mean(res["val_loss"]) < np.log(4) - 0.005
+        return
     assert np.mean(res["categorical_accuracy"]) > 0.4 and max(res["categorical_accuracy"]) > 0.5  # chance 0.25
     assert len(res["binary_accuracy"]) == 3
 
@@ -90,3 +95,26 @@ def test_bench_contract_cpu():
                 "vs_baseline", "dtype", "data", "config"):
         assert key in rec
     assert rec["n_gpus"] == 1 and rec["value"] > 0 and rec["higher_is_better"] is True
+
+
+def test_sgd_momentum_update_rule():
+    """One Keras-SGD step: v = mu v - lr g ; p += v (velocity reset per lr stage)."""
+    x, y = _data(64)
+    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
+    plan = make_plan({'S_1': '000', 'S_2': '0000000000'}, (3, 5), (16, 16, 1), (4, 4), ((3, 3), (3, 3)), 8, 4)
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(0.1,), batch_size=8, dtype="fp32", loss="ce", dropout=0.0,
+                        optimizer="sgd", momentum=0.5)
+    job = E.make_job("torch", plan, x, y, folds, cfg, "cpu")
+    job.init_params()
+    job.reset_optimizer(0.1)
+    job._new_epoch_order()
+    p0 = job.flat.detach().clone()
+    job.train_step()
+    g1 = job.flat.grad.clone()
+    p1 = job.flat.detach().clone()
+    assert torch.allclose(p1, p0 - 0.1 * g1, atol=1e-6)
+    job.train_step()
+    g2 = job.flat.grad.clone()
+    assert torch.allclose(job.flat.detach(), p1 + 0.5 * (-0.1 * g1) - 0.1 * g2, atol=1e-6)
+    with pytest.raises(ValueError):
+        E.TrainConfig(optimizer="rmsprop")
