@@ -403,7 +403,12 @@ class TorchFoldJob(FoldJob):
         h = torch.baddbmm(P["dense1.b"][:, None, :], feat, P["dense1.w"])
         h = F.relu(h)
         if train and self.cfg.dropout > 0:
-            h = F.dropout(h, self.cfg.dropout, training=True)
+            # job-owned generator (not torch's global RNG): the oracle is deterministic
+            if self.drop_gen is None:
+                self.drop_gen = torch.Generator(device=self.device)
+                self.drop_gen.manual_seed(_rng.stable_hash(self.base_seed, "dropout") & 0x7FFFFFFF)
+            keep = torch.rand(h.shape, generator=self.drop_gen, device=self.device) >= self.cfg.dropout
+            h = h * keep.to(h.dtype) / (1.0 - self.cfg.dropout)
         return torch.baddbmm(P["dense2.b"][:, None, :], h, P["dense2.w"])
 
     def _gather(self, idx):
