@@ -296,32 +296,55 @@ class HipFoldJob(FoldJob):
         self.adam_args = aa
 
     # -------------------------------------------------------------- protocol
-    def init_params(self):
+    def _build_init_table(self):
+        """Segment table of the one-launch Philox Glorot initialiser (K11):
+        every conv kernel, W1 and W2 of every fold; biases stay zero."""
         G = self.G
-        with torch.no_grad():
-            self.flat.zero_()
+        segs, blocks, seeds = [], [], []
 
-            def glorot(view, fan_in, fan_out, g, name):
-                limit = math.sqrt(6.0 / (fan_in + fan_out))
-                gen = torch.Generator(device=self.device)
-                gen.manual_seed(_rng.stable_hash(self._fold_seed(g), name) & 0x7FFFFFFF)
-                vals = torch.rand(view.shape, generator=gen, device=self.device) * (2 * limit) - limit
-                view.copy_(vals)
+        def add(t, d, r, fan_in, fan_out, name):
+            assert t.is_contiguous() and t.numel() == G * int(np.prod(d))
+            seeds.append([_rng.stable_hash(self._fold_seed(g), name) & 0x7FFFFFFFFFFFFFFF for g in range(G)])
+            sg = K.InitSeg()
+            sg.p = t.data_ptr()
+            for i in range(4):
+                sg.d[i], sg.r[i] = int(d[i]), int(r[i])
+            sg.G, sg.tag = G, len(segs)
+            sg.limit = math.sqrt(6.0 / (fan_in + fan_out))
+            idx = len(segs)
+            segs.append(sg)
+            for o in range(0, t.numel(), 256):
+                blocks.append((idx, o))
 
-            for L in self.layers:
-                w = L.w[0]
-                for g in range(G):
-                    glorot(w[g, :L.cout, :, :, :L.cin], L.cin * L.KH * L.KW, L.cout * L.KH * L.KW, g,
-                           L.spec.name + ".w")
-            hs, ws, cp = self.shapes[self.last]
-            c_real = self.plan.final_c
-            w1 = self.views["W1"][0].view(G, hs, ws, cp, self.Up)
-            w2 = self.views["W2"][0]
-            for g in range(G):
-                glorot(w1[g, :, :, :c_real, :self.plan.dense_units], self.plan.flatten, self.plan.dense_units, g,
-                       "dense1.w")
-                glorot(w2[g, :self.plan.dense_units, :], self.plan.dense_units, self.plan.classes, g, "dense2.w")
-            self._refresh_copies()
+        for L in self.layers:
+            add(L.w[0], (L.coutp, L.KH, L.KW, L.cinp), (L.cout, L.KH, L.KW, L.cin), L.cin * L.KH * L.KW,
+                L.cout * L.KH * L.KW, L.spec.name + ".w")
+        hs, ws, cp = self.shapes[self.last]
+        add(self.views["W1"][0], (hs, ws, cp, self.Up), (hs, ws, self.plan.final_c, self.plan.dense_units),
+            self.plan.flatten, self.plan.dense_units, "dense1.w")
+        w2 = self.views["W2"][0]
+        add(w2, (1, 1, w2.shape[1], w2.shape[2]), (1, 1, self.plan.dense_units, self.plan.classes),
+            self.plan.dense_units, self.plan.classes, "dense2.w")
+        self.init_seeds = torch.tensor(np.asarray(seeds, np.int64), device=self.device)
+        for k, sg in enumerate(segs):
+            sg.seeds = self.init_seeds[k].data_ptr()
+        arr = (K.InitSeg * len(segs))(*segs)
+        self.init_segs = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8
+                                          ).to(self.device)
+        self.init_blocks = torch.tensor(np.asarray(blocks, np.int32).reshape(-1, 2), device=self.device)
+        ia = K.InitArgs()
+        ia.segs, ia.blocks = self.init_segs.data_ptr(), self.init_blocks.data_ptr()
+        self.init_args = ia
+        self.init_nblocks = len(blocks)
+
+    def init_params(self):
+        """Glorot-uniform kernels (Philox, keyed by fold id and tensor name),
+        zero biases -- Keras defaults, re-drawn per fold."""
+        if getattr(self, "init_args", None) is None:
+            self._build_init_table()
+        self.flat.zero_()
+        K.check(K.lib().gt_glorot_init(self.init_args, self.init_nblocks, self._stream()), "glorot_init")
+        self._refresh_copies()
 
     def _refresh_copies(self):
         for L in self.layers:

@@ -58,6 +58,15 @@ class AdamArgs(C.Structure):
     _fields_ = [("segs", P), ("blocks", P), ("st", P)]
 
 
+class InitSeg(C.Structure):
+    _fields_ = [("p", P), ("seeds", P), ("d", I * 4), ("r", I * 4), ("G", I), ("tag", I), ("limit", C.c_float),
+                ("pad", I)]
+
+
+class InitArgs(C.Structure):
+    _fields_ = [("segs", P), ("blocks", P)]
+
+
 _TYPED = {}
 
 
@@ -85,9 +94,14 @@ def lib():
         L.gt_conv_set_wgs.argtypes = [I]
         L.gt_conv_set_wgs.restype = I
         L.gt_conv_set_stamps.restype = I
-        for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg"):
+        L.gt_glorot_init.argtypes = [C.POINTER(InitArgs), I, P]
+        L.gt_glorot_init.restype = I
+        L.gt_glorot_ref.argtypes = [C.c_uint64, C.c_uint64, I, C.c_float]
+        L.gt_glorot_ref.restype = C.c_float
+        for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg", "gt_sizeof_init_seg"):
             getattr(L, name).restype = C.c_size_t
         assert L.gt_sizeof_conv_args() == C.sizeof(ConvArgs), "ConvArgs ABI mismatch"
+        assert L.gt_sizeof_init_seg() == C.sizeof(InitSeg), "InitSeg ABI mismatch"
         assert L.gt_sizeof_wgrad_args() == C.sizeof(WgradArgs), "WgradArgs ABI mismatch"
         assert L.gt_sizeof_adam_seg() == C.sizeof(AdamSeg), "AdamSeg ABI mismatch"
         _TYPED[id(L)] = True

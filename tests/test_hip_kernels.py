@@ -378,3 +378,37 @@ def test_adam_segments_with_partials_and_transpose():
     W = rp.view(G, co, kh, kw, ci)
     WT = W.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous().to(torch.bfloat16).view(-1)
     assert torch.equal(bfT, WT)
+
+
+def test_glorot_init_kernel():
+    """One-launch Philox Glorot init: real region matches the host reference
+    draw element by element, padding is zero, values span (-limit, limit)."""
+    import ctypes as C
+    Km = K()
+    L = Km.lib()
+    G, d, r = 2, (8, 3, 3, 24), (5, 3, 3, 20)
+    t = torch.full((G,) + d, 7.0, device=DEV)
+    seeds = torch.tensor([1234567, 987654321012], dtype=torch.int64, device=DEV)
+    sg = Km.InitSeg()
+    sg.p, sg.seeds = t.data_ptr(), seeds.data_ptr()
+    for i in range(4):
+        sg.d[i], sg.r[i] = d[i], r[i]
+    sg.G, sg.tag, sg.limit = G, 5, 0.3
+    arr = (Km.InitSeg * 1)(sg)
+    segs = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8).to(DEV)
+    nblk = -(-t.numel() // 256)
+    blocks = torch.tensor([[0, o * 256] for o in range(nblk)], dtype=torch.int32, device=DEV)
+    ia = Km.InitArgs()
+    ia.segs, ia.blocks = segs.data_ptr(), blocks.data_ptr()
+    Km.check(L.gt_glorot_init(ia, nblk, stream()), "init")
+    torch.cuda.synchronize()
+    h = t.cpu()
+    assert (h[:, r[0]:] == 0).all() and (h[..., r[3]:] == 0).all()
+    real = h[:, :r[0], :, :, :r[3]]
+    assert real.abs().max().item() < 0.3 and real.abs().min().item() >= 0.0
+    assert abs(real.mean().item()) < 0.03 and real.std().item() > 0.15      # U(-.3,.3): std .173
+    for g, key in enumerate([1234567, 987654321012]):
+        for (i0, i1, i2, i3) in [(0, 0, 0, 0), (4, 2, 2, 19), (2, 1, 0, 7)]:
+            lin = ((i0 * r[1] + i1) * r[2] + i2) * r[3] + i3
+            ref = L.gt_glorot_ref(C.c_uint64(key), C.c_uint64(lin), 5, C.c_float(0.3))
+            assert abs(h[g, i0, i1, i2, i3].item() - ref) < 1e-7
