@@ -32,7 +32,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--per-gpu", type=int, default=8, help="candidates per GPU per generation")
-    ap.add_argument("--streams", type=int, default=4, help="concurrent candidates per GPU")
+    ap.add_argument("--streams", type=int, default=1, help="concurrent population jobs per GPU")
+    ap.add_argument("--pop-batch", type=int, default=16, help="candidates per population job (shared launches)")
     ap.add_argument("--backend", default=None, help="hip (default on GPU) or torch")
     ap.add_argument("--epochs", default="20,4,1")
     ap.add_argument("--lr", default="1e-3,1e-4,1e-5")
@@ -91,7 +92,7 @@ def run(args):
                  kernel_sizes=((5, 5), (5, 5)), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=args.nfold, epochs=epochs, learning_rate=lrs, batch_size=32, dtype=args.dtype,
                  seed=args.seed, backend=args.backend)
-    evaluator = LocalBatchEvaluator(device=device, streams=args.streams)
+    evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch)
     P = args.per_gpu * comm.world_size
 
     if comm.rank != 0:
@@ -144,7 +145,7 @@ def run(args):
                    "candidates_per_step": P, "per_gpu": args.per_gpu, "nfold": args.nfold,
                    "epochs": list(epochs), "learning_rate": list(lrs), "samples": args.samples,
                    "backend": args.backend or ("hip" if device.type == "cuda" else "torch"),
-                   "streams_per_gpu": args.streams},
+                   "streams_per_gpu": args.streams, "pop_batch": args.pop_batch},
         "best_val_binary_acc": round(best["fitness"], 5),
         "best_genes": best["genes"],
         "timed_candidates": timed_evals,

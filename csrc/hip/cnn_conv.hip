@@ -30,18 +30,51 @@
 
 #include "common.h"
 
-struct ConvArgs {
-  const uint16_t* in[4];     // summed inputs [G][B][H][W][Cinp]
-  const uint16_t* mask;      // optional: staged value *= (mask > 0), same shape as in
-  const int64_t* gather;     // optional: image table [steps][G][B]; in[0] is then the dataset
-  const StepState* st;       // cur_step for the gather table
-  uint16_t* out[4];          // [G][B][H][W][Coutp]
-  const uint16_t* out_mask[4];  // optional per output: final value *= (out_mask > 0) (dz of a ReLU layer)
-  const uint16_t* w;         // [G][Coutp][KH][KW][Cinp] bf16
-  const float* bias;         // [G][Coutp] or null
-  int n_in, n_out, acc_flags, relu;
-  int G, B, H, W, Cinp, Coutp, KH, KW, TH;
+// Population batching: a launch covers the "groups" (candidate x fold
+// replicas) listed in a group table. Activations / gradients live in SLOT
+// tensors [Q][B][H][W][C] (Q = all groups of the job); a group's record says
+// which slots it sums as input, which slots its output goes to, and for each
+// output whether to accumulate and whether to apply the ReLU mask of that
+// slot's activation (the DAG of every candidate is different, the launch is
+// shared).  gtab == nullptr: legacy dense mode (group = blockIdx.y, inputs
+// 0..n_in-1, outputs 0..n_out-1, acc_flags, masks where out_mask[k] != 0).
+struct GroupRec {
+  int g;          // group index into the slot tensors / weights
+  int in_mask;    // bit k: in[k] is summed
+  int out_mask;   // bits 0-7: outputs written, 8-15: accumulate, 16-23: apply out_mask[k] ReLU mask
+  int pad;
 };
+
+#define GT_MAXSLOT 8
+
+struct ConvArgs {
+  const uint16_t* in[GT_MAXSLOT];   // input slot bases [Q][B][H][W][Cinp]
+  const uint16_t* mask;             // optional: staged value *= (mask > 0), same shape as in (legacy mode)
+  const int64_t* gather;            // optional: image table [steps][Q][B]; in[0] is then the dataset
+  const StepState* st;              // cur_step for the gather table
+  uint16_t* out[GT_MAXSLOT];        // output slot bases [Q][B][H][W][Coutp]
+  const uint16_t* out_mask[GT_MAXSLOT];  // per output slot: ReLU-mask source (that slot's activation)
+  const uint16_t* w;                // [Q][Coutp][KH][KW][Cinp] bf16
+  const float* bias;                // [Q][Coutp] or null
+  const GroupRec* gtab;             // [grid.y] or null
+  int n_in, n_out, acc_flags, relu;
+  int G, B, H, W, Cinp, Coutp, KH, KW, TH;   // G = Q (group count of the slot tensors)
+  int ngroups;                      // launch groups (rows of gtab); legacy mode: G
+};
+
+__device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,
+                                              const uint16_t* const* out_mask) {
+  if (gtab) return gtab[y];
+  GroupRec r;
+  r.g = y;
+  r.in_mask = (1 << n_in) - 1;
+  int rm = 0;
+  for (int k = 0; k < n_out; ++k)
+    if (out_mask && out_mask[k]) rm |= 1 << k;
+  r.out_mask = ((1 << n_out) - 1) | ((acc & 0xff) << 8) | (rm << 16);
+  r.pad = 0;
+  return r;
+}
 
 #define CF_KB 16                 // weight K-block: 16 chunks of 8 = 128 k
 #define CF_WLD (CF_KB * 8 + 8)    // LDS row stride of a weight block (272 B: conflict-free b128 reads)
@@ -57,7 +90,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
   const int nth = (a.H + a.TH - 1) / a.TH;
   const int b = blockIdx.x / nth;
   const int h0 = (blockIdx.x % nth) * a.TH;
-  const int g = blockIdx.y;
+  const GroupRec gr = group_rec(a.gtab, blockIdx.y, a.n_in, a.n_out, a.acc_flags, a.out_mask);
+  const int g = gr.g;
   const int co_blk = blockIdx.z * 64;
   const int ph = a.KH >> 1, pw = a.KW >> 1;
   const int PH = a.TH + a.KH - 1, PW = a.W + a.KW - 1;
@@ -99,11 +133,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
   load_wblock(0);
 
   // ---- stage the summed / masked input patch -------------------------------
-  const uint16_t* src[4];
-  for (int k = 0; k < a.n_in; ++k) src[k] = a.in[k] + ((long)g * a.B + b) * img;
+  const uint16_t* src[GT_MAXSLOT];
+  int n_src = 0;
+  for (int k = 0; k < GT_MAXSLOT; ++k)
+    if ((gr.in_mask >> k) & 1) src[n_src++] = a.in[k] + ((long)g * a.B + b) * img;
   if (a.gather) {
     const long id = a.gather[((long)a.st->cur_step * a.G + g) * a.B + b];
     src[0] = a.in[0] + id * img;
+    n_src = 1;
   }
   const uint16_t* msrc = a.mask ? a.mask + ((long)g * a.B + b) * img : nullptr;
   const FastDiv div_ncb(ncb), div_pw(PW);
@@ -116,12 +153,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
     uint4 v = make_uint4(0, 0, 0, 0);
     if (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) {
       const long off = ((long)hh * a.W + ww) * a.Cinp + cb * 8;
-      if (a.n_in == 1 && !msrc) {
+      if (n_src == 1 && !msrc) {
         v = *reinterpret_cast<const uint4*>(src[0] + off);
       } else {
         float acc[8], t[8];
         unpack8(*reinterpret_cast<const uint4*>(src[0] + off), acc);
-        for (int k = 1; k < a.n_in; ++k) {
+        for (int k = 1; k < n_src; ++k) {
           unpack8(*reinterpret_cast<const uint4*>(src[k] + off), t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[j] += t[j];
@@ -218,15 +255,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
         if (a.relu) x = fmaxf(x, 0.f);
         v[i] = x;
       }
-      for (int k = 0; k < a.n_out; ++k) {
+      for (int k = 0; k < GT_MAXSLOT; ++k) {
+        if (!((gr.out_mask >> k) & 1)) continue;
         uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
         float sum[4] = {v[0], v[1], v[2], v[3]};
-        if ((a.acc_flags >> k) & 1) {
+        if ((gr.out_mask >> (8 + k)) & 1) {
           const uint2 old = *dst;
           sum[0] += __uint_as_float(old.x << 16); sum[1] += __uint_as_float(old.x & 0xffff0000u);
           sum[2] += __uint_as_float(old.y << 16); sum[3] += __uint_as_float(old.y & 0xffff0000u);
         }
-        if (a.out_mask[k]) {
+        if ((gr.out_mask >> (16 + k)) & 1) {
           const uint2 m = *reinterpret_cast<const uint2*>(a.out_mask[k] + obase + co0);
           // bf16 > 0  <=>  sign bit clear and not +0
           const uint32_t mw[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
@@ -240,460 +278,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
 }
 
 // ---------------------------------------------------------------------------
-// conv_fwd, LDS-DMA variant (single-input, unmasked layers: most of the DAG)
-// ---------------------------------------------------------------------------
-// The register-staged kernel above is latency-bound: a workgroup walks a chain
-// of dependent global round trips (patch slots, then weight block k+1 behind
-// block k, then bias), and only ~1-5 workgroups per CU exist to hide them.
-// Here every byte reaches LDS through global_load_lds_dwordx4 (no VGPR
-// destination), so the whole patch and the first two weight blocks are in
-// flight at once and the workgroup waits for ONE latency before its MFMAs.
-//   * LDS images are lane-linear (a wave-instruction writes 1 KiB
-//     contiguously); weight rows are 256 B unpadded and XOR-swizzled through
-//     the SOURCE address (chunk c of row r lands at slot c ^ (r & 15)), so the
-//     16 rows an A-fragment read touches hit 16 different bank groups.
-//   * Padding pixels / rows / chunks read a 16-byte zero line.
-//   * Weight blocks > 1 stream through a 2-deep ring with counted vmcnt waits
-//     and raw s_barrier (a __syncthreads() would drain the prefetch).
-
-__device__ __attribute__((aligned(16))) uint4 g_zero16[4];
-
-typedef __attribute__((address_space(1))) const void gvoid_t;
-typedef __attribute__((address_space(3))) void lvoid_t;
-
-__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gvoid_t*)src, (lvoid_t*)lds_wave_base, 16, 0, 0);
-}
-
-// wait until at most n (0..4) LDS-DMA / vector loads of this wave are outstanding
-__device__ __forceinline__ void vm_wait(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-  }
-}
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-}
-
-// Weight-ring depth: as many 16-chunk blocks as the LDS share of one workgroup
-// allows when the grid needs ceil(nwg / 256) workgroups resident per CU (the
-// s2 / deep layers launch only ~1-2 workgroups per CU, so they can keep every
-// block -- or most of them -- resident and issue all weight DMAs at once).
-__host__ __device__ inline int conv_glds_nbuf(int nkb, int wblk, int fixed_bytes, long nwg) {
-  long per_cu = (nwg + 255) / 256;
-  if (per_cu < 1) per_cu = 1;
-  if (per_cu > 8) per_cu = 8;
-  const long budget = 160L * 1024 / per_cu - 1024 - fixed_bytes;
-  long nb = budget / wblk;
-  if (nb > nkb) nb = nkb;
-  if (nb < 2) nb = nkb < 2 ? nkb : 2;
-  return (int)nb;
-}
-
-__device__ __forceinline__ unsigned long long rt_stamp() {
-  unsigned long long t;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
-  return t;
-}
-
-// STAMP (diagnostic build only): per workgroup realtime stamps (100 MHz) at
-// entry / operands staged / MFMAs done / exit -> stamps[wg][4].
-template <int PXG, bool STAMP = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG == 4 ? 3 : CF_WPE)))
-conv_fwd_glds_kernel(ConvArgs a, unsigned long long* stamps = nullptr) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const long wg_lin = ((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
-  if (STAMP && threadIdx.x == 0) stamps[wg_lin * 4 + 0] = rt_stamp();
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int nth = (a.H + a.TH - 1) / a.TH;
-  const int b = blockIdx.x / nth;
-  const int h0 = (blockIdx.x % nth) * a.TH;
-  const int g = blockIdx.y;
-  const int co_blk = blockIdx.z * 64;
-  const int ph = a.KH >> 1, pw = a.KW >> 1;
-  const int PW = a.W + a.KW - 1;
-  const int ncb = a.Cinp >> 3;
-  const long img = (long)a.H * a.W * a.Cinp;
-  const int total = (a.TH + a.KH - 1) * PW * ncb;
-  const int totalr = (total + 255) & ~255;
-  const int nchunks = a.KH * a.KW * ncb;
-  const int Kdim = a.KH * a.KW * a.Cinp;
-  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
-  const int nco = min(64, a.Coutp - co_blk);
-  const int wrows = ((nco + 15) >> 4) << 4;
-  const int wcnt = wrows >> 4;                 // glds per wave per weight block
-  const int wblk = wrows * 256;                // bytes of one block image
-  const int fixed = totalr * 16 + 4 * (nchunks + 4);
-  const int NB = conv_glds_nbuf(nkb, (((min(64, a.Coutp) + 15) >> 4) << 4) * 256, fixed,
-                                (long)gridDim.x * gridDim.y * gridDim.z);
-  const int wstride = (((min(64, a.Coutp) + 15) >> 4) << 4) * 256;   // buffer pitch (host LDS size uses it)
-  char* wbuf = smem;
-  uint4* patch = reinterpret_cast<uint4*>(smem + (size_t)NB * wstride);
-  int* coff = reinterpret_cast<int*>(smem + (size_t)NB * wstride + (size_t)totalr * 16);
-  const uint16_t* wg = a.w + ((long)g * a.Coutp + co_blk) * Kdim;
-  const void* zero = g_zero16;
-
-  auto issue_wblock = [&](int kb, int buf) {
-    for (int q0 = wave * 64; q0 < wrows * 16; q0 += 256) {
-      const int q = q0 + lane, r = q >> 4, c = kb * CF_KB + ((q & 15) ^ (r & 15));
-      const void* src = (r < nco && c < nchunks) ? (const void*)(wg + (long)r * Kdim + c * 8) : zero;
-      glds16(src, wbuf + buf * wstride + q0 * 16);
-    }
-  };
-  // dependent scalar loads first: a plain load issued while DMAs fly makes the
-  // compiler drain them (vmcnt(0)) at its first use
-  const uint16_t* src0 = a.in[0] + ((long)g * a.B + b) * img;
-  if (a.gather) {
-    const long id = a.gather[((long)a.st->cur_step * a.G + g) * a.B + b];
-    src0 = a.in[0] + id * img;
-  }
-  const int kq = lane >> 4, l16 = lane & 15;
-  const int NT = (nco + 15) >> 4;
-  float bias_v[4][4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = co_blk + t * 16 + kq * 4 + i;
-      bias_v[t][i] = (a.bias && t < NT && co < a.Coutp) ? a.bias[(long)g * a.Coutp + co] : 0.f;
-    }
-  issue_wblock(0, 0);
-  {
-    const FastDiv div_ncb(ncb), div_pw(PW);
-    for (int q0 = wave * 64; q0 < total; q0 += 256) {
-      const int q = q0 + lane;
-      uint32_t pix, cbu, pr, pc;
-      div_ncb.divmod((uint32_t)q, pix, cbu);
-      div_pw.divmod(pix, pr, pc);
-      const int hh = h0 - ph + (int)pr, ww = (int)pc - pw;
-      const bool ok = q < total && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
-      const void* src = ok ? (const void*)(src0 + ((long)hh * a.W + ww) * a.Cinp + (int)cbu * 8) : zero;
-      glds16(src, reinterpret_cast<char*>(patch) + q0 * 16);
-    }
-  }
-  for (int kb = 1; kb < NB; ++kb) issue_wblock(kb, kb);
-  {
-    const FastDiv div_ncb(ncb), div_kw(a.KW);
-    for (int c = tid; c < nchunks + 4; c += 256) {
-      if (c < nchunks) {
-        uint32_t kk, cb, kh, kw;
-        div_ncb.divmod((uint32_t)c, kk, cb);
-        div_kw.divmod(kk, kh, kw);
-        coff[c] = ((int)kh * PW + (int)kw) * ncb + (int)cb;
-      } else {
-        coff[c] = -1;
-      }
-    }
-  }
-  // Everything staged so far lands before the first MFMA: hipcc waits
-  // vmcnt(0) before any LDS read that may alias an in-flight LDS-DMA anyway.
-  vm_wait(0);
-  raw_barrier();
-  if (STAMP && threadIdx.x == 0) stamps[wg_lin * 4 + 1] = rt_stamp();
-
-  const int npx = a.TH * a.W;
-  int pbase[PXG];
-  bool pvalid[PXG];
-  int pyy[PXG], pxx[PXG];
-#pragma unroll
-  for (int h = 0; h < PXG; ++h) {
-    const int pl = wave * 16 * PXG + h * 16 + l16;
-    pyy[h] = pl / a.W; pxx[h] = pl % a.W;
-    pvalid[h] = (pl < npx) && (h0 + pyy[h] < a.H);
-    pbase[h] = (pyy[h] * PW + pxx[h]) * ncb;
-  }
-  f32x4_t acc[PXG][4];
-#pragma unroll
-  for (int h = 0; h < PXG; ++h)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[h][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  for (int kb = 0; kb < nkb; ++kb) {
-    const char* wcur = wbuf + (kb % NB) * wstride;
-#pragma unroll
-    for (int kk = 0; kk < CF_KB / 4; ++kk) {
-      const int cl = kk * 4 + kq;
-      if (kb * CF_KB + kk * 4 >= nchunks) break;
-      const int co_off = coff[kb * CF_KB + cl];
-      uint4 bfr[PXG];
-#pragma unroll
-      for (int h = 0; h < PXG; ++h)
-        bfr[h] = (co_off >= 0 && pvalid[h]) ? patch[pbase[h] + co_off] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        if (t < NT) {
-          const uint4 af = *reinterpret_cast<const uint4*>(wcur + (t * 16 + l16) * 256 + ((cl ^ l16) << 4));
-#pragma unroll
-          for (int h = 0; h < PXG; ++h) acc[h][t] = mfma16(af, bfr[h], acc[h][t]);
-        }
-      }
-    }
-    if (kb + NB < nkb) {                   // ring refill (layers whose weights do not fit)
-      raw_barrier();                       // every wave is done with buffer kb % NB
-      issue_wblock(kb + NB, kb % NB);
-      vm_wait(wcnt);                       // block kb+1 landed, kb+NB may fly
-      raw_barrier();
-    }
-  }
-  if (STAMP && threadIdx.x == 0) stamps[wg_lin * 4 + 2] = rt_stamp();
-
-  // ---- epilogue (as the register-staged kernel) ------------------------------
-#pragma unroll
-  for (int h = 0; h < PXG; ++h) {
-    if (!pvalid[h]) continue;
-    const long obase = ((((long)g * a.B + b) * a.H + (h0 + pyy[h])) * a.W + pxx[h]) * a.Coutp;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t >= NT) continue;
-      const int co0 = co_blk + t * 16 + kq * 4;
-      if (co0 >= a.Coutp) continue;
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float x = acc[h][t][i] + bias_v[t][i];
-        if (a.relu) x = fmaxf(x, 0.f);
-        v[i] = x;
-      }
-      for (int k = 0; k < a.n_out; ++k) {
-        uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
-        float sum[4] = {v[0], v[1], v[2], v[3]};
-        if ((a.acc_flags >> k) & 1) {
-          const uint2 old = *dst;
-          sum[0] += __uint_as_float(old.x << 16); sum[1] += __uint_as_float(old.x & 0xffff0000u);
-          sum[2] += __uint_as_float(old.y << 16); sum[3] += __uint_as_float(old.y & 0xffff0000u);
-        }
-        if (a.out_mask[k]) {
-          const uint2 m = *reinterpret_cast<const uint2*>(a.out_mask[k] + obase + co0);
-          const uint32_t mw[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sum[i] = (mw[i] != 0u && mw[i] < 0x8000u) ? sum[i] : 0.f;
-        }
-        *dst = pack4(sum);
-      }
-    }
-  }
-  if (STAMP) {
-    __syncthreads();
-    if (threadIdx.x == 0) stamps[wg_lin * 4 + 3] = rt_stamp();
-  }
-}
-
-// ---------------------------------------------------------------------------
-// conv_fwd, persistent LDS-DMA variant (single-input layers whose weights fit)
-// ---------------------------------------------------------------------------
-// Stamps of the one-tile kernels show every workgroup of a launch moving in
-// lock-step through three bursts -- all operands staged (~4 us, the whole
-// grid's loads at once), MFMAs (LDS-bound), stores -- with the memory system
-// idle during the MFMAs and vice versa, and every workgroup re-reading the
-// fold's weights from L2 (more bytes than the patches for 3x3 layers).
-// Here a workgroup keeps ALL of its fold's weight blocks resident, walks a
-// strided list of output tiles, and DMAs tile i+1's patch into the second
-// patch buffer while it runs tile i's MFMAs and stores.
-//   The DMA of the next patch is issued by inline asm: hipcc does not model it,
-//   so it does not put vmcnt(0) in front of every LDS read of the current tile
-//   (which it does for the builtin); the kernel waits for it by hand
-//   (vmcnt(0) + barrier at the end of each tile). A plain load that hipcc does
-//   track can only over-wait (counters retire in order), never under-wait.
-
-__device__ __forceinline__ void glds16_asm(const void* src, const void* lds_wave_base) {
-  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid_t*)lds_wave_base);
-  uint32_t keep;   // m0 is reserved by the compiler: save / restore it around the DMA
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
-}
-
-#define CP_MAXT 64   // tiles per workgroup (gather ids cached in LDS)
-
-template <int PXG>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG == 4 ? 3 : CF_WPE)))
-conv_fwd_pers_kernel(ConvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int nth = (a.H + a.TH - 1) / a.TH;
-  const int ntile = a.B * nth;
-  const int g = blockIdx.y;
-  const int co_blk = blockIdx.z * 64;
-  const int ph = a.KH >> 1, pw = a.KW >> 1;
-  const int PW = a.W + a.KW - 1;
-  const int ncb = a.Cinp >> 3;
-  const long img = (long)a.H * a.W * a.Cinp;
-  const int total = (a.TH + a.KH - 1) * PW * ncb;
-  const int totalr = (total + 255) & ~255;
-  const int nchunks = a.KH * a.KW * ncb;
-  const int Kdim = a.KH * a.KW * a.Cinp;
-  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
-  const int nco = min(64, a.Coutp - co_blk);
-  const int wrows = ((nco + 15) >> 4) << 4;
-  const int wstride = (((min(64, a.Coutp) + 15) >> 4) << 4) * 256;
-  char* wbuf = smem;
-  char* pbuf = smem + (size_t)nkb * wstride;                          // 2 x totalr x 16 B
-  int* coff = reinterpret_cast<int*>(pbuf + (size_t)2 * totalr * 16);
-  long* gid = reinterpret_cast<long*>(coff + ((nchunks + 4 + 1) & ~1));
-  float* sbias = reinterpret_cast<float*>(gid + CP_MAXT);              // [64]
-  const uint16_t* wg = a.w + ((long)g * a.Coutp + co_blk) * Kdim;
-  const uint16_t* in_fold = a.in[0] + (long)g * a.B * img;
-  const void* zero = g_zero16;
-  const int t0 = blockIdx.x, tstep = gridDim.x;
-  const int my_tiles = t0 < ntile ? (ntile - 1 - t0) / tstep + 1 : 0;
-
-  // gather ids of every tile this workgroup will stage (plain loads, waited below)
-  if (a.gather) {
-    for (int i = tid; i < my_tiles; i += 256) {
-      const int b = (t0 + i * tstep) / nth;
-      gid[i] = a.gather[((long)a.st->cur_step * a.G + g) * a.B + b];
-    }
-  }
-  const int kq = lane >> 4, l16 = lane & 15;
-  const int NT = (nco + 15) >> 4;
-  // bias lives in LDS: an epilogue use of a register loaded from global memory
-  // would make hipcc wait vmcnt(0), i.e. for the next tile's patch DMA
-  if (tid < 64) sbias[tid] = (a.bias && tid < nco) ? a.bias[(long)g * a.Coutp + co_blk + tid] : 0.f;
-  __syncthreads();   // gid / sbias visible (and the plain loads above retired)
-
-  const FastDiv div_ncb(ncb), div_pw(PW);
-  auto issue_patch = [&](int i, int buf) {          // tile t0 + i*tstep -> patch buffer buf
-    const int t = t0 + i * tstep;
-    const int b = t / nth, h0 = (t % nth) * a.TH;
-    const uint16_t* src0 = a.gather ? a.in[0] + gid[i] * img : in_fold + (long)b * img;
-    char* dst = pbuf + (size_t)buf * totalr * 16;
-    for (int q0 = wave * 64; q0 < total; q0 += 256) {
-      const int q = q0 + lane;
-      uint32_t pix, cbu, pr, pc;
-      div_ncb.divmod((uint32_t)q, pix, cbu);
-      div_pw.divmod(pix, pr, pc);
-      const int hh = h0 - ph + (int)pr, ww = (int)pc - pw;
-      const bool ok = q < total && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W;
-      glds16_asm(ok ? (const void*)(src0 + ((long)hh * a.W + ww) * a.Cinp + (int)cbu * 8) : zero, dst + q0 * 16);
-    }
-  };
-  // all weight blocks (resident for the whole launch)
-  for (int kb = 0; kb < nkb; ++kb) {
-    for (int q0 = wave * 64; q0 < wrows * 16; q0 += 256) {
-      const int q = q0 + lane, r = q >> 4, c = kb * CF_KB + ((q & 15) ^ (r & 15));
-      const void* src = (r < nco && c < nchunks) ? (const void*)(wg + (long)r * Kdim + c * 8) : zero;
-      glds16_asm(src, wbuf + (size_t)kb * wstride + q0 * 16);
-    }
-  }
-  if (my_tiles > 0) issue_patch(0, 0);
-  {
-    const FastDiv div_kw(a.KW);
-    for (int c = tid; c < nchunks + 4; c += 256) {
-      if (c < nchunks) {
-        uint32_t kk, cb, kh, kw;
-        div_ncb.divmod((uint32_t)c, kk, cb);
-        div_kw.divmod(kk, kh, kw);
-        coff[c] = ((int)kh * PW + (int)kw) * ncb + (int)cb;
-      } else {
-        coff[c] = -1;
-      }
-    }
-  }
-  vm_wait(0);
-  raw_barrier();
-
-  const int npx = a.TH * a.W;
-  int pbase[PXG], pyy[PXG], pxx[PXG];
-  bool pin[PXG];
-#pragma unroll
-  for (int h = 0; h < PXG; ++h) {
-    const int pl = wave * 16 * PXG + h * 16 + l16;
-    pyy[h] = pl / a.W; pxx[h] = pl % a.W;
-    pin[h] = pl < npx;
-    pbase[h] = (pyy[h] * PW + pxx[h]) * ncb;
-  }
-
-  for (int i = 0; i < my_tiles; ++i) {
-    if (i + 1 < my_tiles) issue_patch(i + 1, (i + 1) & 1);
-    const int t = t0 + i * tstep;
-    const int b = t / nth, h0 = (t % nth) * a.TH;
-    const uint4* patch = reinterpret_cast<const uint4*>(pbuf + (size_t)(i & 1) * totalr * 16);
-    bool pvalid[PXG];
-#pragma unroll
-    for (int h = 0; h < PXG; ++h) pvalid[h] = pin[h] && (h0 + pyy[h] < a.H);
-    f32x4_t acc[PXG][4];
-#pragma unroll
-    for (int h = 0; h < PXG; ++h)
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) acc[h][tt] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    for (int kb = 0; kb < nkb; ++kb) {
-      const char* wcur = wbuf + (size_t)kb * wstride;
-#pragma unroll
-      for (int kk = 0; kk < CF_KB / 4; ++kk) {
-        const int cl = kk * 4 + kq;
-        if (kb * CF_KB + kk * 4 >= nchunks) break;
-        const int co_off = coff[kb * CF_KB + cl];
-        uint4 bfr[PXG];
-#pragma unroll
-        for (int h = 0; h < PXG; ++h)
-          bfr[h] = (co_off >= 0 && pvalid[h]) ? patch[pbase[h] + co_off] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int tt = 0; tt < 4; ++tt) {
-          if (tt < NT) {
-            const uint4 af = *reinterpret_cast<const uint4*>(wcur + (tt * 16 + l16) * 256 + ((cl ^ l16) << 4));
-#pragma unroll
-            for (int h = 0; h < PXG; ++h) acc[h][tt] = mfma16(af, bfr[h], acc[h][tt]);
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int h = 0; h < PXG; ++h) {
-      if (!pvalid[h]) continue;
-      const long obase = ((((long)g * a.B + b) * a.H + (h0 + pyy[h])) * a.W + pxx[h]) * a.Coutp;
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        if (tt >= NT) continue;
-        const int co0 = co_blk + tt * 16 + kq * 4;
-        if (co0 >= a.Coutp) continue;
-        float v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float x = acc[h][tt][j] + sbias[tt * 16 + kq * 4 + j];
-          if (a.relu) x = fmaxf(x, 0.f);
-          v[j] = x;
-        }
-        for (int k = 0; k < a.n_out; ++k) {
-          uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
-          float sum[4] = {v[0], v[1], v[2], v[3]};
-          if ((a.acc_flags >> k) & 1) {
-            const uint2 old = *dst;
-            sum[0] += __uint_as_float(old.x << 16); sum[1] += __uint_as_float(old.x & 0xffff0000u);
-            sum[2] += __uint_as_float(old.y << 16); sum[3] += __uint_as_float(old.y & 0xffff0000u);
-          }
-          if (a.out_mask[k]) {
-            const uint2 m = *reinterpret_cast<const uint2*>(a.out_mask[k] + obase + co0);
-            const uint32_t mw[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) sum[j] = (mw[j] != 0u && mw[j] < 0x8000u) ? sum[j] : 0.f;
-          }
-          *dst = pack4(sum);
-        }
-      }
-    }
-    vm_wait(0);        // next patch landed (this wave's part) ...
-    raw_barrier();     // ... everyone's, and nobody still reads the buffer the next DMA overwrites
-  }
-}
-
-// ---------------------------------------------------------------------------
 // weight gradient (split-K, deterministic partials)
 // ---------------------------------------------------------------------------
 
 struct WgradArgs {
-  const uint16_t* in[4];     // summed inputs of the layer [G][B][H][W][Cinp]
+  const uint16_t* in[GT_MAXSLOT];   // input slots of the layer [Q][B][H][W][Cinp] (summed per group)
   const int64_t* gather;     // optional dataset gather (first layer)
   const StepState* st;
   const uint16_t* dz;        // ReLU-masked grad of the layer output [G][B][H][W][Coutp]
   float* part_w;             // [S][G][Coutp][Kdim]
   float* part_b;             // [S][G][Coutp]
+  const GroupRec* gtab;      // [n_groups] or null (legacy: all G groups, inputs 0..n_in-1)
   int n_in;
   int G, B, H, W, Cinp, Coutp, KH, KW, S, pps;  // pps = pixels per split (multiple of 64)
+  int ngroups;
 };
 
 #define WG_LD 72   // LDS row stride (elements) of the [32 pixel][64] tiles (144 B: 16-B aligned rows)
@@ -733,7 +331,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   const int nb = blockIdx.x;
   const int s = blockIdx.y;
   const int mblocks = (a.Coutp + 63) / 64;
-  const int g = blockIdx.z / mblocks;
+  const GroupRec gr = group_rec(a.gtab, blockIdx.z / mblocks, a.n_in, 0, 0, nullptr);
+  const int g = gr.g;
   const int co_blk = (blockIdx.z % mblocks) * 64;
   const int Kdim = a.KH * a.KW * a.Cinp;
   const int ncb = a.Cinp >> 3;
@@ -760,8 +359,10 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
     if (c_ok[r]) { div_ncb.divmod((uint32_t)(col >> 3), kk, cb); div_kw.divmod(kk, kh, kw); }
     c_kh[r] = (int)kh - (a.KH >> 1); c_kw[r] = (int)kw - (a.KW >> 1); c_cb[r] = (int)cb;
   }
-  const uint16_t* fold_in[4];
-  for (int k = 0; k < a.n_in; ++k) fold_in[k] = a.in[k] + (long)g * a.B * HW * a.Cinp;
+  const uint16_t* fold_in[GT_MAXSLOT];
+  int n_src = 0;
+  for (int k = 0; k < GT_MAXSLOT; ++k)
+    if ((gr.in_mask >> k) & 1) fold_in[n_src++] = a.in[k] + (long)g * a.B * HW * a.Cinp;
   const long fold_out = (long)g * npix * a.Coutp;
 
   const int MT = (min(64, a.Coutp - co_blk) + 15) >> 4;
@@ -800,11 +401,11 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
         const long pix_off = ((long)ih * a.W + iw) * a.Cinp + c_cb[r] * 8;
         if (gimg) {
           sl.xs[r] = *reinterpret_cast<const uint4*>(gimg + pix_off);
-        } else if (a.n_in == 1) {
+        } else if (n_src == 1) {
           sl.xs[r] = *reinterpret_cast<const uint4*>(fold_in[0] + (long)bq * HW * a.Cinp + pix_off);
         } else {
           float xsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t[8];
-          for (int k = 0; k < a.n_in; ++k) {
+          for (int k = 0; k < n_src; ++k) {
             unpack8(*reinterpret_cast<const uint4*>(fold_in[k] + (long)bq * HW * a.Cinp + pix_off), t);
 #pragma unroll
             for (int j = 0; j < 8; ++j) xsum[j] += t[j];
@@ -888,10 +489,13 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// 2x2/2 max-pool (floor) and its backward scatter
+// 2x2/2 max-pool (floor) and its backward scatter. Per group the source slot
+// is x0 or x1 (sel[g]): a stage without a DAG pools its input conv, a stage
+// with one pools its output conv.
 // ---------------------------------------------------------------------------
 
-__global__ void pool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int NB, int H, int W,
+__global__ void pool_fwd_kernel(const uint16_t* __restrict__ x0, const uint16_t* __restrict__ x1,
+                                const int* __restrict__ sel, uint16_t* __restrict__ y, int NB, int B, int H, int W,
                                 int Cp) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
   const long total = (long)NB * Ho * Wo * ncb;
@@ -901,6 +505,7 @@ __global__ void pool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __rest
     const int wo = (int)(r % Wo); r /= Wo;
     const int ho = (int)(r % Ho);
     const long n = r / Ho;
+    const uint16_t* x = (sel && sel[n / B]) ? x1 : x0;
     const uint16_t* base = x + ((n * H + 2 * ho) * W + 2 * wo) * Cp + cb * 8;
     float m[8], t[8];
     unpack8(*reinterpret_cast<const uint4*>(base), m);
@@ -914,9 +519,12 @@ __global__ void pool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __rest
   }
 }
 
-// dx[pixel] = dy[pool cell] if pixel is the cell's first maximum else 0
-__global__ void pool_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy,
-                                uint16_t* __restrict__ dx, int NB, int H, int W, int Cp, int relu_mask) {
+// dx[pixel] = dy[pool cell] if pixel is the cell's first maximum (and, with
+// relu_mask, the maximum is > 0) else 0; dx / x slot chosen per group by sel
+__global__ void pool_bwd_kernel(const uint16_t* __restrict__ x0, const uint16_t* __restrict__ x1,
+                                const int* __restrict__ sel, const uint16_t* __restrict__ dy,
+                                uint16_t* __restrict__ dx0, uint16_t* __restrict__ dx1, int NB, int B, int H, int W,
+                                int Cp, int relu_mask) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
   const long total = (long)NB * H * W * ncb;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
@@ -925,6 +533,9 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* 
     const int w = (int)(r % W); r /= W;
     const int h = (int)(r % H);
     const long n = r / H;
+    const bool s1 = sel && sel[n / B];
+    const uint16_t* x = s1 ? x1 : x0;
+    uint16_t* dx = s1 ? dx1 : dx0;
     float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int ho = h >> 1, wo = w >> 1;
     if (ho < Ho && wo < Wo) {
@@ -955,30 +566,11 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* 
 
 extern "C" {
 
-static int g_conv_mode = 0;   // single-input layers: 1 persistent / one-tile LDS-DMA, 2 one-tile LDS-DMA only, 0 register-staged (fastest measured: profiles/conv_modes.txt)
-static unsigned long long* g_conv_stamps = nullptr;   // diagnostic: stamped LDS-DMA kernel
-static int g_conv_wgs = 512;   // persistent conv: target workgroups per launch
-
-int gt_conv_set_wgs(int n) {
-  const int old = g_conv_wgs;
-  if (n > 0) g_conv_wgs = n;
-  return old;
-}
-
-int gt_conv_set_stamps(void* p) {
-  g_conv_stamps = reinterpret_cast<unsigned long long*>(p);
-  return 0;
-}
-
-int gt_conv_set_mode(int mode) {
-  const int old = g_conv_mode;
-  g_conv_mode = mode;
-  return old;
-}
-
 int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
-  if (a->Cinp % 8 || a->Coutp % 8 || a->n_in < 1 || a->n_in > 4 || a->n_out < 1 || a->n_out > 4) return -1;
+  if (a->Cinp % 8 || a->Coutp % 8) return -1;
+  if (!a->gtab && (a->n_in < 1 || a->n_in > GT_MAXSLOT || a->n_out < 1 || a->n_out > GT_MAXSLOT)) return -1;
   if (a->TH * a->W > 256 || a->TH < 1) return -2;
+  if (a->ngroups < 1) return 0;
   const int nth = (a->H + a->TH - 1) / a->TH;
   const size_t total = (size_t)(a->TH + a->KH - 1) * (a->W + a->KW - 1) * (a->Cinp / 8);
   const int nchunks = a->KH * a->KW * (a->Cinp / 8);
@@ -986,46 +578,7 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   const int wrows = ((std::min(64, a->Coutp) + 15) / 16) * 16;
   const size_t lds = (size_t)(nkb > 1 ? 2 : 1) * wrows * CF_WLD * 2 + total * 16 + 4 * ((size_t)nchunks + 4);
   if (lds > 160 * 1024) return -3;
-  dim3 grid(a->B * nth, a->G, (a->Coutp + 63) / 64);
-  if (g_conv_mode == 1 && a->n_in == 1 && !a->mask && !g_conv_stamps) {
-    // persistent kernel when every weight block + 2 patch buffers fit a 2-per-CU share
-    const size_t totalr = (total + 255) / 256 * 256;
-    const size_t lds_p = (size_t)nkb * wrows * 256 + 2 * totalr * 16 + 4 * ((size_t)nchunks + 6) + 8 * CP_MAXT + 256;
-    const int ntile = a->B * nth;
-    const int per_fold = a->G * ((a->Coutp + 63) / 64);
-    int nwg = (g_conv_wgs + per_fold - 1) / per_fold;
-    if (nwg > ntile) nwg = ntile;
-    if (nwg < (ntile + CP_MAXT - 1) / CP_MAXT) nwg = (ntile + CP_MAXT - 1) / CP_MAXT;
-    if (lds_p <= 80 * 1024 && ntile >= 2 * nwg) {
-      dim3 pg(nwg, a->G, (a->Coutp + 63) / 64);
-      if (a->TH * a->W > 64)
-        hipLaunchKernelGGL(conv_fwd_pers_kernel<2>, pg, dim3(256), lds_p, stream, *a);
-      else
-        hipLaunchKernelGGL(conv_fwd_pers_kernel<1>, pg, dim3(256), lds_p, stream, *a);
-      return (int)hipGetLastError();
-    }
-  }
-  if (g_conv_mode >= 1 && a->n_in == 1 && !a->mask) {
-    const size_t totalr = (total + 255) / 256 * 256;
-    const int fixed = (int)(totalr * 16 + 4 * ((size_t)nchunks + 4));
-    const int NB = conv_glds_nbuf(nkb, wrows * 256, fixed, (long)grid.x * grid.y * grid.z);
-    const size_t lds2 = (size_t)NB * wrows * 256 + fixed;
-    if (lds2 > 160 * 1024) return -3;
-    if (g_conv_stamps) {
-      if (a->TH * a->W > 64)
-        hipLaunchKernelGGL((conv_fwd_glds_kernel<2, true>), grid, dim3(256), lds2, stream, *a, g_conv_stamps);
-      else
-        hipLaunchKernelGGL((conv_fwd_glds_kernel<1, true>), grid, dim3(256), lds2, stream, *a, g_conv_stamps);
-      return (int)hipGetLastError();
-    }
-    if (a->TH * a->W > 128)
-      hipLaunchKernelGGL(conv_fwd_glds_kernel<4>, grid, dim3(256), lds2, stream, *a);
-    else if (a->TH * a->W > 64)
-      hipLaunchKernelGGL(conv_fwd_glds_kernel<2>, grid, dim3(256), lds2, stream, *a);
-    else
-      hipLaunchKernelGGL(conv_fwd_glds_kernel<1>, grid, dim3(256), lds2, stream, *a);
-    return (int)hipGetLastError();
-  }
+  dim3 grid(a->B * nth, a->ngroups, (a->Coutp + 63) / 64);
   if (a->TH * a->W > 128)
     hipLaunchKernelGGL(conv_fwd_kernel<4>, grid, dim3(256), lds, stream, *a);
   else if (a->TH * a->W > 64)
@@ -1036,26 +589,29 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
 }
 
 int gt_conv_wgrad(const WgradArgs* a, hipStream_t stream) {
-  if (a->Cinp % 8 || a->Coutp % 8 || a->pps % 64 || a->n_in < 1 || a->n_in > 4) return -1;
+  if (a->Cinp % 8 || a->Coutp % 8 || a->pps % 64) return -1;
+  if (!a->gtab && (a->n_in < 1 || a->n_in > GT_MAXSLOT)) return -1;
+  if (a->ngroups < 1) return 0;
   const int Kdim = a->KH * a->KW * a->Cinp;
-  dim3 grid((Kdim + (a->part_b ? 8 : 0) + 63) / 64, a->S, a->G * ((a->Coutp + 63) / 64));
+  dim3 grid((Kdim + (a->part_b ? 8 : 0) + 63) / 64, a->S, a->ngroups * ((a->Coutp + 63) / 64));
   hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 
-int gt_pool_fwd(const uint16_t* x, uint16_t* y, int NB, int H, int W, int Cp, hipStream_t stream) {
+int gt_pool_fwd(const uint16_t* x0, const uint16_t* x1, const int* sel, uint16_t* y, int NB, int B, int H, int W,
+                int Cp, hipStream_t stream) {
   const long total = (long)NB * (H / 2) * (W / 2) * (Cp / 8);
-  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x, y, NB, H, W, Cp);
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, y, NB, B, H, W, Cp);
   return (int)hipGetLastError();
 }
 
-int gt_pool_bwd(const uint16_t* x, const uint16_t* dy, uint16_t* dx, int NB, int H, int W, int Cp, int relu_mask,
-                hipStream_t stream) {
+int gt_pool_bwd(const uint16_t* x0, const uint16_t* x1, const int* sel, const uint16_t* dy, uint16_t* dx0,
+                uint16_t* dx1, int NB, int B, int H, int W, int Cp, int relu_mask, hipStream_t stream) {
   const long total = (long)NB * H * W * (Cp / 8);
-  const int blocks = (int)std::min<long>((total + 255) / 256, 8192);
-  hipLaunchKernelGGL(pool_bwd_kernel, dim3(blocks), dim3(256), 0, stream, x, dy, dx, NB, H, W, Cp,
-                     relu_mask);
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, dy, dx0, dx1, NB, B, H, W,
+                     Cp, relu_mask);
   return (int)hipGetLastError();
 }
 

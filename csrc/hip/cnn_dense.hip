@@ -49,6 +49,7 @@ struct DenseFwdArgs {
   float* plog;             // [G][Up/16][B][C] partial logits of this 16-unit tile (fixed-order sum later)
   const StepState* st;
   const int* fold_ids;     // [G]
+  const unsigned* seeds;   // [G] per-group dropout keys (population jobs) or null -> seed
   int G, B, Fp, Up;
   float drop_p;
   int train;
@@ -100,6 +101,7 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
   const uint32_t thr = (uint32_t)(a.drop_p * 4294967296.0);
   const int gstep = a.st ? a.st->global_step : 0;
   const uint32_t fid = a.fold_ids ? (uint32_t)a.fold_ids[g] : (uint32_t)g;
+  const uint32_t seed = a.seeds ? a.seeds[g] : a.seed;
   const int C = a.C;
   const float* w2 = a.w2 + ((long)g * a.Up + u0) * C;
 #pragma unroll
@@ -112,7 +114,7 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
         float z = acc[h][i] + a.bias[(long)g * a.Up + u0 + i];
         z = fmaxf(z, 0.f);
         if (a.train && a.drop_p > 0.f) {
-          const uint32_t r = hash4(a.seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)row, (uint32_t)(u0 + i));
+          const uint32_t r = hash4(seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)row, (uint32_t)(u0 + i));
           z = (r >= thr) ? z * keep_scale : 0.f;
         }
         v[i] = bf2f(f2bf(z));      // the head sees exactly the stored bf16 activation

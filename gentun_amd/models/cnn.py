@@ -104,6 +104,12 @@ class GeneticCnnModel(GentunModel):
         labels = labels_from_onehot(self.y_train)
         return stratified_kfold(labels, self.nfold, seed=self.cfg.seed)
 
+    def member(self, fold_ids=None):
+        """``(plan, folds, fold_ids)`` of this candidate for a population job."""
+        folds = self.make_folds()
+        ids = list(range(self.nfold)) if fold_ids is None else list(fold_ids)
+        return (self.model, [folds[i] for i in ids], ids)
+
     def make_jobs(self, stream=None, fold_ids=None):
         folds = self.make_folds()
         ids = list(range(self.nfold)) if fold_ids is None else list(fold_ids)

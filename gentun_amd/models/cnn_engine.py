@@ -128,53 +128,73 @@ def device_data(x, y, device, layout):
 # ---------------------------------------------------------------------------
 
 class FoldJob(object):
-    """Train one architecture on ``len(folds)`` folds concurrently.
+    """Train one architecture on ``len(folds)`` folds concurrently -- or, with
+    ``members``, several architectures ("population batching"): the groups of
+    the job are every (member, fold) pair, member-major.
 
     ``launch()`` only ENQUEUES work on ``self.stream``; ``finish()`` waits and
-    returns per-fold metrics. Subclasses supply the executor.
+    returns per-fold metrics (a dict; a list of dicts, one per member, when
+    the job was built with ``members``). Subclasses supply the executor.
+
+    Everything random is keyed by (run seed, genes, fold id), never by the
+    group's position in the job, so a candidate's result is the same alone or
+    batched with any other candidates.
     """
 
     layout = "nchw"
 
-    def __init__(self, plan, x, y, folds, cfg, device, fold_ids=None, stream=None):
-        self.plan = plan
+    def __init__(self, plan, x, y, folds, cfg, device, fold_ids=None, stream=None, members=None):
+        self.multi = members is not None
+        if members is None:
+            members = [(plan, folds, list(range(len(folds))) if fold_ids is None else list(fold_ids))]
+        members = [(p, list(f), list(range(len(f))) if ids is None else list(ids)) for p, f, ids in members]
+        if not members or any(len(f) != len(ids) or not f for _, f, ids in members):
+            raise ValueError("every member needs at least one fold and one fold id per fold")
+        self.members = members
+        self.plan = members[0][0]
         self.cfg = cfg
         self.device = torch.device(device)
-        self.folds = folds
-        self.G = len(folds)
-        self.fold_ids = list(range(self.G)) if fold_ids is None else list(fold_ids)
+        # groups = (member, fold) pairs, member-major
+        self.gmember, self.fold_ids, self.folds = [], [], []
+        for c, (_p, f, ids) in enumerate(members):
+            for fold, fid in zip(f, ids):
+                self.gmember.append(c)
+                self.fold_ids.append(int(fid))
+                self.folds.append(fold)
+        self.G = len(self.folds)
         self.data = device_data(x, y, self.device, self.layout)
         self.stream = stream if stream is not None else torch.cuda.current_stream(self.device) \
             if self.device.type == "cuda" else None
         self.B = cfg.batch_size
-        ntr = [len(tr) for tr, _ in folds]
-        nva = [len(va) for _, va in folds]
+        ntr = [len(tr) for tr, _ in self.folds]
+        nva = [len(va) for _, va in self.folds]
         self.ntrain = ntr
         self.nval = nva
         self.steps_per_epoch = int(math.ceil(max(ntr) / self.B))
-        gkey = _rng.stable_hash("cnn", cfg.seed, sorted(plan.genes.items()))
-        self.base_seed = gkey & 0x7FFFFFFFFFFF
+        self.member_seeds = [_rng.stable_hash("cnn", cfg.seed, sorted(p.genes.items())) & 0x7FFFFFFFFFFF
+                             for p, _, _ in members]
+        self.base_seed = self.member_seeds[0]
         # device index tables
         maxn = max(ntr)
         tm = np.zeros((self.G, maxn), np.int64)
-        for g, (tr, _) in enumerate(folds):
+        for g, (tr, _) in enumerate(self.folds):
             tm[g, :len(tr)] = tr
         self.train_mat = torch.from_numpy(tm).to(self.device)
         self.ntrain_t = torch.tensor(ntr, dtype=torch.int64, device=self.device)
         maxv = max(nva)
         vm = np.zeros((self.G, maxv), np.int64)
         vmask = np.zeros((self.G, maxv), np.float32)
-        for g, (_, va) in enumerate(folds):
+        for g, (_, va) in enumerate(self.folds):
             vm[g, :len(va)] = va
             vmask[g, :len(va)] = 1.0
         self.val_mat = torch.from_numpy(vm).to(self.device)
         self.val_mask = torch.from_numpy(vmask).to(self.device)
-        # One generator per fold, keyed by the fold id: a fold's data order is
-        # the same whether it is trained alone or batched with other folds.
+        # One generator per group, keyed by (member seed, fold id): a fold's data
+        # order is the same whether it is trained alone or batched with others.
         self.shuffle_gens = []
-        for fid in self.fold_ids:
+        for g, fid in enumerate(self.fold_ids):
             gen = torch.Generator(device=self.device)
-            gen.manual_seed(_rng.stable_hash(self.base_seed, "shuffle", fid) & 0x7FFFFFFF)
+            gen.manual_seed(_rng.stable_hash(self.member_seeds[self.gmember[g]], "shuffle", fid) & 0x7FFFFFFF)
             self.shuffle_gens.append(gen)
         self.epoch_idx = torch.zeros((self.steps_per_epoch, self.G, self.B), dtype=torch.int64,
                                      device=self.device)
@@ -184,10 +204,12 @@ class FoldJob(object):
     # -- shuffling -----------------------------------------------------------
     def _new_epoch_order(self):
         G, maxn = self.train_mat.shape
-        keys = torch.stack([torch.rand((maxn,), generator=gen, device=self.device) for gen in self.shuffle_gens])
-        valid = torch.arange(maxn, device=self.device)[None, :] < self.ntrain_t[:, None]
-        keys = torch.where(valid, keys, torch.full_like(keys, 2.0))
-        order = torch.argsort(keys, dim=1)
+        # each group draws exactly ntrain keys from its own generator, so its
+        # order does not depend on the other groups of the job
+        keys = torch.full((G, maxn), 2.0, device=self.device)
+        for g, gen in enumerate(self.shuffle_gens):
+            keys[g, :self.ntrain[g]].uniform_(0.0, 1.0, generator=gen)
+        order = torch.argsort(keys, dim=1, stable=True)
         perm = torch.gather(self.train_mat, 1, order)
         pos = torch.arange(self.steps_per_epoch * self.B, device=self.device)[None, :] % self.ntrain_t[:, None]
         idx = torch.gather(perm, 1, pos).view(G, self.steps_per_epoch, self.B)
@@ -195,7 +217,7 @@ class FoldJob(object):
         self.step_ctr.zero_()
 
     def _fold_seed(self, g):
-        return _rng.stable_hash(self.base_seed, "init", self.fold_ids[g]) & 0x7FFFFFFFFFFF
+        return _rng.stable_hash(self.member_seeds[self.gmember[g]], "init", self.fold_ids[g]) & 0x7FFFFFFFFFFF
 
     # -- to implement ----------------------------------------------------------
     def init_params(self):
@@ -270,12 +292,17 @@ class FoldJob(object):
             self._done.synchronize()
         loss, binc, catc = (t.detach().float().cpu().numpy() for t in self._eval)
         nval = np.asarray(self.nval, np.float64)
-        self.result = {
+        per = {
             "val_loss": (loss / nval).tolist(),
             "binary_accuracy": (binc / (nval * self.data.classes)).tolist(),
             "categorical_accuracy": (catc / nval).tolist(),
         }
+        out = []
+        for c in range(len(self.members)):
+            gs = [g for g in range(self.G) if self.gmember[g] == c]
+            out.append({k: [v[g] for g in gs] for k, v in per.items()})
         self._graph = None
+        self.result = out if self.multi else out[0]
         return self.result
 
 
@@ -315,6 +342,8 @@ class TorchFoldJob(FoldJob):
 
     def __init__(self, *a, **kw):
         super(TorchFoldJob, self).__init__(*a, **kw)
+        if len(self.members) != 1:
+            raise ValueError("the torch executor trains one architecture per job")
         plan, G = self.plan, self.G
         shapes = []
         for st in plan.convs():
@@ -472,9 +501,20 @@ def make_job(backend, plan, x, y, folds, cfg, device, fold_ids=None, stream=None
     if backend == "torch":
         return TorchFoldJob(plan, x, y, folds, cfg, device, fold_ids=fold_ids, stream=stream)
     if backend == "hip":
-        from .cnn_hip import HipFoldJob
-        return HipFoldJob(plan, x, y, folds, cfg, device, fold_ids=fold_ids, stream=stream)
+        from .cnn_hip import HipPopJob
+        return HipPopJob(plan, x, y, folds, cfg, device, fold_ids=fold_ids, stream=stream)
     raise ValueError("unknown backend {!r}".format(backend))
+
+
+def make_population_job(backend, members, x, y, cfg, device, stream=None):
+    """One job training several architectures at once: ``members`` is a list
+    of ``(plan, folds, fold_ids)``; ``finish()`` returns one result dict per
+    member. The HIP executor batches them into shared launches; the torch
+    oracle has no such mode and is rejected."""
+    if backend != "hip":
+        raise ValueError("population batching needs the hip backend")
+    from .cnn_hip import HipPopJob
+    return HipPopJob(None, x, y, None, cfg, device, stream=stream, members=members)
 
 
 def default_backend(device):

@@ -1,21 +1,34 @@
-"""HIP executor of the fold-batched Genetic-CNN train step (MI355X path).
+"""HIP executor of the Genetic-CNN train step (MI355X path), population-batched.
 
-Compiles a decoded :class:`~gentun_amd.models.genome.Plan` into a fixed
-sequence of hand-written gfx950 kernel launches (csrc/hip/cnn_conv.hip,
-csrc/hip/cnn_dense.hip) over buffers allocated once per job:
+One job trains ``Q`` groups at once, a group being one cross-validation fold
+of one candidate architecture ("member"). Every candidate of a Genetic-CNN
+search space shares the same *superset* network -- per stage an input conv,
+``K`` DAG node convs, an output conv and a 2x2 pool -- and differs only in
+which nodes exist and which node outputs each node sums
+(gentun/models/keras_models.py:46-118). So instead of one launch per layer
+per candidate, the job issues ONE launch per superset layer for all groups
+that have it: activations live in slot tensors ``[Q][B][H][W][C]``, and a
+per-launch group table (csrc/hip/cnn_conv.hip ``GroupRec``) tells each
+group which slots to sum as input, where to write / accumulate its output
+and where to apply a ReLU mask. Launch count per step is independent of the
+population size and each launch is ``Q`` times larger -- the size at which
+256 CUs fill (SURVEY.md §7.3 hard part 1).
 
-  step_begin -> conv_fwd x L (first one gathers the batch from the
-  device-resident dataset) / pool_fwd -> dense_fwd (+ReLU+dropout) -> head
-  (softmax + loss grad + dW2/db2/db1) -> dense_dgrad -> dense_wgrad_adam
-  (W1 gradient consumed in registers by Adam) -> reverse plan: pool_bwd,
-  conv_wgrad (split-K partials), conv dgrad (= conv_fwd with flipped weights,
-  ReLU mask and DAG fan-out accumulation fused) -> adam_segments.
+Step (one HIP graph, replayed epochs x steps times):
 
-Layouts: activations NHWC bf16 ``[G][B][H][W][Cp]`` with Cp = C rounded up to
-8; fp32 master weights in padded layouts whose padding is zero and stays
-zero (zero inputs produce zero gradients); bf16 weight copies written by the
-optimizer for the next step. Fold index ``G`` is the outermost dimension of
-everything, so one launch trains all folds of the candidate.
+  step_begin -> per stage: conv IN (first stage gathers the batch from the
+  device-resident dataset), conv N_0..N_{K-1} (only groups whose node is
+  active; fused N-ary Add of the node's predecessors), conv OUT (groups
+  whose stage has a DAG), pool (per group: OUT or, without a DAG, IN) ->
+  dense_fwd (+ReLU+dropout+partial logits) -> head (softmax + loss grad +
+  dW2/db2/db1) -> dense_dgrad -> dense_wgrad_adam -> reverse: pool_bwd,
+  per layer conv_wgrad (split-K partials) + dgrad (= conv_fwd with flipped
+  weights, DAG gradient fan-out accumulation and ReLU masks fused per group)
+  -> adam_segments (reduces the partials in fixed order).
+
+Layouts: activations NHWC bf16 with channels padded to 8; fp32 master weights
+in padded layouts whose padding is zero and stays zero; bf16 weight copies
+written by the optimizer. Groups are member-major, fold-minor.
 """
 
 import math
@@ -26,7 +39,7 @@ import torch
 from ..ops import cnn_kernels as K
 from ..utils import rng as _rng
 from .cnn_engine import FoldJob
-from .genome import ConvSpec
+from .genome import decode_stage
 
 
 def pad8(c):
@@ -38,75 +51,165 @@ def round_up(x, m):
 
 
 class _Layer(object):
+    """One superset conv layer ('in', 'node' j or 'out' of a stage)."""
     pass
 
 
-class HipFoldJob(FoldJob):
+def _stage_topology(bits, nodes):
+    """(active, in_sets, sinks) of one stage of one candidate: ``in_sets[j]``
+    = input slot indices of node j (0 = stage input conv, i + 1 = node i)."""
+    if not any(b == '1' for b in bits):
+        return False, None, None
+    preds, _succs, active, outputs = decode_stage(bits, nodes)
+    in_sets = [None] * nodes
+    for j in range(nodes):
+        if active[j]:
+            in_sets[j] = [0] if not preds[j] else [p + 1 for p in preds[j]]
+    return True, in_sets, list(outputs)
+
+
+def _mask(slots):
+    m = 0
+    for k in slots:
+        m |= 1 << k
+    return m
+
+
+class HipPopJob(FoldJob):
     layout = "nhwc8"
 
     def __init__(self, *a, **kw):
-        super(HipFoldJob, self).__init__(*a, **kw)
+        super(HipPopJob, self).__init__(*a, **kw)
         if self.device.type != "cuda":
             raise RuntimeError("the HIP backend needs a GPU device")
         self.L = K.lib()
         if self.cfg.dtype != "bf16":
             raise ValueError("HIP backend computes in bf16 MFMA with fp32 master weights (dtype='bf16')")
-        plan, G, B, dev = self.plan, self.G, self.B, self.device
-        h0, w0, c0 = plan.input_shape
+        p0 = self.plan
+        for p, _, _ in self.members:
+            if (p.nodes, p.input_shape, p.kernels_per_layer, p.kernel_sizes, p.dense_units, p.classes) != \
+                    (p0.nodes, p0.input_shape, p0.kernels_per_layer, p0.kernel_sizes, p0.dense_units, p0.classes):
+                raise ValueError("population members must share the search space (only genes may differ)")
+        Q, B, dev = self.G, self.B, self.device
+        self.Q = Q
+        h0, w0, c0 = p0.input_shape
         if self.data.x.shape[-1] != pad8(c0):
             raise ValueError("dataset channels do not match the plan")
-        self.classes = plan.classes
-        if plan.classes > 16:
+        self.classes = p0.classes
+        if p0.classes > 16:
             raise ValueError("HIP head kernel supports at most 16 classes")
         if B > 64:
             raise ValueError("HIP head kernel supports batch_size <= 64")
-        # ---- activations -----------------------------------------------------
-        self.shapes = {"input": (h0, w0, pad8(c0))}
+        if max(p0.nodes) > K.MAXSLOT:
+            raise ValueError("at most {} nodes per stage".format(K.MAXSLOT))
+        self._build_topology()
+        self._allocate()
+        self.state = torch.zeros(8, dtype=torch.int32, device=dev)
+        self.state_f = self.state.view(torch.float32)
+        self.step_ctr = self.state[0:1]          # StepState.step_ctr (zeroed per epoch by the driver)
+        self.eval_state = torch.zeros(8, dtype=torch.int32, device=dev)
+        self.fold_ids_t = torch.tensor(self.fold_ids, dtype=torch.int32, device=dev)
+        seeds = [_rng.stable_hash(self.member_seeds[self.gmember[q]], "dropout") & 0xFFFFFFFF for q in range(Q)]
+        self.drop_seeds_t = torch.tensor(np.asarray(seeds, np.uint32).view(np.int32), device=dev)
+        self._keep = []          # device group tables referenced by argument structs
+        self._build_adam_table()
+        self._build_args()
+
+    # ------------------------------------------------------------ topology
+    def _build_topology(self):
+        p0, Q = self.plan, self.Q
+        h0, w0, c0 = p0.input_shape
+        # per member, per stage: (active, in_sets, sinks)
+        topo = []
+        for p, _, _ in self.members:
+            topo.append([_stage_topology(p.genes["S_{}".format(s + 1)], p.nodes[s])
+                         for s in range(len(p.kernels_per_layer))])
+        self.stages = []
         self.layers = []
-        for st in plan.steps:
-            hs, ws = plan.stage_hw(st.stage)
-            if isinstance(st, ConvSpec):
+        cin = c0
+        x_slot = "input"
+        for s, cout in enumerate(p0.kernels_per_layer):
+            H, W = h0 >> s, w0 >> s
+            Kn = p0.nodes[s]
+            kh, kw = p0.kernel_sizes[s]
+            if kh % 2 == 0 or kw % 2 == 0:
+                raise ValueError("only odd kernel sizes are supported ('same' padding)")
+            pre = "s{}".format(s + 1)
+            st = {"s": s, "H": H, "W": W, "x_slot": x_slot, "in": pre + "_in", "out": pre + "_out",
+                  "pool": pre + "_pool", "layers": []}
+            # stage-active flag per group
+            st["active"] = [topo[self.gmember[q]][s][0] for q in range(Q)]
+
+            def add(name, kind, j, cin_, k_, slots, rows):
+                if not rows:
+                    return
                 L = _Layer()
-                L.spec = st
-                L.H, L.W = hs, ws
-                L.cin, L.cout = st.cin, st.cout
-                L.cinp, L.coutp = pad8(st.cin), pad8(st.cout)
-                L.KH, L.KW = st.k
+                L.name, L.kind, L.j, L.stage = name, kind, j, s
+                L.H, L.W = H, W
+                L.cin, L.cout = cin_, cout
+                L.cinp, L.coutp = pad8(cin_), pad8(cout)
+                L.KH, L.KW = k_
                 L.Kdim = L.KH * L.KW * L.cinp
-                L.TH = K.conv_tile_rows(L.H, L.W)
-                npix = B * L.H * L.W
-                L.pps, L.S = K.wgrad_split(npix, L.Kdim, L.coutp, G)
-                self.shapes[st.name] = (L.H, L.W, L.coutp)
+                L.TH = K.conv_tile_rows(H, W)
+                L.pps, L.S = K.wgrad_split(self.B * H * W, L.Kdim, L.coutp)
+                L.slots = slots            # input slot names, bit k = slots[k]
+                L.rows = rows              # [(q, in_mask)] ascending q
+                st["layers"].append(L)
                 self.layers.append(L)
-            else:
-                src = st.srcs[0]
-                hh, ww, cc = self.shapes[src]
-                self.shapes[st.name] = (hh // 2, ww // 2, cc)
-        last = plan.steps[-1].name
-        hs, ws, cp = self.shapes[last]
-        self.last = last
-        self.Fp = hs * ws * cp
-        self.Up = round_up(plan.dense_units, 64)
-        self.act = {}
-        self.grad = {}
+
+            add(st["in"], "in", -1, cin, (kh, kw), [x_slot], [(q, 1) for q in range(Q)])
+            node_slots = [st["in"]] + ["{}_n{}".format(pre, i) for i in range(Kn)]
+            for j in range(Kn):
+                rows = []
+                for q in range(Q):
+                    act, in_sets, _ = topo[self.gmember[q]][s]
+                    if act and in_sets[j] is not None:
+                        rows.append((q, _mask(in_sets[j])))
+                add("{}_n{}".format(pre, j), "node", j, cout, (3, 3), node_slots[:j + 1], rows)
+            rows = []
+            for q in range(Q):
+                act, _, sinks = topo[self.gmember[q]][s]
+                if act:
+                    rows.append((q, _mask(sinks)))
+            add(st["out"], "out", -1, cout, (3, 3), node_slots[1:], rows)
+            st["has_out"] = bool(rows)
+            self.stages.append(st)
+            x_slot = st["pool"]
+            cin = cout
+        self.last = x_slot
+        hs, ws = h0 >> len(p0.kernels_per_layer), w0 >> len(p0.kernels_per_layer)
+        if hs < 1 or ws < 1:
+            raise ValueError("input too small for the pooling stages")
+        self.final_hw = (hs, ws)
+        self.final_cp = pad8(p0.kernels_per_layer[-1])
+
+    # ------------------------------------------------------------ buffers
+    def _allocate(self):
+        Q, B, dev, p0 = self.Q, self.B, self.device, self.plan
+        self.shapes = {}
+        for st in self.stages:
+            for L in st["layers"]:
+                self.shapes[L.name] = (L.H, L.W, L.coutp)
+            self.shapes[st["pool"]] = (st["H"] // 2, st["W"] // 2, pad8(p0.kernels_per_layer[st["s"]]))
+        self.act, self.grad = {}, {}
         for name, (hh, ww, cc) in self.shapes.items():
-            if name == "input":
-                continue
-            self.act[name] = torch.zeros((G, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
-            self.grad[name] = torch.zeros((G, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
-        self.hdrop = torch.zeros((G, B, self.Up), dtype=torch.bfloat16, device=dev)
-        self.dH = torch.zeros((G, B, self.Up), dtype=torch.float32, device=dev)
-        self.dz_head = torch.zeros((G, B, plan.classes), dtype=torch.float32, device=dev)
-        self.plog = torch.zeros((G, self.Up // 16, B, plan.classes), dtype=torch.float32, device=dev)
-        # ---- parameters (flat fp32 master + Adam moments) --------------------
+            self.act[name] = torch.zeros((Q, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
+            self.grad[name] = torch.zeros((Q, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
+        hs, ws = self.final_hw
+        self.Fp = hs * ws * self.final_cp
+        self.Up = round_up(p0.dense_units, 64)
+        self.hdrop = torch.zeros((Q, B, self.Up), dtype=torch.bfloat16, device=dev)
+        self.dH = torch.zeros((Q, B, self.Up), dtype=torch.float32, device=dev)
+        self.dz_head = torch.zeros((Q, B, self.classes), dtype=torch.float32, device=dev)
+        self.plog = torch.zeros((Q, self.Up // 16, B, self.classes), dtype=torch.float32, device=dev)
         segs = []
         for L in self.layers:
-            segs.append(("w", L, (G, L.coutp, L.KH, L.KW, L.cinp)))
-            segs.append(("b", L, (G, L.coutp)))
-        segs.append(("W1", None, (G, self.Fp, self.Up)))
-        segs.append(("b1", None, (G, self.Up)))
-        segs.append(("W2", None, (G, self.Up, self.classes)))
-        segs.append(("b2", None, (G, self.classes)))
+            segs.append(("w", L, (Q, L.coutp, L.KH, L.KW, L.cinp)))
+            segs.append(("b", L, (Q, L.coutp)))
+        segs.append(("W1", None, (Q, self.Fp, self.Up)))
+        segs.append(("b1", None, (Q, self.Up)))
+        segs.append(("W2", None, (Q, self.Up, self.classes)))
+        segs.append(("b2", None, (Q, self.classes)))
         total = sum(int(np.prod(s)) for _, _, s in segs)
         self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
         self.m = torch.zeros_like(self.flat)
@@ -123,28 +226,27 @@ class HipFoldJob(FoldJob):
                 self.views[kind] = view
             off += n
         for L in self.layers:
-            L.w_bf = torch.zeros((G, L.coutp, L.KH, L.KW, L.cinp), dtype=torch.bfloat16, device=dev)
-            L.wT_bf = torch.zeros((G, L.cinp, L.KH, L.KW, L.coutp), dtype=torch.bfloat16, device=dev)
-            L.part_w = torch.zeros((L.S, G, L.coutp, L.Kdim), dtype=torch.float32, device=dev)  # split-K partials
-            L.part_b = torch.zeros((L.S, G, L.coutp), dtype=torch.float32, device=dev)
-        self.w1t_bf = torch.zeros((G, self.Up, self.Fp), dtype=torch.bfloat16, device=dev)
-        self.gW2 = torch.zeros((G, self.Up, self.classes), dtype=torch.float32, device=dev)
-        self.gb2 = torch.zeros((G, self.classes), dtype=torch.float32, device=dev)
-        self.gb1 = torch.zeros((G, self.Up), dtype=torch.float32, device=dev)
-        # ---- step state ------------------------------------------------------
-        self.state = torch.zeros(8, dtype=torch.int32, device=dev)
-        self.state_f = self.state.view(torch.float32)
-        self.step_ctr = self.state[0:1]
-        self.eval_state = torch.zeros(8, dtype=torch.int32, device=dev)
-        self.fold_ids_t = torch.tensor(self.fold_ids, dtype=torch.int32, device=dev)
-        self.drop_seed = _rng.stable_hash(self.base_seed, "dropout") & 0xFFFFFFFF
-        self._build_adam_table()
-        self._build_args()
+            L.w_bf = torch.zeros((Q, L.coutp, L.KH, L.KW, L.cinp), dtype=torch.bfloat16, device=dev)
+            L.wT_bf = torch.zeros((Q, L.cinp, L.KH, L.KW, L.coutp), dtype=torch.bfloat16, device=dev)
+            L.part_w = torch.zeros((L.S, Q, L.coutp, L.Kdim), dtype=torch.float32, device=dev)   # split-K partials
+            L.part_b = torch.zeros((L.S, Q, L.coutp), dtype=torch.float32, device=dev)
+        self.w1t_bf = torch.zeros((Q, self.Up, self.Fp), dtype=torch.bfloat16, device=dev)
+        self.gW2 = torch.zeros((Q, self.Up, self.classes), dtype=torch.float32, device=dev)
+        self.gb2 = torch.zeros((Q, self.classes), dtype=torch.float32, device=dev)
+        self.gb1 = torch.zeros((Q, self.Up), dtype=torch.float32, device=dev)
 
-    # ------------------------------------------------------------------ setup
+    def _gtab(self, rows):
+        """Device GroupRec table from ``[(g, in_mask, out_flags)]``."""
+        arr = np.zeros((max(1, len(rows)), 4), np.int32)
+        for i, (g, im, of) in enumerate(rows):
+            arr[i, 0], arr[i, 1], arr[i, 2] = g, im, of
+        t = torch.from_numpy(arr).to(self.device)
+        self._keep.append(t)
+        return t
+
+    # ------------------------------------------------------------ setup
     def _build_adam_table(self):
         segs, blocks = [], []
-        keep = []
 
         def add(p, m, v, g, S, gstride, bf=None, bfT=None, tdims=None):
             sg = K.AdamSeg()
@@ -161,12 +263,14 @@ class HipFoldJob(FoldJob):
             for o in range(0, p.numel(), 256):
                 blocks.append((idx, o))
 
+        # conv layers: one segment per (layer, group that has the layer)
         for L in self.layers:
-            p, m, v = L.w
-            add(p, m, v, L.part_w, L.S, L.part_w[0].numel(), bf=L.w_bf, bfT=L.wT_bf,
-                tdims=(self.G, L.coutp, L.KH, L.KW, L.cinp))
-            p, m, v = L.b
-            add(p, m, v, L.part_b, L.S, L.part_b[0].numel())
+            for q, _ in L.rows:
+                p, m, v = (t[q] for t in L.w)
+                add(p, m, v, L.part_w[0, q], L.S, L.part_w[0].numel(), bf=L.w_bf[q], bfT=L.wT_bf[q],
+                    tdims=(1, L.coutp, L.KH, L.KW, L.cinp))
+                p, m, v = (t[q] for t in L.b)
+                add(p, m, v, L.part_b[0, q], L.S, L.part_b[0].numel())
         for name, g in (("b1", self.gb1), ("W2", self.gW2), ("b2", self.gb2)):
             p, m, v = self.views[name]
             add(p, m, v, g, 1, g.numel())
@@ -175,49 +279,60 @@ class HipFoldJob(FoldJob):
         self.adam_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self.adam_blocks = torch.tensor(np.asarray(blocks, np.int32).reshape(-1, 2), device=self.device)
         self.adam_nblocks = len(blocks)
-        del keep
 
-    def _conv_args(self, L, inputs, outs, acc_flags, w, bias, relu, mask=None, gather=None, st=None, Bn=None):
+    def _conv_args(self, L, in_ptrs, out_ptrs, mask_ptrs, w, bias, relu, rows, gather=None, Cinp=None, Coutp=None):
         a = K.ConvArgs()
-        for i, t in enumerate(inputs):
-            a.inp[i] = t.data_ptr()
-        for i, t in enumerate(outs):
-            a.out[i] = t.data_ptr()
-        a.n_in, a.n_out, a.acc_flags, a.relu = len(inputs), len(outs), acc_flags, relu
-        a.mask = mask.data_ptr() if mask is not None else 0
-        a.gather = gather if gather is not None else 0
-        a.st = st.data_ptr() if st is not None else self.state.data_ptr()
+        for i, p in enumerate(in_ptrs):
+            a.inp[i] = p
+        for i, p in enumerate(out_ptrs):
+            a.out[i] = p
+        for i, p in enumerate(mask_ptrs):
+            a.out_mask[i] = p
+        a.relu = relu
+        a.gather = gather or 0
+        a.st = self.state.data_ptr()
         a.w = w.data_ptr()
         a.bias = bias.data_ptr() if bias is not None else 0
-        a.G, a.B, a.H, a.W = self.G, Bn or self.B, L.H, L.W
+        a.gtab = self._gtab(rows).data_ptr()
+        a.ngroups = len(rows)
+        a.G, a.B, a.H, a.W = self.Q, self.B, L.H, L.W
+        a.Cinp = L.cinp if Cinp is None else Cinp
+        a.Coutp = L.coutp if Coutp is None else Coutp
+        a.KH, a.KW, a.TH = L.KH, L.KW, L.TH
         return a
+
+    def _slot_ptr(self, name, grad=False):
+        if name == "input":
+            return self.data.x.data_ptr()
+        t = (self.grad if grad else self.act).get(name)
+        return t.data_ptr() if t is not None else 0       # a node no group has: never selected
 
     def _build_args(self):
         """Pre-build every launch's argument struct (pointers are fixed)."""
-        G, B = self.G, self.B
-        data = self.data.x
+        Q, B = self.Q, self.B
         gather_train = self.epoch_idx.data_ptr()
         self.fwd_ops = []
-        for st in self.plan.steps:
-            if isinstance(st, ConvSpec):
-                L = next(l for l in self.layers if l.spec is st)
-                if st.inputs == ["input"]:
-                    ins, gather = [data], gather_train
-                else:
-                    ins, gather = [self.act[n] for n in st.inputs], None
-                a = self._conv_args(L, ins, [self.act[st.name]], 0, L.w_bf, L.b[0], 1, gather=gather)
-                a.Cinp, a.Coutp, a.KH, a.KW, a.TH = L.cinp, L.coutp, L.KH, L.KW, L.TH
+        for st in self.stages:
+            for L in st["layers"]:
+                first = L.slots == ["input"]
+                a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [self.act[L.name].data_ptr()], [],
+                                    L.w_bf, L.b[0], 1, [(q, im, 1) for q, im in L.rows],
+                                    gather=gather_train if first else None)
                 self.fwd_ops.append(("conv", a, L))
-            else:
-                hh, ww, cc = self.shapes[st.srcs[0]]
-                self.fwd_ops.append(("pool", (self.act[st.srcs[0]], self.act[st.name], G * B, hh, ww, cc), None))
-        # head
+            sel = torch.tensor([1 if act else 0 for act in st["active"]], dtype=torch.int32, device=self.device)
+            self._keep.append(sel)
+            x1 = self.act[st["out"]] if st["has_out"] else self.act[st["in"]]
+            hh, ww, cc = self.shapes[st["in"]]
+            st["sel"] = sel
+            self.fwd_ops.append(("pool", (self.act[st["in"]].data_ptr(), x1.data_ptr(), sel.data_ptr(),
+                                          self.act[st["pool"]].data_ptr(), Q * B, B, hh, ww, cc), None))
+        # ---- head
         df = K.DenseFwdArgs()
         df.x, df.wt, df.bias, df.out = (self.act[self.last].data_ptr(), self.w1t_bf.data_ptr(),
                                         self.views["b1"][0].data_ptr(), self.hdrop.data_ptr())
-        df.st, df.fold_ids = self.state.data_ptr(), self.fold_ids_t.data_ptr()
-        df.G, df.B, df.Fp, df.Up = G, B, self.Fp, self.Up
-        df.drop_p, df.train, df.seed = self.cfg.dropout, 1, self.drop_seed
+        df.st, df.fold_ids, df.seeds = self.state.data_ptr(), self.fold_ids_t.data_ptr(), self.drop_seeds_t.data_ptr()
+        df.G, df.B, df.Fp, df.Up = Q, B, self.Fp, self.Up
+        df.drop_p, df.train, df.seed = self.cfg.dropout, 1, 0
         df.w2, df.plog, df.C = self.views["W2"][0].data_ptr(), self.plog.data_ptr(), self.classes
         self.dense_fwd_args = df
         hd = K.HeadArgs()
@@ -227,70 +342,75 @@ class HipFoldJob(FoldJob):
         hd.eval_out = 0
         hd.dz = self.dz_head.data_ptr()
         hd.plog = self.plog.data_ptr()
-        hd.G, hd.B, hd.Up, hd.C = G, B, self.Up, self.classes
+        hd.G, hd.B, hd.Up, hd.C = Q, B, self.Up, self.classes
         hd.loss_ce = 1 if self.cfg.loss == "ce" else 0
         hd.drop_scale = 1.0 / (1.0 - self.cfg.dropout) if self.cfg.dropout < 1 else 0.0
         hd.eval = 0
         self.head_args = hd
         dd = K.DenseDgradArgs()
         dd.dH, dd.w1, dd.dx = self.dH.data_ptr(), self.views["W1"][0].data_ptr(), self.grad[self.last].data_ptr()
-        dd.G, dd.B, dd.Fp, dd.Up = G, B, self.Fp, self.Up
+        dd.G, dd.B, dd.Fp, dd.Up = Q, B, self.Fp, self.Up
         self.dense_dgrad_args = dd
         dw = K.DenseWgradAdamArgs()
         p, m, v = self.views["W1"]
         dw.x, dw.dH, dw.p, dw.m, dw.v = self.act[self.last].data_ptr(), self.dH.data_ptr(), p.data_ptr(), \
             m.data_ptr(), v.data_ptr()
         dw.wt, dw.st = self.w1t_bf.data_ptr(), self.state.data_ptr()
-        dw.G, dw.B, dw.Fp, dw.Up = G, B, self.Fp, self.Up
+        dw.G, dw.B, dw.Fp, dw.Up = Q, B, self.Fp, self.Up
         self.dense_wgrad_args = dw
-        # backward: the LAST writer of a ReLU layer's gradient (its first consumer
-        # in forward order) applies the ReLU mask, so every later reader (wgrad,
-        # dgrad) consumes dz = dy * (y > 0) directly
+        # ---- backward. Per group and slot: the FIRST consumer in forward order
+        # is the LAST writer of the slot's gradient and applies its ReLU mask;
+        # earlier writers accumulate.
         first_consumer = {}
-        for st in self.plan.steps:
-            srcs = st.inputs if isinstance(st, ConvSpec) else st.srcs
-            for n in srcs:
-                first_consumer.setdefault(n, st.name)
-        relu_out = {st.name for st in self.plan.steps if isinstance(st, ConvSpec)}
-        self.bwd_ops = []
+        for L in self.layers:
+            for q, im in L.rows:
+                for k, n in enumerate(L.slots):
+                    if (im >> k) & 1:
+                        first_consumer.setdefault((q, n), L.name)
         written = set()
-        for st in reversed(self.plan.steps):
-            if isinstance(st, ConvSpec):
-                L = next(l for l in self.layers if l.spec is st)
+        self.bwd_ops = []
+        for st in reversed(self.stages):
+            hh, ww, cc = self.shapes[st["in"]]
+            x1 = st["out"] if st["has_out"] else st["in"]
+            self.bwd_ops.append(("pool_bwd", (self.act[st["in"]].data_ptr(), self.act[x1].data_ptr(),
+                                              st["sel"].data_ptr(), self.grad[st["pool"]].data_ptr(),
+                                              self.grad[st["in"]].data_ptr(), self.grad[x1].data_ptr(),
+                                              Q * B, B, hh, ww, cc, 1), None))
+            for q in range(Q):
+                written.add((q, st["out"] if st["active"][q] else st["in"]))
+            for L in reversed(st["layers"]):
+                first = L.slots == ["input"]
                 wa = K.WgradArgs()
-                first = st.inputs == ["input"]
-                ins = [data] if first else [self.act[n] for n in st.inputs]
-                for i, t in enumerate(ins):
-                    wa.inp[i] = t.data_ptr()
-                wa.n_in = len(ins)
+                for i, n in enumerate(L.slots):
+                    wa.inp[i] = self._slot_ptr(n)
                 wa.gather = gather_train if first else 0
                 wa.st = self.state.data_ptr()
-                wa.dz = self.grad[st.name].data_ptr()
+                wa.dz = self.grad[L.name].data_ptr()
                 wa.part_w, wa.part_b = L.part_w.data_ptr(), L.part_b.data_ptr()
-                wa.G, wa.B, wa.H, wa.W = G, B, L.H, L.W
+                wa.gtab = self._gtab([(q, im, 0) for q, im in L.rows]).data_ptr()
+                wa.ngroups = len(L.rows)
+                wa.G, wa.B, wa.H, wa.W = Q, B, L.H, L.W
                 wa.Cinp, wa.Coutp, wa.KH, wa.KW, wa.S, wa.pps = L.cinp, L.coutp, L.KH, L.KW, L.S, L.pps
                 self.bwd_ops.append(("wgrad", wa, L))
-                if not first:
-                    outs = [self.grad[n] for n in st.inputs]
-                    flags = 0
-                    for i, n in enumerate(st.inputs):
-                        if n in written:
-                            flags |= 1 << i
-                        written.add(n)
-                    a = self._conv_args(L, [self.grad[st.name]], outs, flags, L.wT_bf, None, 0)
-                    for i, n in enumerate(st.inputs):
-                        if n in relu_out and first_consumer[n] == st.name:
-                            a.out_mask[i] = self.act[n].data_ptr()
-                    a.Cinp, a.Coutp, a.KH, a.KW, a.TH = L.coutp, L.cinp, L.KH, L.KW, L.TH
-                    self.bwd_ops.append(("conv", a, L))
-            else:
-                src = st.srcs[0]
-                if src in written:
-                    raise RuntimeError("pool input with several consumers is not supported")
-                written.add(src)
-                hh, ww, cc = self.shapes[src]
-                self.bwd_ops.append(("pool_bwd", (self.act[src], self.grad[st.name], self.grad[src],
-                                                  G * B, hh, ww, cc, int(src in relu_out)), None))
+                if first:
+                    continue
+                rows = []
+                for q, im in L.rows:
+                    of = 0
+                    for k, n in enumerate(L.slots):
+                        if not (im >> k) & 1:
+                            continue
+                        of |= 1 << k
+                        if (q, n) in written:
+                            of |= 1 << (8 + k)
+                        if n in self.act and L.kind != "in" and first_consumer.get((q, n)) == L.name:
+                            of |= 1 << (16 + k)
+                        written.add((q, n))
+                    rows.append((q, 1, of))
+                a = self._conv_args(L, [self.grad[L.name].data_ptr()], [self._slot_ptr(n, grad=True) for n in L.slots],
+                                    [self._slot_ptr(n) for n in L.slots], L.wT_bf, None, 0, rows,
+                                    Cinp=L.coutp, Coutp=L.cinp)
+                self.bwd_ops.append(("conv", a, L))
         aa = K.AdamArgs()
         aa.segs, aa.blocks, aa.st = self.adam_segs.data_ptr(), self.adam_blocks.data_ptr(), self.state.data_ptr()
         self.adam_args = aa
@@ -298,18 +418,21 @@ class HipFoldJob(FoldJob):
     # -------------------------------------------------------------- protocol
     def _build_init_table(self):
         """Segment table of the one-launch Philox Glorot initialiser (K11):
-        every conv kernel, W1 and W2 of every fold; biases stay zero."""
-        G = self.G
+        every conv kernel, W1 and W2 of every group; biases stay zero. Keys are
+        (member seed, fold id, tensor name), so values do not depend on the
+        batch composition."""
+        Q = self.Q
         segs, blocks, seeds = [], [], []
 
         def add(t, d, r, fan_in, fan_out, name):
-            assert t.is_contiguous() and t.numel() == G * int(np.prod(d))
-            seeds.append([_rng.stable_hash(self._fold_seed(g), name) & 0x7FFFFFFFFFFFFFFF for g in range(G)])
+            assert t.is_contiguous() and t.numel() == Q * int(np.prod(d))
+            seeds.append([_rng.stable_hash(self._fold_seed(g), name) & 0x7FFFFFFFFFFFFFFF for g in range(Q)])
             sg = K.InitSeg()
             sg.p = t.data_ptr()
             for i in range(4):
                 sg.d[i], sg.r[i] = int(d[i]), int(r[i])
-            sg.G, sg.tag = G, len(segs)
+            sg.G = Q
+            sg.tag = _rng.stable_hash("tag", name) & 0x7FFFFFFF
             sg.limit = math.sqrt(6.0 / (fan_in + fan_out))
             idx = len(segs)
             segs.append(sg)
@@ -318,9 +441,10 @@ class HipFoldJob(FoldJob):
 
         for L in self.layers:
             add(L.w[0], (L.coutp, L.KH, L.KW, L.cinp), (L.cout, L.KH, L.KW, L.cin), L.cin * L.KH * L.KW,
-                L.cout * L.KH * L.KW, L.spec.name + ".w")
-        hs, ws, cp = self.shapes[self.last]
-        add(self.views["W1"][0], (hs, ws, cp, self.Up), (hs, ws, self.plan.final_c, self.plan.dense_units),
+                L.cout * L.KH * L.KW, L.name + ".w")
+        hs, ws = self.final_hw
+        add(self.views["W1"][0], (hs, ws, self.final_cp, self.Up),
+            (hs, ws, self.plan.kernels_per_layer[-1], self.plan.dense_units),
             self.plan.flatten, self.plan.dense_units, "dense1.w")
         w2 = self.views["W2"][0]
         add(w2, (1, 1, w2.shape[1], w2.shape[2]), (1, 1, self.plan.dense_units, self.plan.classes),
@@ -338,8 +462,8 @@ class HipFoldJob(FoldJob):
         self.init_nblocks = len(blocks)
 
     def init_params(self):
-        """Glorot-uniform kernels (Philox, keyed by fold id and tensor name),
-        zero biases -- Keras defaults, re-drawn per fold."""
+        """Glorot-uniform kernels (Philox, keyed by member, fold id and tensor
+        name), zero biases -- Keras defaults, re-drawn per fold."""
         if getattr(self, "init_args", None) is None:
             self._build_init_table()
         self.flat.zero_()
@@ -380,8 +504,7 @@ class HipFoldJob(FoldJob):
             if kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_fwd")
             else:
-                x, y, nb, hh, ww, cc = a
-                K.check(L.gt_pool_fwd(x.data_ptr(), y.data_ptr(), nb, hh, ww, cc, s), "pool_fwd")
+                K.check(L.gt_pool_fwd(*a, s), "pool_fwd")
 
     def train_step(self):
         L, s = self.L, self._stream()
@@ -397,22 +520,20 @@ class HipFoldJob(FoldJob):
             elif kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
             else:
-                x, dy, dx, nb, hh, ww, cc, rm = a
-                K.check(L.gt_pool_bwd(x.data_ptr(), dy.data_ptr(), dx.data_ptr(), nb, hh, ww, cc, rm, s),
-                        "pool_bwd")
+                K.check(L.gt_pool_bwd(*a, s), "pool_bwd")
         K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
 
     def evaluate(self):
         """Forward the validation folds in batches of B (no dropout)."""
-        G, B, dev = self.G, self.B, self.device
+        Q, B, dev = self.Q, self.B, self.device
         maxv = self.val_mat.shape[1]
         nch = -(-maxv // B)
-        idx = torch.zeros((G, nch * B), dtype=torch.int64, device=dev)
-        mask = torch.zeros((G, nch * B), dtype=torch.float32, device=dev)
+        idx = torch.zeros((Q, nch * B), dtype=torch.int64, device=dev)
+        mask = torch.zeros((Q, nch * B), dtype=torch.float32, device=dev)
         idx[:, :maxv] = self.val_mat
         mask[:, :maxv] = self.val_mask
-        table = idx.view(G, nch, B).permute(1, 0, 2).contiguous()        # [nch][G][B]
-        out = torch.zeros((nch, G, B, 3), dtype=torch.float32, device=dev)
+        table = idx.view(Q, nch, B).permute(1, 0, 2).contiguous()        # [nch][Q][B]
+        out = torch.zeros((nch, Q, B, 3), dtype=torch.float32, device=dev)
         self._eval_keep = (table, out)
         s = self._stream()
         L = self.L
@@ -438,6 +559,10 @@ class HipFoldJob(FoldJob):
             K.check(L.gt_dense_fwd(df, s), "dense_fwd(eval)")
             hd.gather, hd.eval_out = gptr, out[c].data_ptr()
             K.check(L.gt_head(hd, s), "head(eval)")
-        res = out.permute(1, 0, 2, 3).reshape(G, nch * B, 3) * mask[:, :, None]
+        res = out.permute(1, 0, 2, 3).reshape(Q, nch * B, 3) * mask[:, :, None]
         sums = res.sum(1)
         return sums[:, 0], sums[:, 1], sums[:, 2]
+
+
+# single-candidate name kept for callers of the fold-batched API
+HipFoldJob = HipPopJob

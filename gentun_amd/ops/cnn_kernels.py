@@ -13,23 +13,34 @@ P = C.c_void_p
 I = C.c_int
 
 
+MAXSLOT = 8      # GT_MAXSLOT: input / output slots of one conv launch
+
+
+class GroupRec(C.Structure):
+    """One group (candidate x fold replica) of a population launch:
+    ``in_mask`` bit k = input slot k is summed; ``out_mask`` bits 0-7 = output
+    slots written, 8-15 = accumulate into them, 16-23 = apply that slot's
+    ReLU mask (csrc/hip/cnn_conv.hip GroupRec)."""
+    _fields_ = [("g", I), ("in_mask", I), ("out_mask", I), ("pad", I)]
+
+
 class ConvArgs(C.Structure):
-    _fields_ = [("inp", P * 4), ("mask", P), ("gather", P), ("st", P), ("out", P * 4), ("out_mask", P * 4),
-                ("w", P), ("bias", P),
+    _fields_ = [("inp", P * MAXSLOT), ("mask", P), ("gather", P), ("st", P), ("out", P * MAXSLOT),
+                ("out_mask", P * MAXSLOT), ("w", P), ("bias", P), ("gtab", P),
                 ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
-                ("TH", I)]
+                ("TH", I), ("ngroups", I)]
 
 
 class WgradArgs(C.Structure):
-    _fields_ = [("inp", P * 4), ("gather", P), ("st", P), ("dz", P), ("part_w", P),
-                ("part_b", P), ("n_in", I), ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I),
-                ("KH", I), ("KW", I), ("S", I), ("pps", I)]
+    _fields_ = [("inp", P * MAXSLOT), ("gather", P), ("st", P), ("dz", P), ("part_w", P),
+                ("part_b", P), ("gtab", P), ("n_in", I), ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I),
+                ("Coutp", I), ("KH", I), ("KW", I), ("S", I), ("pps", I), ("ngroups", I)]
 
 
 class DenseFwdArgs(C.Structure):
     _fields_ = [("x", P), ("wt", P), ("bias", P), ("out", P), ("w2", P), ("plog", P), ("st", P), ("fold_ids", P),
-                ("G", I), ("B", I), ("Fp", I), ("Up", I), ("drop_p", C.c_float), ("train", I),
+                ("seeds", P), ("G", I), ("B", I), ("Fp", I), ("Up", I), ("drop_p", C.c_float), ("train", I),
                 ("seed", C.c_uint), ("C", I)]
 
 
@@ -84,16 +95,10 @@ def lib():
         L.gt_adam_segments.restype = I
         L.gt_step_begin.argtypes = [P, P]
         L.gt_step_begin.restype = I
-        L.gt_pool_fwd.argtypes = [P, P, I, I, I, I, P]
+        L.gt_pool_fwd.argtypes = [P, P, P, P, I, I, I, I, I, P]
         L.gt_pool_fwd.restype = I
-        L.gt_pool_bwd.argtypes = [P, P, P, I, I, I, I, I, P]
+        L.gt_pool_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P]
         L.gt_pool_bwd.restype = I
-        L.gt_conv_set_mode.argtypes = [I]
-        L.gt_conv_set_mode.restype = I
-        L.gt_conv_set_stamps.argtypes = [P]
-        L.gt_conv_set_wgs.argtypes = [I]
-        L.gt_conv_set_wgs.restype = I
-        L.gt_conv_set_stamps.restype = I
         L.gt_glorot_init.argtypes = [C.POINTER(InitArgs), I, P]
         L.gt_glorot_init.restype = I
         L.gt_glorot_ref.argtypes = [C.c_uint64, C.c_uint64, I, C.c_float]

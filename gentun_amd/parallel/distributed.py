@@ -214,41 +214,26 @@ def _unit_cost(u):
 
 
 def _evaluate_cnn_units(source, evaluator, nfold):
-    """Launch every unit's fold-batched job on the evaluator's streams; at
-    most one unit in flight per stream (a unit is claimed only when a stream
-    frees up, which is what makes dynamic claiming balance the ranks)."""
-    streams = evaluator.streams() if hasattr(evaluator, "streams") else [None]
-    device = getattr(evaluator, "device", None)
-    rows, window = {}, []
+    """Train this rank's units as population jobs (up to ``pop_batch``
+    candidates x folds per launch, one job per evaluator stream in flight).
+    Units are pulled from ``source`` only when a stream frees up, which is
+    what makes dynamic claiming balance the ranks."""
+    from .evaluators import run_cnn_units
+    rows = {}
 
-    def retire(entry):
-        ui, u, model, jobs, t0 = entry
-        res = [job.finish() for job in jobs]
-        merged = {"binary_accuracy": [], "categorical_accuracy": [], "val_loss": []}
-        for r in res:
-            for k in merged:
-                merged[k].extend(r[k])
-        scores = merged[model.primary_metric()]
-        rows[ui] = _row(ST_OK, float(np.mean(scores)), time.perf_counter() - t0, scores, nfold, u.fold_ids)
+    def done(ind, model, res, wall, ui):
+        scores = res[model.primary_metric()]
+        u = units_by_index[ui]
+        rows[ui] = _row(ST_OK, float(np.mean(scores)), wall, scores, nfold, u.fold_ids)
 
-    it = iter(source)
-    k = 0
-    while True:
-        if len(window) >= len(streams):
-            retire(window.pop(0))
-        nxt = next(it, None)
-        if nxt is None:
-            break
-        ui, u = nxt
-        model = u.ind.build_fitness_model(device=device)
-        jobs = model.make_jobs(stream=streams[k % len(streams)], fold_ids=u.fold_ids)
-        k += 1
-        t0 = time.perf_counter()
-        for job in jobs:
-            job.launch()
-        window.append((ui, u, model, jobs, t0))
-    for entry in window:
-        retire(entry)
+    units_by_index = {}
+
+    def gen():
+        for ui, u in source:
+            units_by_index[ui] = u
+            yield (u.ind, u.fold_ids, ui)
+
+    run_cnn_units(gen(), evaluator, done)
     return rows
 
 

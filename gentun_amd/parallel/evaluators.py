@@ -58,21 +58,25 @@ class SequentialEvaluator(object):
 
 
 class LocalBatchEvaluator(SequentialEvaluator):
-    """Evaluate a batch of individuals on ONE GPU with ``streams`` concurrent
-    candidates (one HIP stream each; every candidate's training is a graph
-    replay loop enqueued asynchronously).
+    """Evaluate a batch of individuals on ONE GPU.
 
-    Species that expose ``build_fitness_model`` (Genetic-CNN) run
-    concurrently; other species fall back to sequential evaluation.
+    Genetic-CNN candidates (species exposing ``build_fitness_model``) on the
+    HIP backend are trained as *population jobs*: up to ``pop_batch``
+    candidates x all their folds share every kernel launch
+    (:class:`~gentun_amd.models.cnn_hip.HipPopJob`); up to ``streams`` such
+    jobs run concurrently on separate HIP streams. Other backends run one
+    fold-batched job per candidate per stream; other species fall back to
+    sequential evaluation.
     """
 
-    def __init__(self, device=None, streams=4, cache=False, event_log=None):
+    def __init__(self, device=None, streams=2, cache=False, event_log=None, pop_batch=16):
         super(LocalBatchEvaluator, self).__init__(cache=cache, event_log=event_log)
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
                 else torch.device("cpu")
         self.device = torch.device(device)
         self.nstreams = max(1, int(streams))
+        self.pop_batch = max(1, int(pop_batch))
         self._streams = None
 
     def streams(self):
@@ -94,40 +98,121 @@ class LocalBatchEvaluator(SequentialEvaluator):
             n += self.evaluate_models(batch)
         return n
 
-    def evaluate_models(self, individuals, order=None):
-        """Run ``individuals`` concurrently; results land in each individual."""
-        streams = self.streams()
-        # Largest first (LPT) keeps the tail short.
-        if order is None:
-            order = sorted(range(len(individuals)),
-                           key=lambda i: -individuals[i].cost() if hasattr(individuals[i], "cost") else 0)
-        window = []          # (ind, model, jobs, t0)
-        k = 0
-
-        def retire(entry):
-            ind, model, jobs, t0 = entry
-            results = [job.finish() for job in jobs]
-            ind.set_fitness(model.collect(results))
+    def evaluate_models(self, individuals):
+        """Train ``individuals`` (all folds); results land in each individual."""
+        def done(ind, model, res, wall, _tag):
+            ind.set_fitness(model.collect([res]))
             ind.fold_scores = list(model.fold_scores)
             self._store(ind)
-            self._log(ind, time.perf_counter() - t0)
+            self._log(ind, wall)
 
-        for i in order:
-            ind = individuals[i]
-            if len(window) >= len(streams):
-                retire(window.pop(0))
+        run_cnn_units([(ind, None, None) for ind in individuals], self, done)
+        self.evaluations += len(individuals)
+        return len(individuals)
+
+
+def _chunks(units, nchunks):
+    """Split cost-sorted units into ``nchunks`` groups of near-equal cost (LPT)."""
+    bins = [[] for _ in range(nchunks)]
+    load = [0.0] * nchunks
+    for u in units:
+        k = min(range(nchunks), key=lambda i: (load[i], len(bins[i])))
+        bins[k].append(u)
+        load[k] += u[3]
+    return [b for b in bins if b]
+
+
+def run_cnn_units(units, evaluator, done):
+    """Train Genetic-CNN work units ``(ind, fold_ids or None, tag)`` on the
+    evaluator's device and call ``done(ind, model, result, wall_s, tag)`` per unit
+    (``result`` = per-fold metric lists of the unit's folds).
+
+    ``units`` may be an iterator (dynamic scheduling claims units lazily):
+    units are pulled ``pop_batch`` at a time whenever a stream is free."""
+    streams = evaluator.streams() if hasattr(evaluator, "streams") else [None]
+    device = getattr(evaluator, "device", None)
+    pop_batch = getattr(evaluator, "pop_batch", 1)
+    from ..models import cnn_engine as E
+    it = iter(units)
+    window = []          # (job, [(ind, model, tag)], t0)
+
+    def retire(entry):
+        job, items, t0, multi = entry
+        res = job.finish()
+        res = res if multi else [res]
+        wall = time.perf_counter() - t0
+        for (ind, model, tag), r in zip(items, res):
+            done(ind, model, r, wall, tag)
+
+    pending = []
+    k = 0
+    exhausted = False
+    while True:
+        if not exhausted and len(pending) < pop_batch * len(streams):
+            # pull enough units to fill every stream with a batch
+            while len(pending) < pop_batch * len(streams):
+                nxt = next(it, None)
+                if nxt is None:
+                    exhausted = True
+                    break
+                ind, fold_ids, tag = nxt
+                model = ind.build_fitness_model(device=device)
+                cost = float(ind.cost()) if hasattr(ind, "cost") else 1.0
+                nf = len(fold_ids) if fold_ids is not None else model.nfold
+                pending.append((ind, model, fold_ids, cost * nf, tag))
+        if not pending:
+            break
+        if len(window) >= len(streams):
+            retire(window.pop(0))
+        pending.sort(key=lambda e: -e[3])
+        hip = all(e[1].backend == "hip" for e in pending) and pop_batch > 1
+        if hip:
+            free = len(streams) - len(window)
+            nchunks = min(free, max(1, -(-len(pending) // pop_batch))) if exhausted else 1
+            take = pending[:pop_batch * nchunks] if exhausted else pending[:pop_batch]
+            pending = pending[len(take):]
+            chunks = _chunks([(e[0], e[1], e[2], e[3], e[4]) for e in take], nchunks)
+            for ch in chunks:
+                if len(window) >= len(streams):
+                    retire(window.pop(0))
+                stream = streams[k % len(streams)]
+                k += 1
+                members, items = [], []
+                for ind, model, fold_ids, _c, tag in ch:
+                    members.append(model.member(fold_ids))
+                    items.append((ind, model, tag))
+                m0 = ch[0][1]
+                job = E.make_population_job("hip", members, m0.x_train, m0.y_train, m0.cfg, m0.device,
+                                            stream=stream)
+                t0 = time.perf_counter()
+                job.launch()
+                window.append((job, items, t0, True))
+        else:
+            ind, model, fold_ids, _c, tag = pending.pop(0)
             stream = streams[k % len(streams)]
             k += 1
-            model = ind.build_fitness_model(device=self.device)
-            jobs = model.make_jobs(stream=stream)
+            jobs = model.make_jobs(stream=stream, fold_ids=fold_ids)
             t0 = time.perf_counter()
             for job in jobs:
                 job.launch()
-            window.append((ind, model, jobs, t0))
-        for entry in window:
-            retire(entry)
-        self.evaluations += len(individuals)
-        return len(individuals)
+            window.append((_MultiJob(jobs), [(ind, model, tag)], t0, False))
+    for entry in window:
+        retire(entry)
+
+
+class _MultiJob(object):
+    """Several per-fold-group jobs of one candidate seen as one result."""
+
+    def __init__(self, jobs):
+        self.jobs = jobs
+
+    def finish(self):
+        merged = {"val_loss": [], "binary_accuracy": [], "categorical_accuracy": []}
+        for job in self.jobs:
+            r = job.finish()
+            for k2 in merged:
+                merged[k2].extend(r[k2])
+        return merged
 
 
 def stable_order_key(ind):

@@ -51,14 +51,9 @@ def pack_w(w_oihw, coutp, cinp):
 @pytest.mark.parametrize("H,W,cin,cout,k,nin", [(32, 32, 3, 20, 5, 1), (32, 32, 20, 20, 3, 3), (16, 16, 20, 50, 5, 1),
                                                (16, 16, 50, 50, 3, 2), (8, 8, 64, 128, 3, 1), (7, 7, 50, 50, 3, 4),
                                                (28, 28, 1, 20, 5, 1), (16, 16, 50, 200, 5, 1)])
-@pytest.mark.parametrize("mode", [0, 1, 2])
-def test_conv_fwd(H, W, cin, cout, k, nin, mode):
-    """Single-input layers: mode 1 = persistent LDS-DMA kernel (forced onto
-    this small grid with a tiny workgroup target), 2 = one-tile LDS-DMA
-    kernel, 0 = register-staged kernel (always used for N-ary sums)."""
+def test_conv_fwd(H, W, cin, cout, k, nin):
+    """Dense (legacy) group mode: every group, inputs 0..nin-1 summed."""
     Km = K()
-    Km.lib().gt_conv_set_mode(mode)
-    Km.lib().gt_conv_set_wgs(8 if mode == 1 else 512)
     torch.manual_seed(0)
     G, B = 2, 3
     cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
@@ -78,10 +73,9 @@ def test_conv_fwd(H, W, cin, cout, k, nin, mode):
     a.w, a.bias = wp.data_ptr(), bp.data_ptr()
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
     a.TH = Km.conv_tile_rows(H, W)
+    a.ngroups = G
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv")
     torch.cuda.synchronize()
-    Km.lib().gt_conv_set_mode(0)
-    Km.lib().gt_conv_set_wgs(512)
     for g in range(G):
         # the fused Add is rounded to bf16 before the MFMA: mirror that
         xsum = bf(sum(x[g] for x in xs)).float()
@@ -93,8 +87,8 @@ def test_conv_fwd(H, W, cin, cout, k, nin, mode):
             assert out[g, ..., cout:].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("staged_mask,wgs", [(True, 512), (False, 512), (False, 4)])
-def test_conv_dgrad_mask_and_accumulate(staged_mask, wgs):
+@pytest.mark.parametrize("staged_mask", [True, False])
+def test_conv_dgrad_mask_and_accumulate(staged_mask):
     """dgrad = conv of (dy * (y>0)) with flipped/transposed weights, fanned out
     into two outputs, one accumulating. ``staged_mask``: the ReLU mask is
     applied while staging (register kernel); else dy arrives pre-masked (the
@@ -128,18 +122,93 @@ def test_conv_dgrad_mask_and_accumulate(staged_mask, wgs):
     a.n_in, a.n_out, a.acc_flags, a.relu = 1, 2, 2, 0
     a.w, a.bias = wT.data_ptr(), 0
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.TH = G, B, H, W, coutp, cinp, k, k, 4
-    Km.lib().gt_conv_set_wgs(wgs)
-    Km.lib().gt_conv_set_mode(0 if staged_mask else 1)     # 1: persistent (wgs 4) / one-tile LDS-DMA
+    a.ngroups = G
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "dgrad")
     torch.cuda.synchronize()
-    Km.lib().gt_conv_set_wgs(512)
-    Km.lib().gt_conv_set_mode(0)
     got0 = out0[..., :cin].float().permute(0, 1, 4, 2, 3)
     tol = 2e-2 * ref.abs().max().item()
     assert (got0 - ref).abs().max().item() < tol
     got1 = out1[..., :cin].float().permute(0, 1, 4, 2, 3)
     ref1 = (ref + prev[..., :cin].float().permute(0, 1, 4, 2, 3)) * (pmask[..., :cin] > 0).permute(0, 1, 4, 2, 3)
     assert (got1 - ref1).abs().max().item() < tol + 2e-2 * ref1.abs().max().item()
+
+
+def test_conv_group_table_slots_accumulate_mask():
+    """Population mode: a launch over a SUBSET of groups, each summing its own
+    input slots and writing / accumulating / ReLU-masking its own outputs;
+    groups outside the table are untouched."""
+    Km = K()
+    torch.manual_seed(7)
+    Q, B, H, W, cin, cout, k = 4, 2, 16, 16, 20, 20, 3
+    cp = 24
+    slots = [bf(torch.randn(Q, B, H, W, cp, device=DEV)) for _ in range(3)]
+    for s in slots:
+        s[..., cin:] = 0
+    w = bf(torch.randn(Q, cout, cin, k, k, device=DEV) * 0.2).float()
+    wp = torch.stack([pack_w(w[g], cp, cp) for g in range(Q)]).to(torch.bfloat16).contiguous()
+    bias = torch.zeros(Q, cp, device=DEV)
+    bias[:, :cout] = torch.randn(Q, cout, device=DEV) * 0.1
+    out0 = torch.full((Q, B, H, W, cp), 3.0, dtype=torch.bfloat16, device=DEV)
+    out1 = bf(torch.randn(Q, B, H, W, cp, device=DEV))
+    out1[..., cout:] = 0
+    prev1 = out1.clone()
+    mask1 = bf(torch.randn(Q, B, H, W, cp, device=DEV))
+    # group 3: slots {0, 2} -> write out0; group 1: slot {1} -> accumulate into out1, then ReLU-mask
+    rows = torch.tensor([[3, 0b101, 0b1, 0], [1, 0b010, 0b10 | (0b10 << 8) | (0b10 << 16), 0]],
+                        dtype=torch.int32, device=DEV)
+    a = Km.ConvArgs()
+    for i, s in enumerate(slots):
+        a.inp[i] = s.data_ptr()
+    a.out[0], a.out[1] = out0.data_ptr(), out1.data_ptr()
+    a.out_mask[1] = mask1.data_ptr()
+    a.gtab, a.ngroups = rows.data_ptr(), 2
+    a.relu = 1
+    a.w, a.bias = wp.data_ptr(), bias.data_ptr()
+    a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = Q, B, H, W, cp, cp, k, k
+    a.TH = Km.conv_tile_rows(H, W)
+    Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv(gtab)")
+    torch.cuda.synchronize()
+
+    def ref(g, ins):
+        x = bf(sum(slots[i][g].float() for i in ins))[..., :cin].permute(0, 3, 1, 2).float()
+        return conv_ref([x], w[g], bias[g, :cout], True).permute(0, 2, 3, 1)
+
+    r3 = ref(3, [0, 2])
+    tol = 2e-2 * r3.abs().max().item() + 1e-2
+    assert (out0[3, ..., :cout].float() - r3).abs().max().item() < tol
+    r1 = (ref(1, [1]) + prev1[1, ..., :cout].float()) * (mask1[1, ..., :cout].float() > 0)
+    assert (out1[1, ..., :cout].float() - r1).abs().max().item() < tol + 2e-2 * r1.abs().max().item()
+    for g in (0, 2):
+        assert torch.all(out0[g] == 3.0)
+        assert torch.equal(out1[g], prev1[g])
+    assert torch.all(out0[1] == 3.0) and torch.equal(out1[3], prev1[3])
+
+
+def test_pool_group_select():
+    """Per-group pool source (x0 or x1) and gradient target."""
+    Km = K()
+    torch.manual_seed(8)
+    Q, B, H, W, cp = 3, 2, 8, 8, 8
+    x0 = bf(torch.randn(Q, B, H, W, cp, device=DEV))
+    x1 = bf(torch.randn(Q, B, H, W, cp, device=DEV))
+    sel = torch.tensor([0, 1, 0], dtype=torch.int32, device=DEV)
+    y = torch.zeros(Q, B, H // 2, W // 2, cp, dtype=torch.bfloat16, device=DEV)
+    Km.check(Km.lib().gt_pool_fwd(x0.data_ptr(), x1.data_ptr(), sel.data_ptr(), y.data_ptr(), Q * B, B, H, W, cp,
+                                  stream()), "pool")
+    dy = bf(torch.randn_like(y.float()))
+    dx0 = torch.full_like(x0, 5.0)
+    dx1 = torch.full_like(x1, 5.0)
+    Km.check(Km.lib().gt_pool_bwd(x0.data_ptr(), x1.data_ptr(), sel.data_ptr(), dy.data_ptr(), dx0.data_ptr(),
+                                  dx1.data_ptr(), Q * B, B, H, W, cp, 1, stream()), "poolb")
+    torch.cuda.synchronize()
+    for g in range(Q):
+        src = (x1 if sel[g] else x0)[g].float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+        yr = F.max_pool2d(src, 2, 2)
+        assert torch.equal(y[g].float().permute(0, 3, 1, 2), yr.detach())
+        yr.backward(dy[g].float().permute(0, 3, 1, 2))
+        got = (dx1 if sel[g] else dx0)[g].float().permute(0, 3, 1, 2)
+        assert torch.allclose(got, src.grad * (src > 0), atol=1e-6)
+        assert torch.all((dx0 if sel[g] else dx1)[g] == 5.0)
 
 
 @pytest.mark.parametrize("H,W,cin,cout,k,nin,first", [(32, 32, 3, 20, 5, 1, True), (16, 16, 50, 50, 3, 2, False),
@@ -181,6 +250,7 @@ def test_conv_wgrad(H, W, cin, cout, k, nin, first):
     a.st = st.data_ptr()
     a.dz, a.part_w, a.part_b = dz_p.data_ptr(), pw.data_ptr(), pb.data_ptr()
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.S, a.pps = G, B, H, W, cinp, coutp, k, k, S, pps
+    a.ngroups = G
     Km.check(Km.lib().gt_conv_wgrad(a, stream()), "wgrad")
     torch.cuda.synchronize()
     got = pw.sum(0).view(G, coutp, k, k, cinp)[:, :cout, :, :, :cin].permute(0, 1, 4, 2, 3)
@@ -202,12 +272,14 @@ def test_pool_fwd_bwd(H, W):
     y.backward(dy)
     xp = nhwc_pad(x, cp).to(torch.bfloat16).contiguous()
     yp = torch.zeros(N, H // 2, W // 2, cp, dtype=torch.bfloat16, device=DEV)
-    Km.check(Km.lib().gt_pool_fwd(xp.data_ptr(), yp.data_ptr(), N, H, W, cp, stream()), "pool")
+    Km.check(Km.lib().gt_pool_fwd(xp.data_ptr(), 0, 0, yp.data_ptr(), N, 1, H, W, cp, stream()), "pool")
     dyp = nhwc_pad(dy, cp).to(torch.bfloat16).contiguous()
     dxp = torch.full((N, H, W, cp), 7.0, dtype=torch.bfloat16, device=DEV)
-    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), dyp.data_ptr(), dxp.data_ptr(), N, H, W, cp, 0, stream()), "poolb")
+    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), 0, 0, dyp.data_ptr(), dxp.data_ptr(), 0, N, 1, H, W, cp, 0,
+                                  stream()), "poolb")
     dxm = torch.full((N, H, W, cp), 7.0, dtype=torch.bfloat16, device=DEV)
-    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), dyp.data_ptr(), dxm.data_ptr(), N, H, W, cp, 1, stream()), "poolm")
+    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), 0, 0, dyp.data_ptr(), dxm.data_ptr(), 0, N, 1, H, W, cp, 1,
+                                  stream()), "poolm")
     torch.cuda.synchronize()
     assert torch.equal(yp[..., :C].float().permute(0, 3, 1, 2), y.detach())
     assert torch.allclose(dxp[..., :C].float().permute(0, 3, 1, 2), xr.grad, atol=1e-6)

@@ -67,3 +67,24 @@ def test_hip_fold_subset_equals_batched():
     full = E.make_job("hip", plan, x, y, folds, cfg, dev, fold_ids=[0, 1, 2]).launch().finish()
     one = E.make_job("hip", plan, x, y, [folds[1]], cfg, dev, fold_ids=[1]).launch().finish()
     assert one["val_loss"][0] == full["val_loss"][1]
+
+
+def test_population_batch_invariance():
+    """A candidate's per-fold result is bit-identical whether it trains alone
+    or batched with other architectures in one population job (shared
+    launches, per-group tables; SURVEY.md §7.3 hard part 4)."""
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.genome import make_plan
+    x, y, folds, _ = _setup(n=600)
+    dev = torch.device("cuda", 0)
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce")
+    genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '000', 'S_2': '0000000000'},
+             {'S_1': '111', 'S_2': '1111111111'}, {'S_1': '010', 'S_2': '1000000001'}]
+    plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
+    alone = [E.make_job("hip", p, x, y, folds, cfg, dev).launch().finish() for p in plans]
+    members = [(p, folds, [0, 1, 2]) for p in plans]
+    members[3] = (plans[3], [folds[2], folds[0]], [2, 0])        # a subset of folds, out of order
+    pop = E.make_population_job("hip", members, x, y, cfg, dev).launch().finish()
+    for i in range(3):
+        assert pop[i] == alone[i], (i, pop[i], alone[i])
+    assert pop[3]["val_loss"] == [alone[3]["val_loss"][2], alone[3]["val_loss"][0]]

@@ -15,12 +15,9 @@ from gentun_amd.ops import cnn_kernels as K
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 TILES = tuple(int(t) for t in os.environ.get("GENTUN_TILES", "128").split(","))
-MODES = tuple(int(t) for t in os.environ.get("GENTUN_CONV_MODES", "0,1,2").split(","))
 dev = torch.device("cuda", 0)
 L = K.lib()
-if os.environ.get("GENTUN_CONV_WGS"):
-    L.gt_conv_set_wgs(int(os.environ["GENTUN_CONV_WGS"]))
-G, B = 5, 32
+G, B = int(os.environ.get("GENTUN_BENCH_G", "5")), 32
 
 
 def pad8(c):
@@ -85,12 +82,12 @@ for name, H, cin, cout, k, nin in shapes:
     a.n_in, a.n_out, a.acc_flags, a.relu = nin, 1, 0, 1
     a.w, a.bias, a.st = w.data_ptr(), bias.data_ptr(), st.data_ptr()
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.TH = G, B, H, W, cinp, coutp, k, k, TH
-    for tp, mode in [(t, m) for t in TILES for m in MODES]:
+    a.ngroups = G
+    for tp in TILES:
         a.TH = K.conv_tile_rows(H, W, tp)
-        L.gt_conv_set_mode(mode)
         us = timeit(lambda st: K.check(L.gt_conv_fwd(a, st), "fwd")) if only_k in (None, "conv_fwd") else 0.0
         byt = (nin * G * B * H * W * cinp + G * B * H * W * coutp) * 2
-        print(json.dumps({"kernel": "conv_fwd", "tile": tp, "mode": mode, "shape": name, "us": round(us, 2),
+        print(json.dumps({"kernel": "conv_fwd", "tile": tp, "shape": name, "us": round(us, 2),
                           "tflops": round(flops / max(us, 1e-9) / 1e6, 2),
                           "gbs": round(byt / max(us, 1e-9) / 1e3, 1)}), flush=True)
     # dgrad
@@ -99,15 +96,14 @@ for name, H, cin, cout, k, nin in shapes:
     d.n_in, d.n_out, d.acc_flags, d.relu = 1, 1, 0, 0
     d.w, d.bias, d.st = wT.data_ptr(), 0, st.data_ptr()
     d.G, d.B, d.H, d.W, d.Cinp, d.Coutp, d.KH, d.KW, d.TH = G, B, H, W, coutp, cinp, k, k, TH
-    for tp, mode in [(t, m) for t in TILES for m in MODES]:
+    d.ngroups = G
+    for tp in TILES:
         d.TH = K.conv_tile_rows(H, W, tp)
-        L.gt_conv_set_mode(mode)
         us = timeit(lambda st: K.check(L.gt_conv_fwd(d, st), "dgrad")) if only_k in (None, "conv_dgrad") else 0.0
         byt = (2 * G * B * H * W * coutp + G * B * H * W * cinp) * 2
-        print(json.dumps({"kernel": "conv_dgrad", "tile": tp, "mode": mode, "shape": name, "us": round(us, 2),
+        print(json.dumps({"kernel": "conv_dgrad", "tile": tp, "shape": name, "us": round(us, 2),
                           "tflops": round(flops / max(us, 1e-9) / 1e6, 2),
                           "gbs": round(byt / max(us, 1e-9) / 1e3, 1)}), flush=True)
-    L.gt_conv_set_mode(0)
     # wgrad
     npix = B * H * W
     Kdim = k * k * cinp
@@ -120,6 +116,7 @@ for name, H, cin, cout, k, nin in shapes:
     wa.n_in, wa.gather, wa.st = nin, 0, st.data_ptr()
     wa.dz, wa.part_w, wa.part_b = dy.data_ptr(), pw.data_ptr(), pb.data_ptr()
     wa.G, wa.B, wa.H, wa.W, wa.Cinp, wa.Coutp, wa.KH, wa.KW, wa.S, wa.pps = G, B, H, W, cinp, coutp, k, k, S, pps
+    wa.ngroups = G
     us = timeit(lambda st: K.check(L.gt_conv_wgrad(wa, st), "wgrad")) if only_k in (None, "conv_wgrad") else 0.0
     byt = (nin * G * B * H * W * cinp + 2 * G * B * H * W * coutp) * 2 + S * G * coutp * Kdim * 4
     print(json.dumps({"kernel": "conv_wgrad", "shape": name, "us": round(us, 2), "tflops": round(flops / max(us, 1e-9) / 1e6, 2),

@@ -1,0 +1,55 @@
+"""Throughput of population-batched training: P random S=(3,5) candidates
+split into jobs of ``pop_batch`` on ``streams`` streams, 1 epoch each.
+
+usage: python tools/probe_pop.py [P] [pop_batch] [streams] [epochs] [samples]
+"""
+import json
+import os
+import random
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+
+from gentun_amd.models import cnn_engine as E
+from gentun_amd.models.genome import make_plan
+from gentun_amd.utils.data import make_cifar_like, stratified_kfold
+
+P = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+pb = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+ns = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+epochs = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+n = int(sys.argv[5]) if len(sys.argv) > 5 else 10000
+dev = torch.device("cuda", 0)
+x, y = make_cifar_like(n=n, seed=0)
+folds = stratified_kfold(np.argmax(y, 1), 5, seed=0)
+rnd = random.Random(0)
+plans = []
+for _ in range(P):
+    g = {"S_1": "".join(rnd.choice("01") for _ in range(3)), "S_2": "".join(rnd.choice("01") for _ in range(10))}
+    plans.append(make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10))
+cfg = E.TrainConfig(epochs=(epochs,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce")
+streams = [torch.cuda.Stream(dev) for _ in range(ns)]
+# warm-up (allocator, code objects)
+E.make_population_job("hip", [(plans[0], folds, list(range(5)))], x, y, cfg, dev).launch().finish()
+torch.cuda.synchronize()
+t = time.perf_counter()
+jobs = []
+for i in range(0, P, pb):
+    members = [(p, folds, list(range(5))) for p in plans[i:i + pb]]
+    jobs.append(E.make_population_job("hip", members, x, y, cfg, dev, stream=streams[len(jobs) % ns]))
+tb = time.perf_counter()
+for j in jobs:
+    j.launch()
+tl = time.perf_counter()
+res = [r for j in jobs for r in j.finish()]
+torch.cuda.synchronize()
+dt = time.perf_counter() - t
+steps = jobs[0].steps_per_epoch * epochs
+print(json.dumps({"P": P, "pop_batch": pb, "streams": ns, "steps": steps, "s": round(dt, 3),
+                  "build_s": round(tb - t, 3), "enqueue_s": round(tl - tb, 3),
+                  "ms_per_step": round(1000 * dt / steps, 3), "ms_per_cand_step": round(1000 * dt / steps / P, 4),
+                  "cand_per_hour_full_protocol": round(3600 * P / (dt / steps * 6250), 1),
+                  "cat_acc": [round(float(np.mean(r["categorical_accuracy"])), 3) for r in res]}), flush=True)
