@@ -1,0 +1,66 @@
+// Argument blocks of the Genetic-CNN convolution kernels (shared by the
+// generic kernels in cnn_conv.hip and the shape-specialised ones in
+// cnn_conv_fast.hip). Layouts must match gentun_amd/ops/cnn_kernels.py.
+#pragma once
+#include "common.h"
+
+// Population batching: a launch covers the "groups" (candidate x fold
+// replicas) listed in a group table. Activations / gradients live in SLOT
+// tensors [Q][B][H][W][C] (Q = all groups of the job); a group's record says
+// which slots it sums as input, which slots its output goes to, and for each
+// output whether to accumulate and whether to apply the ReLU mask of that
+// slot's activation (the DAG of every candidate is different, the launch is
+// shared).  gtab == nullptr: legacy dense mode (group = blockIdx.y, inputs
+// 0..n_in-1, outputs 0..n_out-1, acc_flags, masks where out_mask[k] != 0).
+struct GroupRec {
+  int g;          // group index into the slot tensors / weights
+  int in_mask;    // bit k: in[k] is summed
+  int out_mask;   // bits 0-7: outputs written, 8-15: accumulate, 16-23: apply out_mask[k] ReLU mask
+  int pad;
+};
+
+#define GT_MAXSLOT 8
+
+struct ConvArgs {
+  const uint16_t* in[GT_MAXSLOT];   // input slot bases [Q][B][H][W][Cinp]
+  const uint16_t* mask;             // optional: staged value *= (mask > 0), same shape as in (legacy mode)
+  const int64_t* gather;            // optional: image table [steps][Q][B]; in[0] is then the dataset
+  const StepState* st;              // cur_step for the gather table
+  uint16_t* out[GT_MAXSLOT];        // output slot bases [Q][B][H][W][Coutp]
+  const uint16_t* out_mask[GT_MAXSLOT];  // per output slot: ReLU-mask source (that slot's activation)
+  const uint16_t* w;                // [Q][Coutp][KH][KW][Cinp] bf16
+  const float* bias;                // [Q][Coutp] or null
+  const GroupRec* gtab;             // [grid.y] or null
+  int n_in, n_out, acc_flags, relu;
+  int G, B, H, W, Cinp, Coutp, KH, KW, TH;   // G = Q (group count of the slot tensors)
+  int ngroups;                      // launch groups (rows of gtab); legacy mode: G
+};
+
+__device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,
+                                              const uint16_t* const* out_mask) {
+  if (gtab) return gtab[y];
+  GroupRec r;
+  r.g = y;
+  r.in_mask = (1 << n_in) - 1;
+  int rm = 0;
+  for (int k = 0; k < n_out; ++k)
+    if (out_mask && out_mask[k]) rm |= 1 << k;
+  r.out_mask = ((1 << n_out) - 1) | ((acc & 0xff) << 8) | (rm << 16);
+  r.pad = 0;
+  return r;
+}
+
+// Weight gradient (split-K, deterministic partials).
+struct WgradArgs {
+  const uint16_t* in[GT_MAXSLOT];   // input slots of the layer [Q][B][H][W][Cinp] (summed per group)
+  const int64_t* gather;     // optional dataset gather (first layer)
+  const StepState* st;
+  const uint16_t* dz;        // ReLU-masked grad of the layer output [G][B][H][W][Coutp]
+  float* part_w;             // [S][G][Coutp][Kdim]
+  float* part_b;             // [S][G][Coutp]
+  const GroupRec* gtab;      // [n_groups] or null (legacy: all G groups, inputs 0..n_in-1)
+  int n_in;
+  int G, B, H, W, Cinp, Coutp, KH, KW, S, pps;  // pps = pixels per split (multiple of 64)
+  int ngroups;
+};
+

@@ -99,6 +99,8 @@ def lib():
         L.gt_pool_fwd.restype = I
         L.gt_pool_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P]
         L.gt_pool_bwd.restype = I
+        L.gt_conv_set_fast.argtypes = [I]
+        L.gt_conv_set_fast.restype = I
         L.gt_glorot_init.argtypes = [C.POINTER(InitArgs), I, P]
         L.gt_glorot_init.restype = I
         L.gt_glorot_ref.argtypes = [C.c_uint64, C.c_uint64, I, C.c_float]
@@ -141,11 +143,16 @@ def wgrad_blocks(kdim, with_bias=True):
     return -(-(kdim + (8 if with_bias else 0)) // 64)
 
 
-def wgrad_split(npix, kdim, coutp, G=None, target_blocks=200):
+WGRAD_TARGET_BLOCKS = int(__import__("os").environ.get("GENTUN_WGRAD_TARGET", "50"))
+
+
+def wgrad_split(npix, kdim, coutp, G=None, target_blocks=None):
     """(pixels per split, splits) for conv_wgrad: ~``target_blocks``
     workgroups PER FOLD (the split never depends on how many folds share a
     launch, so a fold's gradient summation order -- and its result -- is the
     same alone or batched), 64-pixel K-steps, >= 2 K-steps per workgroup."""
+    if target_blocks is None:
+        target_blocks = WGRAD_TARGET_BLOCKS
     nb = wgrad_blocks(kdim)
     mb = -(-coutp // 64)
     per = max(1, nb * mb)

@@ -87,22 +87,23 @@ def test_conv_fwd(H, W, cin, cout, k, nin):
             assert out[g, ..., cout:].abs().max().item() == 0
 
 
-@pytest.mark.parametrize("staged_mask", [True, False])
-def test_conv_dgrad_mask_and_accumulate(staged_mask):
+@pytest.mark.parametrize("staged_mask,k", [(True, 3), (False, 3), (False, 5)])
+def test_conv_dgrad_mask_and_accumulate(staged_mask, k):
     """dgrad = conv of (dy * (y>0)) with flipped/transposed weights, fanned out
     into two outputs, one accumulating. ``staged_mask``: the ReLU mask is
     applied while staging (register kernel); else dy arrives pre-masked (the
     LDS-DMA kernel's single-input path)."""
     Km = K()
     torch.manual_seed(1)
-    G, B, H, W, cin, cout, k = 2, 2, 16, 16, 20, 50, 3
+    G, B, H, W, cin, cout = 2, 2, 16, 16, 20, 50
     cinp, coutp = 24, 56
     x = bf(torch.randn(G, B, cin, H, W, device=DEV)).float()
     w = bf(torch.randn(G, cout, cin, k, k, device=DEV) * 0.2).float()
-    y = torch.stack([F.relu(F.conv2d(x[g], w[g], padding=1)) for g in range(G)])
+    y = torch.stack([F.relu(F.conv2d(x[g], w[g], padding=k // 2)) for g in range(G)])
     dy = bf(torch.randn_like(y)).float()
     y = bf(y).float()
-    ref = torch.stack([torch.nn.grad.conv2d_input(x[g].shape, w[g], dy[g] * (y[g] > 0), padding=1) for g in range(G)])
+    ref = torch.stack([torch.nn.grad.conv2d_input(x[g].shape, w[g], dy[g] * (y[g] > 0), padding=k // 2)
+                       for g in range(G)])
     wp = torch.stack([pack_w(w[g], coutp, cinp) for g in range(G)]).float()
     wT = wp.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous().to(torch.bfloat16)
     dy_p = torch.stack([nhwc_pad(dy[g], coutp) for g in range(G)]).to(torch.bfloat16).contiguous()
@@ -133,13 +134,15 @@ def test_conv_dgrad_mask_and_accumulate(staged_mask):
     assert (got1 - ref1).abs().max().item() < tol + 2e-2 * ref1.abs().max().item()
 
 
-def test_conv_group_table_slots_accumulate_mask():
+@pytest.mark.parametrize("H", [16, 32])
+def test_conv_group_table_slots_accumulate_mask(H):
     """Population mode: a launch over a SUBSET of groups, each summing its own
     input slots and writing / accumulating / ReLU-masking its own outputs;
-    groups outside the table are untouched."""
+    groups outside the table are untouched (H=32: shape-specialised kernel,
+    H=16: generic kernel)."""
     Km = K()
     torch.manual_seed(7)
-    Q, B, H, W, cin, cout, k = 4, 2, 16, 16, 20, 20, 3
+    Q, B, W, cin, cout, k = 4, 2, H, 20, 20, 3
     cp = 24
     slots = [bf(torch.randn(Q, B, H, W, cp, device=DEV)) for _ in range(3)]
     for s in slots:
@@ -484,3 +487,44 @@ def test_glorot_init_kernel():
             lin = ((i0 * r[1] + i1) * r[2] + i2) * r[3] + i3
             ref = L.gt_glorot_ref(C.c_uint64(key), C.c_uint64(lin), 5, C.c_float(0.3))
             assert abs(h[g, i0, i1, i2, i3].item() - ref) < 1e-7
+
+
+@pytest.mark.parametrize("H,cin,cout,k,nin,dgrad", [(32, 3, 20, 5, 1, False), (32, 20, 20, 3, 2, False),
+                                                    (16, 20, 50, 5, 1, False), (16, 50, 50, 3, 3, False),
+                                                    (32, 20, 20, 3, 1, True), (16, 50, 50, 3, 1, True),
+                                                    (16, 50, 20, 5, 1, True)])
+def test_conv_fast_equals_generic(H, cin, cout, k, nin, dgrad):
+    """The shape-specialised kernels (cnn_conv_fast.hip) walk the reduction in
+    the generic kernel's chunk order: outputs are bit-identical, in group-table
+    mode with accumulation and ReLU masks."""
+    Km = K()
+    torch.manual_seed(11)
+    Q, B, W = 5, 4, H
+    cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
+    ins = [bf(torch.randn(Q, B, H, W, cinp, device=DEV)) for _ in range(nin)]
+    w = bf(torch.randn(Q, coutp, k, k, cinp, device=DEV) * 0.2)
+    bias = torch.randn(Q, coutp, device=DEV) * 0.1
+    prev = bf(torch.randn(Q, B, H, W, coutp, device=DEV))
+    mask = bf(torch.randn(Q, B, H, W, coutp, device=DEV))
+    rows = torch.tensor([[4, (1 << nin) - 1, 0b11 | (0b10 << 8) | (0b10 << 16), 0],
+                         [1, (1 << nin) - 1, 0b01, 0], [2, 1, 0b10 | (0b10 << 16), 0]], dtype=torch.int32, device=DEV)
+    outs = []
+    for fast in (0, 1):
+        o0 = torch.zeros(Q, B, H, W, coutp, dtype=torch.bfloat16, device=DEV)
+        o1 = prev.clone()
+        a = Km.ConvArgs()
+        for i, s in enumerate(ins):
+            a.inp[i] = s.data_ptr()
+        a.out[0], a.out[1], a.out_mask[1] = o0.data_ptr(), o1.data_ptr(), mask.data_ptr()
+        a.gtab, a.ngroups, a.relu = rows.data_ptr(), 3, 0 if dgrad else 1
+        a.w, a.bias = w.data_ptr(), 0 if dgrad else bias.data_ptr()
+        a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = Q, B, H, W, cinp, coutp, k, k
+        a.TH = Km.conv_tile_rows(H, W)
+        old = Km.lib().gt_conv_set_fast(fast)
+        Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv")
+        Km.lib().gt_conv_set_fast(old)
+        torch.cuda.synchronize()
+        outs.append((o0, o1))
+    assert outs[0][0].abs().max().item() > 0
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -17,6 +17,7 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 TILES = tuple(int(t) for t in os.environ.get("GENTUN_TILES", "128").split(","))
 dev = torch.device("cuda", 0)
 L = K.lib()
+L.gt_conv_set_fast(int(os.environ.get("GENTUN_CONV_FAST", "1")))
 G, B = int(os.environ.get("GENTUN_BENCH_G", "5")), 32
 
 
