@@ -34,6 +34,8 @@ struct ConvArgs {
   int n_in, n_out, acc_flags, relu;
   int G, B, H, W, Cinp, Coutp, KH, KW, TH;   // G = Q (group count of the slot tensors)
   int ngroups;                      // launch groups (rows of gtab); legacy mode: G
+  uint16_t* xsum;                   // optional [Q][B][H][W][Cinp]: groups summing >1 input slot write the sum
+                                    // (the layer's wgrad then reads one tensor instead of re-summing)
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

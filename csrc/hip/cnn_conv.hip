@@ -127,6 +127,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
     }
     patch[i] = v;
   }
+  if (a.xsum && n_src > 1) {
+    // the summed input of this band (patch interior) for the layer's wgrad
+    __syncthreads();
+    uint16_t* xo = a.xsum + ((long)g * a.B + b) * img + (long)h0 * a.W * a.Cinp;
+    for (int i = tid; i < a.TH * a.W * ncb; i += 256) {
+      const int cb = i % ncb, pix = i / ncb;
+      const int r = pix / a.W, cc = pix % a.W;
+      if (h0 + r < a.H)
+        *reinterpret_cast<uint4*>(xo + (long)i * 8) = patch[((r + ph) * PW + cc + pw) * ncb + cb];
+    }
+  }
   {
     const FastDiv div_kw(a.KW);
     for (int c = tid; c < nchunks + 4; c += 256) {
@@ -506,6 +517,7 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
 // ---------------------------------------------------------------------------
 
 extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream);
+extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream);
 
 extern "C" {
 
@@ -547,6 +559,10 @@ int gt_conv_wgrad(const WgradArgs* a, hipStream_t stream) {
   if (a->Cinp % 8 || a->Coutp % 8 || a->pps % 64) return -1;
   if (!a->gtab && (a->n_in < 1 || a->n_in > GT_MAXSLOT)) return -1;
   if (a->ngroups < 1) return 0;
+  if (g_conv_fast) {
+    const int rc = gt_wgrad_fast(a, stream);
+    if (rc != -100) return rc;
+  }
   const int Kdim = a->KH * a->KW * a->Cinp;
   dim3 grid((Kdim + (a->part_b ? 8 : 0) + 63) / 64, a->S, a->ngroups * ((a->Coutp + 63) / 64));
   hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, stream, *a);

@@ -83,16 +83,10 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
   for (int s = 0; s < PF; ++s) load_a(s, areg[s]);
 
   // ---- patch: summed inputs (or gathered dataset image), zero halo --------
-  const uint16_t* src[GT_MAXSLOT];
-  int n_src = 0;
-#pragma unroll
-  for (int k = 0; k < GT_MAXSLOT; ++k)
-    if ((gr.in_mask >> k) & 1) src[n_src++] = a.in[k] + ((long)g * a.B + b) * img;
-  if (a.gather) {
-    const long id = a.gather[((long)a.st->cur_step * a.G + g) * a.B + b];
-    src[0] = a.in[0] + id * img;
-    n_src = 1;
-  }
+  const long gimg = ((long)g * a.B + b) * img;
+  const int n_src = a.gather ? 1 : __builtin_popcount(gr.in_mask);
+  const uint16_t* src0 = a.gather ? a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img
+                                  : a.in[__builtin_ctz(gr.in_mask | 0x100) & 7] + gimg;
   long poff[NPT];
   bool pok[NPT];
 #pragma unroll
@@ -108,7 +102,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
     uint4 v[NPT];
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
-      v[j] = pok[j] ? *reinterpret_cast<const uint4*>(src[0] + poff[j]) : make_uint4(0, 0, 0, 0);
+      v[j] = pok[j] ? *reinterpret_cast<const uint4*>(src0 + poff[j]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
       if (tid + 256 * j < NP) patch[tid + 256 * j] = v[j];
@@ -118,13 +112,26 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
       if (tid + 256 * j >= NP) continue;
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t8[8];
       if (pok[j]) {
-        for (int k = 0; k < n_src; ++k) {
-          unpack8(*reinterpret_cast<const uint4*>(src[k] + poff[j]), t8);
+#pragma unroll
+        for (int k = 0; k < GT_MAXSLOT; ++k) {
+          if (!((gr.in_mask >> k) & 1)) continue;
+          unpack8(*reinterpret_cast<const uint4*>(a.in[k] + gimg + poff[j]), t8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) acc[e] += t8[e];
         }
       }
       patch[tid + 256 * j] = pack8(acc);
+    }
+  }
+  if (a.xsum && n_src > 1) {
+    // the summed input of this band (interior of the patch) for the layer's wgrad
+    __syncthreads();
+    uint16_t* xo = a.xsum + ((long)g * a.B + b) * img + (long)h0 * W * NCBI * 8;
+    for (int i = tid; i < TH * W * NCBI; i += 256) {
+      const int cb = i % NCBI, pix = i / NCBI;
+      const int r = pix / W, c = pix % W;
+      if (h0 + r < a.H)
+        *reinterpret_cast<uint4*>(xo + (long)i * 8) = patch[((r + KH / 2) * PW + c + KW / 2) * NCBI + cb];
     }
   }
   // chunk c -> patch offset of its (kh, kw, cb) relative to the output pixel
@@ -236,5 +243,221 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   CONV_FAST_CASE(5, 5, 3, 16, 16, 4)         // s2 input conv (20 -> 50)
   CONV_FAST_CASE(3, 3, 7, 16, 16, 4)         // s2 nodes / output conv, and their dgrad (50 -> 50)
   CONV_FAST_CASE(5, 5, 7, 16, 16, 2)         // s2 input conv dgrad (50 -> 20)
+  return -100;
+}
+
+// ===========================================================================
+// Weight gradient, shape-specialised:
+//   dW[co][kh][kw][ci] (+ db[co]) = sum_px dz[px][co] * x[px + (kh, kw)][ci]
+// One workgroup = one group x one split (a contiguous range of R-row image
+// bands) and owns the WHOLE dW of the layer in registers: wave w accumulates
+// k-column tiles w, w+4, ... for every output-channel tile. Per band, the
+// dz rows and the zero-haloed input rows (DAG inputs summed, batch gather for
+// the first layer) are staged into LDS with all loads in flight; each 32-pixel
+// K-step then reads both MFMA operands with ds_read_b64_tr_b16 (A = dz^T,
+// B = shifted input) at per-lane addresses fixed for the whole kernel plus
+// compile-time K-step offsets -- no index math in the loop. The bias gradient
+// is an extra "ones" column. The workgroup writes one fp32 partial
+// [S][G][Coutp][Kdim] (+ [S][G][Coutp]) that Adam reduces in fixed order.
+// ===========================================================================
+
+typedef __attribute__((ext_vector_type(4))) short wf_short4_t;
+typedef __attribute__((ext_vector_type(8))) short wf_short8_t;
+
+__device__ __forceinline__ uint4 tr_pair(const char* lo_addr, const char* hi_addr) {
+  typedef __attribute__((address_space(3))) wf_short4_t lds_s4;
+  const wf_short4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(lo_addr));
+  const wf_short4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(hi_addr));
+  const wf_short8_t v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(uint4, v);
+}
+
+__device__ __attribute__((aligned(16))) uint4 wf_zero16[1];
+
+typedef __attribute__((address_space(3))) void wf_lvoid_t;
+
+// one 16-byte chunk per lane into LDS at wave base + 16 * lane. Inline asm so
+// hipcc does not see an LDS write it would fence every later LDS read behind
+// (it waits vmcnt(0) before any ds_read that may alias an in-flight builtin
+// DMA): the kernel waits for its DMAs explicitly (vmcnt(0) + barrier) before
+// reading the buffer they fill. m0 is saved / restored around the DMA.
+__device__ __forceinline__ void wf_glds16(const void* src, const void* lds_wave_base) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(wf_lvoid_t*)lds_wave_base);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(l) : "memory");
+}
+
+template <int KH, int KW, int NCBI, int NCBO, int W, int R, int NW>
+__global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
+  constexpr int NT_ = NW * 64;                     // threads
+  constexpr int PW = W + KW - 1, PR = R + KH - 1;
+  constexpr int NCH = KH * KW * NCBI;              // weight chunks (8 input channels each)
+  constexpr int NKT = (NCH + 1 + 1) / 2;           // 16-column tiles incl. the bias chunk
+  constexpr int MT = (NCBO * 8 + 15) / 16;         // output-channel tiles
+  constexpr int TPW = (NKT + NW - 1) / NW;         // k-column tiles per wave
+  constexpr int KS = R * W / 32;                   // K-steps per band
+  constexpr int XCH = PR * PW * NCBI;              // staged input chunks per band
+  constexpr int DCH = R * W * NCBO;                // staged dz chunks per band
+  constexpr int XT = (XCH + NT_ - 1) / NT_, DT = (DCH + NT_ - 1) / NT_;
+  constexpr int XCR = (XCH + 63) / 64 * 64, DCR = (DCH + 63) / 64 * 64;   // wave-granular LDS images
+  constexpr int XROW = NCBI * 16, DROW = NCBO * 16;   // LDS bytes per pixel
+  static_assert(R * W % 32 == 0 && (W == 16 || W == 32), "bands must be whole 32-pixel K-steps");
+
+  // two band buffers (DMA of band i+1 overlaps the MFMAs of band i); whole
+  // NT_-chunk rows so every DMA wave-instruction has a full 1 KiB target
+  __shared__ __attribute__((aligned(16))) uint4 xs[2][XCR];
+  __shared__ __attribute__((aligned(16))) uint4 ds[2][DCR];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int s = blockIdx.x;
+  const GroupRec gr = group_rec(a.gtab, blockIdx.y, a.n_in, 0, 0, nullptr);
+  const int g = gr.g;
+  const int nbi = a.H / R;                                     // bands per image
+  const int bps = a.pps / (R * W);                             // bands per split
+  const int band0 = s * bps;
+  const int band1 = min(band0 + bps, a.B * nbi);
+  const long img_in = (long)a.H * W * NCBI * 8, img_out = (long)a.H * W * NCBO * 8;
+  const int first_in = __builtin_ctz(gr.in_mask | 0x100);
+  const bool single = __builtin_popcount(gr.in_mask) == 1 || a.gather;
+  const long fold_off = (long)g * a.B * img_in;
+
+  auto issue = [&](int band, int buf) {
+    const int b = band / nbi, h0 = (band - b * nbi) * R;
+    const uint16_t* src0 = a.gather ? a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img_in
+                                    : a.in[first_in & 7] + fold_off + (long)b * img_in;
+#pragma unroll
+    for (int j = 0; j < XT; ++j) {
+      const int i = tid + NT_ * j;
+      const int cb = i % NCBI, pix = i / NCBI;
+      const int hh = h0 - KH / 2 + pix / PW, ww = pix % PW - KW / 2;
+      const bool ok = i < XCH && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
+      const long off = ((long)hh * W + ww) * (NCBI * 8) + cb * 8;
+      if (single) {
+        if (NT_ * j + 64 * wave < XCR)          // wave-uniform: whole 1 KiB targets only
+          wf_glds16(ok ? (const void*)(src0 + off) : (const void*)wf_zero16, &xs[buf][NT_ * j + 64 * wave]);
+      } else if (i < XCH) {
+        // N-ary DAG input: sum in fp32 through registers
+        float sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t8[8];
+        if (ok) {
+#pragma unroll
+          for (int k = 0; k < GT_MAXSLOT; ++k) {
+            if (!((gr.in_mask >> k) & 1)) continue;
+            unpack8(*reinterpret_cast<const uint4*>(a.in[k] + fold_off + (long)b * img_in + off), t8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sum[e] += t8[e];
+          }
+        }
+        xs[buf][i] = pack8(sum);
+      }
+    }
+    const char* dsrc = reinterpret_cast<const char*>(a.dz + (long)g * a.B * img_out + (long)b * img_out +
+                                                     (long)h0 * W * NCBO * 8);
+#pragma unroll
+    for (int j = 0; j < DT; ++j) {
+      const int i = tid + NT_ * j;
+      if (NT_ * j + 64 * wave < DCR)
+        wf_glds16(i < DCH ? (const void*)(dsrc + (long)i * 16) : (const void*)wf_zero16, &ds[buf][NT_ * j + 64 * wave]);
+    }
+  };
+
+  // ---- per-lane operand addresses (fixed for the whole kernel) -------------
+  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, l16 = lane & 15;
+  const int px0 = 8 * gq + q;                                  // lane's first K row (pixel of a K-step)
+  const int prow = px0 / W, pcol = px0 % W;                    // its position inside the band
+  const int xlane = (prow * PW + pcol) * XROW;
+  const int dlane = px0 * DROW + p * 8;
+  int xoff[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int n = wave + NW * t;
+    int c = 2 * n + (p >> 1);
+    if (c >= NCH) c = 0;                                       // bias / padding columns: any valid row
+    const int kk = c / NCBI, cb = c % NCBI;
+    xoff[t] = xlane + ((kk / KW) * PW + (kk % KW)) * XROW + cb * 16 + (p & 1) * 8;
+  }
+  const bool ones_lane = l16 == (NCH & 1) * 8;                 // the bias column inside its tile
+
+  f32x4_t acc[MT][TPW];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[m][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  if (band0 < band1) issue(band0, 0);
+  int cur = 0;
+  for (int band = band0; band < band1; ++band, cur ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                      // band landed everywhere; buffer cur^1 no longer read
+    if (band + 1 < band1) issue(band + 1, cur ^ 1);
+    const char* xb = reinterpret_cast<const char*>(xs[cur]);
+    const char* db = reinterpret_cast<const char*>(ds[cur]) + dlane;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int xrow_off = ((ks * 32) / W) * PW * XROW;        // compile-time after unrolling
+      uint4 afr[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const char* d0 = db + ks * 32 * DROW + m * 32;
+        afr[m] = tr_pair(d0, d0 + 4 * DROW);
+      }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int n = wave + NW * t;
+        if (n >= NKT) continue;
+        const char* x0 = xb + xrow_off + xoff[t];
+        uint4 bfr = tr_pair(x0, x0 + 4 * XROW);
+        if (n == NCH / 2 && ones_lane) bfr = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][t] = mfma16(afr[m], bfr, acc[m][t]);
+      }
+    }
+  }
+
+  // ---- partial out: lane holds rows 4*kq..+3 (co) of column l16 (k col) ------
+  const int kq = lane >> 4;
+  constexpr int Kdim = NCH * 8;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int n = wave + NW * t;
+    if (n >= NKT) continue;
+    const int col = n * 16 + l16;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = m * 16 + kq * 4 + i;
+        if (co >= a.Coutp) continue;
+        if (col < Kdim)
+          a.part_w[(((long)s * a.G + g) * a.Coutp + co) * Kdim + col] = acc[m][t][i];
+        else if (col == Kdim && a.part_b)
+          a.part_b[((long)s * a.G + g) * a.Coutp + co] = acc[m][t][i];
+      }
+  }
+}
+
+#define WGRAD_FAST_CASE(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_)                                              \
+  if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->Coutp == NCBO_ * 8 && a->W == W_ &&     \
+      a->H % R_ == 0 && a->pps % (R_ * W_) == 0) {                                                        \
+    dim3 grid(a->S, a->ngroups);                                                                         \
+    hipLaunchKernelGGL((wgrad_fast_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_>), grid, dim3(NW_ * 64), 0, stream, *a); \
+    return (int)hipGetLastError();                                                                       \
+  }
+
+// 1 if a specialised wgrad exists for this geometry (the host then sizes the
+// split in whole bands: pps multiple of R*W)
+extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, int W) {
+  if (KH == 5 && KW == 5 && Cinp == 8 && Coutp == 24 && W == 32 && H % 8 == 0) return 8 * 32;
+  if (KH == 3 && KW == 3 && Cinp == 24 && Coutp == 24 && W == 32 && H % 8 == 0) return 8 * 32;
+  if (KH == 5 && KW == 5 && Cinp == 24 && Coutp == 56 && W == 16 && H % 16 == 0) return 16 * 16;
+  if (KH == 3 && KW == 3 && Cinp == 56 && Coutp == 56 && W == 16 && H % 16 == 0) return 16 * 16;
+  return 0;
+}
+
+extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
+  WGRAD_FAST_CASE(5, 5, 1, 3, 32, 8, 4)      // s1 input conv (3 -> 20)
+  WGRAD_FAST_CASE(3, 3, 3, 3, 32, 8, 4)      // s1 nodes / output conv (20 -> 20)
+  WGRAD_FAST_CASE(5, 5, 3, 7, 16, 16, 8)     // s2 input conv (20 -> 50)
+  WGRAD_FAST_CASE(3, 3, 7, 7, 16, 16, 8)     // s2 nodes / output conv (50 -> 50)
   return -100;
 }

@@ -100,8 +100,8 @@ class HipPopJob(FoldJob):
             raise ValueError("HIP head kernel supports at most 16 classes")
         if B > 64:
             raise ValueError("HIP head kernel supports batch_size <= 64")
-        if max(p0.nodes) > K.MAXSLOT:
-            raise ValueError("at most {} nodes per stage".format(K.MAXSLOT))
+        if max(p0.nodes) > K.MAXSLOT - 2:
+            raise ValueError("at most {} nodes per stage".format(K.MAXSLOT - 2))
         self._build_topology()
         self._allocate()
         self.state = torch.zeros(8, dtype=torch.int32, device=dev)
@@ -151,7 +151,8 @@ class HipPopJob(FoldJob):
                 L.KH, L.KW = k_
                 L.Kdim = L.KH * L.KW * L.cinp
                 L.TH = K.conv_tile_rows(H, W)
-                L.pps, L.S = K.wgrad_split(self.B * H * W, L.Kdim, L.coutp)
+                L.pps, L.S = K.wgrad_split(self.B * H * W, L.Kdim, L.coutp,
+                                           band=K.wgrad_band(L.KH, L.KW, L.cinp, L.coutp, H, W))
                 L.slots = slots            # input slot names, bit k = slots[k]
                 L.rows = rows              # [(q, in_mask)] ascending q
                 st["layers"].append(L)
@@ -195,6 +196,13 @@ class HipPopJob(FoldJob):
         for name, (hh, ww, cc) in self.shapes.items():
             self.act[name] = torch.zeros((Q, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
             self.grad[name] = torch.zeros((Q, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
+        # layers where some group sums >1 input: the forward conv writes that
+        # sum once ("<layer>_xin") and the layer's wgrad reads it as one slot
+        for L in self.layers:
+            L.xin = None
+            if any(bin(im).count("1") > 1 for _, im in L.rows):
+                L.xin = L.name + "_xin"
+                self.act[L.xin] = torch.zeros((Q, B, L.H, L.W, L.cinp), dtype=torch.bfloat16, device=dev)
         hs, ws = self.final_hw
         self.Fp = hs * ws * self.final_cp
         self.Up = round_up(p0.dense_units, 64)
@@ -318,6 +326,8 @@ class HipPopJob(FoldJob):
                 a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [self.act[L.name].data_ptr()], [],
                                     L.w_bf, L.b[0], 1, [(q, im, 1) for q, im in L.rows],
                                     gather=gather_train if first else None)
+                if L.xin is not None:
+                    a.xsum = self.act[L.xin].data_ptr()
                 self.fwd_ops.append(("conv", a, L))
             sel = torch.tensor([1 if act else 0 for act in st["active"]], dtype=torch.int32, device=self.device)
             self._keep.append(sel)
@@ -381,13 +391,15 @@ class HipPopJob(FoldJob):
             for L in reversed(st["layers"]):
                 first = L.slots == ["input"]
                 wa = K.WgradArgs()
-                for i, n in enumerate(L.slots):
+                wslots = L.slots + ([L.xin] if L.xin is not None else [])
+                for i, n in enumerate(wslots):
                     wa.inp[i] = self._slot_ptr(n)
                 wa.gather = gather_train if first else 0
                 wa.st = self.state.data_ptr()
                 wa.dz = self.grad[L.name].data_ptr()
                 wa.part_w, wa.part_b = L.part_w.data_ptr(), L.part_b.data_ptr()
-                wa.gtab = self._gtab([(q, im, 0) for q, im in L.rows]).data_ptr()
+                xbit = 1 << len(L.slots)
+                wa.gtab = self._gtab([(q, xbit if bin(im).count("1") > 1 else im, 0) for q, im in L.rows]).data_ptr()
                 wa.ngroups = len(L.rows)
                 wa.G, wa.B, wa.H, wa.W = Q, B, L.H, L.W
                 wa.Cinp, wa.Coutp, wa.KH, wa.KW, wa.S, wa.pps = L.cinp, L.coutp, L.KH, L.KW, L.S, L.pps
@@ -543,6 +555,7 @@ class HipPopJob(FoldJob):
             if kind == "conv":
                 b = K.ConvArgs.from_buffer_copy(a)
                 b.st = self.eval_state.data_ptr()
+                b.xsum = 0
                 ops.append((kind, b, Lr))
             else:
                 ops.append((kind, a, Lr))

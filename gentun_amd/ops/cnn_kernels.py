@@ -29,7 +29,7 @@ class ConvArgs(C.Structure):
                 ("out_mask", P * MAXSLOT), ("w", P), ("bias", P), ("gtab", P),
                 ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
-                ("TH", I), ("ngroups", I)]
+                ("TH", I), ("ngroups", I), ("xsum", P)]
 
 
 class WgradArgs(C.Structure):
@@ -99,6 +99,8 @@ def lib():
         L.gt_pool_fwd.restype = I
         L.gt_pool_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P]
         L.gt_pool_bwd.restype = I
+        L.gt_wgrad_fast_band.argtypes = [I, I, I, I, I, I]
+        L.gt_wgrad_fast_band.restype = I
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
         L.gt_glorot_init.argtypes = [C.POINTER(InitArgs), I, P]
@@ -144,13 +146,28 @@ def wgrad_blocks(kdim, with_bias=True):
 
 
 WGRAD_TARGET_BLOCKS = int(__import__("os").environ.get("GENTUN_WGRAD_TARGET", "50"))
+WGRAD_FAST_SPLITS = int(__import__("os").environ.get("GENTUN_WGRAD_SPLITS", "8"))
 
 
-def wgrad_split(npix, kdim, coutp, G=None, target_blocks=None):
+def wgrad_band(KH, KW, cinp, coutp, H, W):
+    """Pixels per band of the shape-specialised wgrad kernel (0: generic)."""
+    L = lib()
+    if not L.gt_conv_set_fast(1):       # probe + restore the fast-path switch
+        L.gt_conv_set_fast(0)
+        return 0
+    return int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W))
+
+
+def wgrad_split(npix, kdim, coutp, G=None, target_blocks=None, band=0):
     """(pixels per split, splits) for conv_wgrad: ~``target_blocks``
     workgroups PER FOLD (the split never depends on how many folds share a
     launch, so a fold's gradient summation order -- and its result -- is the
     same alone or batched), 64-pixel K-steps, >= 2 K-steps per workgroup."""
+    if band:
+        # specialised kernel: one workgroup per split, splits of whole bands
+        nb = npix // band
+        bps = -(-nb // max(1, WGRAD_FAST_SPLITS))
+        return bps * band, -(-nb // bps)
     if target_blocks is None:
         target_blocks = WGRAD_TARGET_BLOCKS
     nb = wgrad_blocks(kdim)

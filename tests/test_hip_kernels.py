@@ -528,3 +528,52 @@ def test_conv_fast_equals_generic(H, cin, cout, k, nin, dgrad):
     assert outs[0][0].abs().max().item() > 0
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("H,cin,cout,k,nin,first", [(32, 3, 20, 5, 1, True), (32, 20, 20, 3, 2, False),
+                                                    (16, 20, 50, 5, 1, False), (16, 50, 50, 3, 3, False),
+                                                    (16, 50, 50, 3, 1, False)])
+def test_conv_wgrad_fast(H, cin, cout, k, nin, first):
+    """Shape-specialised wgrad (whole-dW workgroups over image bands, LDS-DMA
+    double buffering, transposed LDS reads) vs a PyTorch fp32 reference, in
+    group-table mode over a subset of groups (DAG input sums, batch gather)."""
+    Km = K()
+    torch.manual_seed(12)
+    Q, B, W = 3, 4, H
+    cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
+    band = Km.wgrad_band(k, k, cinp, coutp, H, W)
+    assert band > 0
+    xs = [bf(torch.randn(Q, B, cin, H, W, device=DEV)).float() for _ in range(nin)]
+    dz = bf(torch.randn(Q, B, cout, H, W, device=DEV)).float()
+    x_in = [torch.stack([nhwc_pad(x[g], cinp) for g in range(Q)]).to(torch.bfloat16).contiguous() for x in xs]
+    gather = None
+    if first:
+        data = torch.zeros(3 * Q * B, H, W, cinp, dtype=torch.bfloat16, device=DEV)
+        perm = torch.randperm(3 * Q * B, device=DEV)[:Q * B]
+        data[perm] = x_in[0].view(Q * B, H, W, cinp)
+        gather = perm.view(1, Q, B).to(torch.int64).contiguous()
+        x_in = [data]
+    dz_p = torch.stack([nhwc_pad(dz[g], coutp) for g in range(Q)]).to(torch.bfloat16).contiguous()
+    Kdim = k * k * cinp
+    pps, S = Km.wgrad_split(B * H * W, Kdim, coutp, band=band)
+    pw = torch.full((S, Q, coutp, Kdim), 9.0, device=DEV)
+    pb = torch.full((S, Q, coutp), 9.0, device=DEV)
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    rows = torch.tensor([[2, (1 << nin) - 1, 0, 0], [0, (1 << nin) - 1, 0, 0]], dtype=torch.int32, device=DEV)
+    a = Km.WgradArgs()
+    for i, t in enumerate(x_in):
+        a.inp[i] = t.data_ptr()
+    a.gather = gather.data_ptr() if gather is not None else 0
+    a.st, a.gtab, a.ngroups = st.data_ptr(), rows.data_ptr(), 2
+    a.dz, a.part_w, a.part_b = dz_p.data_ptr(), pw.data_ptr(), pb.data_ptr()
+    a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.S, a.pps = Q, B, H, W, cinp, coutp, k, k, S, pps
+    Km.check(Km.lib().gt_conv_wgrad(a, stream()), "wgrad_fast")
+    torch.cuda.synchronize()
+    xsum = bf(sum(xs)).float()
+    for g in (0, 2):
+        ref = torch.nn.grad.conv2d_weight(xsum[g], (cout, cin, k, k), dz[g], padding=k // 2)
+        got = pw[:, g].sum(0).view(coutp, k, k, cinp)[:cout, :, :, :cin].permute(0, 3, 1, 2)
+        assert (got - ref).abs().max().item() < 1e-2 * ref.abs().max().item() + 1e-3
+        refb = dz[g].sum((0, 2, 3))
+        assert (pb[:, g].sum(0)[:cout] - refb).abs().max().item() < 1e-2 * refb.abs().max().item() + 1e-3
+    assert torch.all(pw[:, 1] == 9.0)          # group 1 is not in the table: untouched

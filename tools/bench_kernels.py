@@ -108,7 +108,7 @@ for name, H, cin, cout, k, nin in shapes:
     # wgrad
     npix = B * H * W
     Kdim = k * k * cinp
-    pps, S = K.wgrad_split(npix, Kdim, coutp, G)
+    pps, S = K.wgrad_split(npix, Kdim, coutp, G, band=K.wgrad_band(k, k, cinp, coutp, H, W))
     pw = torch.zeros(S, G, coutp, Kdim, device=dev)
     pb = torch.zeros(S, G, coutp, device=dev)
     wa = K.WgradArgs()
