@@ -43,7 +43,10 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
   static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == 4, "tile shape");
   static_assert(W % 16 == 0 || 16 % W == 0, "pixel groups must tile image rows");
 
-  __shared__ __attribute__((aligned(16))) uint4 patch[NP];
+  constexpr int OROW = NT * 16 + 4;                 // fp32 output-tile row (conflict-free float4 writes)
+  constexpr int SM = (NP > TP * OROW / 4) ? NP : TP * OROW / 4;
+  __shared__ __attribute__((aligned(16))) uint4 smem[SM];   // patch, then the output tile
+  uint4* patch = smem;
   __shared__ int coff[NKS * 4];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
@@ -107,20 +110,36 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
     for (int j = 0; j < NPT; ++j)
       if (tid + 256 * j < NP) patch[tid + 256 * j] = v[j];
   } else {
+    // N-ary DAG input: chunks in batches of JB; per slot, the batch's loads are
+    // all in flight, then an fp32 accumulate (one rounding to bf16 at the end)
+    constexpr int JB = NPT < 5 ? NPT : 5;
 #pragma unroll
-    for (int j = 0; j < NPT; ++j) {
-      if (tid + 256 * j >= NP) continue;
-      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t8[8];
-      if (pok[j]) {
+    for (int j0 = 0; j0 < NPT; j0 += JB) {
+      float acc8[JB][8];
 #pragma unroll
-        for (int k = 0; k < GT_MAXSLOT; ++k) {
-          if (!((gr.in_mask >> k) & 1)) continue;
-          unpack8(*reinterpret_cast<const uint4*>(a.in[k] + gimg + poff[j]), t8);
+      for (int j = 0; j < JB; ++j)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[e] += t8[e];
+        for (int e = 0; e < 8; ++e) acc8[j][e] = 0.f;
+#pragma unroll
+      for (int k = 0; k < GT_MAXSLOT; ++k) {
+        if (!((gr.in_mask >> k) & 1)) continue;
+        const uint16_t* sk = a.in[k] + gimg;
+        uint4 v[JB];
+#pragma unroll
+        for (int j = 0; j < JB; ++j)
+          v[j] = (j0 + j < NPT && pok[j0 + j]) ? *reinterpret_cast<const uint4*>(sk + poff[j0 + j])
+                                                : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < JB; ++j) {
+          float t8[8];
+          unpack8(v[j], t8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc8[j][e] += t8[e];
         }
       }
-      patch[tid + 256 * j] = pack8(acc);
+#pragma unroll
+      for (int j = 0; j < JB; ++j)
+        if (j0 + j < NPT && tid + 256 * (j0 + j) < NP) patch[tid + 256 * (j0 + j)] = pack8(acc8[j]);
     }
   }
   if (a.xsum && n_src > 1) {
@@ -183,41 +202,59 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
       for (int h = 0; h < PG; ++h) acc[t][h] = mfma16(acur[t], bfr[h], acc[t][h]);
   }
 
-  // ---- epilogue --------------------------------------------------------------
+  // ---- epilogue: accumulators -> fp32 tile in LDS -> 16-byte row stores ------
+  // (a lane holds 4 channels of one pixel per tile: 8-byte scattered stores
+  // are store-issue bound; through LDS every store is a contiguous 16 B of the
+  // band, which is one contiguous range of the NHWC output)
+  __syncthreads();                                   // everyone is done with the patch
+  float* otile = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int h = 0; h < PG; ++h) {
-    const int p = (pgw + h) * 16 + l16;
-    const int y = h0 + p / W, x = p % W;
-    if (y >= a.H) continue;
-    const long obase = ((((long)g * a.B + b) * a.H + y) * W + x) * a.Coutp;
+  for (int t = 0; t < CT; ++t) {
+    const int co0 = (wco + t) * 16 + kq * 4;
 #pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const int co0 = (wco + t) * 16 + kq * 4;
-      if (co0 >= a.Coutp) continue;
-      float v[4];
+    for (int h = 0; h < PG; ++h) {
+      const int p = (pgw + h) * 16 + l16;
+      float4 v;
+      v.x = acc[t][h][0] + bias_v[t][0];
+      v.y = acc[t][h][1] + bias_v[t][1];
+      v.z = acc[t][h][2] + bias_v[t][2];
+      v.w = acc[t][h][3] + bias_v[t][3];
+      if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+      *reinterpret_cast<float4*>(otile + p * OROW + co0) = v;
+    }
+  }
+  __syncthreads();
+  const int ncbo = a.Coutp >> 3;
+  const long obase = (((long)g * a.B + b) * a.H + h0) * W * a.Coutp;
+  for (int i = tid; i < TP * ncbo; i += 256) {
+    const int p = i / ncbo, cb = i - p * ncbo;
+    const float4 lo = *reinterpret_cast<const float4*>(otile + p * OROW + cb * 8);
+    const float4 hi = *reinterpret_cast<const float4*>(otile + p * OROW + cb * 8 + 4);
+    const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const long off = obase + (long)i * 8;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float xv = acc[t][h][i] + bias_v[t][i];
-        if (a.relu) xv = fmaxf(xv, 0.f);
-        v[i] = xv;
+    for (int k = 0; k < GT_MAXSLOT; ++k) {
+      if (!((gr.out_mask >> k) & 1)) continue;
+      uint4* dst = reinterpret_cast<uint4*>(a.out[k] + off);
+      float sum[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sum[e] = v[e];
+      if ((gr.out_mask >> (8 + k)) & 1) {
+        float o[8];
+        unpack8(*dst, o);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sum[e] += o[e];
       }
-      for (int k = 0; k < GT_MAXSLOT; ++k) {
-        if (!((gr.out_mask >> k) & 1)) continue;
-        uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
-        float sum[4] = {v[0], v[1], v[2], v[3]};
-        if ((gr.out_mask >> (8 + k)) & 1) {
-          const uint2 old = *dst;
-          sum[0] += __uint_as_float(old.x << 16); sum[1] += __uint_as_float(old.x & 0xffff0000u);
-          sum[2] += __uint_as_float(old.y << 16); sum[3] += __uint_as_float(old.y & 0xffff0000u);
-        }
-        if ((gr.out_mask >> (16 + k)) & 1) {
-          const uint2 m = *reinterpret_cast<const uint2*>(a.out_mask[k] + obase + co0);
-          const uint32_t mw[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
+      if ((gr.out_mask >> (16 + k)) & 1) {
+        const uint4 m = *reinterpret_cast<const uint4*>(a.out_mask[k] + off);
+        const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) sum[i] = (mw[i] != 0u && mw[i] < 0x8000u) ? sum[i] : 0.f;
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t hbits = (e & 1) ? (mw[e >> 1] >> 16) : (mw[e >> 1] & 0xffffu);
+          sum[e] = (hbits != 0u && hbits < 0x8000u) ? sum[e] : 0.f;   // bf16 > 0
         }
-        *dst = pack4(sum);
       }
+      *dst = pack8(sum);
     }
   }
 }

@@ -39,11 +39,15 @@ __device__ __forceinline__ float opt_update(const StepState* st, float p, float 
 
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;  // NaN
-  u += 0x7fffu + ((u >> 16) & 1u);                      // round to nearest even
-  return (uint16_t)(u >> 16);
+// round to nearest even; a plain conversion compiles to the gfx950
+// v_cvt_pk_bf16_f32 (one instruction per pair, NaN stays NaN)
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
@@ -57,17 +61,17 @@ __device__ __forceinline__ void unpack8(const uint4& v, float* f) {
 
 __device__ __forceinline__ uint4 pack8(const float* f) {
   uint4 v;
-  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
-  v.z = (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16);
-  v.w = (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16);
+  v.x = pack2bf(f[0], f[1]);
+  v.y = pack2bf(f[2], f[3]);
+  v.z = pack2bf(f[4], f[5]);
+  v.w = pack2bf(f[6], f[7]);
   return v;
 }
 
 __device__ __forceinline__ uint2 pack4(const float* f) {
   uint2 v;
-  v.x = (uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16);
-  v.y = (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16);
+  v.x = pack2bf(f[0], f[1]);
+  v.y = pack2bf(f[2], f[3]);
   return v;
 }
 

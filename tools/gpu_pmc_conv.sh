@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE GRBM_COUNT"
 P2="SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SALU FETCH_SIZE GRBM_GUI_ACTIVE"
 P3="WRITE_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"
-for spec in conv_fwd:1 conv_fwd:4 conv_dgrad:1 conv_wgrad:1 conv_wgrad:4; do
+for spec in ${SPECS:-conv_fwd:1 conv_fwd:4 conv_wgrad:1 conv_wgrad:4}; do
   for m in 0; do
     i=0
     for P in "$P1" "$P2" "$P3"; do
