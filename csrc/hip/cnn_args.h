@@ -36,6 +36,7 @@ struct ConvArgs {
   int ngroups;                      // launch groups (rows of gtab); legacy mode: G
   uint16_t* xsum;                   // optional [Q][B][H][W][Cinp]: groups summing >1 input slot write the sum
                                     // (the layer's wgrad then reads one tensor instead of re-summing)
+  int dbg;                          // diagnostics only (0 in production): bit 0 skip MFMA, 1 skip stores, 2 skip loads
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

@@ -101,7 +101,11 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
     pok[j] = i < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
     poff[j] = ((long)hh * W + ww) * (NCBI * 8) + cb * 8;
   }
-  if (n_src == 1) {
+  if (a.dbg & 4) {
+#pragma unroll
+    for (int j = 0; j < NPT; ++j)
+      if (tid + 256 * j < NP) patch[tid + 256 * j] = make_uint4(0, 0, 0, 0);
+  } else if (n_src == 1) {
     uint4 v[NPT];
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
@@ -183,6 +187,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
 #pragma unroll
     for (int h = 0; h < PG; ++h) acc[t][h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  if (!(a.dbg & 1))
 #pragma unroll
   for (int s = 0; s < NKS; ++s) {
     const uint4* pb = patch + lbase + gbase + coff[s * 4 + kq];
@@ -226,6 +231,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
   __syncthreads();
   const int ncbo = a.Coutp >> 3;
   const long obase = (((long)g * a.B + b) * a.H + h0) * W * a.Coutp;
+  if (!(a.dbg & 2))
   for (int i = tid; i < TP * ncbo; i += 256) {
     const int p = i / ncbo, cb = i - p * ncbo;
     const float4 lo = *reinterpret_cast<const float4*>(otile + p * OROW + cb * 8);
