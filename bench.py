@@ -31,7 +31,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--per-gpu", type=int, default=8, help="candidates per GPU per generation")
+    ap.add_argument("--per-gpu", type=int, default=16, help="candidates per GPU per generation")
     ap.add_argument("--streams", type=int, default=1, help="concurrent population jobs per GPU")
     ap.add_argument("--pop-batch", type=int, default=16, help="candidates per population job (shared launches)")
     ap.add_argument("--backend", default=None, help="hip (default on GPU) or torch")

@@ -350,7 +350,8 @@ struct DenseWgradAdamArgs {
   uint16_t* wt;        // [G][Up][Fp] bf16 copy (transposed)
   const StepState* st;
   int G, B, Fp, Up;
-};
+  int Cp, Cr, Ur;      // feature = pixel * Cp + channel; channels >= Cr and units >= Ur are padding
+};                     // (zero forever: skipped, 13 % of the layer's optimizer traffic)
 
 // grid (Fp/16, G), 256 threads. Thread: unit quad q (4 units), rows fr, fr+2, ..., fr+14.
 __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArgs a) {
@@ -366,7 +367,7 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
   __syncthreads();
   const float lr_t = a.st->lr_t;
   const float* dH = a.dH + (long)g * a.B * a.Up;
-  const int nq = a.Up >> 2;
+  const int nq = a.Ur > 0 ? (a.Ur + 3) >> 2 : a.Up >> 2;
   const int fr = tid >> 7;
   for (int q = tid & 127; q < nq; q += 128) {
     const int u0 = q * 4;
@@ -385,6 +386,11 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
     for (int r = 0; r < 8; ++r) {
       const int f = f0 + fr + 2 * r;
       if (f >= a.Fp) continue;
+      if (a.Cp > 0 && f % a.Cp >= a.Cr) {      // padded channel: weights stay 0, only the bf16 tile
+#pragma unroll
+        for (int i = 0; i < 4; ++i) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
+        continue;
+      }
       const long off = ((long)g * a.Fp + f) * a.Up + u0;
       float4 pp = *reinterpret_cast<float4*>(a.p + off);
       float4 mm = *reinterpret_cast<float4*>(a.m + off);
@@ -403,7 +409,8 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
   __syncthreads();
   // transposed bf16 copy: wt[u][f0 .. f0+15] (32 contiguous bytes per unit)
   uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
-  for (int i = tid; i < a.Up * 2; i += 256) {
+  const int nu = a.Ur > 0 ? ((a.Ur + 3) >> 2) << 2 : a.Up;
+  for (int i = tid; i < nu * 2; i += 256) {
     const int u = i >> 1, half = i & 1;
     if (f0 + half * 8 + 8 <= a.Fp) {
       *reinterpret_cast<uint4*>(wt + (long)u * a.Fp + f0 + half * 8) =

@@ -367,6 +367,7 @@ class HipPopJob(FoldJob):
             m.data_ptr(), v.data_ptr()
         dw.wt, dw.st = self.w1t_bf.data_ptr(), self.state.data_ptr()
         dw.G, dw.B, dw.Fp, dw.Up = Q, B, self.Fp, self.Up
+        dw.Cp, dw.Cr, dw.Ur = self.final_cp, self.plan.kernels_per_layer[-1], self.plan.dense_units
         self.dense_wgrad_args = dw
         # ---- backward. Per group and slot: the FIRST consumer in forward order
         # is the LAST writer of the slot's gradient and applies its ReLU mask;

@@ -56,7 +56,7 @@ class DenseDgradArgs(C.Structure):
 
 class DenseWgradAdamArgs(C.Structure):
     _fields_ = [("x", P), ("dH", P), ("p", P), ("m", P), ("v", P), ("wt", P), ("st", P),
-                ("G", I), ("B", I), ("Fp", I), ("Up", I)]
+                ("G", I), ("B", I), ("Fp", I), ("Up", I), ("Cp", I), ("Cr", I), ("Ur", I)]
 
 
 class AdamSeg(C.Structure):
