@@ -84,46 +84,73 @@ struct Quantized {
   std::vector<int> nbins;               // per feature
 };
 
+// One feature column -> bins (exact: <= kMaxBin distinct values keep one bin
+// each, otherwise kMaxBin equal-count quantile cuts). Writes bin b of row i
+// at out[i * stride].
+static int quantize_column(const float* X, int n, int F, int f, uint8_t* out, size_t stride,
+                           std::vector<float>& col, std::vector<float>& sorted) {
+  for (int i = 0; i < n; ++i) {
+    float v = X[(size_t)i * F + f];
+    col[i] = std::isnan(v) ? -std::numeric_limits<float>::infinity() : v;
+  }
+  sorted = col;
+  std::sort(sorted.begin(), sorted.end());
+  std::vector<float> uniq;
+  uniq.reserve(256);
+  for (int i = 0; i < n; ++i)
+    if (uniq.empty() || sorted[i] != uniq.back()) {
+      uniq.push_back(sorted[i]);
+      if ((int)uniq.size() > kMaxBin) break;
+    }
+  std::vector<float> upper;           // bin b holds values <= upper[b]
+  if ((int)uniq.size() <= kMaxBin) {
+    upper = uniq;
+  } else {
+    // quantile cuts: kMaxBin bins of ~equal counts
+    upper.reserve(kMaxBin);
+    for (int b = 1; b <= kMaxBin; ++b) {
+      size_t idx = std::min<size_t>((size_t)n - 1, (size_t)((double)b * n / kMaxBin) - (b == kMaxBin ? 1 : 0));
+      float v = sorted[idx];
+      if (upper.empty() || v > upper.back()) upper.push_back(v);
+    }
+    upper.back() = sorted[n - 1];
+  }
+  for (int i = 0; i < n; ++i) {
+    int b = (int)(std::lower_bound(upper.begin(), upper.end(), col[i]) - upper.begin());
+    if (b >= (int)upper.size()) b = (int)upper.size() - 1;
+    out[(size_t)i * stride] = (uint8_t)b;
+  }
+  return (int)upper.size();
+}
+
+// Columns are independent: one thread per stripe of features (the per-column
+// sort dominates: ~n log n per feature). feature_major: bins[f][n] (the GPU
+// histogram layout) instead of bins[n][F].
+static void quantize_into(const float* X, int n, int F, uint8_t* bins, int* nbins, bool feature_major) {
+  int nt = (int)std::max(1u, std::thread::hardware_concurrency());
+  nt = std::min(nt, std::max(1, F));
+  auto work = [&](int t) {
+    std::vector<float> col(n), sorted;
+    for (int f = t; f < F; f += nt)
+      nbins[f] = feature_major ? quantize_column(X, n, F, f, bins + (size_t)f * n, 1, col, sorted)
+                               : quantize_column(X, n, F, f, bins + f, (size_t)F, col, sorted);
+  };
+  if (nt == 1 || (size_t)n * F < (1u << 16)) {
+    nt = 1;
+    work(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t) th.emplace_back(work, t);
+  for (auto& x : th) x.join();
+}
+
 Quantized quantize(const float* X, int n, int F) {
   Quantized q;
   q.n = n; q.F = F;
   q.bins.resize((size_t)n * F);
   q.nbins.resize(F);
-  std::vector<float> col(n);
-  for (int f = 0; f < F; ++f) {
-    for (int i = 0; i < n; ++i) {
-      float v = X[(size_t)i * F + f];
-      col[i] = std::isnan(v) ? -std::numeric_limits<float>::infinity() : v;
-    }
-    std::vector<float> sorted(col);
-    std::sort(sorted.begin(), sorted.end());
-    std::vector<float> uniq;
-    uniq.reserve(256);
-    for (int i = 0; i < n; ++i)
-      if (uniq.empty() || sorted[i] != uniq.back()) {
-        uniq.push_back(sorted[i]);
-        if ((int)uniq.size() > kMaxBin) break;
-      }
-    std::vector<float> upper;           // bin b holds values <= upper[b]
-    if ((int)uniq.size() <= kMaxBin) {
-      upper = uniq;
-    } else {
-      // quantile cuts: kMaxBin bins of ~equal counts
-      upper.reserve(kMaxBin);
-      for (int b = 1; b <= kMaxBin; ++b) {
-        size_t idx = std::min<size_t>((size_t)n - 1, (size_t)((double)b * n / kMaxBin) - (b == kMaxBin ? 1 : 0));
-        float v = sorted[idx];
-        if (upper.empty() || v > upper.back()) upper.push_back(v);
-      }
-      upper.back() = sorted[n - 1];
-    }
-    q.nbins[f] = (int)upper.size();
-    for (int i = 0; i < n; ++i) {
-      int b = (int)(std::lower_bound(upper.begin(), upper.end(), col[i]) - upper.begin());
-      if (b >= (int)upper.size()) b = (int)upper.size() - 1;
-      q.bins[(size_t)i * F + f] = (uint8_t)b;
-    }
-  }
+  quantize_into(X, n, F, q.bins.data(), q.nbins.data(), false);
   return q;
 }
 
@@ -434,9 +461,13 @@ int gbdt_cv(const float* X, int n, int F, const float* y, const int* fold_of, in
 
 // Quantise only (exposed for the HIP path and tests): bins out [n][F], nbins out [F].
 int gbdt_quantize(const float* X, int n, int F, uint8_t* bins_out, int* nbins_out) {
-  Quantized q = quantize(X, n, F);
-  std::memcpy(bins_out, q.bins.data(), q.bins.size());
-  std::memcpy(nbins_out, q.nbins.data(), sizeof(int) * F);
+  quantize_into(X, n, F, bins_out, nbins_out, false);
+  return 0;
+}
+
+// Feature-major bins [F][n] for the GPU histogram path.
+int gbdt_quantize_fm(const float* X, int n, int F, uint8_t* bins_out, int* nbins_out) {
+  quantize_into(X, n, F, bins_out, nbins_out, true);
   return 0;
 }
 

@@ -247,8 +247,9 @@ uint64_t smix(uint64_t x) {
 extern "C" {
 
 // Same contract as gbdt_cv (csrc/gbdt/engine.cpp) for objectives 0-3 and
-// metrics rmse/mae/logloss/error; bins are precomputed on the host.
-int gbdt_cv_hip(const uint8_t* bins_rowmajor, const int* nbins_h, int n, int F, const float* y_h,
+// metrics rmse/mae/logloss/error; bins are precomputed on the host,
+// FEATURE-MAJOR [F][n] (gbdt_quantize_fm; cached per dataset by the caller).
+int gbdt_cv_hip(const uint8_t* binsT, const int* nbins_h, int n, int F, const float* y_h,
                 const int* fold_h, int nfold, const double* P, int objective, const int* metrics, int n_metrics,
                 int num_boost_round, int early_stopping_rounds, unsigned long long seed, double* out_hist) {
   if (objective > 3 || n_metrics != 1 || metrics[0] > 3) return -1;
@@ -256,9 +257,6 @@ int gbdt_cv_hip(const uint8_t* bins_rowmajor, const int* nbins_h, int n, int F, 
   const int metric = metrics[0];
   const int max_depth = std::max(0, (int)P[2]);
   // ---- device buffers
-  std::vector<uint8_t> binsT((size_t)n * F);
-  for (int i = 0; i < n; ++i)
-    for (int f = 0; f < F; ++f) binsT[(size_t)f * n + i] = bins_rowmajor[(size_t)i * F + f];
   uint8_t *d_bins, *d_fok;
   float *d_y, *d_margin, *d_leaf;
   int *d_fold, *d_node, *d_nb;
@@ -282,7 +280,7 @@ int gbdt_cv_hip(const uint8_t* bins_rowmajor, const int* nbins_h, int n, int F, 
   HC(hipMalloc(&d_tree, sizeof(int4) * 2 * max_nodes * 2));
   HC(hipMalloc(&d_leaf, sizeof(float) * 2 * max_nodes * 2));
   HC(hipMalloc(&d_met, sizeof(double) * 4));
-  HC(hipMemcpy(d_bins, binsT.data(), (size_t)n * F, hipMemcpyHostToDevice));
+  HC(hipMemcpy(d_bins, binsT, (size_t)n * F, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_y, y_h, sizeof(float) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_fold, fold_h, sizeof(int) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_nb, nbins_h, sizeof(int) * F, hipMemcpyHostToDevice));

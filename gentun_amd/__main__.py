@@ -32,7 +32,8 @@ def _common(ap):
     ap.add_argument("--checkpoint-dir", default=None)
     ap.add_argument("--resume", default=None, help="checkpoint file or directory to continue from")
     ap.add_argument("--events", default=None, help="JSONL event log path")
-    ap.add_argument("--streams", type=int, default=4, help="concurrent candidates per GPU")
+    ap.add_argument("--streams", type=int, default=1, help="concurrent population jobs per GPU")
+    ap.add_argument("--pop-batch", type=int, default=16, help="Genetic-CNN candidates sharing each kernel launch")
 
 
 def _device():
@@ -52,7 +53,7 @@ def _run_search(args, species, x, y, extra, maximize):
     from .utils import rng
     device = _device()
     comm = from_env(device=device)
-    evaluator = LocalBatchEvaluator(device=device, streams=args.streams)
+    evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch)
     if comm.rank != 0:
         GentunWorker(species, x, y, comm=comm, evaluator=evaluator).work()
         return None

@@ -53,6 +53,7 @@ def resolve_params(params):
 
 def cv(params, x, y, num_boost_round=10, nfold=3, early_stopping_rounds=None, seed=0, device=None,
        nthreads=0, folds=None):
+    x_key = x                     # dataset identity: the GPU path caches its bins per dataset
     x, y = _as_arrays(x, y)
     p, obj = resolve_params(params)
     num_class = int(params.get("num_class", 0) or 0)
@@ -77,7 +78,7 @@ def cv(params, x, y, num_boost_round=10, nfold=3, early_stopping_rounds=None, se
     if device is not None and str(device).startswith("cuda"):
         from . import gbdt_hip
         kept = gbdt_hip.cv(x, y, fold_of, len(folds), parr, obj, num_class, marr, nrounds,
-                           early_stopping_rounds or 0, seed, hist)
+                           early_stopping_rounds or 0, seed, hist, x_key=x_key)
     if kept is None:
         lib = _lib.gbdt()
         kept = lib.gbdt_cv(x.ctypes.data, n, x.shape[1], y.ctypes.data, fold_of.ctypes.data, len(folds),

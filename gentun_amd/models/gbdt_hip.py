@@ -31,13 +31,30 @@ def _fn():
     return f
 
 
-def cv(x, y, fold_of, nfold, parr, obj, num_class, marr, nrounds, esr, seed, hist):
-    from . import gbdt
+_QCACHE = []      # (x object, shape, binsT, nbins): every GA candidate reuses its dataset's bins
+
+
+def quantize_fm(x):
+    """Feature-major uint8 bins [F][n] + bins per feature, cached per dataset
+    object (quantisation is per-dataset work, not per-candidate)."""
+    for ent in _QCACHE:
+        if ent[0] is x and ent[1] == x.shape:
+            return ent[2], ent[3]
+    xc = np.ascontiguousarray(x, dtype=np.float32)
+    n, f = xc.shape
+    bins = np.zeros((f, n), np.uint8)
+    nb = np.zeros(f, np.int32)
+    _lib.gbdt().gbdt_quantize_fm(xc.ctypes.data, n, f, bins.ctypes.data, nb.ctypes.data)
+    _QCACHE.append((x, x.shape, bins, nb))
+    while len(_QCACHE) > 2:
+        _QCACHE.pop(0)
+    return bins, nb
+
+
+def cv(x, y, fold_of, nfold, parr, obj, num_class, marr, nrounds, esr, seed, hist, x_key=None):
     if not supported(obj, marr):
         return None
-    bins, nb = gbdt.quantize(x)
-    bins = np.ascontiguousarray(bins)
-    nb = np.ascontiguousarray(nb.astype(np.int32))
+    bins, nb = quantize_fm(x if x_key is None else x_key)
     fold_of = np.ascontiguousarray(fold_of.astype(np.int32))
     y = np.ascontiguousarray(y.astype(np.float32))
     marr = np.ascontiguousarray(marr.astype(np.int32))

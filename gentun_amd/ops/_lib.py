@@ -60,6 +60,8 @@ def gbdt():
                                 c.c_void_p]
         lib.gbdt_quantize.restype = c.c_int
         lib.gbdt_quantize.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
+        lib.gbdt_quantize_fm.restype = c.c_int
+        lib.gbdt_quantize_fm.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p]
         lib._typed = True
     return lib
 

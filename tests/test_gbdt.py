@@ -99,3 +99,16 @@ def test_iris_ga_baseline_cfg1():
     best = ga.run(2)
     assert best.get_fitness() < 0.35
     assert len(ga.history) == 2
+
+
+def test_quantize_feature_major_matches_and_caches():
+    """The GPU path's feature-major bins are the transpose of the CPU engine's
+    row-major bins, and are computed once per dataset object."""
+    from gentun_amd.models import gbdt_hip
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((3000, 7)).astype(np.float32)
+    x[:, 3] = np.round(x[:, 3])                      # few distinct values -> exact bins
+    b, nb = gbdt.quantize(x)
+    bt, nb2 = gbdt_hip.quantize_fm(x)
+    assert np.array_equal(b.T, bt) and np.array_equal(nb, nb2)
+    assert gbdt_hip.quantize_fm(x)[0] is bt
