@@ -54,3 +54,20 @@ def test_glyph_dataset():
     # determinism
     x2, _ = make_cifar_like(n=500, seed=1)
     assert np.array_equal(x, x2)
+
+
+def test_reference_module_paths_import():
+    """Every module path of the reference package resolves (code written as
+    ``from gentun.master import DistributedPopulation`` runs unchanged)."""
+    import importlib
+    for mod, names in [("gentun.algorithms", ["GeneticAlgorithm", "RussianRouletteGA"]),
+                       ("gentun.populations", ["Population", "GridPopulation"]),
+                       ("gentun.individuals", ["XgboostIndividual", "GeneticCnnIndividual", "random_log_uniform"]),
+                       ("gentun.master", ["DistributedPopulation", "DistributedGridPopulation"]),
+                       ("gentun.worker", ["GentunWorker"]),
+                       ("gentun.models.generic_models", ["GentunModel"]),
+                       ("gentun.models.keras_models", ["GeneticCnnModel"]),
+                       ("gentun.models.xgboost_models", ["XgboostModel"])]:
+        m = importlib.import_module(mod)
+        for n in names:
+            assert hasattr(m, n), (mod, n)
