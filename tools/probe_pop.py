@@ -27,9 +27,12 @@ x, y = make_cifar_like(n=n, seed=0)
 folds = stratified_kfold(np.argmax(y, 1), 5, seed=0)
 rnd = random.Random(0)
 plans = []
+deep = os.environ.get("SPACE") == "deep"          # BASELINE cfg 4: S=(3,4,5), kernels (20,50,100)
+nodes = (3, 4, 5) if deep else (3, 5)
+kernels = (20, 50, 100) if deep else (20, 50)
 for _ in range(P):
-    g = {"S_1": "".join(rnd.choice("01") for _ in range(3)), "S_2": "".join(rnd.choice("01") for _ in range(10))}
-    plans.append(make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10))
+    g = {"S_{}".format(s + 1): "".join(rnd.choice("01") for _ in range(k * (k - 1) // 2)) for s, k in enumerate(nodes)}
+    plans.append(make_plan(g, nodes, (32, 32, 3), kernels, ((5, 5),) * len(nodes), 500, 10))
 cfg = E.TrainConfig(epochs=(epochs,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce")
 streams = [torch.cuda.Stream(dev) for _ in range(ns)]
 # warm-up (allocator, code objects)
