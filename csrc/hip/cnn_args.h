@@ -37,6 +37,8 @@ struct ConvArgs {
   uint16_t* xsum;                   // optional [Q][B][H][W][Cinp]: groups summing >1 input slot write the sum
                                     // (the layer's wgrad then reads one tensor instead of re-summing)
   int dbg;                          // diagnostics only (0 in production): bit 0 skip MFMA, 1 skip stores, 2 skip loads
+  int epi_bf16;                     // 1: output tile staged in bf16 (forward launches: no accumulate / mask,
+                                    //    same bits, half the LDS); 0: fp32 tile (exact accumulate)
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

@@ -26,6 +26,22 @@
 
 #include "cnn_args.h"
 
+// LDS bytes of one launch: the patch or the output tile (fp32, or bf16 for
+// forward launches -- measured 7-9 % faster: more workgroups per CU), whichever is larger
+template <int KH, int KW, int NCBI, int W, int TH, int NT>
+struct FastCfg {
+  static constexpr int PW = W + KW - 1;
+  static constexpr int NP = (TH + KH - 1) * PW * NCBI;
+  static constexpr int TP = TH * W;
+  static constexpr int OROW = NT * 16 + 4;          // fp32 tile row (floats)
+  static constexpr int OROWB = NT * 16 + 8;         // bf16 tile row (elements)
+  static size_t lds(bool bf16) {
+    const size_t p = (size_t)NP * 16;
+    const size_t o = bf16 ? (size_t)TP * OROWB * 2 : (size_t)TP * OROW * 4;
+    return p > o ? p : o;
+  }
+};
+
 template <int KH, int KW, int NCBI, int W, int TH, int NT>
 __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
   constexpr int PH = TH + KH - 1, PW = W + KW - 1;
@@ -43,9 +59,9 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
   static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == 4, "tile shape");
   static_assert(W % 16 == 0 || 16 % W == 0, "pixel groups must tile image rows");
 
-  constexpr int OROW = NT * 16 + 4;                 // fp32 output-tile row (conflict-free float4 writes)
-  constexpr int SM = (NP > TP * OROW / 4) ? NP : TP * OROW / 4;
-  __shared__ __attribute__((aligned(16))) uint4 smem[SM];   // patch, then the output tile
+  using FC = FastCfg<KH, KW, NCBI, W, TH, NT>;
+  constexpr int OROW = FC::OROW, OROWB = FC::OROWB;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];   // patch, then the output tile
   uint4* patch = smem;
   __shared__ int coff[NKS * 4];
 
@@ -212,6 +228,38 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
   // are store-issue bound; through LDS every store is a contiguous 16 B of the
   // band, which is one contiguous range of the NHWC output)
   __syncthreads();                                   // everyone is done with the patch
+  const int ncbo = a.Coutp >> 3;
+  const long obase = (((long)g * a.B + b) * a.H + h0) * W * a.Coutp;
+  if (a.epi_bf16) {
+    // forward launches: values rounded once to bf16 in the tile, copied out
+    uint16_t* ot = reinterpret_cast<uint16_t*>(smem);
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const int co0 = (wco + t) * 16 + kq * 4;
+#pragma unroll
+      for (int h = 0; h < PG; ++h) {
+        const int p = (pgw + h) * 16 + l16;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = acc[t][h][i] + bias_v[t][i];
+          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+        }
+        *reinterpret_cast<uint2*>(ot + p * OROWB + co0) = pack4(v);
+      }
+    }
+    __syncthreads();
+    if (!(a.dbg & 2))
+    for (int i = tid; i < TP * ncbo; i += 256) {
+      const int p = i / ncbo, cb = i - p * ncbo;
+      const uint4 val = *reinterpret_cast<const uint4*>(ot + p * OROWB + cb * 8);
+#pragma unroll
+      for (int k = 0; k < GT_MAXSLOT; ++k)
+        if ((gr.out_mask >> k) & 1) *reinterpret_cast<uint4*>(a.out[k] + obase + (long)i * 8) = val;
+    }
+    return;
+  }
+  // accumulators -> fp32 tile in LDS -> 16-byte row stores (exact accumulate / mask)
   float* otile = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
@@ -229,8 +277,6 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
     }
   }
   __syncthreads();
-  const int ncbo = a.Coutp >> 3;
-  const long obase = (((long)g * a.B + b) * a.H + h0) * W * a.Coutp;
   if (!(a.dbg & 2))
   for (int i = tid; i < TP * ncbo; i += 256) {
     const int p = i / ncbo, cb = i - p * ncbo;
@@ -273,7 +319,8 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
 #define CONV_FAST_CASE(KH_, KW_, NCBI_, W_, TH_, NT_)                                                   \
   if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->W == W_ && nt == NT_ && a->H % TH_ == 0) { \
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
-    hipLaunchKernelGGL((conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_>), grid, dim3(256), 0, stream, *a); \
+    const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_>::lds(a->epi_bf16 != 0);                   \
+    hipLaunchKernelGGL((conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_>), grid, dim3(256), lds, stream, *a); \
     return (int)hipGetLastError();                                                                      \
   }
 

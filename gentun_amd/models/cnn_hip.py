@@ -328,6 +328,7 @@ class HipPopJob(FoldJob):
                                     gather=gather_train if first else None)
                 if L.xin is not None:
                     a.xsum = self.act[L.xin].data_ptr()
+                a.epi_bf16 = 1            # forward outputs never accumulate: bf16 output tile
                 self.fwd_ops.append(("conv", a, L))
             sel = torch.tensor([1 if act else 0 for act in st["active"]], dtype=torch.int32, device=self.device)
             self._keep.append(sel)

@@ -577,3 +577,31 @@ def test_conv_wgrad_fast(H, cin, cout, k, nin, first):
         refb = dz[g].sum((0, 2, 3))
         assert (pb[:, g].sum(0)[:cout] - refb).abs().max().item() < 1e-2 * refb.abs().max().item() + 1e-3
     assert torch.all(pw[:, 1] == 9.0)          # group 1 is not in the table: untouched
+
+
+@pytest.mark.parametrize("H,cin,cout,k", [(32, 20, 20, 3), (16, 50, 50, 3), (16, 20, 50, 5), (32, 3, 20, 5)])
+def test_conv_fast_bf16_tile_forward(H, cin, cout, k):
+    """Forward launches stage the output tile in bf16 (epi_bf16): same bits as
+    the fp32-tile epilogue when nothing accumulates."""
+    Km = K()
+    torch.manual_seed(13)
+    Q, B, W = 3, 4, H
+    cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
+    x = bf(torch.randn(Q, B, H, W, cinp, device=DEV))
+    w = bf(torch.randn(Q, coutp, k, k, cinp, device=DEV) * 0.2)
+    bias = torch.randn(Q, coutp, device=DEV) * 0.1
+    rows = torch.tensor([[2, 1, 1, 0], [0, 1, 1, 0]], dtype=torch.int32, device=DEV)
+    outs = []
+    for e in (0, 1):
+        o = torch.full((Q, B, H, W, coutp), 7.0, dtype=torch.bfloat16, device=DEV)
+        a = Km.ConvArgs()
+        a.inp[0], a.out[0] = x.data_ptr(), o.data_ptr()
+        a.gtab, a.ngroups, a.relu, a.epi_bf16 = rows.data_ptr(), 2, 1, e
+        a.w, a.bias = w.data_ptr(), bias.data_ptr()
+        a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = Q, B, H, W, cinp, coutp, k, k
+        a.TH = Km.conv_tile_rows(H, W)
+        Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv")
+        torch.cuda.synchronize()
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1])
+    assert torch.all(outs[1][1] == 7.0)

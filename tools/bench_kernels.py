@@ -85,6 +85,7 @@ for name, H, cin, cout, k, nin in shapes:
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.TH = G, B, H, W, cinp, coutp, k, k, TH
     a.ngroups = G
     a.dbg = int(os.environ.get("GENTUN_CONV_DBG", "0"))
+    a.epi_bf16 = int(os.environ.get("GENTUN_EPI_BF16", "0"))
     for tp in TILES:
         a.TH = K.conv_tile_rows(H, W, tp)
         us = timeit(lambda st: K.check(L.gt_conv_fwd(a, st), "fwd")) if only_k in (None, "conv_fwd") else 0.0
