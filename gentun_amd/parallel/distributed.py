@@ -261,12 +261,18 @@ class DistributedPopulation(Population):
     def __init__(self, species, x_train=None, y_train=None, individual_list=None, size=None,
                  crossover_rate=0.5, mutation_rate=0.015, maximize=True, additional_parameters=None,
                  host='localhost', port=5672, user='guest', password='guest', rabbit_queue='rpc_queue',
-                 comm=None, evaluator=None, split_folds=True, schedule="dynamic"):
+                 comm=None, evaluator=None, split_folds=True, schedule="auto"):
         self.comm = comm if comm is not None else _comm_from_args(host, port)
         if evaluator is None:
             evaluator = LocalBatchEvaluator()
-        if schedule not in ("dynamic", "lpt"):
-            raise ValueError("schedule must be 'dynamic' or 'lpt'")
+        if schedule not in ("auto", "dynamic", "lpt"):
+            raise ValueError("schedule must be 'auto', 'dynamic' or 'lpt'")
+        if schedule == "auto":
+            # a population-batched evaluator trains all of a rank's candidates in
+            # shared launches: balance the per-rank SUM of costs up front (LPT);
+            # dynamic claiming in cost order would hand one rank the most expensive
+            # batch. One-at-a-time evaluators keep the pull-queue behaviour.
+            schedule = "lpt" if getattr(evaluator, "pop_batch", 1) > 1 else "dynamic"
         self.local_evaluator = evaluator
         self.split_folds = split_folds
         self.schedule = schedule

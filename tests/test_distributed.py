@@ -230,3 +230,15 @@ def test_ticket_counters():
     for t in ts:
         t.join()
     assert sorted(got) == list(range(100))
+
+
+def test_auto_schedule_follows_the_evaluator():
+    """Population-batched evaluators get static LPT (balanced per-rank cost
+    sums); one-at-a-time evaluators keep dynamic pull-queue claiming."""
+    from gentun_amd.parallel import LocalComm
+    from gentun_amd.parallel.distributed import DistributedPopulation
+    from gentun_amd.parallel.evaluators import LocalBatchEvaluator, SequentialEvaluator
+    import torch
+    mk = lambda ev: DistributedPopulation(BitIndividual, None, None, size=6, comm=LocalComm(), evaluator=ev)
+    assert mk(LocalBatchEvaluator(device=torch.device("cpu"), pop_batch=16)).schedule == "lpt"
+    assert mk(SequentialEvaluator()).schedule == "dynamic"
