@@ -118,3 +118,25 @@ def test_sgd_momentum_update_rule():
     assert torch.allclose(job.flat.detach(), p1 + 0.5 * (-0.1 * g1) - 0.1 * g2, atol=1e-6)
     with pytest.raises(ValueError):
         E.TrainConfig(optimizer="rmsprop")
+
+
+def test_bench_contract_two_ranks_gloo():
+    """The driver's multi-GPU launch (torch.distributed.run, one process per
+    rank) rehearsed on CPU with gloo: one JSON line from rank 0, n_gpus = 2,
+    whole-job candidates counted once."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+           "--warmup", "0", "--per-gpu", "1", "--epochs", "1", "--lr", "1e-3", "--samples", "120", "--nfold", "2",
+           "--backend", "torch"]
+    out = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip().startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["timed_candidates"] == 2 and rec["value"] > 0
+    assert rec["config"]["parallelism"] == "population-dp2"
