@@ -28,13 +28,13 @@
 
 // LDS bytes of one launch: the patch or the output tile (fp32, or bf16 for
 // forward launches -- measured 7-9 % faster: more workgroups per CU), whichever is larger
-template <int KH, int KW, int NCBI, int W, int TH, int NT>
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO>
 struct FastCfg {
   static constexpr int PW = W + KW - 1;
   static constexpr int NP = (TH + KH - 1) * PW * NCBI;
   static constexpr int TP = TH * W;
-  static constexpr int OROW = NT * 16 + 4;          // fp32 tile row (floats)
-  static constexpr int OROWB = NT * 16 + 8;         // bf16 tile row (elements)
+  static constexpr int OROW = NT * 16 + 4;          // fp32 tile row (floats; conflict-free float4 writes)
+  static constexpr int OROWB = NT * 16 + 8;         // bf16 tile row (elements; conflict-free 8-byte writes)
   static size_t lds(bool bf16) {
     const size_t p = (size_t)NP * 16;
     const size_t o = bf16 ? (size_t)TP * OROWB * 2 : (size_t)TP * OROW * 4;
@@ -42,8 +42,13 @@ struct FastCfg {
   }
 };
 
-template <int KH, int KW, int NCBI, int W, int TH, int NT>
-__global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
+// occupancy targets (measured, profiles/conv_occupancy.txt): 4 waves / SIMD
+// (<= 128 registers) for 32-channel output tiles, 3 for the 5x5 64-channel
+// tile; the 3x3 56-channel-input tile spills at 3 and keeps 2
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO>
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))
+conv_fast_kernel(ConvArgs a) {
   constexpr int PH = TH + KH - 1, PW = W + KW - 1;
   constexpr int NP = PH * PW * NCBI;                // patch chunks (16 B)
   constexpr int NPT = (NP + 255) / 256;             // patch chunks per thread
@@ -59,7 +64,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
   static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == 4, "tile shape");
   static_assert(W % 16 == 0 || 16 % W == 0, "pixel groups must tile image rows");
 
-  using FC = FastCfg<KH, KW, NCBI, W, TH, NT>;
+  using FC = FastCfg<KH, KW, NCBI, W, TH, NT, NCO>;
   constexpr int OROW = FC::OROW, OROWB = FC::OROWB;
   extern __shared__ __attribute__((aligned(16))) uint4 smem[];   // patch, then the output tile
   uint4* patch = smem;
@@ -88,8 +93,8 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
     const int co = (wco + t) * 16 + l16;
-    wok[t] = co < a.Coutp;
-    wrow[t] = a.w + ((long)g * a.Coutp + (wok[t] ? co : 0)) * (NCH * 8);
+    wok[t] = co < NCO * 8;
+    wrow[t] = a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8);
   }
   uint4 areg[PF][CT];
   auto load_a = [&](int s, uint4* dst) {
@@ -98,8 +103,6 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
     for (int t = 0; t < CT; ++t)
       dst[t] = (wok[t] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[t] + c * 8) : make_uint4(0, 0, 0, 0);
   };
-#pragma unroll
-  for (int s = 0; s < PF; ++s) load_a(s, areg[s]);
 
   // ---- patch: summed inputs (or gathered dataset image), zero halo --------
   const long gimg = ((long)g * a.B + b) * img;
@@ -178,6 +181,10 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
     const int kk = c / NCBI, cb = c % NCBI;
     coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
   }
+  // first PF k-steps of weights in flight before the barrier (after the patch
+  // staging: its registers are dead by now -- lower peak register pressure)
+#pragma unroll
+  for (int s = 0; s < PF; ++s) load_a(s, areg[s]);
   // bias of this lane's output channels (forward only)
   float bias_v[CT][4];
 #pragma unroll
@@ -185,7 +192,7 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int co = (wco + t) * 16 + kq * 4 + i;
-      bias_v[t][i] = (a.bias && co < a.Coutp) ? a.bias[(long)g * a.Coutp + co] : 0.f;
+      bias_v[t][i] = (a.bias && co < NCO * 8) ? a.bias[(long)g * (NCO * 8) + co] : 0.f;
     }
   __syncthreads();
 
@@ -213,25 +220,21 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
       const int p = h * 16;                        // relative to the wave's first group
       bfr[h] = pb[((p / W) * PW + (p % W)) * NCBI];
     }
-    uint4 acur[CT];
-#pragma unroll
-    for (int t = 0; t < CT; ++t) acur[t] = areg[s % PF][t];
-    if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
 #pragma unroll
     for (int t = 0; t < CT; ++t)
 #pragma unroll
-      for (int h = 0; h < PG; ++h) acc[t][h] = mfma16(acur[t], bfr[h], acc[t][h]);
+      for (int h = 0; h < PG; ++h) acc[t][h] = mfma16(areg[s % PF][t], bfr[h], acc[t][h]);
+    if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
   }
 
   // ---- epilogue: accumulators -> fp32 tile in LDS -> 16-byte row stores ------
   // (a lane holds 4 channels of one pixel per tile: 8-byte scattered stores
   // are store-issue bound; through LDS every store is a contiguous 16 B of the
   // band, which is one contiguous range of the NHWC output)
-  __syncthreads();                                   // everyone is done with the patch
-  const int ncbo = a.Coutp >> 3;
-  const long obase = (((long)g * a.B + b) * a.H + h0) * W * a.Coutp;
   if (a.epi_bf16) {
-    // forward launches: values rounded once to bf16 in the tile, copied out
+    // forward launches: values rounded once to bf16 in an LDS tile, copied out
+    // as contiguous 16-byte chunks of the band (one contiguous NHWC range)
+    __syncthreads();                                 // everyone is done with the patch
     uint16_t* ot = reinterpret_cast<uint16_t*>(smem);
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
@@ -249,9 +252,13 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
+    const long obase = (((long)g * a.B + b) * a.H + h0) * W * (NCO * 8);
     if (!(a.dbg & 2))
-    for (int i = tid; i < TP * ncbo; i += 256) {
-      const int p = i / ncbo, cb = i - p * ncbo;
+#pragma unroll
+    for (int j = 0; j < (TP * NCO + 255) / 256; ++j) {
+      const int i = tid + 256 * j;
+      if (i >= TP * NCO) break;
+      const int p = i / NCO, cb = i - p * NCO;
       const uint4 val = *reinterpret_cast<const uint4*>(ot + p * OROWB + cb * 8);
 #pragma unroll
       for (int k = 0; k < GT_MAXSLOT; ++k)
@@ -259,7 +266,9 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
     }
     return;
   }
-  // accumulators -> fp32 tile in LDS -> 16-byte row stores (exact accumulate / mask)
+  // data gradient (DAG fan-out: several output slots, accumulate, ReLU masks):
+  // fp32 tile in LDS, then contiguous 16-byte read-modify-write per slot
+  __syncthreads();                                   // everyone is done with the patch
   float* otile = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
@@ -277,14 +286,17 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
     }
   }
   __syncthreads();
-  if (!(a.dbg & 2))
-  for (int i = tid; i < TP * ncbo; i += 256) {
-    const int p = i / ncbo, cb = i - p * ncbo;
+  if (a.dbg & 2) return;
+  const long obase = (((long)g * a.B + b) * a.H + h0) * W * (NCO * 8);
+#pragma unroll
+  for (int j = 0; j < (TP * NCO + 255) / 256; ++j) {
+    const int i = tid + 256 * j;
+    if (i >= TP * NCO) break;
+    const int p = i / NCO, cb = i - p * NCO;
     const float4 lo = *reinterpret_cast<const float4*>(otile + p * OROW + cb * 8);
     const float4 hi = *reinterpret_cast<const float4*>(otile + p * OROW + cb * 8 + 4);
     const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     const long off = obase + (long)i * 8;
-#pragma unroll
     for (int k = 0; k < GT_MAXSLOT; ++k) {
       if (!((gr.out_mask >> k) & 1)) continue;
       uint4* dst = reinterpret_cast<uint4*>(a.out[k] + off);
@@ -316,23 +328,23 @@ __global__ void __launch_bounds__(256) conv_fast_kernel(ConvArgs a) {
 // (the caller then uses the generic kernel)
 // ---------------------------------------------------------------------------
 
-#define CONV_FAST_CASE(KH_, KW_, NCBI_, W_, TH_, NT_)                                                   \
-  if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->W == W_ && nt == NT_ && a->H % TH_ == 0) { \
+#define CONV_FAST_CASE(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)                                              \
+  if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->W == W_ && a->Coutp == NCO_ * 8 &&    \
+      (NCO_ * 8 + 15) / 16 == NT_ && a->H % TH_ == 0) {                                                 \
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
-    const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_>::lds(a->epi_bf16 != 0);                   \
-    hipLaunchKernelGGL((conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_>), grid, dim3(256), lds, stream, *a); \
+    const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_>::lds(a->epi_bf16 != 0);             \
+    hipLaunchKernelGGL((conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_>), grid, dim3(256), lds, stream, *a); \
     return (int)hipGetLastError();                                                                      \
   }
 
 extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
-  const int nt = (a->Coutp + 15) / 16;
   // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
-  CONV_FAST_CASE(5, 5, 1, 32, 8, 2)          // s1 input conv (3 -> 20)
-  CONV_FAST_CASE(3, 3, 3, 32, 8, 2)          // s1 nodes / output conv, and their dgrad (20 -> 20)
-  CONV_FAST_CASE(5, 5, 3, 16, 16, 4)         // s2 input conv (20 -> 50)
-  CONV_FAST_CASE(3, 3, 7, 16, 16, 4)         // s2 nodes / output conv, and their dgrad (50 -> 50)
-  CONV_FAST_CASE(5, 5, 7, 16, 16, 2)         // s2 input conv dgrad (50 -> 20)
+  CONV_FAST_CASE(5, 5, 1, 32, 8, 2, 3)       // s1 input conv (3 -> 20)
+  CONV_FAST_CASE(3, 3, 3, 32, 8, 2, 3)       // s1 nodes / output conv, and their dgrad (20 -> 20)
+  CONV_FAST_CASE(5, 5, 3, 16, 16, 4, 7)      // s2 input conv (20 -> 50)
+  CONV_FAST_CASE(3, 3, 7, 16, 16, 4, 7)      // s2 nodes / output conv, and their dgrad (50 -> 50)
+  CONV_FAST_CASE(5, 5, 7, 16, 16, 2, 3)      // s2 input conv dgrad (50 -> 20)
   return -100;
 }
 

@@ -35,8 +35,9 @@ for _ in range(P):
     plans.append(make_plan(g, nodes, (32, 32, 3), kernels, ((5, 5),) * len(nodes), 500, 10))
 cfg = E.TrainConfig(epochs=(epochs,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce")
 streams = [torch.cuda.Stream(dev) for _ in range(ns)]
-# warm-up (allocator, code objects)
-E.make_population_job("hip", [(plans[0], folds, list(range(5)))], x, y, cfg, dev).launch().finish()
+# warm-up (allocator, code objects); WARM=0 keeps profiles free of the small warm-up job
+if os.environ.get("WARM", "1") != "0":
+    E.make_population_job("hip", [(plans[0], folds, list(range(5)))], x, y, cfg, dev).launch().finish()
 torch.cuda.synchronize()
 t = time.perf_counter()
 jobs = []
