@@ -390,7 +390,9 @@ __device__ __forceinline__ void wf_glds16(const void* src, const void* lds_wave_
                : "=&s"(keep) : "v"(src), "s"(l) : "memory");
 }
 
-template <int KH, int KW, int NCBI, int NCBO, int W, int R, int NW>
+// NB = LDS band buffers: 2 overlaps band i+1's DMA with band i's MFMAs; 1
+// halves the LDS so more workgroups share a CU
+template <int KH, int KW, int NCBI, int NCBO, int W, int R, int NW, int NB>
 __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
   constexpr int NT_ = NW * 64;                     // threads
   constexpr int PW = W + KW - 1, PR = R + KH - 1;
@@ -408,8 +410,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
 
   // two band buffers (DMA of band i+1 overlaps the MFMAs of band i); whole
   // NT_-chunk rows so every DMA wave-instruction has a full 1 KiB target
-  __shared__ __attribute__((aligned(16))) uint4 xs[2][XCR];
-  __shared__ __attribute__((aligned(16))) uint4 ds[2][DCR];
+  __shared__ __attribute__((aligned(16))) uint4 xs[NB][XCR];
+  __shared__ __attribute__((aligned(16))) uint4 ds[NB][DCR];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int s = blockIdx.x;
@@ -488,10 +490,10 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
 
   if (band0 < band1) issue(band0, 0);
   int cur = 0;
-  for (int band = band0; band < band1; ++band, cur ^= 1) {
+  for (int band = band0; band < band1; ++band, cur ^= (NB - 1)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();                      // band landed everywhere; buffer cur^1 no longer read
-    if (band + 1 < band1) issue(band + 1, cur ^ 1);
+    if (NB == 2 && band + 1 < band1) issue(band + 1, cur ^ 1);
     const char* xb = reinterpret_cast<const char*>(xs[cur]);
     const char* db = reinterpret_cast<const char*>(ds[cur]) + dlane;
 #pragma unroll
@@ -513,6 +515,10 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[m][t] = mfma16(afr[m], bfr, acc[m][t]);
       }
+    }
+    if (NB == 1 && band + 1 < band1) {
+      __syncthreads();                    // every wave is done reading the single buffer
+      issue(band + 1, 0);
     }
   }
 
@@ -538,11 +544,22 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
   }
 }
 
-#define WGRAD_FAST_CASE(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_)                                              \
+static int g_wgrad_nb = 0;   // 0: per-shape default, 1 / 2: force band buffers (A/B switch)
+
+extern "C" int gt_wgrad_set_nb(int nb) {
+  const int old = g_wgrad_nb;
+  g_wgrad_nb = nb;
+  return old;
+}
+
+#define WGRAD_FAST_CASE(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_)                                         \
   if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->Coutp == NCBO_ * 8 && a->W == W_ &&     \
       a->H % R_ == 0 && a->pps % (R_ * W_) == 0) {                                                        \
     dim3 grid(a->S, a->ngroups);                                                                         \
-    hipLaunchKernelGGL((wgrad_fast_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_>), grid, dim3(NW_ * 64), 0, stream, *a); \
+    if ((g_wgrad_nb ? g_wgrad_nb : NB_) == 1)                                                            \
+      hipLaunchKernelGGL((wgrad_fast_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1>), grid, dim3(NW_ * 64), 0, stream, *a); \
+    else                                                                                                 \
+      hipLaunchKernelGGL((wgrad_fast_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 2>), grid, dim3(NW_ * 64), 0, stream, *a); \
     return (int)hipGetLastError();                                                                       \
   }
 
@@ -556,10 +573,18 @@ extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, in
   return 0;
 }
 
+// Preferred splits per group (measured, profiles/wgrad_splits.txt): many small
+// workgroups for the 32-wide stage (single LDS buffer, 4+ per CU), few large
+// ones for the 16-wide stage (double-buffered, fewer partials for Adam).
+extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, int W) {
+  (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H;
+  return W >= 32 ? 16 : 4;
+}
+
 extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
-  WGRAD_FAST_CASE(5, 5, 1, 3, 32, 8, 4)      // s1 input conv (3 -> 20)
-  WGRAD_FAST_CASE(3, 3, 3, 3, 32, 8, 4)      // s1 nodes / output conv (20 -> 20)
-  WGRAD_FAST_CASE(5, 5, 3, 7, 16, 16, 8)     // s2 input conv (20 -> 50)
-  WGRAD_FAST_CASE(3, 3, 7, 7, 16, 16, 8)     // s2 nodes / output conv (50 -> 50)
+  WGRAD_FAST_CASE(5, 5, 1, 3, 32, 8, 4, 1)      // s1 input conv (3 -> 20)
+  WGRAD_FAST_CASE(3, 3, 3, 3, 32, 8, 4, 1)      // s1 nodes / output conv (20 -> 20)
+  WGRAD_FAST_CASE(5, 5, 3, 7, 16, 16, 8, 2)     // s2 input conv (20 -> 50)
+  WGRAD_FAST_CASE(3, 3, 7, 7, 16, 16, 8, 2)     // s2 nodes / output conv (50 -> 50)
   return -100;
 }

@@ -99,7 +99,11 @@ def lib():
         L.gt_pool_fwd.restype = I
         L.gt_pool_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P]
         L.gt_pool_bwd.restype = I
+        L.gt_wgrad_set_nb.argtypes = [I]
+        L.gt_wgrad_set_nb.restype = I
         L.gt_wgrad_fast_band.argtypes = [I, I, I, I, I, I]
+        L.gt_wgrad_fast_splits.argtypes = [I, I, I, I, I, I]
+        L.gt_wgrad_fast_splits.restype = I
         L.gt_wgrad_fast_band.restype = I
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
@@ -146,16 +150,18 @@ def wgrad_blocks(kdim, with_bias=True):
 
 
 WGRAD_TARGET_BLOCKS = int(__import__("os").environ.get("GENTUN_WGRAD_TARGET", "50"))
-WGRAD_FAST_SPLITS = int(__import__("os").environ.get("GENTUN_WGRAD_SPLITS", "8"))
+WGRAD_FAST_SPLITS = int(__import__("os").environ.get("GENTUN_WGRAD_SPLITS", "0"))   # 0: per-shape default
 
 
 def wgrad_band(KH, KW, cinp, coutp, H, W):
-    """Pixels per band of the shape-specialised wgrad kernel (0: generic)."""
+    """``(pixels per band, preferred splits)`` of the shape-specialised wgrad
+    kernel, or ``(0, 0)`` for the generic one."""
     L = lib()
     if not L.gt_conv_set_fast(1):       # probe + restore the fast-path switch
         L.gt_conv_set_fast(0)
-        return 0
-    return int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W))
+        return 0, 0
+    band = int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W))
+    return band, (int(L.gt_wgrad_fast_splits(KH, KW, cinp, coutp, H, W)) if band else 0)
 
 
 def wgrad_split(npix, kdim, coutp, G=None, target_blocks=None, band=0):
@@ -163,10 +169,14 @@ def wgrad_split(npix, kdim, coutp, G=None, target_blocks=None, band=0):
     workgroups PER FOLD (the split never depends on how many folds share a
     launch, so a fold's gradient summation order -- and its result -- is the
     same alone or batched), 64-pixel K-steps, >= 2 K-steps per workgroup."""
+    band, splits = band if isinstance(band, tuple) else (band, 8)
     if band:
-        # specialised kernel: one workgroup per split, splits of whole bands
+        # specialised kernel: one workgroup per split, splits of whole bands;
+        # the split count is a per-shape constant (never depends on how many
+        # groups share the launch: a fold's summation order is batch-invariant)
+        splits = WGRAD_FAST_SPLITS or splits
         nb = npix // band
-        bps = -(-nb // max(1, WGRAD_FAST_SPLITS))
+        bps = -(-nb // max(1, splits))
         return bps * band, -(-nb // bps)
     if target_blocks is None:
         target_blocks = WGRAD_TARGET_BLOCKS

@@ -533,7 +533,8 @@ def test_conv_fast_equals_generic(H, cin, cout, k, nin, dgrad):
 @pytest.mark.parametrize("H,cin,cout,k,nin,first", [(32, 3, 20, 5, 1, True), (32, 20, 20, 3, 2, False),
                                                     (16, 20, 50, 5, 1, False), (16, 50, 50, 3, 3, False),
                                                     (16, 50, 50, 3, 1, False)])
-def test_conv_wgrad_fast(H, cin, cout, k, nin, first):
+@pytest.mark.parametrize("splits,nb", [(None, 0), (2, 1), (2, 2)])
+def test_conv_wgrad_fast(H, cin, cout, k, nin, first, splits, nb):
     """Shape-specialised wgrad (whole-dW workgroups over image bands, LDS-DMA
     double buffering, transposed LDS reads) vs a PyTorch fp32 reference, in
     group-table mode over a subset of groups (DAG input sums, batch gather)."""
@@ -542,7 +543,10 @@ def test_conv_wgrad_fast(H, cin, cout, k, nin, first):
     Q, B, W = 3, 4, H
     cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
     band = Km.wgrad_band(k, k, cinp, coutp, H, W)
-    assert band > 0
+    assert band[0] > 0
+    if splits:
+        band = (band[0], splits)          # several bands per workgroup
+    old_nb = Km.lib().gt_wgrad_set_nb(nb)
     xs = [bf(torch.randn(Q, B, cin, H, W, device=DEV)).float() for _ in range(nin)]
     dz = bf(torch.randn(Q, B, cout, H, W, device=DEV)).float()
     x_in = [torch.stack([nhwc_pad(x[g], cinp) for g in range(Q)]).to(torch.bfloat16).contiguous() for x in xs]
@@ -569,6 +573,7 @@ def test_conv_wgrad_fast(H, cin, cout, k, nin, first):
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.S, a.pps = Q, B, H, W, cinp, coutp, k, k, S, pps
     Km.check(Km.lib().gt_conv_wgrad(a, stream()), "wgrad_fast")
     torch.cuda.synchronize()
+    Km.lib().gt_wgrad_set_nb(old_nb)
     xsum = bf(sum(xs)).float()
     for g in (0, 2):
         ref = torch.nn.grad.conv2d_weight(xsum[g], (cout, cin, k, k), dz[g], padding=k // 2)

@@ -18,6 +18,7 @@ TILES = tuple(int(t) for t in os.environ.get("GENTUN_TILES", "128").split(","))
 dev = torch.device("cuda", 0)
 L = K.lib()
 L.gt_conv_set_fast(int(os.environ.get("GENTUN_CONV_FAST", "1")))
+L.gt_wgrad_set_nb(int(os.environ.get("GENTUN_WGRAD_NB", "0")))
 G, B = int(os.environ.get("GENTUN_BENCH_G", "5")), 32
 
 
