@@ -450,10 +450,10 @@ __global__ void pool_fwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
                                 const int* __restrict__ sel, uint16_t* __restrict__ y, int NB, int B, int H, int W,
                                 int Cp) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
-  const long total = (long)NB * Ho * Wo * ncb;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  const uint32_t total = (uint32_t)NB * Ho * Wo * ncb;       // < 2^31 (host-checked): 32-bit index math
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int cb = (int)(i % ncb);
-    long r = i / ncb;
+    uint32_t r = i / ncb;
     const int wo = (int)(r % Wo); r /= Wo;
     const int ho = (int)(r % Ho);
     const long n = r / Ho;
@@ -478,10 +478,10 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
                                 uint16_t* __restrict__ dx0, uint16_t* __restrict__ dx1, int NB, int B, int H, int W,
                                 int Cp, int relu_mask) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
-  const long total = (long)NB * H * W * ncb;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+  const uint32_t total = (uint32_t)NB * H * W * ncb;         // < 2^31 (host-checked): 32-bit index math
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int cb = (int)(i % ncb);
-    long r = i / ncb;
+    uint32_t r = i / ncb;
     const int w = (int)(r % W); r /= W;
     const int h = (int)(r % H);
     const long n = r / H;
@@ -572,6 +572,7 @@ int gt_conv_wgrad(const WgradArgs* a, hipStream_t stream) {
 int gt_pool_fwd(const uint16_t* x0, const uint16_t* x1, const int* sel, uint16_t* y, int NB, int B, int H, int W,
                 int Cp, hipStream_t stream) {
   const long total = (long)NB * (H / 2) * (W / 2) * (Cp / 8);
+  if ((long)NB * H * W * (Cp / 8) >= (1L << 31)) return -4;
   const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, y, NB, B, H, W, Cp);
   return (int)hipGetLastError();
@@ -580,6 +581,7 @@ int gt_pool_fwd(const uint16_t* x0, const uint16_t* x1, const int* sel, uint16_t
 int gt_pool_bwd(const uint16_t* x0, const uint16_t* x1, const int* sel, const uint16_t* dy, uint16_t* dx0,
                 uint16_t* dx1, int NB, int B, int H, int W, int Cp, int relu_mask, hipStream_t stream) {
   const long total = (long)NB * H * W * (Cp / 8);
+  if (total >= (1L << 31)) return -4;
   const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
   hipLaunchKernelGGL(pool_bwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, dy, dx0, dx1, NB, B, H, W,
                      Cp, relu_mask);

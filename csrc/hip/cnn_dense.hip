@@ -441,7 +441,7 @@ struct AdamArgs {
 __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
   const int2 blk = a.blocks[blockIdx.x];
   const AdamSeg sg = a.segs[blk.x];
-  const long i = (long)blk.y + threadIdx.x;
+  const int i = blk.y + (int)threadIdx.x;          // segments are < 2^31 elements
   if (i >= sg.n) return;
   float gr = 0.f;
   for (int s = 0; s < sg.S; ++s) gr += sg.g[(long)s * sg.gstride + i];
@@ -452,13 +452,15 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
   const uint16_t pb = f2bf(p);
   if (sg.bf) sg.bf[i] = pb;
   if (sg.bfT) {
-    long r = i;
-    const int ci = (int)(r % sg.tCi); r /= sg.tCi;
-    const int kw = (int)(r % sg.tKW); r /= sg.tKW;
-    const int kh = (int)(r % sg.tKH); r /= sg.tKH;
-    const int co = (int)(r % sg.tCo);
-    const long gg = r / sg.tCo;
-    const long o = ((((gg * sg.tCi + ci) * sg.tKH + (sg.tKH - 1 - kh)) * sg.tKW) + (sg.tKW - 1 - kw)) * sg.tCo + co;
+    // flipped / transposed dgrad copy: 32-bit index math (64-bit division is
+    // a long software sequence on the GPU)
+    uint32_t r = (uint32_t)i;
+    const uint32_t ci = r % (uint32_t)sg.tCi; r /= (uint32_t)sg.tCi;
+    const uint32_t kw = r % (uint32_t)sg.tKW; r /= (uint32_t)sg.tKW;
+    const uint32_t kh = r % (uint32_t)sg.tKH; r /= (uint32_t)sg.tKH;
+    const uint32_t co = r % (uint32_t)sg.tCo;
+    const uint32_t gg = r / (uint32_t)sg.tCo;
+    const long o = ((((long)gg * sg.tCi + ci) * sg.tKH + (sg.tKH - 1 - kh)) * sg.tKW + (sg.tKW - 1 - kw)) * sg.tCo + co;
     sg.bfT[o] = pb;
   }
 }
