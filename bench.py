@@ -69,8 +69,10 @@ def run(args):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     import torch
     if torch.cuda.is_available():
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        # one rank per GPU; more ranks than GPUs (a 1-GPU multi-rank rehearsal) share devices
+        dev_index = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
 
@@ -81,7 +83,9 @@ def run(args):
     from gentun_amd.utils.data import make_cifar_like
 
     if world > 1:
-        comm = DistComm(backend="nccl" if device.type == "cuda" else "gloo", device=device)
+        # RCCL (backend "nccl") over xGMI between GPUs; GENTUN_DIST_BACKEND=gloo for rehearsals
+        backend = os.environ.get("GENTUN_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
+        comm = DistComm(backend=backend, device=device)
     else:
         comm = LocalComm()
 
@@ -128,7 +132,8 @@ def run(args):
 
     cph = 3600.0 * timed_evals / elapsed
     out = {
-        "metric": "candidates/hour (Genetic-CNN S=(3,5), CIFAR-10-shaped, 5-fold CV, epochs (20,4,1))",
+        "metric": "candidates/hour (Genetic-CNN S=(3,5), CIFAR-10-shaped, {}-fold CV, epochs ({}))".format(
+            args.nfold, ",".join(str(e) for e in epochs)),
         "value": round(cph, 2),
         "unit": "candidates/hour",
         "n_gpus": comm.world_size,
