@@ -112,6 +112,11 @@ class HipPopJob(FoldJob):
         seeds = [_rng.stable_hash(self.member_seeds[self.gmember[q]], "dropout") & 0xFFFFFFFF for q in range(Q)]
         self.drop_seeds_t = torch.tensor(np.asarray(seeds, np.uint32).view(np.int32), device=dev)
         self._keep = []          # device group tables referenced by argument structs
+        # weight-gradient side stream: every conv wgrad and the dense W1
+        # optimizer run concurrently with the data-gradient chain (fork / join
+        # edges inside the captured step graph)
+        self.side = torch.cuda.Stream(dev)
+        self.overlap = True
         self._build_adam_table()
         self._build_args()
 
@@ -521,20 +526,40 @@ class HipPopJob(FoldJob):
                 K.check(L.gt_pool_fwd(*a, s), "pool_fwd")
 
     def train_step(self):
-        L, s = self.L, self._stream()
+        L = self.L
+        main = torch.cuda.current_stream(self.device)
+        s = main.cuda_stream
         K.check(L.gt_step_begin(self.state.data_ptr(), s), "step_begin")
         self._run_fwd(s, self.fwd_ops)
         K.check(L.gt_dense_fwd(self.dense_fwd_args, s), "dense_fwd")
         K.check(L.gt_head(self.head_args, s), "head")
-        K.check(L.gt_dense_dgrad(self.dense_dgrad_args, s), "dense_dgrad")
-        K.check(L.gt_dense_wgrad_adam(self.dense_wgrad_args, s), "dense_wgrad_adam")
+        K.check(L.gt_dense_dgrad(self.dense_dgrad_args, s), "dense_dgrad")   # reads W1 before its update
+        side = self.side if self.overlap else main
+        ss = side.cuda_stream
+
+        def fork():
+            if side is not main:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                side.wait_event(ev)
+
+        # W1 gradient + Adam only needs dH and the pooled features: it overlaps
+        # the whole conv backward. Each layer's wgrad reads its final dz and its
+        # (unchanged) inputs: it overlaps the layer's dgrad and everything after.
+        fork()
+        K.check(L.gt_dense_wgrad_adam(self.dense_wgrad_args, ss), "dense_wgrad_adam")
         for kind, a, _ in self.bwd_ops:
             if kind == "wgrad":
-                K.check(L.gt_conv_wgrad(a, s), "conv_wgrad")
+                fork()
+                K.check(L.gt_conv_wgrad(a, ss), "conv_wgrad")
             elif kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
             else:
                 K.check(L.gt_pool_bwd(*a, s), "pool_bwd")
+        if side is not main:
+            ev = torch.cuda.Event()
+            ev.record(side)
+            main.wait_event(ev)
         K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
 
     def evaluate(self):
