@@ -32,6 +32,7 @@ written by the optimizer. Groups are member-major, fold-minor.
 """
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -39,7 +40,7 @@ import torch
 from ..ops import cnn_kernels as K
 from ..utils import rng as _rng
 from .cnn_engine import FoldJob
-from .genome import decode_stage
+from .pop_schedule import PopulationSchedule
 
 
 def pad8(c):
@@ -48,31 +49,6 @@ def pad8(c):
 
 def round_up(x, m):
     return (x + m - 1) // m * m
-
-
-class _Layer(object):
-    """One superset conv layer ('in', 'node' j or 'out' of a stage)."""
-    pass
-
-
-def _stage_topology(bits, nodes):
-    """(active, in_sets, sinks) of one stage of one candidate: ``in_sets[j]``
-    = input slot indices of node j (0 = stage input conv, i + 1 = node i)."""
-    if not any(b == '1' for b in bits):
-        return False, None, None
-    preds, _succs, active, outputs = decode_stage(bits, nodes)
-    in_sets = [None] * nodes
-    for j in range(nodes):
-        if active[j]:
-            in_sets[j] = [0] if not preds[j] else [p + 1 for p in preds[j]]
-    return True, in_sets, list(outputs)
-
-
-def _mask(slots):
-    m = 0
-    for k in slots:
-        m |= 1 << k
-    return m
 
 
 class HipPopJob(FoldJob):
@@ -86,10 +62,6 @@ class HipPopJob(FoldJob):
         if self.cfg.dtype != "bf16":
             raise ValueError("HIP backend computes in bf16 MFMA with fp32 master weights (dtype='bf16')")
         p0 = self.plan
-        for p, _, _ in self.members:
-            if (p.nodes, p.input_shape, p.kernels_per_layer, p.kernel_sizes, p.dense_units, p.classes) != \
-                    (p0.nodes, p0.input_shape, p0.kernels_per_layer, p0.kernel_sizes, p0.dense_units, p0.classes):
-                raise ValueError("population members must share the search space (only genes may differ)")
         Q, B, dev = self.G, self.B, self.device
         self.Q = Q
         h0, w0, c0 = p0.input_shape
@@ -116,73 +88,29 @@ class HipPopJob(FoldJob):
         # optimizer run concurrently with the data-gradient chain (fork / join
         # edges inside the captured step graph)
         self.side = torch.cuda.Stream(dev)
+        # the dense W1 optimizer (the largest single launch) on a stream of its
+        # own, so it does not sit in front of the first conv wgrads
+        self.side2 = torch.cuda.Stream(dev)
         self.overlap = True
+        self.w1_stream = os.environ.get("GENTUN_W1_STREAM", "1") != "0"
         self._build_adam_table()
         self._build_args()
 
     # ------------------------------------------------------------ topology
     def _build_topology(self):
+        """Superset layers / per-group launch records (models/pop_schedule.py)
+        plus the device geometry of every layer."""
         p0, Q = self.plan, self.Q
-        h0, w0, c0 = p0.input_shape
-        # per member, per stage: (active, in_sets, sinks)
-        topo = []
-        for p, _, _ in self.members:
-            topo.append([_stage_topology(p.genes["S_{}".format(s + 1)], p.nodes[s])
-                         for s in range(len(p.kernels_per_layer))])
-        self.stages = []
-        self.layers = []
-        cin = c0
-        x_slot = "input"
-        for s, cout in enumerate(p0.kernels_per_layer):
-            H, W = h0 >> s, w0 >> s
-            Kn = p0.nodes[s]
-            kh, kw = p0.kernel_sizes[s]
-            if kh % 2 == 0 or kw % 2 == 0:
-                raise ValueError("only odd kernel sizes are supported ('same' padding)")
-            pre = "s{}".format(s + 1)
-            st = {"s": s, "H": H, "W": W, "x_slot": x_slot, "in": pre + "_in", "out": pre + "_out",
-                  "pool": pre + "_pool", "layers": []}
-            # stage-active flag per group
-            st["active"] = [topo[self.gmember[q]][s][0] for q in range(Q)]
-
-            def add(name, kind, j, cin_, k_, slots, rows):
-                if not rows:
-                    return
-                L = _Layer()
-                L.name, L.kind, L.j, L.stage = name, kind, j, s
-                L.H, L.W = H, W
-                L.cin, L.cout = cin_, cout
-                L.cinp, L.coutp = pad8(cin_), pad8(cout)
-                L.KH, L.KW = k_
-                L.Kdim = L.KH * L.KW * L.cinp
-                L.TH = K.conv_tile_rows(H, W)
-                L.pps, L.S = K.wgrad_split(self.B * H * W, L.Kdim, L.coutp,
-                                           band=K.wgrad_band(L.KH, L.KW, L.cinp, L.coutp, H, W))
-                L.slots = slots            # input slot names, bit k = slots[k]
-                L.rows = rows              # [(q, in_mask)] ascending q
-                st["layers"].append(L)
-                self.layers.append(L)
-
-            add(st["in"], "in", -1, cin, (kh, kw), [x_slot], [(q, 1) for q in range(Q)])
-            node_slots = [st["in"]] + ["{}_n{}".format(pre, i) for i in range(Kn)]
-            for j in range(Kn):
-                rows = []
-                for q in range(Q):
-                    act, in_sets, _ = topo[self.gmember[q]][s]
-                    if act and in_sets[j] is not None:
-                        rows.append((q, _mask(in_sets[j])))
-                add("{}_n{}".format(pre, j), "node", j, cout, (3, 3), node_slots[:j + 1], rows)
-            rows = []
-            for q in range(Q):
-                act, _, sinks = topo[self.gmember[q]][s]
-                if act:
-                    rows.append((q, _mask(sinks)))
-            add(st["out"], "out", -1, cout, (3, 3), node_slots[1:], rows)
-            st["has_out"] = bool(rows)
-            self.stages.append(st)
-            x_slot = st["pool"]
-            cin = cout
-        self.last = x_slot
+        h0, w0, _ = p0.input_shape
+        self.sched = PopulationSchedule([self.members[self.gmember[q]][0] for q in range(Q)])
+        self.stages, self.layers = self.sched.stages, self.sched.layers
+        for L in self.layers:
+            L.cinp, L.coutp = pad8(L.cin), pad8(L.cout)
+            L.Kdim = L.KH * L.KW * L.cinp
+            L.TH = K.conv_tile_rows(L.H, L.W)
+            L.pps, L.S = K.wgrad_split(self.B * L.H * L.W, L.Kdim, L.coutp,
+                                       band=K.wgrad_band(L.KH, L.KW, L.cinp, L.coutp, L.H, L.W))
+        self.last = self.sched.last
         hs, ws = h0 >> len(p0.kernels_per_layer), w0 >> len(p0.kernels_per_layer)
         if hs < 1 or ws < 1:
             raise ValueError("input too small for the pooling stages")
@@ -194,9 +122,9 @@ class HipPopJob(FoldJob):
         Q, B, dev, p0 = self.Q, self.B, self.device, self.plan
         self.shapes = {}
         for st in self.stages:
-            for L in st["layers"]:
+            for L in st.layers:
                 self.shapes[L.name] = (L.H, L.W, L.coutp)
-            self.shapes[st["pool"]] = (st["H"] // 2, st["W"] // 2, pad8(p0.kernels_per_layer[st["s"]]))
+            self.shapes[st.pool] = (st.H // 2, st.W // 2, pad8(p0.kernels_per_layer[st.s]))
         self.act, self.grad = {}, {}
         for name, (hh, ww, cc) in self.shapes.items():
             self.act[name] = torch.zeros((Q, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
@@ -204,9 +132,7 @@ class HipPopJob(FoldJob):
         # layers where some group sums >1 input: the forward conv writes that
         # sum once ("<layer>_xin") and the layer's wgrad reads it as one slot
         for L in self.layers:
-            L.xin = None
-            if any(bin(im).count("1") > 1 for _, im in L.rows):
-                L.xin = L.name + "_xin"
+            if L.xin is not None:
                 self.act[L.xin] = torch.zeros((Q, B, L.H, L.W, L.cinp), dtype=torch.bfloat16, device=dev)
         hs, ws = self.final_hw
         self.Fp = hs * ws * self.final_cp
@@ -326,7 +252,7 @@ class HipPopJob(FoldJob):
         gather_train = self.epoch_idx.data_ptr()
         self.fwd_ops = []
         for st in self.stages:
-            for L in st["layers"]:
+            for L in st.layers:
                 first = L.slots == ["input"]
                 a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [self.act[L.name].data_ptr()], [],
                                     L.w_bf, L.b[0], 1, [(q, im, 1) for q, im in L.rows],
@@ -335,13 +261,13 @@ class HipPopJob(FoldJob):
                     a.xsum = self.act[L.xin].data_ptr()
                 a.epi_bf16 = 1            # forward outputs never accumulate: bf16 output tile
                 self.fwd_ops.append(("conv", a, L))
-            sel = torch.tensor([1 if act else 0 for act in st["active"]], dtype=torch.int32, device=self.device)
+            sel = torch.tensor(self.sched.pool_source(st), dtype=torch.int32, device=self.device)
             self._keep.append(sel)
-            x1 = self.act[st["out"]] if st["has_out"] else self.act[st["in"]]
-            hh, ww, cc = self.shapes[st["in"]]
-            st["sel"] = sel
-            self.fwd_ops.append(("pool", (self.act[st["in"]].data_ptr(), x1.data_ptr(), sel.data_ptr(),
-                                          self.act[st["pool"]].data_ptr(), Q * B, B, hh, ww, cc), None))
+            x1 = self.act[self.sched.pool_x1(st)]
+            hh, ww, cc = self.shapes[st.inp]
+            st.sel = sel
+            self.fwd_ops.append(("pool", (self.act[st.inp].data_ptr(), x1.data_ptr(), sel.data_ptr(),
+                                          self.act[st.pool].data_ptr(), Q * B, B, hh, ww, cc), None))
         # ---- head
         df = K.DenseFwdArgs()
         df.x, df.wt, df.bias, df.out = (self.act[self.last].data_ptr(), self.w1t_bf.data_ptr(),
@@ -375,28 +301,21 @@ class HipPopJob(FoldJob):
         dw.G, dw.B, dw.Fp, dw.Up = Q, B, self.Fp, self.Up
         dw.Cp, dw.Cr, dw.Ur = self.final_cp, self.plan.kernels_per_layer[-1], self.plan.dense_units
         self.dense_wgrad_args = dw
-        # ---- backward. Per group and slot: the FIRST consumer in forward order
-        # is the LAST writer of the slot's gradient and applies its ReLU mask;
-        # earlier writers accumulate.
-        first_consumer = {}
-        for L in self.layers:
-            for q, im in L.rows:
-                for k, n in enumerate(L.slots):
-                    if (im >> k) & 1:
-                        first_consumer.setdefault((q, n), L.name)
-        written = set()
+        # ---- backward (records: models/pop_schedule.py PopulationSchedule.backward)
         self.bwd_ops = []
-        for st in reversed(self.stages):
-            hh, ww, cc = self.shapes[st["in"]]
-            x1 = st["out"] if st["has_out"] else st["in"]
-            self.bwd_ops.append(("pool_bwd", (self.act[st["in"]].data_ptr(), self.act[x1].data_ptr(),
-                                              st["sel"].data_ptr(), self.grad[st["pool"]].data_ptr(),
-                                              self.grad[st["in"]].data_ptr(), self.grad[x1].data_ptr(),
-                                              Q * B, B, hh, ww, cc, 1), None))
-            for q in range(Q):
-                written.add((q, st["out"] if st["active"][q] else st["in"]))
-            for L in reversed(st["layers"]):
-                first = L.slots == ["input"]
+        for rec in self.sched.backward():
+            if rec[0] == "pool_bwd":
+                st = rec[1]
+                hh, ww, cc = self.shapes[st.inp]
+                x1 = self.sched.pool_x1(st)
+                self.bwd_ops.append(("pool_bwd", (self.act[st.inp].data_ptr(), self.act[x1].data_ptr(),
+                                                  st.sel.data_ptr(), self.grad[st.pool].data_ptr(),
+                                                  self.grad[st.inp].data_ptr(), self.grad[x1].data_ptr(),
+                                                  Q * B, B, hh, ww, cc, 1), None))
+                continue
+            kind, L, rows = rec
+            first = L.slots == ["input"]
+            if kind == "wgrad":
                 wa = K.WgradArgs()
                 wslots = L.slots + ([L.xin] if L.xin is not None else [])
                 for i, n in enumerate(wslots):
@@ -405,30 +324,17 @@ class HipPopJob(FoldJob):
                 wa.st = self.state.data_ptr()
                 wa.dz = self.grad[L.name].data_ptr()
                 wa.part_w, wa.part_b = L.part_w.data_ptr(), L.part_b.data_ptr()
-                xbit = 1 << len(L.slots)
-                wa.gtab = self._gtab([(q, xbit if bin(im).count("1") > 1 else im, 0) for q, im in L.rows]).data_ptr()
-                wa.ngroups = len(L.rows)
+                wa.gtab = self._gtab([(q, im, 0) for q, im in rows]).data_ptr()
+                wa.ngroups = len(rows)
                 wa.G, wa.B, wa.H, wa.W = Q, B, L.H, L.W
                 wa.Cinp, wa.Coutp, wa.KH, wa.KW, wa.S, wa.pps = L.cinp, L.coutp, L.KH, L.KW, L.S, L.pps
                 self.bwd_ops.append(("wgrad", wa, L))
-                if first:
-                    continue
-                rows = []
-                for q, im in L.rows:
-                    of = 0
-                    for k, n in enumerate(L.slots):
-                        if not (im >> k) & 1:
-                            continue
-                        of |= 1 << k
-                        if (q, n) in written:
-                            of |= 1 << (8 + k)
-                        if n in self.act and L.kind != "in" and first_consumer.get((q, n)) == L.name:
-                            of |= 1 << (16 + k)
-                        written.add((q, n))
-                    rows.append((q, 1, of))
+            else:
+                # dgrad = conv with flipped, transposed weights; per group the
+                # fan-out flags (write / accumulate / ReLU mask per input slot)
                 a = self._conv_args(L, [self.grad[L.name].data_ptr()], [self._slot_ptr(n, grad=True) for n in L.slots],
-                                    [self._slot_ptr(n) for n in L.slots], L.wT_bf, None, 0, rows,
-                                    Cinp=L.coutp, Coutp=L.cinp)
+                                    [self._slot_ptr(n) for n in L.slots], L.wT_bf, None, 0,
+                                    [(q, 1, of) for q, of in rows], Cinp=L.coutp, Coutp=L.cinp)
                 self.bwd_ops.append(("conv", a, L))
         aa = K.AdamArgs()
         aa.segs, aa.blocks, aa.st = self.adam_segs.data_ptr(), self.adam_blocks.data_ptr(), self.state.data_ptr()
@@ -535,31 +441,33 @@ class HipPopJob(FoldJob):
         K.check(L.gt_head(self.head_args, s), "head")
         K.check(L.gt_dense_dgrad(self.dense_dgrad_args, s), "dense_dgrad")   # reads W1 before its update
         side = self.side if self.overlap else main
+        side2 = (self.side2 if self.w1_stream else side) if self.overlap else main
         ss = side.cuda_stream
 
-        def fork():
-            if side is not main:
+        def fork(stream):
+            if stream is not main:
                 ev = torch.cuda.Event()
                 ev.record(main)
-                side.wait_event(ev)
+                stream.wait_event(ev)
 
         # W1 gradient + Adam only needs dH and the pooled features: it overlaps
         # the whole conv backward. Each layer's wgrad reads its final dz and its
         # (unchanged) inputs: it overlaps the layer's dgrad and everything after.
-        fork()
-        K.check(L.gt_dense_wgrad_adam(self.dense_wgrad_args, ss), "dense_wgrad_adam")
+        fork(side2)
+        K.check(L.gt_dense_wgrad_adam(self.dense_wgrad_args, side2.cuda_stream), "dense_wgrad_adam")
         for kind, a, _ in self.bwd_ops:
             if kind == "wgrad":
-                fork()
+                fork(side)
                 K.check(L.gt_conv_wgrad(a, ss), "conv_wgrad")
             elif kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
             else:
                 K.check(L.gt_pool_bwd(*a, s), "pool_bwd")
-        if side is not main:
-            ev = torch.cuda.Event()
-            ev.record(side)
-            main.wait_event(ev)
+        for stream in (side, side2):
+            if stream is not main:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                main.wait_event(ev)
         K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
 
     def evaluate(self):
