@@ -25,15 +25,33 @@ def _floats(s):
 
 
 def _common(ap):
+    from .config import RunConfig
+    d = RunConfig.from_env()          # GENTUN_* environment over the defaults; flags win over both
     ap.add_argument("--pop", type=int, default=20)
     ap.add_argument("--gens", type=int, default=10)
     ap.add_argument("--algorithm", choices=("roulette", "tournament"), default="roulette")
-    ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--checkpoint-dir", default=None)
+    ap.add_argument("--seed", type=int, default=d.seed)
+    ap.add_argument("--checkpoint-dir", default=d.checkpoint_dir)
     ap.add_argument("--resume", default=None, help="checkpoint file or directory to continue from")
-    ap.add_argument("--events", default=None, help="JSONL event log path")
-    ap.add_argument("--streams", type=int, default=1, help="concurrent population jobs per GPU")
-    ap.add_argument("--pop-batch", type=int, default=16, help="Genetic-CNN candidates sharing each kernel launch")
+    ap.add_argument("--events", default=d.events, help="JSONL event log path")
+    ap.add_argument("--streams", type=int, default=d.streams, help="concurrent population jobs per GPU")
+    ap.add_argument("--pop-batch", type=int, default=d.pop_batch,
+                    help="Genetic-CNN candidates sharing each kernel launch")
+    ap.add_argument("--pairing", choices=RunConfig.CHOICES["pairing"], default=d.pairing,
+                    help="RussianRouletteGA pairs: reference (overlapping) or disjoint")
+    ap.add_argument("--schedule", choices=RunConfig.CHOICES["schedule"], default=d.schedule,
+                    help="distributed (candidate, fold) unit schedule")
+    ap.add_argument("--collective-timeout", type=int, default=d.collective_timeout_s,
+                    help="seconds before a collective with a dead rank fails the run")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default=d.backend)
+
+
+def _config(args):
+    from .config import RunConfig
+    return RunConfig(seed=args.seed, checkpoint_dir=args.checkpoint_dir, events=args.events,
+                     collective_timeout_s=args.collective_timeout, dtype=getattr(args, "dtype", "bf16"),
+                     loss=getattr(args, "loss", "bce_compat"), pairing=args.pairing, streams=args.streams,
+                     pop_batch=args.pop_batch, schedule=args.schedule, backend=args.backend)
 
 
 def _device():
@@ -51,25 +69,31 @@ def _run_search(args, species, x, y, extra, maximize):
     from .parallel import LocalBatchEvaluator, from_env
     from .parallel.distributed import DistributedPopulation, GentunWorker
     from .utils import rng
+    cfg = _config(args)
     device = _device()
-    comm = from_env(device=device)
-    evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch)
+    comm = from_env(backend=cfg.backend, timeout_s=cfg.collective_timeout_s, device=device)
+    evaluator = LocalBatchEvaluator(device=device, streams=cfg.streams, pop_batch=cfg.pop_batch)
     if comm.rank != 0:
         GentunWorker(species, x, y, comm=comm, evaluator=evaluator).work()
         return None
-    cls = RussianRouletteGA if args.algorithm == "roulette" else GeneticAlgorithm
-    log = EventLog(args.events) if args.events else None
+    roulette = args.algorithm == "roulette"
+    cls = RussianRouletteGA if roulette else GeneticAlgorithm
+    ga_kw = {"pairing": cfg.pairing} if roulette else {}
+    log = EventLog(cfg.events) if cfg.events else None
+    if log is not None:
+        log.write("config", **cfg.to_dict())
     if args.resume:
         def factory(inds):
             return DistributedPopulation(species, x, y, individual_list=inds, maximize=maximize,
-                                         additional_parameters=extra, comm=comm, evaluator=evaluator)
-        ga = cls.resume(args.resume, species, x, y, population_factory=factory, checkpoint_dir=args.checkpoint_dir,
+                                         additional_parameters=extra, comm=comm, evaluator=evaluator,
+                                         schedule=cfg.schedule)
+        ga = cls.resume(args.resume, species, x, y, population_factory=factory, checkpoint_dir=cfg.checkpoint_dir,
                         event_log=log)
     else:
-        rng.seed(args.seed)
+        rng.seed(cfg.seed)
         pop = DistributedPopulation(species, x, y, size=args.pop, maximize=maximize, additional_parameters=extra,
-                                    comm=comm, evaluator=evaluator)
-        ga = cls(pop, seed=args.seed, checkpoint_dir=args.checkpoint_dir, event_log=log)
+                                    comm=comm, evaluator=evaluator, schedule=cfg.schedule)
+        ga = cls(pop, seed=cfg.seed, checkpoint_dir=cfg.checkpoint_dir, event_log=log, **ga_kw)
     best = ga.run(args.gens)
     ga.population.shutdown()
     out = {"best_fitness": best.get_fitness(), "best_genes": best.get_genes(),
@@ -91,7 +115,7 @@ def cmd_cnn(args):
     extra = dict(nodes=nodes, input_shape=shape, kernels_per_layer=kernels, kernel_sizes=ks,
                  dense_units=args.dense, dropout_probability=args.dropout, classes=args.classes, nfold=args.nfold,
                  epochs=_ints(args.epochs), learning_rate=_floats(args.lr), batch_size=args.batch, loss=args.loss,
-                 seed=args.seed, optimizer=args.optimizer, momentum=args.momentum)
+                 seed=args.seed, optimizer=args.optimizer, momentum=args.momentum, dtype=args.dtype)
     return _run_search(args, GeneticCnnIndividual, x, y, extra, maximize=True)
 
 
@@ -127,6 +151,11 @@ def cmd_info(_args):
     print(json.dumps(info))
 
 
+def _env_default(name):
+    from .config import RunConfig
+    return getattr(RunConfig.from_env(), name)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="python -m gentun_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -146,7 +175,9 @@ def main(argv=None):
     c.add_argument("--epochs", default="20,4,1")
     c.add_argument("--lr", default="1e-3,1e-4,1e-5")
     c.add_argument("--batch", type=int, default=32)
-    c.add_argument("--loss", choices=("bce_compat", "ce"), default="bce_compat")
+    c.add_argument("--loss", choices=("bce_compat", "ce"), default=_env_default("loss"))
+    c.add_argument("--dtype", choices=("bf16", "fp32"), default=_env_default("dtype"),
+                   help="bf16 MFMA with fp32 master weights (HIP path), or fp32 (PyTorch path)")
     c.add_argument("--optimizer", choices=("adam", "sgd"), default="adam")
     c.add_argument("--momentum", type=float, default=0.9, help="SGD momentum")
     c.set_defaults(fn=cmd_cnn)

@@ -1,0 +1,87 @@
+"""Runtime configuration of a search run.
+
+The reference has constructor kwargs only (gentun/individuals.py:158-160,
+221-223; broker settings gentun/master.py:88-90). Those kwargs are kept
+unchanged; this dataclass holds the settings the reference never had --
+run seed, checkpointing, collective timeout, compute dtype, loss mode,
+roulette pairing, evaluator shape -- with ``GENTUN_*`` environment
+overrides, so a ``torchrun`` launch can be configured without touching the
+command line. The CLI (``python -m gentun_amd``) takes its defaults from
+:meth:`RunConfig.from_env`, so an explicit flag wins over the environment,
+which wins over the defaults below.
+"""
+
+import dataclasses
+import json
+import os
+
+
+@dataclasses.dataclass
+class RunConfig(object):
+    seed: int = 0                       # run seed: GA RNG, fold split, keyed weight init / dropout
+    checkpoint_dir: str = None          # one JSON checkpoint per generation (checkpoint.py)
+    events: str = None                  # JSONL event log (metrics.py)
+    collective_timeout_s: int = 1800    # RCCL / gloo collective timeout (a dead rank fails the run)
+    dtype: str = "bf16"                 # CNN compute: 'bf16' MFMA (fp32 master weights) or 'fp32'
+    loss: str = "bce_compat"            # 'bce_compat' (reference: softmax + binary_crossentropy) or 'ce'
+    pairing: str = "reference"          # RussianRouletteGA pairs: 'reference' (overlapping) or 'disjoint'
+    streams: int = 1                    # concurrent population jobs per GPU
+    pop_batch: int = 16                 # Genetic-CNN candidates sharing each kernel launch
+    schedule: str = "auto"              # distributed unit schedule: 'auto' | 'lpt' | 'dynamic'
+    backend: str = None                 # torch.distributed backend (None: nccl=RCCL on GPU, gloo on CPU)
+
+    # env var -> field
+    ENV = {
+        "GENTUN_SEED": "seed",
+        "GENTUN_CHECKPOINT_DIR": "checkpoint_dir",
+        "GENTUN_EVENTS": "events",
+        "GENTUN_COLLECTIVE_TIMEOUT_S": "collective_timeout_s",
+        "GENTUN_DTYPE": "dtype",
+        "GENTUN_LOSS": "loss",
+        "GENTUN_PAIRING": "pairing",
+        "GENTUN_STREAMS": "streams",
+        "GENTUN_POP_BATCH": "pop_batch",
+        "GENTUN_SCHEDULE": "schedule",
+        "GENTUN_DIST_BACKEND": "backend",
+    }
+    CHOICES = {
+        "dtype": ("bf16", "fp32"),
+        "loss": ("bce_compat", "ce"),
+        "pairing": ("reference", "disjoint"),
+        "schedule": ("auto", "lpt", "dynamic"),
+        "backend": (None, "nccl", "gloo"),
+    }
+
+    def __post_init__(self):
+        self.validate()
+
+    def validate(self):
+        for name, allowed in self.CHOICES.items():
+            if getattr(self, name) not in allowed:
+                raise ValueError("{}={!r}: expected one of {}".format(name, getattr(self, name), allowed))
+        for name in ("streams", "pop_batch", "collective_timeout_s"):
+            if int(getattr(self, name)) < 1:
+                raise ValueError("{} must be >= 1".format(name))
+        return self
+
+    @classmethod
+    def from_env(cls, environ=None, **overrides):
+        """Defaults, then ``GENTUN_*`` variables, then ``overrides``."""
+        env = os.environ if environ is None else environ
+        kw = {}
+        types = {f.name: f.type for f in dataclasses.fields(cls)}
+        for var, name in cls.ENV.items():
+            if var in env and env[var] != "":
+                raw = env[var]
+                kw[name] = int(raw) if types[name] in (int, "int") else raw
+        kw.update({k: v for k, v in overrides.items() if v is not None})
+        return cls(**kw)
+
+    def replace(self, **changes):
+        return dataclasses.replace(self, **changes)
+
+    def to_dict(self):
+        return dataclasses.asdict(self)
+
+    def to_json(self):
+        return json.dumps(self.to_dict(), sort_keys=True)

@@ -1,0 +1,48 @@
+"""RunConfig (gentun_amd/config.py): defaults, GENTUN_* overrides, validation,
+and the CLI precedence flag > environment > default."""
+
+import pytest
+
+from gentun_amd.config import RunConfig
+
+
+def test_defaults_match_reference_semantics():
+    c = RunConfig()
+    assert (c.loss, c.pairing, c.dtype, c.schedule) == ("bce_compat", "reference", "bf16", "auto")
+    assert c.collective_timeout_s > 0 and c.backend is None
+
+
+def test_env_overrides_and_types():
+    env = {"GENTUN_SEED": "7", "GENTUN_LOSS": "ce", "GENTUN_POP_BATCH": "8", "GENTUN_PAIRING": "disjoint",
+           "GENTUN_CHECKPOINT_DIR": "/tmp/ck", "GENTUN_DIST_BACKEND": "gloo", "GENTUN_STREAMS": ""}
+    c = RunConfig.from_env(env)
+    assert c.seed == 7 and isinstance(c.seed, int)
+    assert (c.loss, c.pop_batch, c.pairing, c.checkpoint_dir, c.backend) == ("ce", 8, "disjoint", "/tmp/ck", "gloo")
+    assert c.streams == 1                                   # empty variable = unset
+    assert RunConfig.from_env(env, seed=3, loss=None).seed == 3     # explicit overrides win, None = keep
+
+
+@pytest.mark.parametrize("bad", [{"loss": "mse"}, {"pairing": "x"}, {"dtype": "fp16"}, {"streams": 0},
+                                 {"schedule": "round_robin"}, {"backend": "mpi"}])
+def test_validation(bad):
+    with pytest.raises(ValueError):
+        RunConfig(**bad)
+
+
+def test_roundtrip_json():
+    import json
+    c = RunConfig(seed=5, events="e.jsonl")
+    assert RunConfig(**json.loads(c.to_json())) == c
+    assert c.replace(seed=6).seed == 6 and c.seed == 5
+
+
+def test_cli_precedence(monkeypatch):
+    import argparse
+    from gentun_amd import __main__ as cli
+    monkeypatch.setenv("GENTUN_POP_BATCH", "4")
+    monkeypatch.setenv("GENTUN_PAIRING", "disjoint")
+    ap = argparse.ArgumentParser()
+    cli._common(ap)
+    args = ap.parse_args(["--pop-batch", "2"])
+    cfg = cli._config(args)
+    assert cfg.pop_batch == 2 and cfg.pairing == "disjoint" and cfg.streams == 1
