@@ -41,17 +41,22 @@ template <int PXG>   // 16-pixel groups per wave (tile = 64 * PXG pixels)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG == 4 ? 3 : CF_WPE))) conv_fwd_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
-  const int nth = (a.H + a.TH - 1) / a.TH;
-  const int b = blockIdx.x / nth;
-  const int h0 = (blockIdx.x % nth) * a.TH;
+  // tile = NI whole images (small images: the launcher passes TH = NI * H so
+  // the weights staged per workgroup serve up to 256 pixels) or TH rows of one
+  const int NI = a.TH > a.H ? a.TH / a.H : 1;
+  const int THr = a.TH > a.H ? a.H : a.TH;            // rows per image in the tile
+  const int nth = (a.H + THr - 1) / THr;
+  const int b0 = (blockIdx.x / nth) * NI;
+  const int h0 = (blockIdx.x % nth) * THr;
   const GroupRec gr = group_rec(a.gtab, blockIdx.y, a.n_in, a.n_out, a.acc_flags, a.out_mask);
   const int g = gr.g;
   const int co_blk = blockIdx.z * 64;
   const int ph = a.KH >> 1, pw = a.KW >> 1;
-  const int PH = a.TH + a.KH - 1, PW = a.W + a.KW - 1;
+  const int PH = THr + a.KH - 1, PW = a.W + a.KW - 1;
   const int ncb = a.Cinp >> 3;
   const long img = (long)a.H * a.W * a.Cinp;
-  const int total = PH * PW * ncb;
+  const int pimg = PH * PW * ncb;                       // patch chunks per image
+  const int total = NI * pimg;
   const int nchunks = a.KH * a.KW * ncb;
   const int Kdim = a.KH * a.KW * a.Cinp;
   // LDS carve: [weight blocks: nbuf x wrows x CF_WLD][patch][chunk offset table].
@@ -86,34 +91,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
   };
   load_wblock(0);
 
-  // ---- stage the summed / masked input patch -------------------------------
-  const uint16_t* src[GT_MAXSLOT];
-  int n_src = 0;
-  for (int k = 0; k < GT_MAXSLOT; ++k)
-    if ((gr.in_mask >> k) & 1) src[n_src++] = a.in[k] + ((long)g * a.B + b) * img;
-  if (a.gather) {
-    const long id = a.gather[((long)a.st->cur_step * a.G + g) * a.B + b];
-    src[0] = a.in[0] + id * img;
-    n_src = 1;
-  }
-  const uint16_t* msrc = a.mask ? a.mask + ((long)g * a.B + b) * img : nullptr;
-  const FastDiv div_ncb(ncb), div_pw(PW);
+  // ---- stage the summed / masked input patch of every image ----------------
+  const int n_src = a.gather ? 1 : __builtin_popcount(gr.in_mask);
+  const FastDiv div_ncb(ncb), div_pw(PW), div_pimg(pimg);
   for (int i = tid; i < total; i += 256) {
-    uint32_t pix, cbu, pr, pc;
-    div_ncb.divmod((uint32_t)i, pix, cbu);
+    uint32_t im, r, pix, cbu, pr, pc;
+    div_pimg.divmod((uint32_t)i, im, r);
+    div_ncb.divmod(r, pix, cbu);
     div_pw.divmod(pix, pr, pc);
-    const int cb = (int)cbu;
+    const int cb = (int)cbu, b = b0 + (int)im;
     const int hh = h0 - ph + (int)pr, ww = (int)pc - pw;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) {
+    if (b < a.B && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) {
       const long off = ((long)hh * a.W + ww) * a.Cinp + cb * 8;
-      if (n_src == 1 && !msrc) {
-        v = *reinterpret_cast<const uint4*>(src[0] + off);
+      const long ioff = ((long)g * a.B + b) * img;
+      const uint16_t* msrc = a.mask ? a.mask + ioff : nullptr;
+      if (a.gather) {
+        v = *reinterpret_cast<const uint4*>(a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img + off);
+      } else if (n_src == 1 && !msrc) {
+        v = *reinterpret_cast<const uint4*>(a.in[__builtin_ctz(gr.in_mask | 0x100) & 7] + ioff + off);
       } else {
-        float acc[8], t[8];
-        unpack8(*reinterpret_cast<const uint4*>(src[0] + off), acc);
-        for (int k = 1; k < n_src; ++k) {
-          unpack8(*reinterpret_cast<const uint4*>(src[k] + off), t);
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t[8];
+        for (int k = 0; k < GT_MAXSLOT; ++k) {
+          if (!((gr.in_mask >> k) & 1)) continue;
+          unpack8(*reinterpret_cast<const uint4*>(a.in[k] + ioff + off), t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[j] += t[j];
         }
@@ -128,14 +129,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
     patch[i] = v;
   }
   if (a.xsum && n_src > 1) {
-    // the summed input of this band (patch interior) for the layer's wgrad
+    // the summed input of this tile (patch interiors) for the layer's wgrad
     __syncthreads();
-    uint16_t* xo = a.xsum + ((long)g * a.B + b) * img + (long)h0 * a.W * a.Cinp;
-    for (int i = tid; i < a.TH * a.W * ncb; i += 256) {
-      const int cb = i % ncb, pix = i / ncb;
+    const int per = THr * a.W * ncb;
+    for (int i = tid; i < NI * per; i += 256) {
+      const int im = i / per, q = i - im * per;
+      const int cb = q % ncb, pix = q / ncb;
       const int r = pix / a.W, cc = pix % a.W;
-      if (h0 + r < a.H)
-        *reinterpret_cast<uint4*>(xo + (long)i * 8) = patch[((r + ph) * PW + cc + pw) * ncb + cb];
+      if (b0 + im < a.B && h0 + r < a.H) {
+        uint16_t* xo = a.xsum + ((long)g * a.B + b0 + im) * img + (long)h0 * a.W * a.Cinp;
+        *reinterpret_cast<uint4*>(xo + (long)q * 8) = patch[im * pimg + ((r + ph) * PW + cc + pw) * ncb + cb];
+      }
     }
   }
   {
@@ -157,16 +161,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
   // ---- MFMA main loop: each wave = 32 pixels (2 B fragments) x all co tiles --
   const int wave = tid >> 6, lane = tid & 63;
   const int kq = lane >> 4, l16 = lane & 15;
-  const int npx = a.TH * a.W;
+  const int ipx = THr * a.W;                            // tile pixels per image
   int pbase[PXG];
   bool pvalid[PXG];
-  int pyy[PXG], pxx[PXG];
+  int pyy[PXG], pxx[PXG], pim[PXG];
 #pragma unroll
   for (int h = 0; h < PXG; ++h) {
     const int pl = wave * 16 * PXG + h * 16 + l16;
-    pyy[h] = pl / a.W; pxx[h] = pl % a.W;
-    pvalid[h] = (pl < npx) && (h0 + pyy[h] < a.H);
-    pbase[h] = (pyy[h] * PW + pxx[h]) * ncb;
+    pim[h] = pl / ipx;
+    const int pp = pl - pim[h] * ipx;
+    pyy[h] = pp / a.W; pxx[h] = pp % a.W;
+    pvalid[h] = (pl < NI * ipx) && (h0 + pyy[h] < a.H) && (b0 + pim[h] < a.B);
+    pbase[h] = pim[h] * pimg + (pyy[h] * PW + pxx[h]) * ncb;
   }
   const int nco = min(64, a.Coutp - co_blk);
   const int NT = (nco + 15) >> 4;
@@ -206,7 +212,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
 #pragma unroll
   for (int h = 0; h < PXG; ++h) {
     if (!pvalid[h]) continue;
-    const long obase = ((((long)g * a.B + b) * a.H + (h0 + pyy[h])) * a.W + pxx[h]) * a.Coutp;
+    const long obase = ((((long)g * a.B + b0 + pim[h]) * a.H + (h0 + pyy[h])) * a.W + pxx[h]) * a.Coutp;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       if (t >= NT) continue;
@@ -522,6 +528,13 @@ extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream);
 extern "C" {
 
 static int g_conv_fast = 1;   // shape-specialised kernels (cnn_conv_fast.hip) where one matches
+static int g_conv_imgs = 2;   // max whole small images per generic-conv workgroup (2: measured best, deep space)
+
+int gt_conv_set_imgs(int n) {
+  const int old = g_conv_imgs;
+  g_conv_imgs = n < 1 ? 1 : n;
+  return old;
+}
 
 int gt_conv_set_fast(int on) {
   const int old = g_conv_fast;
@@ -536,22 +549,36 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
     if (rc != -100) return rc;
   }
   if (!a->gtab && (a->n_in < 1 || a->n_in > GT_MAXSLOT || a->n_out < 1 || a->n_out > GT_MAXSLOT)) return -1;
-  if (a->TH * a->W > 256 || a->TH < 1) return -2;
+  if (a->TH * a->W > 256 || a->TH < 1 || a->TH > a->H) return -2;
   if (a->ngroups < 1) return 0;
-  const int nth = (a->H + a->TH - 1) / a->TH;
-  const size_t total = (size_t)(a->TH + a->KH - 1) * (a->W + a->KW - 1) * (a->Cinp / 8);
   const int nchunks = a->KH * a->KW * (a->Cinp / 8);
   const int nkb = (nchunks + CF_KB - 1) / CF_KB;
   const int wrows = ((std::min(64, a->Coutp) + 15) / 16) * 16;
-  const size_t lds = (size_t)(nkb > 1 ? 2 : 1) * wrows * CF_WLD * 2 + total * 16 + 4 * ((size_t)nchunks + 4);
-  if (lds > 160 * 1024) return -3;
-  dim3 grid(a->B * nth, a->ngroups, (a->Coutp + 63) / 64);
-  if (a->TH * a->W > 128)
-    hipLaunchKernelGGL(conv_fwd_kernel<4>, grid, dim3(256), lds, stream, *a);
-  else if (a->TH * a->W > 64)
-    hipLaunchKernelGGL(conv_fwd_kernel<2>, grid, dim3(256), lds, stream, *a);
+  auto lds_of = [&](int ni, int th) {
+    const size_t total = (size_t)ni * (th + a->KH - 1) * (a->W + a->KW - 1) * (a->Cinp / 8);
+    return (size_t)(nkb > 1 ? 2 : 1) * wrows * CF_WLD * 2 + total * 16 + 4 * ((size_t)nchunks + 4);
+  };
+  // small images: several whole images per workgroup (up to 256 pixels), so
+  // one staged weight block serves 4x the pixels (8x8 stages: weight traffic
+  // per image was 6x the patch's)
+  int ni = 1;
+  if (a->TH == a->H && 2 * a->H * a->W <= 256) {
+    ni = std::min(g_conv_imgs, 256 / (a->H * a->W));
+    while (ni > 1 && lds_of(ni, a->H) > 160 * 1024) --ni;
+  }
+  if (lds_of(ni, a->TH) > 160 * 1024) return -3;
+  ConvArgs t = *a;
+  if (ni > 1) t.TH = ni * a->H;                      // kernel: TH > H = ni whole images per tile
+  const int nth = ni > 1 ? 1 : (a->H + a->TH - 1) / a->TH;
+  const int tile = ni > 1 ? ni * a->H * a->W : a->TH * a->W;
+  const size_t lds = lds_of(ni, ni > 1 ? a->H : a->TH);
+  dim3 grid(((a->B + ni - 1) / ni) * nth, a->ngroups, (a->Coutp + 63) / 64);
+  if (tile > 128)
+    hipLaunchKernelGGL(conv_fwd_kernel<4>, grid, dim3(256), lds, stream, t);
+  else if (tile > 64)
+    hipLaunchKernelGGL(conv_fwd_kernel<2>, grid, dim3(256), lds, stream, t);
   else
-    hipLaunchKernelGGL(conv_fwd_kernel<1>, grid, dim3(256), lds, stream, *a);
+    hipLaunchKernelGGL(conv_fwd_kernel<1>, grid, dim3(256), lds, stream, t);
   return (int)hipGetLastError();
 }
 

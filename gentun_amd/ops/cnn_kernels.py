@@ -6,6 +6,7 @@ interleave with torch's own and are captured by HIP graphs.
 """
 
 import ctypes as C
+import os
 
 from . import _lib
 
@@ -107,6 +108,10 @@ def lib():
         L.gt_wgrad_fast_band.restype = I
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
+        L.gt_conv_set_imgs.argtypes = [I]
+        L.gt_conv_set_imgs.restype = I
+        if os.environ.get("GENTUN_CONV_IMGS"):
+            L.gt_conv_set_imgs(int(os.environ["GENTUN_CONV_IMGS"]))
         L.gt_glorot_init.argtypes = [C.POINTER(InitArgs), I, P]
         L.gt_glorot_init.restype = I
         L.gt_glorot_ref.argtypes = [C.c_uint64, C.c_uint64, I, C.c_float]

@@ -610,3 +610,70 @@ def test_conv_fast_bf16_tile_forward(H, cin, cout, k):
         outs.append(o)
     assert torch.equal(outs[0], outs[1])
     assert torch.all(outs[1][1] == 7.0)
+
+
+@pytest.mark.parametrize("H,cin,cout,k,first", [(8, 104, 104, 3, False), (8, 56, 104, 5, False),
+                                                (8, 104, 56, 5, False), (7, 50, 50, 3, False),
+                                                (8, 3, 24, 5, True)])
+def test_conv_small_images_multi_tile(H, cin, cout, k, first):
+    """Generic conv with several whole small images per workgroup (8x8 stages
+    of the deep S=(3,4,5) space): bit-identical to one image per workgroup
+    (same per-pixel reduction order), correct against PyTorch, in group-table
+    mode with N-ary input sums (+ the input-sum copy for the wgrad), batch
+    gather, a batch that is not a multiple of the images per tile, and groups
+    outside the table left untouched."""
+    Km = K()
+    L = Km.lib()
+    torch.manual_seed(21)
+    Q, B, W = 3, 6, H
+    cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
+    nin = 1 if first else 3
+    slots = [bf(torch.randn(Q, B, H, W, cinp, device=DEV)) for _ in range(nin)]
+    for s in slots:
+        s[..., cin:] = 0
+    gather = None
+    if first:
+        data = torch.zeros(2 * Q * B, H, W, cinp, dtype=torch.bfloat16, device=DEV)
+        perm = torch.randperm(2 * Q * B, device=DEV)[:Q * B]
+        data[perm] = slots[0].view(Q * B, H, W, cinp)
+        gather = perm.view(1, Q, B).to(torch.int64).contiguous()
+    w = bf(torch.randn(Q, cout, cin, k, k, device=DEV) * 0.1).float()
+    wp = torch.stack([pack_w(w[g], coutp, cinp) for g in range(Q)]).to(torch.bfloat16).contiguous()
+    bias = torch.zeros(Q, coutp, device=DEV)
+    bias[:, :cout] = torch.randn(Q, cout, device=DEV) * 0.1
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    in_mask = 1 if first else 0b111
+    rows = torch.tensor([[2, in_mask, 1, 0], [0, 1 if first else 0b101, 1, 0]], dtype=torch.int32, device=DEV)
+    outs, xsums = [], []
+    for imgs in (1, 4):
+        out = torch.full((Q, B, H, W, coutp), 5.0, dtype=torch.bfloat16, device=DEV)
+        xs = torch.zeros(Q, B, H, W, cinp, dtype=torch.bfloat16, device=DEV)
+        a = Km.ConvArgs()
+        if first:
+            a.inp[0], a.gather, a.st = data.data_ptr(), gather.data_ptr(), st.data_ptr()
+        else:
+            for i, s in enumerate(slots):
+                a.inp[i] = s.data_ptr()
+            a.xsum = xs.data_ptr()
+        a.out[0] = out.data_ptr()
+        a.gtab, a.ngroups, a.relu = rows.data_ptr(), 2, 1
+        a.w, a.bias = wp.data_ptr(), bias.data_ptr()
+        a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = Q, B, H, W, cinp, coutp, k, k
+        a.TH = Km.conv_tile_rows(H, W)
+        old = L.gt_conv_set_imgs(imgs)
+        Km.check(L.gt_conv_fwd(a, stream()), "conv(imgs={})".format(imgs))
+        L.gt_conv_set_imgs(old)
+        torch.cuda.synchronize()
+        outs.append(out)
+        xsums.append(xs)
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(xsums[0], xsums[1])
+    assert torch.all(outs[1][1] == 5.0)
+    for g, ins in ((2, [0, 1, 2][:nin]), (0, [0] if first else [0, 2])):
+        xsum = bf(sum(slots[i][g].float() for i in ins))
+        if len(ins) > 1:
+            assert torch.equal(xsums[1][g], xsum)
+        x = xsum[..., :cin].permute(0, 3, 1, 2).float()
+        r = conv_ref([x], w[g], bias[g, :cout], True).permute(0, 2, 3, 1)
+        tol = 2e-2 * r.abs().max().item() + 1e-2
+        assert (outs[1][g, ..., :cout].float() - r).abs().max().item() < tol
