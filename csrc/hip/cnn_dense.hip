@@ -429,8 +429,11 @@ struct AdamSeg {
   uint16_t* bf;          // optional bf16 copy (same layout)
   uint16_t* bfT;         // optional flipped/transposed conv copy [G][Ci][KH][KW][Co]
   long n, gstride;
-  int S, tG, tCo, tKH, tKW, tCi, pad;
+  int S, tG, tCo, tKH, tKW, tCi;
+  int tiled;             // 1: blocks are (group, 64-column) tiles of a [Co][KH*KW*Ci] weight (Co <= 128)
 };
+
+#define ADAM_TK 64
 
 struct AdamArgs {
   const AdamSeg* segs;
@@ -441,6 +444,43 @@ struct AdamArgs {
 __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
   const int2 blk = a.blocks[blockIdx.x];
   const AdamSeg sg = a.segs[blk.x];
+  if (sg.tiled) {
+    // conv weight tile: Co rows x ADAM_TK reduction columns (row-contiguous
+    // reads of p/m/v/partials), bf16 values staged in LDS, then the flipped /
+    // transposed dgrad copy written as 16-byte runs along co -- one element per
+    // thread scattered 2-byte stores over a 1-2 KB stride instead (every store
+    // its own L2 transaction: the kernel's old bottleneck)
+    __shared__ __attribute__((aligned(16))) uint16_t tile[ADAM_TK][128 + 8];
+    const int Co = sg.tCo, Ci = sg.tCi, KH = sg.tKH, KW = sg.tKW;
+    const int Kd = KH * KW * Ci;
+    const int nkt = (Kd + ADAM_TK - 1) / ADAM_TK;
+    const int gg = blk.y / nkt, k0 = (blk.y - gg * nkt) * ADAM_TK;
+    const long base = (long)gg * Co * Kd;
+    const float lr_t = a.st->lr_t;
+    for (int idx = threadIdx.x; idx < Co * ADAM_TK; idx += 256) {
+      const int co = idx / ADAM_TK, kk = idx % ADAM_TK, k = k0 + kk;
+      if (k >= Kd) continue;
+      const long i = base + (long)co * Kd + k;
+      float gr = 0.f;
+      for (int s = 0; s < sg.S; ++s) gr += sg.g[(long)s * sg.gstride + i];
+      float m = sg.m[i], v = sg.v[i];
+      const float p = opt_update(a.st, sg.p[i], gr, m, v, lr_t);
+      sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
+      const uint16_t pb = f2bf(p);
+      if (sg.bf) sg.bf[i] = pb;
+      tile[kk][co] = pb;
+    }
+    __syncthreads();
+    const int nc8 = Co >> 3;
+    for (int idx = threadIdx.x; idx < ADAM_TK * nc8; idx += 256) {
+      const int kk = idx / nc8, c8 = idx - kk * nc8, k = k0 + kk;
+      if (k >= Kd) continue;
+      const int ci = k % Ci, r = k / Ci, kw = r % KW, kh = r / KW;
+      const long o = ((((long)gg * Ci + ci) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * Co + c8 * 8;
+      *reinterpret_cast<uint4*>(sg.bfT + o) = *reinterpret_cast<const uint4*>(&tile[kk][c8 * 8]);
+    }
+    return;
+  }
   const int i = blk.y + (int)threadIdx.x;          // segments are < 2^31 elements
   if (i >= sg.n) return;
   float gr = 0.f;

@@ -195,12 +195,18 @@ class HipPopJob(FoldJob):
             sg.n = p.numel()
             sg.gstride = gstride
             sg.S = S
+            ntiles = 0
             if tdims is not None:
                 sg.tG, sg.tCo, sg.tKH, sg.tKW, sg.tCi = tdims
+                ntiles = K.adam_tiles(*tdims) if bfT is not None else 0
+            sg.tiled = 1 if ntiles else 0
             idx = len(segs)
             segs.append(sg)
-            for o in range(0, p.numel(), 256):
-                blocks.append((idx, o))
+            if ntiles:
+                blocks.extend((idx, t) for t in range(ntiles))
+            else:
+                for o in range(0, p.numel(), 256):
+                    blocks.append((idx, o))
 
         # conv layers: one segment per (layer, group that has the layer)
         for L in self.layers:

@@ -63,7 +63,18 @@ class DenseWgradAdamArgs(C.Structure):
 class AdamSeg(C.Structure):
     _fields_ = [("p", P), ("m", P), ("v", P), ("g", P), ("bf", P), ("bfT", P), ("n", C.c_long),
                 ("gstride", C.c_long), ("S", I), ("tG", I), ("tCo", I), ("tKH", I), ("tKW", I), ("tCi", I),
-                ("pad", I)]
+                ("tiled", I)]
+
+ADAM_TK = 64        # adam_segments transpose tiles: tCo rows x ADAM_TK reduction columns
+
+
+def adam_tiles(tG, tCo, tKH, tKW, tCi):
+    """Blocks of a tiled conv-weight segment (csrc/hip/cnn_dense.hip, tiled
+    path), or 0 when the segment cannot be tiled (then: 256-element blocks)."""
+    if tCo > 128 or tCo % 8:
+        return 0
+    kd = tKH * tKW * tCi
+    return tG * (-(-kd // ADAM_TK))
 
 
 class AdamArgs(C.Structure):

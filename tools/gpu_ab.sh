@@ -15,3 +15,8 @@ for i in 1 2 3; do
   timeout -k 10 200 python tools/probe_pop.py 16 16 1 $EP 10000 > gpurun_out/ab_new_$i.log 2>&1 || { tail -20 gpurun_out/ab_new_$i.log; exit 1; }
   echo "old: $(grep -o '"ms_per_cand_step": [0-9.]*' gpurun_out/ab_old_$i.log)  new: $(grep -o '"ms_per_cand_step": [0-9.]*' gpurun_out/ab_new_$i.log)"
 done
+if [ -n "$DEEP" ]; then
+  (cd ab_old && SPACE=deep timeout -k 10 300 python tools/probe_pop.py 16 16 1 1 10000) > gpurun_out/ab_deep_old.log 2>&1 || { tail -20 gpurun_out/ab_deep_old.log; exit 1; }
+  SPACE=deep timeout -k 10 300 python tools/probe_pop.py 16 16 1 1 10000 > gpurun_out/ab_deep_new.log 2>&1 || { tail -20 gpurun_out/ab_deep_new.log; exit 1; }
+  echo "deep old: $(grep -o '"ms_per_cand_step": [0-9.]*' gpurun_out/ab_deep_old.log)  new: $(grep -o '"ms_per_cand_step": [0-9.]*' gpurun_out/ab_deep_new.log)"
+fi
