@@ -45,23 +45,26 @@ struct FastCfg {
 // occupancy targets (measured, profiles/conv_occupancy.txt): 4 waves / SIMD
 // (<= 128 registers) for 32-channel output tiles, 3 for the 5x5 64-channel
 // tile; the 3x3 56-channel-input tile spills at 3 and keeps 2
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO>
-__global__ void __launch_bounds__(256)
-__attribute__((amdgpu_waves_per_eu(NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))
+// tile; NWV = 8 waves per workgroup: half the pixels per wave (fewer
+// registers, 4 waves / SIMD) for the same 256-pixel tile
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4>
+__global__ void __launch_bounds__(NWV * 64)
+__attribute__((amdgpu_waves_per_eu(NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4))))
 conv_fast_kernel(ConvArgs a) {
+  constexpr int NTH = NWV * 64;                     // threads
   constexpr int PH = TH + KH - 1, PW = W + KW - 1;
   constexpr int NP = PH * PW * NCBI;                // patch chunks (16 B)
-  constexpr int NPT = (NP + 255) / 256;             // patch chunks per thread
+  constexpr int NPT = (NP + NTH - 1) / NTH;             // patch chunks per thread
   constexpr int NCH = KH * KW * NCBI;               // reduction chunks
   constexpr int NKS = (NCH + 3) / 4;                // k-steps (32 k each)
   constexpr int TP = TH * W;                        // tile pixels
   constexpr int NPG = TP / 16;                      // pixel groups
   constexpr int CT = NT >= 2 ? 2 : 1;               // co tiles per wave
   constexpr int WC = NT / CT;                       // waves along co
-  constexpr int WP = 4 / WC;                        // waves along pixels
+  constexpr int WP = NWV / WC;                        // waves along pixels
   constexpr int PG = NPG / WP;                      // pixel groups per wave
   constexpr int PF = NKS < 4 ? NKS : 4;             // weight prefetch depth (k-steps)
-  static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == 4, "tile shape");
+  static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == NWV, "tile shape");
   static_assert(W % 16 == 0 || 16 % W == 0, "pixel groups must tile image rows");
 
   using FC = FastCfg<KH, KW, NCBI, W, TH, NT, NCO>;
@@ -113,7 +116,7 @@ conv_fast_kernel(ConvArgs a) {
   bool pok[NPT];
 #pragma unroll
   for (int j = 0; j < NPT; ++j) {
-    const int i = tid + 256 * j;
+    const int i = tid + NTH * j;
     const int cb = i % NCBI, pix = i / NCBI;
     const int pr = pix / PW, pc = pix % PW;
     const int hh = h0 - KH / 2 + pr, ww = pc - KW / 2;
@@ -123,7 +126,7 @@ conv_fast_kernel(ConvArgs a) {
   if (a.dbg & 4) {
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
-      if (tid + 256 * j < NP) patch[tid + 256 * j] = make_uint4(0, 0, 0, 0);
+      if (tid + NTH * j < NP) patch[tid + NTH * j] = make_uint4(0, 0, 0, 0);
   } else if (n_src == 1) {
     uint4 v[NPT];
 #pragma unroll
@@ -131,7 +134,7 @@ conv_fast_kernel(ConvArgs a) {
       v[j] = pok[j] ? *reinterpret_cast<const uint4*>(src0 + poff[j]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
-      if (tid + 256 * j < NP) patch[tid + 256 * j] = v[j];
+      if (tid + NTH * j < NP) patch[tid + NTH * j] = v[j];
   } else {
     // N-ary DAG input: chunks in batches of JB; per slot, the batch's loads are
     // all in flight, then an fp32 accumulate (one rounding to bf16 at the end)
@@ -162,14 +165,14 @@ conv_fast_kernel(ConvArgs a) {
       }
 #pragma unroll
       for (int j = 0; j < JB; ++j)
-        if (j0 + j < NPT && tid + 256 * (j0 + j) < NP) patch[tid + 256 * (j0 + j)] = pack8(acc8[j]);
+        if (j0 + j < NPT && tid + NTH * (j0 + j) < NP) patch[tid + NTH * (j0 + j)] = pack8(acc8[j]);
     }
   }
   if (a.xsum && n_src > 1) {
     // the summed input of this band (interior of the patch) for the layer's wgrad
     __syncthreads();
     uint16_t* xo = a.xsum + ((long)g * a.B + b) * img + (long)h0 * W * NCBI * 8;
-    for (int i = tid; i < TH * W * NCBI; i += 256) {
+    for (int i = tid; i < TH * W * NCBI; i += NTH) {
       const int cb = i % NCBI, pix = i / NCBI;
       const int r = pix / W, c = pix % W;
       if (h0 + r < a.H)
@@ -177,7 +180,7 @@ conv_fast_kernel(ConvArgs a) {
     }
   }
   // chunk c -> patch offset of its (kh, kw, cb) relative to the output pixel
-  for (int c = tid; c < NKS * 4; c += 256) {
+  for (int c = tid; c < NKS * 4; c += NTH) {
     const int kk = c / NCBI, cb = c % NCBI;
     coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
   }
@@ -255,8 +258,8 @@ conv_fast_kernel(ConvArgs a) {
     const long obase = (((long)g * a.B + b) * a.H + h0) * W * (NCO * 8);
     if (!(a.dbg & 2))
 #pragma unroll
-    for (int j = 0; j < (TP * NCO + 255) / 256; ++j) {
-      const int i = tid + 256 * j;
+    for (int j = 0; j < (TP * NCO + NTH - 1) / NTH; ++j) {
+      const int i = tid + NTH * j;
       if (i >= TP * NCO) break;
       const int p = i / NCO, cb = i - p * NCO;
       const uint4 val = *reinterpret_cast<const uint4*>(ot + p * OROWB + cb * 8);
@@ -289,8 +292,8 @@ conv_fast_kernel(ConvArgs a) {
   if (a.dbg & 2) return;
   const long obase = (((long)g * a.B + b) * a.H + h0) * W * (NCO * 8);
 #pragma unroll
-  for (int j = 0; j < (TP * NCO + 255) / 256; ++j) {
-    const int i = tid + 256 * j;
+  for (int j = 0; j < (TP * NCO + NTH - 1) / NTH; ++j) {
+    const int i = tid + NTH * j;
     if (i >= TP * NCO) break;
     const int p = i / NCO, cb = i - p * NCO;
     const float4 lo = *reinterpret_cast<const float4*>(otile + p * OROW + cb * 8);
@@ -328,23 +331,45 @@ conv_fast_kernel(ConvArgs a) {
 // (the caller then uses the generic kernel)
 // ---------------------------------------------------------------------------
 
-#define CONV_FAST_CASE(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)                                              \
-  if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->W == W_ && a->Coutp == NCO_ * 8 &&    \
-      (NCO_ * 8 + 15) / 16 == NT_ && a->H % TH_ == 0) {                                                 \
+static int g_conv_nwv = 0;   // waves per workgroup override for the 8-wave-capable shapes (0: per-shape default)
+
+extern "C" int gt_conv_set_nwv(int n) {
+  const int old = g_conv_nwv;
+  g_conv_nwv = n;
+  return old;
+}
+
+#define CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                      \
+  {                                                                                                     \
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
     const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_>::lds(a->epi_bf16 != 0);             \
-    hipLaunchKernelGGL((conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_>), grid, dim3(256), lds, stream, *a); \
+    hipLaunchKernelGGL((conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_>), grid, dim3(NWV_ * 64), lds, \
+                       stream, *a);                                                                     \
     return (int)hipGetLastError();                                                                      \
+  }
+
+#define CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)                                             \
+  (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->W == W_ && a->Coutp == NCO_ * 8 &&       \
+   (NCO_ * 8 + 15) / 16 == NT_ && a->H % TH_ == 0)
+
+#define CONV_FAST_CASE(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)                                              \
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 4)
+
+// shapes with an 8-wave instantiation: `def_` waves unless overridden
+#define CONV_FAST_CASE2(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, def_)                                       \
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
+    if ((g_conv_nwv ? g_conv_nwv : def_) == 8) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 8)  \
+    CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 4)                                            \
   }
 
 extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
   // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
-  CONV_FAST_CASE(5, 5, 1, 32, 8, 2, 3)       // s1 input conv (3 -> 20)
-  CONV_FAST_CASE(3, 3, 3, 32, 8, 2, 3)       // s1 nodes / output conv, and their dgrad (20 -> 20)
-  CONV_FAST_CASE(5, 5, 3, 16, 16, 4, 7)      // s2 input conv (20 -> 50)
-  CONV_FAST_CASE(3, 3, 7, 16, 16, 4, 7)      // s2 nodes / output conv, and their dgrad (50 -> 50)
-  CONV_FAST_CASE(5, 5, 7, 16, 16, 2, 3)      // s2 input conv dgrad (50 -> 20)
+  CONV_FAST_CASE2(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
+  CONV_FAST_CASE2(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
+  CONV_FAST_CASE2(5, 5, 3, 16, 16, 4, 7, 4)  // s2 input conv (20 -> 50)
+  CONV_FAST_CASE2(3, 3, 7, 16, 16, 4, 7, 8)  // s2 nodes / output conv, and their dgrad (50 -> 50)
+  CONV_FAST_CASE2(5, 5, 7, 16, 16, 2, 3, 4)  // s2 input conv dgrad (50 -> 20)
   return -100;
 }
 

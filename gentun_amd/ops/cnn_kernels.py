@@ -119,6 +119,10 @@ def lib():
         L.gt_wgrad_fast_band.restype = I
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
+        L.gt_conv_set_nwv.argtypes = [I]
+        L.gt_conv_set_nwv.restype = I
+        if os.environ.get("GENTUN_CONV_NWV"):
+            L.gt_conv_set_nwv(int(os.environ["GENTUN_CONV_NWV"]))
         L.gt_conv_set_imgs.argtypes = [I]
         L.gt_conv_set_imgs.restype = I
         if os.environ.get("GENTUN_CONV_IMGS"):
