@@ -51,7 +51,10 @@ def load(name):
 
 
 def gbdt():
-    lib = load("libgentun_gbdt.so")
+    """The C++ GBDT engine. ``GENTUN_GBDT_LIB`` names an alternative build of
+    it (e.g. ``libgentun_gbdt_asan.so``, the host ASan/UBSan build)."""
+    alt = os.environ.get("GENTUN_GBDT_LIB")
+    lib = load(os.path.basename(alt) if alt else "libgentun_gbdt.so")
     if not getattr(lib, "_typed", False):
         c = ctypes
         lib.gbdt_cv.restype = c.c_int

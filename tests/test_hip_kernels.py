@@ -342,15 +342,27 @@ def _adam_ref(p, m, v, g, lr, t):
     return p - lr_t * m / (v.sqrt() + 1e-7), m, v
 
 
-def test_dense_wgrad_adam_and_step_begin():
+@pytest.mark.parametrize("Fp,Cp,Cr,Ur", [(400, 0, 0, 0), (392, 56, 50, 500)])
+def test_dense_wgrad_adam_and_step_begin(Fp, Cp, Cr, Ur):
+    """Fused dW1 + Adam + transposed bf16 copy; second case: a feature count
+    that is not a multiple of the 16-row tile plus padded channels / units
+    (skipped by the kernel, zero in the reference)."""
     Km = K()
     torch.manual_seed(5)
-    G, B, Fp, Up = 2, 32, 400, 512
+    G, B, Up = 2, 32, 512
     x = bf(torch.randn(G, B, Fp, device=DEV)).float()
     dH = torch.randn(G, B, Up, device=DEV)
     p = torch.randn(G, Fp, Up, device=DEV)
     m = torch.randn(G, Fp, Up, device=DEV) * 0.01
     v = torch.rand(G, Fp, Up, device=DEV) * 0.01
+    if Cp:
+        pad_f = (torch.arange(Fp, device=DEV) % Cp) >= Cr
+        pad_u = torch.arange(Up, device=DEV) >= Ur
+        x[:, :, pad_f] = 0
+        dH[:, :, pad_u] = 0
+        for t in (p, m, v):
+            t[:, pad_f, :] = 0
+            t[:, :, pad_u] = 0
     st = torch.zeros(8, dtype=torch.int32, device=DEV)
     stf = st.view(torch.float32)
     stf[2] = 4.0   # t before this step
@@ -364,6 +376,7 @@ def test_dense_wgrad_adam_and_step_begin():
     a.x, a.dH, a.p, a.m, a.v, a.wt, a.st = xb.data_ptr(), dH.data_ptr(), p.data_ptr(), m.data_ptr(), v.data_ptr(), \
         wt.data_ptr(), st.data_ptr()
     a.G, a.B, a.Fp, a.Up = G, B, Fp, Up
+    a.Cp, a.Cr, a.Ur = Cp, Cr, Ur
     Km.check(Km.lib().gt_dense_wgrad_adam(a, stream()), "wgrad_adam")
     torch.cuda.synchronize()
     assert st[1].item() == 0 and st[0].item() == 1 and abs(stf[2].item() - 5.0) < 1e-6

@@ -25,6 +25,14 @@ TARGETS = {
         "deps": [],
         "kind": "cxx",
     },
+    # host sanitizer build of the GBDT engine: ASan + UBSan,
+    # loaded through GENTUN_GBDT_LIB by tests/test_sanitizers.py
+    "libgentun_gbdt_asan.so": {
+        "sources": ["csrc/gbdt/engine.cpp"],
+        "deps": [],
+        "kind": "cxx_asan",
+        "optional": True,
+    },
     "libgentun_hip.so": {
         "sources": sorted(glob.glob(os.path.join(ROOT, "csrc", "hip", "*.hip"))),
         "deps": sorted(glob.glob(os.path.join(ROOT, "csrc", "hip", "*.h"))),
@@ -63,6 +71,9 @@ def build_target(name, verbose=False, force=False):
     tmp = lib + ".tmp.{}".format(os.getpid())
     if spec["kind"] == "cxx":
         cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-march=x86-64-v2", "-pthread", "-o", tmp] + srcs
+    elif spec["kind"] == "cxx_asan":
+        cmd = ["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fno-omit-frame-pointer",
+               "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-o", tmp] + srcs
     else:
         cc = hipcc()
         if cc is None:
@@ -78,7 +89,9 @@ def build_target(name, verbose=False, force=False):
 
 def build_all(verbose=False, force=False):
     out = {}
-    for name in TARGETS:
+    for name, spec in TARGETS.items():
+        if spec.get("optional"):
+            continue            # built on demand (sanitizer builds)
         out[name] = build_target(name, verbose=verbose, force=force)
     return out
 
