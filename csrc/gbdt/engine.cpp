@@ -56,6 +56,10 @@ struct Rng {
   double uniform() { return (next() >> 11) * (1.0 / 9007199254740992.0); }
 };
 
+inline double row_uniform(uint64_t key, uint64_t row) {
+  return (splitmix(key ^ splitmix(row)) >> 11) * (1.0 / 9007199254740992.0);
+}
+
 inline double threshold_l1(double g, double alpha) {
   if (g > alpha) return g - alpha;
   if (g < -alpha) return g + alpha;
@@ -414,7 +418,10 @@ int gbdt_cv(const float* X, int n, int F, const float* y, const int* fold_of, in
       std::vector<int> rows;
       rows.reserve(fs.train.size());
       if (p.subsample < 1.0) {
-        for (int i : fs.train) if (rng.uniform() < p.subsample) rows.push_back(i);
+        // counter-based Bernoulli per row, keyed by one draw of the stream: the
+        // GPU path (csrc/hip/gbdt_hist.hip root_rows_kernel) samples the same rows in parallel
+        const uint64_t key = rng.next();
+        for (int i : fs.train) if (row_uniform(key, (uint64_t)i) < p.subsample) rows.push_back(i);
       } else {
         rows = fs.train;
       }

@@ -2,35 +2,45 @@
 // host driver that runs xgboost-style k-fold CV with them (SURVEY.md §2.4
 // G2-G8; reference call site gentun/models/xgboost_models.py:32-36).
 //
-// Device layout: feature-major uint8 bins binsT[F][n] (a workgroup reading
-// one feature for consecutive rows is coalesced), per-fold margins, grad/hess
-// and a row -> node map. One tree level = one histogram launch:
-//   grid (feature blocks of FB features, row chunks); each workgroup keeps a
-//   private LDS histogram [FB][nodes_in_group][256 bins] of (G, H), filled
-//   with LDS float atomics, then flushed with one global float atomic per
-//   (feature, node, bin) it touched (Guideline 12: partial reduce first).
-// Split search: one wave per (node, feature) scans the 256-bin prefix sums
-// with xgboost's CalcGain (lambda, alpha L1 soft-threshold, max_delta_step,
-// min_child_weight) and reduces the best gain with shuffles; the host picks
-// the best feature per node (gamma pruning) and issues the partition kernel.
-// Histogram float atomics make the last bits order-dependent (like
-// xgboost's gpu_hist); the CPU engine (csrc/gbdt/engine.cpp) is the
-// bit-reproducible reference.
+// Layout: ROW-major uint8 bins [n][Fs] (Fs = F rounded up to 4), so one row's
+// bins are a contiguous 32-byte run per 32-feature block. Each tree level keeps
+// the active rows grouped by node in an index list (one contiguous segment per
+// node, partitioned level by level), which gives the gpu_hist structure:
+//   * histograms are built only for the SMALLER child of every split (its own
+//     rows, gathered through the index list); the sibling is parent - built
+//     (subtraction trick), so a level touches <= n/2 rows, not n per 16 nodes;
+//   * a histogram workgroup = one row chunk of one node x 32 features: 8 lanes
+//     read a row's 32 bins as 4-byte words, LDS float atomics into a
+//     [32][257] float2 histogram (+1 float2 pad per feature spreads the banks),
+//     then one global float atomic per non-zero entry (Guideline 12);
+//   * the partition is one pass: left rows fill the parent's segment from its
+//     start, right rows from its end (workgroup ballot scans + one cursor
+//     atomic per wave side), so child segments need no count pre-pass.
+// Split search: one wave per (node, feature) scans the 256-bin prefix sums with
+// xgboost's CalcGain (lambda, alpha L1 soft-threshold, max_delta_step,
+// min_child_weight); a per-node reduction picks the best feature on the device
+// and the host only applies gamma pruning and lays out the next level.
+// Histogram float atomics make the last bits order-dependent (like xgboost's
+// gpu_hist); the CPU engine (csrc/gbdt/engine.cpp) is the bit-reproducible
+// reference.
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #define GB_BINS 256
-#define GB_FB 2          // features per histogram workgroup
-#define GB_NG 16         // nodes per histogram pass
+#define HB_F 32          // features per histogram workgroup
+#define HB_STRIDE 514    // floats per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
 
 namespace {
-
 struct DevParams {
   float min_child_weight, lambda, alpha, max_delta_step;
 };
@@ -55,13 +65,11 @@ __device__ __forceinline__ float dev_gain(const DevParams& p, float G, float H) 
   return p.alpha == 0.f ? r : r + p.alpha * fabsf(w);
 }
 
-// ---- G2: gradients ---------------------------------------------------------
+// ---- G2: gradients (all rows; only indexed rows are ever read) -------------
 // obj 0 squared error, 1 reg:logistic, 2 binary:logistic (scale_pos_weight)
 __global__ void grad_kernel(const float* __restrict__ margin, const float* __restrict__ y,
-                            const int* __restrict__ node_of_row, float2* __restrict__ gh, int n, int obj,
-                            float spw) {
+                            float2* __restrict__ gh, int n, int obj, float spw) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    if (node_of_row[i] < 0) { gh[i] = make_float2(0.f, 0.f); continue; }
     float g, h;
     if (obj == 0) { g = margin[i] - y[i]; h = 1.f; }
     else {
@@ -73,41 +81,122 @@ __global__ void grad_kernel(const float* __restrict__ margin, const float* __res
   }
 }
 
-// ---- G3: histograms ---------------------------------------------------------
-// node_of_row holds the level-local node index (0 .. nodes-1) or -1.
-__global__ void __launch_bounds__(256) hist_kernel(const uint8_t* __restrict__ binsT, const float2* __restrict__ gh,
-                                                   const int* __restrict__ node_of_row, float2* __restrict__ hist,
-                                                   int n, int F, int node_lo, int nodes_in_pass, int rows_per_block) {
-  __shared__ float2 lh[GB_FB][GB_NG][GB_BINS];
-  const int f0 = blockIdx.x * GB_FB;
-  for (int i = threadIdx.x; i < GB_FB * GB_NG * GB_BINS; i += 256) (&lh[0][0][0])[i] = make_float2(0.f, 0.f);
+// ---- G3: histograms -----------------------------------------------------------
+// work chunk: (level-local node, first index in the row list, row count)
+// grid (chunks, feature blocks of HB_F), 512 threads = 64 row lanes x 8 word lanes;
+// each lane keeps HB_U rows' loads in flight (the row gather is latency-bound)
+#define HB_T 512
+#define HB_U 8
+__global__ void __launch_bounds__(HB_T) hist_kernel(const uint8_t* __restrict__ bins, int Fs, int F,
+                                                    const int* __restrict__ rows, const float2* __restrict__ gh,
+                                                    const int4* __restrict__ chunks, float2* __restrict__ hist,
+                                                    float2* __restrict__ hist_part) {
+  __shared__ float lh[HB_F * HB_STRIDE];
+  const int4 c = chunks[blockIdx.x];
+  const int fb = blockIdx.y * HB_F, tid = threadIdx.x;
+  constexpr int RL = HB_T / 8;                  // row lanes
+  for (int i = tid; i < HB_F * HB_STRIDE; i += HB_T) lh[i] = 0.f;
   __syncthreads();
-  const int r0 = blockIdx.y * rows_per_block;
-  const int r1 = min(n, r0 + rows_per_block);
-  for (int r = r0 + threadIdx.x; r < r1; r += 256) {
-    const int nd = node_of_row[r] - node_lo;
-    if (nd < 0 || nd >= nodes_in_pass) continue;
-    const float2 v = gh[r];
+  const int wl = tid & 7, rl = tid >> 3;
+  const int f4 = fb + wl * 4;
+  if (f4 < F) {
+    const int* rp = rows + c.y;
+    float* my = lh + wl * 4 * HB_STRIDE;
+    int i = rl;
+    for (; i + (HB_U - 1) * RL < c.z; i += HB_U * RL) {
+      int r[HB_U];
+      float2 g[HB_U];
+      uint32_t w[HB_U];
 #pragma unroll
-    for (int j = 0; j < GB_FB; ++j) {
-      if (f0 + j >= F) break;
-      const int b = binsT[(long)(f0 + j) * n + r];
-      atomicAdd(&lh[j][nd][b].x, v.x);
-      atomicAdd(&lh[j][nd][b].y, v.y);
+      for (int u = 0; u < HB_U; ++u) r[u] = rp[i + RL * u];
+#pragma unroll
+      for (int u = 0; u < HB_U; ++u) {
+        g[u] = gh[r[u]];
+        w[u] = *reinterpret_cast<const uint32_t*>(bins + (size_t)r[u] * Fs + f4);
+      }
+#pragma unroll
+      for (int u = 0; u < HB_U; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float* d = my + k * HB_STRIDE + 2 * ((w[u] >> (8 * k)) & 255u);
+          atomicAdd(d, g[u].x);
+          atomicAdd(d + 1, g[u].y);
+        }
+    }
+    for (; i < c.z; i += RL) {
+      const int r = rp[i];
+      const float2 g = gh[r];
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(bins + (size_t)r * Fs + f4);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float* d = my + k * HB_STRIDE + 2 * ((w >> (8 * k)) & 255u);
+        atomicAdd(d, g.x);
+        atomicAdd(d + 1, g.y);
+      }
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < GB_FB * nodes_in_pass * GB_BINS; i += 256) {
-    const int j = i / (nodes_in_pass * GB_BINS);
-    const int rem = i % (nodes_in_pass * GB_BINS);
-    const int nd = rem / GB_BINS, b = rem % GB_BINS;
-    if (f0 + j >= F) continue;
-    const float2 v = lh[j][nd][b];
-    if (v.x != 0.f || v.y != 0.f) {
-      float2* dst = &hist[(((long)(node_lo + nd)) * F + f0 + j) * GB_BINS + b];
-      atomicAdd(&dst->x, v.x);
-      atomicAdd(&dst->y, v.y);
+  // flush with plain stores, no global atomics: a node that fits one chunk is
+  // written straight into its histogram, otherwise into partial slot c.w
+  // (reduce_kernel sums a node's partials in slot order)
+  float* dst = reinterpret_cast<float*>(c.w < 0 ? hist + (size_t)c.x * F * GB_BINS
+                                                : hist_part + (size_t)c.w * F * GB_BINS) + (size_t)fb * 2 * GB_BINS;
+  const int nf = min(HB_F, F - fb);
+  for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
+    const int fl = i >> 9, j = i & 511;
+    dst[(size_t)fl * 2 * GB_BINS + j] = lh[fl * HB_STRIDE + j];
+  }
+}
+
+// node histogram = sum of its partial slots; red = (node, first slot, slots)
+__global__ void __launch_bounds__(256) reduce_kernel(const float* __restrict__ part, float* __restrict__ hist,
+                                                     const int4* __restrict__ red, int F) {
+  const int4 rd = red[blockIdx.x];
+  const size_t per = (size_t)F * 2 * GB_BINS;
+  for (size_t e = threadIdx.x + (size_t)blockIdx.y * 256; e < per; e += (size_t)gridDim.y * 256) {
+    float acc = 0.f;
+    for (int sl = 0; sl < rd.z; ++sl) acc += part[(size_t)(rd.y + sl) * per + e];
+    hist[(size_t)rd.x * per + e] = acc;
+  }
+}
+
+// root rows of fold k: rows of the other folds, Bernoulli(subsample) by a
+// counter-based hash keyed by one draw of the tree's stream (engine.cpp
+// row_uniform); unordered compaction (ballot + one counter atomic per wave)
+__global__ void __launch_bounds__(256) root_rows_kernel(const int* __restrict__ fold_of, int fold, int n,
+                                                        unsigned long long key, double subsample,
+                                                        int* __restrict__ rows, int* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const int i = base + threadIdx.x;
+    bool keep = i < n && fold_of[i] != fold;
+    if (keep && subsample < 1.0) {
+      unsigned long long x = (unsigned long long)i + 0x9E3779B97F4A7C15ull;
+      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
+      x = (key ^ x) + 0x9E3779B97F4A7C15ull;
+      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
+      keep = (double)(x >> 11) * (1.0 / 9007199254740992.0) < subsample;
     }
+    const unsigned long long m = __ballot(keep);
+    int b0 = 0;
+    if (lane == 0 && m) b0 = atomicAdd(count, __popcll(m));
+    b0 = __shfl(b0, 0);
+    if (keep) rows[b0 + __popcll(m & below)] = i;
+  }
+}
+
+// sibling = parent (previous level) - built child; pairs (other, parent_prev, built)
+__global__ void __launch_bounds__(256) subtract_kernel(const float2* __restrict__ prev, float2* __restrict__ cur,
+                                                       const int4* __restrict__ pairs, int F) {
+  const int4 pr = pairs[blockIdx.x];
+  const size_t per = (size_t)F * GB_BINS;
+  const float2* P = prev + (size_t)pr.y * per;
+  const float2* B = cur + (size_t)pr.z * per;
+  float2* O = cur + (size_t)pr.x * per;
+  for (size_t i = threadIdx.x + (size_t)blockIdx.y * 256; i < per; i += (size_t)gridDim.y * 256) {
+    const float2 a = P[i], b = B[i];
+    O[i] = make_float2(a.x - b.x, a.y - b.y);
   }
 }
 
@@ -167,26 +256,84 @@ __global__ void totals_kernel(const float2* __restrict__ hist, float2* __restric
   if (lane == 0) tot[node] = make_float2(g, hh);
 }
 
-// ---- G5: partition: level-local node -> child index of the next level --------
-// split table per level node: (feature, bin, left_child_next, right_child_next) or feature < 0 = leaf
-__global__ void partition_kernel(const uint8_t* __restrict__ binsT, int* __restrict__ node_of_row,
-                                 const int4* __restrict__ split, int n) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int nd = node_of_row[i];
-    if (nd < 0) continue;
-    const int4 s = split[nd];
-    if (s.x < 0) { node_of_row[i] = -1; continue; }
-    node_of_row[i] = (binsT[(long)s.x * n + i] <= s.y) ? s.z : s.w;
+// best feature per node: ties -> lower feature (the host scan order of the CPU engine)
+struct NodeBest { float gain; int bin; float GL, HL; int feature; int pad[3]; };
+
+__global__ void __launch_bounds__(256) best_kernel(const SplitOut* __restrict__ cand, NodeBest* __restrict__ out,
+                                                   int F) {
+  __shared__ float sg[256];
+  __shared__ int sf[256];
+  const int node = blockIdx.x, tid = threadIdx.x;
+  float bg = 0.f;
+  int bf = -1;
+  for (int f = tid; f < F; f += 256) {
+    const SplitOut& c = cand[(size_t)node * F + f];
+    if (c.bin >= 0 && c.gain > bg) { bg = c.gain; bf = f; }
+  }
+  sg[tid] = bg; sf[tid] = bf;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      const float og = sg[tid + o];
+      const int of = sf[tid + o];
+      if (of >= 0 && (sf[tid] < 0 || og > sg[tid] || (og == sg[tid] && of < sf[tid]))) { sg[tid] = og; sf[tid] = of; }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    NodeBest b = {0.f, -1, 0.f, 0.f, -1, {0, 0, 0}};
+    if (sf[0] >= 0) {
+      const SplitOut& c = cand[(size_t)node * F + sf[0]];
+      b.gain = c.gain; b.bin = c.bin; b.GL = c.GL; b.HL = c.HL; b.feature = sf[0];
+    }
+    out[node] = b;
+  }
+}
+
+// ---- G5: partition ---------------------------------------------------------------
+// chunks of split nodes' rows: (node, first index, count); split[node] = (feature, bin);
+// cursors[node] = (next left slot, end of the right region); left grows up, right grows down
+__global__ void __launch_bounds__(256) partition_kernel(const uint8_t* __restrict__ bins, int Fs,
+                                                        const int* __restrict__ rows_in, int* __restrict__ rows_out,
+                                                        const int4* __restrict__ chunks,
+                                                        const int2* __restrict__ split, int2* __restrict__ cursors) {
+  __shared__ int wl_cnt[4], wr_cnt[4], wl_base[4], wr_base[4];
+  const int4 c = chunks[blockIdx.x];
+  const int2 sp = split[c.x];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int base = 0; base < c.z; base += 256) {
+    const int i = base + tid;
+    const bool valid = i < c.z;
+    const int r = valid ? rows_in[c.y + i] : 0;
+    const bool left = valid && bins[(size_t)r * Fs + sp.x] <= (uint8_t)sp.y;
+    const bool right = valid && !left;
+    const unsigned long long lm = __ballot(left), rm = __ballot(right);
+    if (lane == 0) { wl_cnt[wv] = __popcll(lm); wr_cnt[wv] = __popcll(rm); }
+    __syncthreads();
+    if (tid == 0) {
+      int tl = 0, tr = 0;
+      for (int w = 0; w < 4; ++w) { tl += wl_cnt[w]; tr += wr_cnt[w]; }
+      const int l0 = atomicAdd(&cursors[c.x].x, tl);
+      const int r0 = atomicSub(&cursors[c.x].y, tr) - tr;
+      int al = l0, ar = r0;
+      for (int w = 0; w < 4; ++w) { wl_base[w] = al; al += wl_cnt[w]; wr_base[w] = ar; ar += wr_cnt[w]; }
+    }
+    __syncthreads();
+    if (left) rows_out[wl_base[wv] + __popcll(lm & below)] = r;
+    if (right) rows_out[wr_base[wv] + __popcll(rm & below)] = r;
+    __syncthreads();
   }
 }
 
 // ---- G6: prediction update by tree traversal (all rows, train and test) -----
-__global__ void predict_kernel(const uint8_t* __restrict__ binsT, const int4* __restrict__ tree,
+__global__ void predict_kernel(const uint8_t* __restrict__ bins, int Fs, const int4* __restrict__ tree,
                                const float* __restrict__ leaf, float* __restrict__ margin, int n) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int k = 0;
     int4 t = tree[0];
-    while (t.x >= 0) { k = (binsT[(long)t.x * n + i] <= t.y) ? t.z : t.w; t = tree[k]; }
+    const uint8_t* row = bins + (size_t)i * Fs;
+    while (t.x >= 0) { k = (row[t.x] <= t.y) ? t.z : t.w; t = tree[k]; }
     margin[i] += leaf[k];
   }
 }
@@ -247,40 +394,65 @@ uint64_t smix(uint64_t x) {
 extern "C" {
 
 // Same contract as gbdt_cv (csrc/gbdt/engine.cpp) for objectives 0-3 and
-// metrics rmse/mae/logloss/error; bins are precomputed on the host,
-// FEATURE-MAJOR [F][n] (gbdt_quantize_fm; cached per dataset by the caller).
-int gbdt_cv_hip(const uint8_t* binsT, const int* nbins_h, int n, int F, const float* y_h,
+// metrics rmse/mae/logloss/error. bins: ROW-major [n][Fs] uint8 (Fs >= F,
+// Fs % 4 == 0), precomputed on the host. cache_key != 0 keeps the device copy
+// of the bins across calls for the same key (one dataset, many candidates).
+int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F, const float* y_h,
                 const int* fold_h, int nfold, const double* P, int objective, const int* metrics, int n_metrics,
-                int num_boost_round, int early_stopping_rounds, unsigned long long seed, double* out_hist) {
-  if (objective > 3 || n_metrics != 1 || metrics[0] > 3) return -1;
+                int num_boost_round, int early_stopping_rounds, unsigned long long seed, long long cache_key,
+                double* out_hist) {
+  if (objective > 3 || n_metrics != 1 || metrics[0] > 3 || Fs % 4 || Fs < F || n <= 0) return -1;
   const int obj = objective == 0 ? 0 : (objective == 1 ? 1 : 2);
   const int metric = metrics[0];
-  const int max_depth = std::max(0, (int)P[2]);
+  const int max_depth = std::max(0, std::min((int)P[2], 12));
+  static std::mutex mu;                    // one cv at a time per process (device bins cache)
+  std::lock_guard<std::mutex> lock(mu);
   // ---- device buffers
-  uint8_t *d_bins, *d_fok;
+  static uint8_t* c_bins = nullptr;        // cached bins (cache_key)
+  static long long c_key = 0;
+  static size_t c_bytes = 0;
+  const size_t nbytes = (size_t)n * Fs;
+  if (cache_key == 0 || cache_key != c_key || c_bytes != nbytes || c_bins == nullptr) {
+    if (c_bins) (void)hipFree(c_bins);
+    c_bins = nullptr; c_key = 0; c_bytes = 0;
+    HC(hipMalloc(&c_bins, nbytes));
+    HC(hipMemcpy(c_bins, bins_h, nbytes, hipMemcpyHostToDevice));
+    c_key = cache_key; c_bytes = nbytes;
+  }
+  const uint8_t* d_bins = c_bins;
   float *d_y, *d_margin, *d_leaf;
-  int *d_fold, *d_node, *d_nb;
-  float2 *d_gh, *d_hist, *d_tot;
-  int4 *d_split, *d_tree;
-  SplitOut* d_best;
+  int *d_fold, *d_nb, *d_rows[3];
+  float2 *d_gh, *d_hist[2], *d_tot;
+  uint8_t* d_fok;
+  int4 *d_chunks, *d_tree, *d_pairs;
+  int2 *d_split, *d_cur;
+  SplitOut* d_cand;
+  NodeBest* d_best;
   double* d_met;
-  const int max_nodes = 1 << std::min(max_depth, 12);
-  HC(hipMalloc(&d_bins, (size_t)n * F));
+  const int max_level_nodes = 1 << max_depth;                         // nodes on the deepest level
+  const int max_hist_nodes = 1 << std::max(0, max_depth - 1);         // levels that are split searched
+  const size_t hist_node = (size_t)F * GB_BINS;
   HC(hipMalloc(&d_y, sizeof(float) * n));
   HC(hipMalloc(&d_fold, sizeof(int) * n));
-  HC(hipMalloc(&d_node, sizeof(int) * n));
+  for (int b = 0; b < 3; ++b) HC(hipMalloc(&d_rows[b], sizeof(int) * n));
   HC(hipMalloc(&d_margin, sizeof(float) * (size_t)n * nfold));
   HC(hipMalloc(&d_gh, sizeof(float2) * n));
-  HC(hipMalloc(&d_hist, sizeof(float2) * (size_t)max_nodes * F * GB_BINS));
-  HC(hipMalloc(&d_tot, sizeof(float2) * max_nodes));
-  HC(hipMalloc(&d_best, sizeof(SplitOut) * (size_t)max_nodes * F));
+  for (int b = 0; b < 2; ++b) HC(hipMalloc(&d_hist[b], sizeof(float2) * (size_t)max_hist_nodes * hist_node));
+  HC(hipMalloc(&d_tot, sizeof(float2) * max_level_nodes));
+  HC(hipMalloc(&d_cand, sizeof(SplitOut) * (size_t)max_hist_nodes * F));
+  HC(hipMalloc(&d_best, sizeof(NodeBest) * max_hist_nodes));
   HC(hipMalloc(&d_nb, sizeof(int) * F));
   HC(hipMalloc(&d_fok, F));
-  HC(hipMalloc(&d_split, sizeof(int4) * max_nodes));
-  HC(hipMalloc(&d_tree, sizeof(int4) * 2 * max_nodes * 2));
-  HC(hipMalloc(&d_leaf, sizeof(float) * 2 * max_nodes * 2));
+  const int max_chunks = 4096 + 2 * max_level_nodes;
+  HC(hipMalloc(&d_chunks, sizeof(int4) * max_chunks));
+  HC(hipMalloc(&d_pairs, sizeof(int4) * max_level_nodes));
+  int4* d_reds;
+  HC(hipMalloc(&d_reds, sizeof(int4) * max_chunks));
+  HC(hipMalloc(&d_split, sizeof(int2) * max_level_nodes));
+  HC(hipMalloc(&d_cur, sizeof(int2) * max_level_nodes));
+  HC(hipMalloc(&d_tree, sizeof(int4) * 2 * max_level_nodes * 2));
+  HC(hipMalloc(&d_leaf, sizeof(float) * 2 * max_level_nodes * 2));
   HC(hipMalloc(&d_met, sizeof(double) * 4));
-  HC(hipMemcpy(d_bins, binsT, (size_t)n * F, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_y, y_h, sizeof(float) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_fold, fold_h, sizeof(int) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_nb, nbins_h, sizeof(int) * F, hipMemcpyHostToDevice));
@@ -292,25 +464,49 @@ int gbdt_cv_hip(const uint8_t* binsT, const int* nbins_h, int n, int F, const fl
   }
   DevParams dp{(float)P[1], (float)P[8], (float)P[9], (float)P[4]};
   const int blocks = std::min(2048, (n + 255) / 256);
-  const int rows_per_block = std::max(4096, (n + 1023) / 1024);
-  const int row_chunks = (n + rows_per_block - 1) / rows_per_block;
-  std::vector<int> node0(n);
+  const int nfb = (F + HB_F - 1) / HB_F;
+  int* d_count;
+  HC(hipMalloc(&d_count, sizeof(int)));
+  float2* d_part = nullptr;                // partial histograms of multi-chunk nodes
+  int part_cap = 0;
+  std::vector<int4> reds;
   std::vector<uint8_t> fok(F);
-  std::vector<SplitOut> best((size_t)max_nodes * F);
-  std::vector<float2> tot(max_nodes);
+  std::vector<NodeBest> best(max_hist_nodes);
+  std::vector<int4> chunks, pairs;
+  std::vector<int2> split, cur;
+  std::vector<float2> tot;
+
+  struct Node { int gnode, start, count, parent; float G, H; bool built; };
+  // chunk a set of (node, start, count) segments into row chunks of <= R rows
+  auto add_chunks = [&](std::vector<int4>& out, int node, int start, int count, int R) {
+    for (int o = 0; o < count; o += R) out.push_back(make_int4(node, start + o, std::min(R, count - o), 0));
+  };
   const bool lower_better = true;
   double best_score = INFINITY;
   int best_round = 0, rounds_done = 0;
+  // GENTUN_GBDT_TIMING=1: host wall time per phase (each phase ends in a blocking copy)
+  static const bool timing = std::getenv("GENTUN_GBDT_TIMING") != nullptr;
+  double ph[6] = {0, 0, 0, 0, 0, 0};    // rows, hist, split, partition, predict+metric, trees
+  auto now = []() { return std::chrono::steady_clock::now(); };
+  auto since = [&](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double>(now() - t).count();
+  };
   for (int round = 0; round < num_boost_round; ++round) {
     double trv[64], tev[64];
     for (int k = 0; k < nfold; ++k) {
+      auto t0 = now();
       // same splitmix stream and draw order as the CPU engine (engine.cpp round_fold / build_tree)
       uint64_t rs = smix(seed ^ smix((uint64_t)k * 1000003ull + (uint64_t)round * 7919ull + 17));
       auto next = [&]() { rs = smix(rs); return rs; };
       auto uni = [&]() { return (next() >> 11) * (1.0 / 9007199254740992.0); };
-      // row sample of the fold's training rows -> level-0 node map
-      for (int i = 0; i < n; ++i) node0[i] = (fold_h[i] != k && (P[5] >= 1.0 || uni() < P[5])) ? 0 : -1;
-      HC(hipMemcpy(d_node, node0.data(), sizeof(int) * n, hipMemcpyHostToDevice));
+      const unsigned long long row_key = P[5] < 1.0 ? next() : 0ull;   // engine.cpp: one draw keys the rows
+      HC(hipMemsetAsync(d_count, 0, sizeof(int), 0));
+      hipLaunchKernelGGL(root_rows_kernel, dim3(blocks), dim3(256), 0, 0, d_fold, k, n, row_key, P[5], d_rows[0],
+                         d_count);
+      int nroot = 0;
+      HC(hipMemcpy(&nroot, d_count, sizeof(int), hipMemcpyDeviceToHost));
+      ph[0] += since(t0);
+      ph[5] += 1;
       // colsample_bytree
       std::vector<int> feats(F);
       for (int f = 0; f < F; ++f) feats[f] = f;
@@ -321,21 +517,74 @@ int gbdt_cv_hip(const uint8_t* binsT, const int* nbins_h, int n, int F, const fl
         std::sort(feats.begin(), feats.end());
       }
       float* margin = d_margin + (size_t)k * n;
-      hipLaunchKernelGGL(grad_kernel, dim3(blocks), dim3(256), 0, 0, margin, d_y, d_node, d_gh, n, obj,
-                         (float)P[10]);
-      // tree nodes in BFS order; level-local ids map to global node ids
+      hipLaunchKernelGGL(grad_kernel, dim3(blocks), dim3(256), 0, 0, margin, d_y, d_gh, n, obj, (float)P[10]);
       std::vector<int4> tree(1, make_int4(-1, 0, 0, 0));
       std::vector<float> leaf(1, 0.f);
-      std::vector<int> level_nodes(1, 0);
-      for (int depth = 0; depth <= max_depth && !level_nodes.empty(); ++depth) {
-        const int L = (int)level_nodes.size();
-        HC(hipMemset(d_hist, 0, sizeof(float2) * (size_t)L * F * GB_BINS));
-        for (int lo = 0; lo < L; lo += GB_NG) {
-          dim3 grid((F + GB_FB - 1) / GB_FB, row_chunks);
-          hipLaunchKernelGGL(hist_kernel, grid, dim3(256), 0, 0, d_bins, d_gh, d_node, d_hist, n, F, lo,
-                             std::min(GB_NG, L - lo), rows_per_block);
+      std::vector<Node> level(1, Node{0, 0, nroot, -1, 0.f, 0.f, true});
+      int rb = 0;                   // row-list buffer holding this level's segments
+      int hb = 0;                   // histogram buffer of this level
+      for (int depth = 0; depth <= max_depth && !level.empty(); ++depth) {
+        const int L = (int)level.size();
+        if (depth == max_depth && depth > 0) {   // deepest level: leaves only, totals from the parent splits
+          for (const Node& nd : level) leaf[nd.gnode] = (float)(h_weight(P, nd.G, nd.H) * P[0]);
+          break;
         }
-        hipLaunchKernelGGL(totals_kernel, dim3(L), dim3(64), 0, 0, d_hist, d_tot, F);
+        // ---- histograms: built children over their rows, siblings by subtraction
+        auto t1 = now();
+        float2* hcur = d_hist[hb];
+        chunks.clear(); pairs.clear(); reds.clear();
+        long long built_rows = 0;
+        for (const Node& nd : level) if (nd.built) built_rows += nd.count;
+        const int R = std::max(2048, (int)((built_rows + 63) / 64));
+        int nslots = 0;
+        for (int j = 0; j < L; ++j) {
+          const Node& nd = level[j];
+          if (!nd.built) {
+            pairs.push_back(make_int4(j, nd.parent, j ^ 1, 0));   // siblings are adjacent (2i, 2i+1)
+          } else if (nd.count <= R) {                             // one chunk: written in place
+            chunks.push_back(make_int4(j, nd.start, nd.count, -1));
+          } else {                                                // partial slots + reduction
+            const int first = nslots;
+            for (int o = 0; o < nd.count; o += R)
+              chunks.push_back(make_int4(j, nd.start + o, std::min(R, nd.count - o), nslots++));
+            reds.push_back(make_int4(j, first, nslots - first, 0));
+          }
+        }
+        if ((int)chunks.size() > max_chunks || (int)reds.size() > max_chunks) return -3;
+        if (nslots > part_cap) {
+          if (d_part) (void)hipFree(d_part);
+          part_cap = std::max(nslots, 2 * part_cap);
+          HC(hipMalloc(&d_part, sizeof(float2) * (size_t)part_cap * hist_node));
+        }
+        if (!chunks.empty()) {
+          HC(hipMemcpy(d_chunks, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice));
+          hipLaunchKernelGGL(hist_kernel, dim3((unsigned)chunks.size(), nfb), dim3(HB_T), 0, 0, d_bins, Fs, F,
+                             d_rows[rb], d_gh, d_chunks, hcur, d_part);
+        }
+        if (!reds.empty()) {
+          HC(hipMemcpy(d_reds, reds.data(), sizeof(int4) * reds.size(), hipMemcpyHostToDevice));
+          hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)reds.size(), std::max(1, (int)(hist_node * 2 / 4096))),
+                             dim3(256), 0, 0, reinterpret_cast<const float*>(d_part),
+                             reinterpret_cast<float*>(hcur), d_reds, F);
+        }
+        if (!pairs.empty()) {
+          HC(hipMemcpy(d_pairs, pairs.data(), sizeof(int4) * pairs.size(), hipMemcpyHostToDevice));
+          hipLaunchKernelGGL(subtract_kernel, dim3((unsigned)pairs.size(), std::max(1, (int)(hist_node / 2048))),
+                             dim3(256), 0, 0, d_hist[hb ^ 1], hcur, d_pairs, F);
+        }
+        // ---- node totals: root from its histogram, children from the parent's split
+        if (depth == 0) {
+          hipLaunchKernelGGL(totals_kernel, dim3(1), dim3(64), 0, 0, hcur, d_tot, F);
+          float2 t0;
+          HC(hipMemcpy(&t0, d_tot, sizeof(float2), hipMemcpyDeviceToHost));
+          level[0].G = t0.x; level[0].H = t0.y;
+        } else {
+          tot.resize(L);
+          for (int j = 0; j < L; ++j) tot[j] = make_float2(level[j].G, level[j].H);
+          HC(hipMemcpy(d_tot, tot.data(), sizeof(float2) * L, hipMemcpyHostToDevice));
+        }
+        if (timing) { HC(hipDeviceSynchronize()); ph[1] += since(t1); t1 = now(); }
+        // ---- split search (colsample_bylevel draw as in the CPU engine)
         std::fill(fok.begin(), fok.end(), 0);
         std::vector<int> lf = feats;
         if (P[7] < 1.0 && lf.size() > 1) {
@@ -346,46 +595,68 @@ int gbdt_cv_hip(const uint8_t* binsT, const int* nbins_h, int n, int F, const fl
         }
         for (int f : lf) fok[f] = 1;
         HC(hipMemcpy(d_fok, fok.data(), F, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(split_kernel, dim3(F, L), dim3(64), 0, 0, d_hist, d_nb, d_fok, d_tot, d_best, F, dp);
-        HC(hipMemcpy(best.data(), d_best, sizeof(SplitOut) * (size_t)L * F, hipMemcpyDeviceToHost));
-        HC(hipMemcpy(tot.data(), d_tot, sizeof(float2) * L, hipMemcpyDeviceToHost));
-        std::vector<int4> split(L);
-        std::vector<int> next;
+        hipLaunchKernelGGL(split_kernel, dim3(F, L), dim3(64), 0, 0, hcur, d_nb, d_fok, d_tot, d_cand, F, dp);
+        hipLaunchKernelGGL(best_kernel, dim3(L), dim3(256), 0, 0, d_cand, d_best, F);
+        HC(hipMemcpy(best.data(), d_best, sizeof(NodeBest) * L, hipMemcpyDeviceToHost));
+        if (timing) { ph[2] += since(t1); t1 = now(); }
+        // ---- host: leaves, gamma pruning, next level layout
+        split.assign(L, make_int2(-1, 0));
+        cur.assign(L, make_int2(0, 0));
+        chunks.clear();
+        std::vector<Node> nextl;
+        std::vector<int> split_of;       // level node -> index of its left child in nextl (or -1)
+        split_of.assign(L, -1);
         for (int j = 0; j < L; ++j) {
-          const int gnode = level_nodes[j];
-          const double G = tot[j].x, H = tot[j].y;
-          leaf[gnode] = (float)(h_weight(P, G, H) * P[0]);
-          int bf = -1;
-          SplitOut bs = {0.f, -1, 0.f, 0.f};
-          if (depth < max_depth) {
-            for (int f = 0; f < F; ++f) {
-              const SplitOut& c = best[(size_t)j * F + f];
-              if (c.bin >= 0 && c.gain > bs.gain + 1e-12f) { bs = c; bf = f; }
-            }
-          }
-          if (bf < 0 || bs.gain < P[3] || bs.gain <= 1e-12) {
-            split[j] = make_int4(-1, 0, 0, 0);
+          Node& nd = level[j];
+          leaf[nd.gnode] = (float)(h_weight(P, nd.G, nd.H) * P[0]);
+          const NodeBest& b = best[j];
+          if (depth >= max_depth || b.feature < 0 || b.bin < 0 || b.gain < P[3] || b.gain <= 1e-12f ||
+              nd.count <= 0)
             continue;
-          }
           const int li = (int)tree.size();
           tree.push_back(make_int4(-1, 0, 0, 0));
           tree.push_back(make_int4(-1, 0, 0, 0));
           leaf.push_back(0.f);
           leaf.push_back(0.f);
-          tree[gnode] = make_int4(bf, bs.bin, li, li + 1);
-          split[j] = make_int4(bf, bs.bin, (int)next.size(), (int)next.size() + 1);
-          next.push_back(li);
-          next.push_back(li + 1);
+          tree[nd.gnode] = make_int4(b.feature, b.bin, li, li + 1);
+          split[j] = make_int2(b.feature, b.bin);
+          cur[j] = make_int2(nd.start, nd.start + nd.count);
+          split_of[j] = (int)nextl.size();
+          nextl.push_back(Node{li, nd.start, 0, j, b.GL, b.HL, false});
+          nextl.push_back(Node{li + 1, 0, 0, j, nd.G - b.GL, nd.H - b.HL, false});
+          add_chunks(chunks, j, nd.start, nd.count, 4096);
         }
-        if (next.empty()) break;
-        HC(hipMemcpy(d_split, split.data(), sizeof(int4) * L, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(256), 0, 0, d_bins, d_node, d_split, n);
-        level_nodes = next;
+        if (nextl.empty()) break;
+        if ((int)chunks.size() > max_chunks) return -3;
+        // ---- partition the split nodes' rows into the other row buffer
+        const int ob = (rb == 1) ? 2 : 1;
+        HC(hipMemcpy(d_split, split.data(), sizeof(int2) * L, hipMemcpyHostToDevice));
+        HC(hipMemcpy(d_cur, cur.data(), sizeof(int2) * L, hipMemcpyHostToDevice));
+        HC(hipMemcpy(d_chunks, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(partition_kernel, dim3((unsigned)chunks.size()), dim3(256), 0, 0, d_bins, Fs,
+                           d_rows[rb], d_rows[ob], d_chunks, d_split, d_cur);
+        HC(hipMemcpy(cur.data(), d_cur, sizeof(int2) * L, hipMemcpyDeviceToHost));
+        for (int j = 0; j < L; ++j) {
+          if (split_of[j] < 0) continue;
+          const Node& nd = level[j];
+          const int lc = cur[j].x - nd.start;
+          Node& l = nextl[split_of[j]];
+          Node& r = nextl[split_of[j] + 1];
+          l.count = lc;
+          r.start = nd.start + lc; r.count = nd.count - lc;
+          l.parent = r.parent = j;
+          (l.count <= r.count ? l : r).built = true;     // smaller child: histogram; sibling: subtraction
+        }
+        if (timing) ph[3] += since(t1);
+        level.swap(nextl);
+        rb = ob;
+        hb ^= 1;
       }
+      auto t4 = now();
       HC(hipMemcpy(d_tree, tree.data(), sizeof(int4) * tree.size(), hipMemcpyHostToDevice));
       HC(hipMemcpy(d_leaf, leaf.data(), sizeof(float) * leaf.size(), hipMemcpyHostToDevice));
-      hipLaunchKernelGGL(predict_kernel, dim3(blocks), dim3(256), 0, 0, d_bins, d_tree, d_leaf, margin, n);
-      HC(hipMemset(d_met, 0, sizeof(double) * 4));
+      hipLaunchKernelGGL(predict_kernel, dim3(blocks), dim3(256), 0, 0, d_bins, Fs, d_tree, d_leaf, margin, n);
+      HC(hipMemsetAsync(d_met, 0, sizeof(double) * 4, 0));
       hipLaunchKernelGGL(metric_kernel, dim3(std::min(blocks, 1024)), dim3(256), 0, 0, margin, d_y, d_fold, k, n,
                          metric, obj, d_met);
       double met[4];
@@ -393,6 +664,7 @@ int gbdt_cv_hip(const uint8_t* binsT, const int* nbins_h, int n, int F, const fl
       double tr = met[0] / std::max(1.0, met[1]), te = met[2] / std::max(1.0, met[3]);
       if (metric == 0) { tr = std::sqrt(tr); te = std::sqrt(te); }
       trv[k] = tr; tev[k] = te;
+      ph[4] += since(t4);
     }
     double trm = 0, tem = 0, trs = 0, tes = 0;
     for (int k = 0; k < nfold; ++k) { trm += trv[k]; tem += tev[k]; }
@@ -404,9 +676,16 @@ int gbdt_cv_hip(const uint8_t* binsT, const int* nbins_h, int n, int F, const fl
     if (lower_better ? tem < best_score : tem > best_score) { best_score = tem; best_round = round; }
     if (early_stopping_rounds > 0 && round - best_round >= early_stopping_rounds) break;
   }
-  for (void* p : {(void*)d_bins, (void*)d_y, (void*)d_fold, (void*)d_node, (void*)d_margin, (void*)d_gh,
-                  (void*)d_hist, (void*)d_tot, (void*)d_best, (void*)d_nb, (void*)d_fok, (void*)d_split,
-                  (void*)d_tree, (void*)d_leaf, (void*)d_met})
+  if (timing)
+    std::fprintf(stderr, "[gbdt_hip] trees %.0f  rows %.3fs  hist %.3fs  split %.3fs  partition %.3fs  "
+                 "predict+metric %.3fs\n", ph[5], ph[0], ph[1], ph[2], ph[3], ph[4]);
+  (void)hipFree(d_count);
+  (void)hipFree(d_reds);
+  if (d_part) (void)hipFree(d_part);
+  for (void* p : {(void*)d_y, (void*)d_fold, (void*)d_rows[0], (void*)d_rows[1], (void*)d_rows[2],
+                  (void*)d_margin, (void*)d_gh, (void*)d_hist[0], (void*)d_hist[1], (void*)d_tot, (void*)d_cand,
+                  (void*)d_best, (void*)d_nb, (void*)d_fok, (void*)d_chunks, (void*)d_pairs, (void*)d_split,
+                  (void*)d_cur, (void*)d_tree, (void*)d_leaf, (void*)d_met})
     (void)hipFree(p);
   return early_stopping_rounds > 0 ? best_round + 1 : rounds_done;
 }

@@ -1,5 +1,6 @@
 """MI355X GBDT path: host quantisation (C++), histogram / split / partition /
-predict kernels on the GPU (csrc/hip/gbdt_hist.hip). Used by
+predict kernels on the GPU (csrc/hip/gbdt_hist.hip: row-major bins, per-node
+row segments, smaller-child histograms + subtraction). Used by
 :func:`gentun_amd.models.gbdt.cv` when ``device`` is a CUDA/HIP device;
 objectives reg:linear/squarederror, reg:logistic, binary:logistic and the
 rmse/mae/logloss/error metrics run on the GPU, anything else falls back to
@@ -24,41 +25,50 @@ def _fn():
     f = L.gbdt_cv_hip
     if not getattr(f, "_typed", False):
         c = ctypes
-        f.argtypes = [c.c_void_p, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int, c.c_void_p,
-                      c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_ulonglong, c.c_void_p]
+        f.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int,
+                      c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_ulonglong, c.c_longlong,
+                      c.c_void_p]
         f.restype = c.c_int
         f._typed = True
     return f
 
 
-_QCACHE = []      # (x object, shape, binsT, nbins): every GA candidate reuses its dataset's bins
+_QCACHE = []      # (x object, shape, bins, nbins, key): every GA candidate reuses its dataset's bins
+_KEYS = [0]
 
 
-def quantize_fm(x):
-    """Feature-major uint8 bins [F][n] + bins per feature, cached per dataset
-    object (quantisation is per-dataset work, not per-candidate)."""
+def quantize_rm(x):
+    """Row-major uint8 bins [n][Fs] (Fs = F rounded up to 4, zero padding) +
+    bins per feature + a cache key, computed once per dataset object: the
+    device keeps its copy of the bins for that key across candidates."""
     for ent in _QCACHE:
         if ent[0] is x and ent[1] == x.shape:
-            return ent[2], ent[3]
+            return ent[2], ent[3], ent[4]
     xc = np.ascontiguousarray(x, dtype=np.float32)
     n, f = xc.shape
-    bins = np.zeros((f, n), np.uint8)
+    b = np.zeros((n, f), np.uint8)
     nb = np.zeros(f, np.int32)
-    _lib.gbdt().gbdt_quantize_fm(xc.ctypes.data, n, f, bins.ctypes.data, nb.ctypes.data)
-    _QCACHE.append((x, x.shape, bins, nb))
+    _lib.gbdt().gbdt_quantize(xc.ctypes.data, n, f, b.ctypes.data, nb.ctypes.data)
+    fs = (f + 3) // 4 * 4
+    if fs != f:
+        bp = np.zeros((n, fs), np.uint8)
+        bp[:, :f] = b
+        b = bp
+    _KEYS[0] += 1
+    _QCACHE.append((x, x.shape, b, nb, _KEYS[0]))
     while len(_QCACHE) > 2:
         _QCACHE.pop(0)
-    return bins, nb
+    return b, nb, _KEYS[0]
 
 
 def cv(x, y, fold_of, nfold, parr, obj, num_class, marr, nrounds, esr, seed, hist, x_key=None):
     if not supported(obj, marr):
         return None
-    bins, nb = quantize_fm(x if x_key is None else x_key)
+    bins, nb, key = quantize_rm(x if x_key is None else x_key)
     fold_of = np.ascontiguousarray(fold_of.astype(np.int32))
     y = np.ascontiguousarray(y.astype(np.float32))
     marr = np.ascontiguousarray(marr.astype(np.int32))
-    kept = _fn()(bins.ctypes.data, nb.ctypes.data, x.shape[0], x.shape[1], y.ctypes.data, fold_of.ctypes.data,
-                 int(nfold), parr.ctypes.data, int(obj), marr.ctypes.data, len(marr), int(nrounds), int(esr),
-                 ctypes.c_ulonglong(seed & 0xFFFFFFFFFFFFFFFF), hist.ctypes.data)
+    kept = _fn()(bins.ctypes.data, bins.shape[1], nb.ctypes.data, x.shape[0], x.shape[1], y.ctypes.data,
+                 fold_of.ctypes.data, int(nfold), parr.ctypes.data, int(obj), marr.ctypes.data, len(marr),
+                 int(nrounds), int(esr), ctypes.c_ulonglong(seed & 0xFFFFFFFFFFFFFFFF), key, hist.ctypes.data)
     return kept

@@ -101,14 +101,23 @@ def test_iris_ga_baseline_cfg1():
     assert len(ga.history) == 2
 
 
-def test_quantize_feature_major_matches_and_caches():
-    """The GPU path's feature-major bins are the transpose of the CPU engine's
-    row-major bins, and are computed once per dataset object."""
+def test_quantize_gpu_layout_matches_and_caches():
+    """The GPU path's bins are the CPU engine's row-major bins padded to a
+    4-byte row stride, computed once per dataset object (stable cache key);
+    the feature-major layout of the engine is the transpose."""
     from gentun_amd.models import gbdt_hip
+    from gentun_amd.ops import _lib
     rng = np.random.default_rng(5)
     x = rng.standard_normal((3000, 7)).astype(np.float32)
     x[:, 3] = np.round(x[:, 3])                      # few distinct values -> exact bins
     b, nb = gbdt.quantize(x)
-    bt, nb2 = gbdt_hip.quantize_fm(x)
-    assert np.array_equal(b.T, bt) and np.array_equal(nb, nb2)
-    assert gbdt_hip.quantize_fm(x)[0] is bt
+    br, nb2, key = gbdt_hip.quantize_rm(x)
+    assert br.shape == (3000, 8) and not br[:, 7].any()
+    assert np.array_equal(b, br[:, :7]) and np.array_equal(nb, nb2)
+    again = gbdt_hip.quantize_rm(x)
+    assert again[0] is br and again[2] == key
+    bt = np.zeros((7, 3000), np.uint8)
+    nb3 = np.zeros(7, np.int32)
+    xc = np.ascontiguousarray(x)
+    _lib.gbdt().gbdt_quantize_fm(xc.ctypes.data, 3000, 7, bt.ctypes.data, nb3.ctypes.data)
+    assert np.array_equal(b.T, bt)

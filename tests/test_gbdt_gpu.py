@@ -37,3 +37,31 @@ def test_hip_binary_logistic_and_early_stopping():
     gpu = gbdt.cv(p, x, yb, num_boost_round=200, nfold=5, early_stopping_rounds=10, device="cuda:0")
     assert abs(cpu['test-logloss-mean'][-1] - gpu['test-logloss-mean'][-1]) < 0.03
     assert gpu['test-logloss-mean'][-1] == min(gpu['test-logloss-mean'])
+
+
+@pytest.mark.parametrize("f,depth", [(10, 9), (7, 1), (33, 6)])
+def test_hip_deep_trees_odd_feature_counts(f, depth):
+    """Row-segment partition + subtraction over many levels, feature counts
+    that are not multiples of the 4-byte row word / 32-feature block."""
+    x, y = make_regression(n=30000, f=f, seed=7)
+    p = {'objective': 'reg:linear', 'eta': 0.3, 'max_depth': depth, 'min_child_weight': 0}
+    cpu = gbdt.cv(p, x, y, num_boost_round=15, nfold=3, seed=1)
+    gpu = gbdt.cv(p, x, y, num_boost_round=15, nfold=3, seed=1, device="cuda:0")
+    a, b = np.array(cpu['test-rmse-mean']), np.array(gpu['test-rmse-mean'])
+    assert len(a) == len(b)
+    assert np.max(np.abs(a - b) / a) < 0.03, (a, b)
+    tr_a, tr_b = np.array(cpu['train-rmse-mean']), np.array(gpu['train-rmse-mean'])
+    assert np.max(np.abs(tr_a - tr_b) / tr_a) < 0.03, (tr_a, tr_b)
+
+
+def test_hip_bins_cache_reused_across_candidates():
+    """Second candidate on the same dataset object reuses the device bins
+    (cache key) and still matches a fresh upload (up to the float-atomic
+    histogram order, which can flip near-tie splits)."""
+    from gentun_amd.models import gbdt_hip
+    x, y = make_regression(n=8000, f=12, seed=9)
+    p = {'objective': 'reg:linear', 'eta': 0.3, 'max_depth': 4}
+    first = gbdt.cv(p, x, y, num_boost_round=10, nfold=2, seed=0, device="cuda:0")
+    second = gbdt.cv(p, x, y, num_boost_round=10, nfold=2, seed=0, device="cuda:0")
+    assert gbdt_hip.quantize_rm(x)[2] == gbdt_hip.quantize_rm(x)[2]
+    np.testing.assert_allclose(first['test-rmse-mean'], second['test-rmse-mean'], rtol=1e-2)
