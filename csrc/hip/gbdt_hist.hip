@@ -37,8 +37,8 @@
 #include <vector>
 
 #define GB_BINS 256
-#define HB_F 32          // features per histogram workgroup
-#define HB_STRIDE 514    // floats per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
+#define HB_F 16          // features per histogram workgroup
+#define HB_STRIDE 514    // int64 per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
 
 namespace {
 struct DevParams {
@@ -82,26 +82,55 @@ __global__ void grad_kernel(const float* __restrict__ margin, const float* __res
 }
 
 // ---- G3: histograms -----------------------------------------------------------
-// work chunk: (level-local node, first index in the row list, row count)
-// grid (chunks, feature blocks of HB_F), 512 threads = 64 row lanes x 8 word lanes;
-// each lane keeps HB_U rows' loads in flight (the row gather is latency-bound)
+// Fixed-point LDS accumulation: LDS float atomics measured 7x slower than the
+// same loop with plain adds (profiles/gbdt_probe_depth6_10.log), so every
+// row's (g, h) is scaled by a power of two chosen from the tree's max |g|,
+// |h| and the row count (no overflow for any node) and summed with 64-bit
+// integer LDS atomics: exact, order-independent sums -> the histograms (and
+// with the fixed-order partial reduction, the whole GPU boosting run) are
+// bitwise reproducible, unlike float atomics.
+
+// max |g|, max |h| over all rows (bit patterns of non-negative floats order as ints)
+__global__ void gh_max_kernel(const float2* __restrict__ gh, int n, unsigned int* __restrict__ mx) {
+  unsigned int mg = 0, mh = 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float2 v = gh[i];
+    mg = max(mg, __float_as_uint(fabsf(v.x)));
+    mh = max(mh, __float_as_uint(fabsf(v.y)));
+  }
+  for (int o = 32; o > 0; o >>= 1) { mg = max(mg, __shfl_xor(mg, o)); mh = max(mh, __shfl_xor(mh, o)); }
+  if ((threadIdx.x & 63) == 0) { atomicMax(&mx[0], mg); atomicMax(&mx[1], mh); }
+}
+
+// scale exponent: max * 2^se * n < 2^62
+__device__ __forceinline__ int fx_exp(unsigned int maxbits, int lg_n) {
+  int e = 0;
+  (void)frexpf(__uint_as_float(maxbits), &e);          // max < 2^e
+  return min(100, 61 - e - lg_n);
+}
+
+// grid (chunks, feature blocks of HB_F), HB_T threads = HB_T/4 row lanes x 4 word
+// lanes (16 features = 4 x 4 bin bytes per row); each lane keeps HB_U rows' loads in flight
 #define HB_T 512
-#define HB_U 8
+#define HB_U 4
 __global__ void __launch_bounds__(HB_T) hist_kernel(const uint8_t* __restrict__ bins, int Fs, int F,
                                                     const int* __restrict__ rows, const float2* __restrict__ gh,
                                                     const int4* __restrict__ chunks, float2* __restrict__ hist,
-                                                    float2* __restrict__ hist_part) {
-  __shared__ float lh[HB_F * HB_STRIDE];
+                                                    unsigned long long* __restrict__ hist_part,
+                                                    const unsigned int* __restrict__ mx, int lg_n) {
+  __shared__ unsigned long long lh[HB_F * HB_STRIDE];
   const int4 c = chunks[blockIdx.x];
   const int fb = blockIdx.y * HB_F, tid = threadIdx.x;
-  constexpr int RL = HB_T / 8;                  // row lanes
-  for (int i = tid; i < HB_F * HB_STRIDE; i += HB_T) lh[i] = 0.f;
+  constexpr int RL = HB_T / 4;                  // row lanes
+  for (int i = tid; i < HB_F * HB_STRIDE; i += HB_T) lh[i] = 0ull;
+  const int seg = fx_exp(mx[0], lg_n), seh = fx_exp(mx[1], lg_n);
+  const float sg = ldexpf(1.f, seg), sh = ldexpf(1.f, seh);
   __syncthreads();
-  const int wl = tid & 7, rl = tid >> 3;
+  const int wl = tid & 3, rl = tid >> 2;
   const int f4 = fb + wl * 4;
   if (f4 < F) {
     const int* rp = rows + c.y;
-    float* my = lh + wl * 4 * HB_STRIDE;
+    unsigned long long* my = lh + wl * 4 * HB_STRIDE;
     int i = rl;
     for (; i + (HB_U - 1) * RL < c.z; i += HB_U * RL) {
       int r[HB_U];
@@ -115,48 +144,65 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(const uint8_t* __restrict__ 
         w[u] = *reinterpret_cast<const uint32_t*>(bins + (size_t)r[u] * Fs + f4);
       }
 #pragma unroll
-      for (int u = 0; u < HB_U; ++u)
+      for (int u = 0; u < HB_U; ++u) {
+        const unsigned long long qg = (unsigned long long)llrintf(g[u].x * sg);
+        const unsigned long long qh = (unsigned long long)llrintf(g[u].y * sh);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          float* d = my + k * HB_STRIDE + 2 * ((w[u] >> (8 * k)) & 255u);
-          atomicAdd(d, g[u].x);
-          atomicAdd(d + 1, g[u].y);
+          unsigned long long* d = my + k * HB_STRIDE + 2 * ((w[u] >> (8 * k)) & 255u);
+          atomicAdd(d, qg);
+          atomicAdd(d + 1, qh);
         }
+      }
     }
     for (; i < c.z; i += RL) {
       const int r = rp[i];
       const float2 g = gh[r];
       const uint32_t w = *reinterpret_cast<const uint32_t*>(bins + (size_t)r * Fs + f4);
+      const unsigned long long qg = (unsigned long long)llrintf(g.x * sg);
+      const unsigned long long qh = (unsigned long long)llrintf(g.y * sh);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        float* d = my + k * HB_STRIDE + 2 * ((w >> (8 * k)) & 255u);
-        atomicAdd(d, g.x);
-        atomicAdd(d + 1, g.y);
+        unsigned long long* d = my + k * HB_STRIDE + 2 * ((w >> (8 * k)) & 255u);
+        atomicAdd(d, qg);
+        atomicAdd(d + 1, qh);
       }
     }
   }
   __syncthreads();
   // flush with plain stores, no global atomics: a node that fits one chunk is
-  // written straight into its histogram, otherwise into partial slot c.w
-  // (reduce_kernel sums a node's partials in slot order)
-  float* dst = reinterpret_cast<float*>(c.w < 0 ? hist + (size_t)c.x * F * GB_BINS
-                                                : hist_part + (size_t)c.w * F * GB_BINS) + (size_t)fb * 2 * GB_BINS;
+  // written straight into its (float) histogram, otherwise its exact integer
+  // sums go to partial slot c.w (reduce_kernel adds a node's slots exactly,
+  // so the result does not depend on which rows a chunk got)
   const int nf = min(HB_F, F - fb);
-  for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
-    const int fl = i >> 9, j = i & 511;
-    dst[(size_t)fl * 2 * GB_BINS + j] = lh[fl * HB_STRIDE + j];
+  if (c.w < 0) {
+    float* dst = reinterpret_cast<float*>(hist + (size_t)c.x * F * GB_BINS) + (size_t)fb * 2 * GB_BINS;
+    const float ig = ldexpf(1.f, -seg), ih = ldexpf(1.f, -seh);
+    for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
+      const int fl = i >> 9, j = i & 511;
+      const long long v = (long long)lh[fl * HB_STRIDE + j];
+      dst[(size_t)fl * 2 * GB_BINS + j] = (float)v * ((j & 1) ? ih : ig);
+    }
+  } else {
+    unsigned long long* dst = hist_part + ((size_t)c.w * F + fb) * 2 * GB_BINS;
+    for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
+      const int fl = i >> 9, j = i & 511;
+      dst[(size_t)fl * 2 * GB_BINS + j] = lh[fl * HB_STRIDE + j];
+    }
   }
 }
 
 // node histogram = sum of its partial slots; red = (node, first slot, slots)
-__global__ void __launch_bounds__(256) reduce_kernel(const float* __restrict__ part, float* __restrict__ hist,
-                                                     const int4* __restrict__ red, int F) {
+__global__ void __launch_bounds__(256) reduce_kernel(const unsigned long long* __restrict__ part,
+                                                     float* __restrict__ hist, const int4* __restrict__ red, int F,
+                                                     const unsigned int* __restrict__ mx, int lg_n) {
   const int4 rd = red[blockIdx.x];
   const size_t per = (size_t)F * 2 * GB_BINS;
+  const float ig = ldexpf(1.f, -fx_exp(mx[0], lg_n)), ih = ldexpf(1.f, -fx_exp(mx[1], lg_n));
   for (size_t e = threadIdx.x + (size_t)blockIdx.y * 256; e < per; e += (size_t)gridDim.y * 256) {
-    float acc = 0.f;
+    unsigned long long acc = 0;
     for (int sl = 0; sl < rd.z; ++sl) acc += part[(size_t)(rd.y + sl) * per + e];
-    hist[(size_t)rd.x * per + e] = acc;
+    hist[(size_t)rd.x * per + e] = (float)(long long)acc * ((e & 1) ? ih : ig);
   }
 }
 
@@ -368,7 +414,7 @@ __global__ void metric_kernel(const float* __restrict__ margin, const float* __r
       for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x < 4) atomicAdd(&out[threadIdx.x], red[threadIdx.x][0]);
+  if (threadIdx.x < 4) out[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];   // host sums in block order
 }
 
 inline double h_thr(double g, double a) { return g > a ? g - a : (g < -a ? g + a : 0.0); }
@@ -452,7 +498,7 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   HC(hipMalloc(&d_cur, sizeof(int2) * max_level_nodes));
   HC(hipMalloc(&d_tree, sizeof(int4) * 2 * max_level_nodes * 2));
   HC(hipMalloc(&d_leaf, sizeof(float) * 2 * max_level_nodes * 2));
-  HC(hipMalloc(&d_met, sizeof(double) * 4));
+  HC(hipMalloc(&d_met, sizeof(double) * 4 * 1024));
   HC(hipMemcpy(d_y, y_h, sizeof(float) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_fold, fold_h, sizeof(int) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_nb, nbins_h, sizeof(int) * F, hipMemcpyHostToDevice));
@@ -467,7 +513,11 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   const int nfb = (F + HB_F - 1) / HB_F;
   int* d_count;
   HC(hipMalloc(&d_count, sizeof(int)));
-  float2* d_part = nullptr;                // partial histograms of multi-chunk nodes
+  unsigned int* d_mx;                      // max |g|, |h| of the current tree (fixed-point scale)
+  HC(hipMalloc(&d_mx, 2 * sizeof(unsigned int)));
+  int lg_n = 0;
+  while ((1ll << lg_n) < (long long)n + 1) ++lg_n;
+  unsigned long long* d_part = nullptr;    // exact partial histograms of multi-chunk nodes
   int part_cap = 0;
   std::vector<int4> reds;
   std::vector<uint8_t> fok(F);
@@ -518,6 +568,8 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
       }
       float* margin = d_margin + (size_t)k * n;
       hipLaunchKernelGGL(grad_kernel, dim3(blocks), dim3(256), 0, 0, margin, d_y, d_gh, n, obj, (float)P[10]);
+      HC(hipMemsetAsync(d_mx, 0, 2 * sizeof(unsigned int), 0));
+      hipLaunchKernelGGL(gh_max_kernel, dim3(std::min(blocks, 512)), dim3(256), 0, 0, d_gh, n, d_mx);
       std::vector<int4> tree(1, make_int4(-1, 0, 0, 0));
       std::vector<float> leaf(1, 0.f);
       std::vector<Node> level(1, Node{0, 0, nroot, -1, 0.f, 0.f, true});
@@ -554,18 +606,17 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
         if (nslots > part_cap) {
           if (d_part) (void)hipFree(d_part);
           part_cap = std::max(nslots, 2 * part_cap);
-          HC(hipMalloc(&d_part, sizeof(float2) * (size_t)part_cap * hist_node));
+          HC(hipMalloc(&d_part, sizeof(unsigned long long) * 2 * (size_t)part_cap * hist_node));
         }
         if (!chunks.empty()) {
           HC(hipMemcpy(d_chunks, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice));
           hipLaunchKernelGGL(hist_kernel, dim3((unsigned)chunks.size(), nfb), dim3(HB_T), 0, 0, d_bins, Fs, F,
-                             d_rows[rb], d_gh, d_chunks, hcur, d_part);
+                             d_rows[rb], d_gh, d_chunks, hcur, d_part, d_mx, lg_n);
         }
         if (!reds.empty()) {
           HC(hipMemcpy(d_reds, reds.data(), sizeof(int4) * reds.size(), hipMemcpyHostToDevice));
           hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)reds.size(), std::max(1, (int)(hist_node * 2 / 4096))),
-                             dim3(256), 0, 0, reinterpret_cast<const float*>(d_part),
-                             reinterpret_cast<float*>(hcur), d_reds, F);
+                             dim3(256), 0, 0, d_part, reinterpret_cast<float*>(hcur), d_reds, F, d_mx, lg_n);
         }
         if (!pairs.empty()) {
           HC(hipMemcpy(d_pairs, pairs.data(), sizeof(int4) * pairs.size(), hipMemcpyHostToDevice));
@@ -656,11 +707,14 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
       HC(hipMemcpy(d_tree, tree.data(), sizeof(int4) * tree.size(), hipMemcpyHostToDevice));
       HC(hipMemcpy(d_leaf, leaf.data(), sizeof(float) * leaf.size(), hipMemcpyHostToDevice));
       hipLaunchKernelGGL(predict_kernel, dim3(blocks), dim3(256), 0, 0, d_bins, Fs, d_tree, d_leaf, margin, n);
-      HC(hipMemsetAsync(d_met, 0, sizeof(double) * 4, 0));
-      hipLaunchKernelGGL(metric_kernel, dim3(std::min(blocks, 1024)), dim3(256), 0, 0, margin, d_y, d_fold, k, n,
-                         metric, obj, d_met);
-      double met[4];
-      HC(hipMemcpy(met, d_met, sizeof(met), hipMemcpyDeviceToHost));
+      const int mblocks = std::min(blocks, 1024);
+      hipLaunchKernelGGL(metric_kernel, dim3(mblocks), dim3(256), 0, 0, margin, d_y, d_fold, k, n, metric, obj,
+                         d_met);
+      std::vector<double> mpart((size_t)mblocks * 4);
+      HC(hipMemcpy(mpart.data(), d_met, sizeof(double) * mpart.size(), hipMemcpyDeviceToHost));
+      double met[4] = {0, 0, 0, 0};
+      for (int b = 0; b < mblocks; ++b)
+        for (int q = 0; q < 4; ++q) met[q] += mpart[(size_t)b * 4 + q];
       double tr = met[0] / std::max(1.0, met[1]), te = met[2] / std::max(1.0, met[3]);
       if (metric == 0) { tr = std::sqrt(tr); te = std::sqrt(te); }
       trv[k] = tr; tev[k] = te;
@@ -680,6 +734,7 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
     std::fprintf(stderr, "[gbdt_hip] trees %.0f  rows %.3fs  hist %.3fs  split %.3fs  partition %.3fs  "
                  "predict+metric %.3fs\n", ph[5], ph[0], ph[1], ph[2], ph[3], ph[4]);
   (void)hipFree(d_count);
+  (void)hipFree(d_mx);
   (void)hipFree(d_reds);
   if (d_part) (void)hipFree(d_part);
   for (void* p : {(void*)d_y, (void*)d_fold, (void*)d_rows[0], (void*)d_rows[1], (void*)d_rows[2],
