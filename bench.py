@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--space", choices=("default", "deep"), default="default",
+                    help="default: S=(3,5) kernels (20,50) (headline); deep: BASELINE cfg 4, S=(3,4,5) kernels "
+                         "(20,50,100) on 32x32 inputs")
     return ap.parse_args()
 
 
@@ -92,8 +95,10 @@ def run(args):
     epochs = tuple(int(e) for e in args.epochs.split(","))
     lrs = tuple(float(x) for x in args.lr.split(","))
     x, y = make_cifar_like(n=args.samples, seed=0)
-    extra = dict(nodes=(3, 5), input_shape=(32, 32, 3), kernels_per_layer=(20, 50),
-                 kernel_sizes=((5, 5), (5, 5)), dense_units=500, dropout_probability=0.5, classes=10,
+    nodes, kernels = ((3, 4, 5), (20, 50, 100)) if args.space == "deep" else ((3, 5), (20, 50))
+    space = "S=({}) kernels ({})".format(",".join(map(str, nodes)), ",".join(map(str, kernels)))
+    extra = dict(nodes=nodes, input_shape=(32, 32, 3), kernels_per_layer=kernels,
+                 kernel_sizes=((5, 5),) * len(nodes), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=args.nfold, epochs=epochs, learning_rate=lrs, batch_size=32, dtype=args.dtype,
                  seed=args.seed, backend=args.backend)
     evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch)
@@ -132,8 +137,8 @@ def run(args):
 
     cph = 3600.0 * timed_evals / elapsed
     out = {
-        "metric": "candidates/hour (Genetic-CNN S=(3,5), CIFAR-10-shaped, {}-fold CV, epochs ({}))".format(
-            args.nfold, ",".join(str(e) for e in epochs)),
+        "metric": "candidates/hour (Genetic-CNN {}, CIFAR-10-shaped, {}-fold CV, epochs ({}))".format(
+            space.split(" kernels")[0], args.nfold, ",".join(str(e) for e in epochs)),
         "value": round(cph, 2),
         "unit": "candidates/hour",
         "n_gpus": comm.world_size,
@@ -145,7 +150,7 @@ def run(args):
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (CIFAR-10-shaped 10k x 32x32x3 coloured stroke glyphs + clutter + noise; random-init weights)",
-        "config": {"model": "Genetic-CNN S=(3,5) kernels (20,50) dense 500", "global_batch": 32 * args.nfold,
+        "config": {"model": "Genetic-CNN {} dense 500".format(space), "global_batch": 32 * args.nfold,
                    "seq_len": None, "parallelism": "population-dp{}".format(comm.world_size),
                    "candidates_per_step": P, "per_gpu": args.per_gpu, "nfold": args.nfold,
                    "epochs": list(epochs), "learning_rate": list(lrs), "samples": args.samples,
