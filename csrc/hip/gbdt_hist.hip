@@ -81,6 +81,21 @@ __global__ void grad_kernel(const float* __restrict__ margin, const float* __res
   }
 }
 
+// multi:softmax / multi:softprob, class c of K: softmax over the row's K
+// margins (engine.cpp: g = p_c - [y == c], h = max(2 p_c (1 - p_c), 1e-16))
+__global__ void grad_multi_kernel(const float* __restrict__ margin, const float* __restrict__ y,
+                                  float2* __restrict__ gh, int n, int K, int c) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float* m = margin + (size_t)i * K;
+    float mx = m[0];
+    for (int k = 1; k < K; ++k) mx = fmaxf(mx, m[k]);
+    float z = 0.f;
+    for (int k = 0; k < K; ++k) z += expf(m[k] - mx);
+    const float p = expf(m[c] - mx) / z;
+    gh[i] = make_float2(p - ((int)y[i] == c ? 1.f : 0.f), fmaxf(2.f * p * (1.f - p), 1e-16f));
+  }
+}
+
 // ---- G3: histograms -----------------------------------------------------------
 // Fixed-point LDS accumulation: LDS float atomics measured 7x slower than the
 // same loop with plain adds (profiles/gbdt_probe_depth6_10.log), so every
@@ -374,35 +389,48 @@ __global__ void __launch_bounds__(256) partition_kernel(const uint8_t* __restric
 
 // ---- G6: prediction update by tree traversal (all rows, train and test) -----
 __global__ void predict_kernel(const uint8_t* __restrict__ bins, int Fs, const int4* __restrict__ tree,
-                               const float* __restrict__ leaf, float* __restrict__ margin, int n) {
+                               const float* __restrict__ leaf, float* __restrict__ margin, int n, int K, int c) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     int k = 0;
     int4 t = tree[0];
     const uint8_t* row = bins + (size_t)i * Fs;
     while (t.x >= 0) { k = (row[t.x] <= t.y) ? t.z : t.w; t = tree[k]; }
-    margin[i] += leaf[k];
+    margin[(size_t)i * K + c] += leaf[k];
   }
 }
 
 // ---- G8: metric partial sums over a fold's train / test rows -----------------
 // out[0..3] = (train sum, train count, test sum, test count); metric 0 rmse, 1 mae, 2 logloss, 3 error
 __global__ void metric_kernel(const float* __restrict__ margin, const float* __restrict__ y,
-                              const int* __restrict__ fold_of, int fold, int n, int metric, int obj,
+                              const int* __restrict__ fold_of, int fold, int n, int metric, int objective, int K,
                               double* __restrict__ out) {
+  // engine.cpp eval_metric: rmse/mae on sigmoid(margin) for reg:logistic / binary:logistic,
+  // logloss on sigmoid, error thresholds margin 0 for binary:logitraw, merror / mlogloss over K
   __shared__ double red[4][256];
   double s[4] = {0, 0, 0, 0};
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    float pred = margin[i];
-    if (obj != 0 && metric != 3) pred = 1.f / (1.f + expf(-pred));
+    const float* m = margin + (size_t)i * K;
+    const float sig = 1.f / (1.f + expf(-m[0]));
     float v;
-    if (metric == 0) { const float d = pred - y[i]; v = d * d; }
-    else if (metric == 1) v = fabsf(pred - y[i]);
-    else if (metric == 2) {
-      const float pc = fminf(fmaxf(pred, 1e-15f), 1.f - 1e-15f);
+    if (metric == 0 || metric == 1) {
+      const float d = ((objective == 1 || objective == 2) ? sig : m[0]) - y[i];
+      v = metric == 0 ? d * d : fabsf(d);
+    } else if (metric == 2) {
+      const float pc = fminf(fmaxf(sig, 1e-15f), 1.f - 1e-15f);
       v = -(y[i] * logf(pc) + (1.f - y[i]) * logf(1.f - pc));
+    } else if (metric == 3) {
+      const bool pos = (objective == 3) ? (m[0] > 0.f) : (sig > 0.5f);
+      v = (pos != (y[i] > 0.5f)) ? 1.f : 0.f;
     } else {
-      const float pp = (obj == 0) ? pred : 1.f / (1.f + expf(-pred));
-      v = ((pp > 0.5f) ? 1.f : 0.f) != (y[i] > 0.5f ? 1.f : 0.f) ? 1.f : 0.f;
+      int arg = 0;
+      float mx = m[0];
+      for (int k = 1; k < K; ++k) if (m[k] > mx) { mx = m[k]; arg = k; }
+      if (metric == 5) v = (arg != (int)y[i]) ? 1.f : 0.f;
+      else {
+        float z = 0.f;
+        for (int k = 0; k < K; ++k) z += expf(m[k] - mx);
+        v = -logf(fmaxf(1e-15f, expf(m[(int)y[i]] - mx) / z));
+      }
     }
     const int k = (fold_of[i] == fold) ? 2 : 0;
     s[k] += v; s[k + 1] += 1.0;
@@ -439,17 +467,22 @@ uint64_t smix(uint64_t x) {
 
 extern "C" {
 
-// Same contract as gbdt_cv (csrc/gbdt/engine.cpp) for objectives 0-3 and
-// metrics rmse/mae/logloss/error. bins: ROW-major [n][Fs] uint8 (Fs >= F,
+// Same contract as gbdt_cv (csrc/gbdt/engine.cpp) for every objective
+// (reg:linear/squarederror, reg:logistic, binary:logistic/logitraw,
+// multi:softmax/softprob: one tree per class) and every metric but auc
+// (rmse, mae, logloss, error, merror, mlogloss; early stopping on the last). bins: ROW-major [n][Fs] uint8 (Fs >= F,
 // Fs % 4 == 0), precomputed on the host. cache_key != 0 keeps the device copy
 // of the bins across calls for the same key (one dataset, many candidates).
 int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F, const float* y_h,
-                const int* fold_h, int nfold, const double* P, int objective, const int* metrics, int n_metrics,
-                int num_boost_round, int early_stopping_rounds, unsigned long long seed, long long cache_key,
-                double* out_hist) {
-  if (objective > 3 || n_metrics != 1 || metrics[0] > 3 || Fs % 4 || Fs < F || n <= 0) return -1;
+                const int* fold_h, int nfold, const double* P, int objective, int num_class, const int* metrics,
+                int n_metrics, int num_boost_round, int early_stopping_rounds, unsigned long long seed,
+                long long cache_key, double* out_hist) {
+  if (objective < 0 || objective > 5 || n_metrics < 1 || Fs % 4 || Fs < F || n <= 0 || nfold <= 0) return -1;
+  for (int mi = 0; mi < n_metrics; ++mi)
+    if (metrics[mi] < 0 || metrics[mi] > 6 || metrics[mi] == 4) return -1;   // auc: CPU engine
+  const bool multi = objective >= 4;
+  const int K = multi ? std::max(2, num_class) : 1;
   const int obj = objective == 0 ? 0 : (objective == 1 ? 1 : 2);
-  const int metric = metrics[0];
   const int max_depth = std::max(0, std::min((int)P[2], 12));
   static std::mutex mu;                    // one cv at a time per process (device bins cache)
   std::lock_guard<std::mutex> lock(mu);
@@ -481,7 +514,7 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   HC(hipMalloc(&d_y, sizeof(float) * n));
   HC(hipMalloc(&d_fold, sizeof(int) * n));
   for (int b = 0; b < 3; ++b) HC(hipMalloc(&d_rows[b], sizeof(int) * n));
-  HC(hipMalloc(&d_margin, sizeof(float) * (size_t)n * nfold));
+  HC(hipMalloc(&d_margin, sizeof(float) * (size_t)n * nfold * K));
   HC(hipMalloc(&d_gh, sizeof(float2) * n));
   for (int b = 0; b < 2; ++b) HC(hipMalloc(&d_hist[b], sizeof(float2) * (size_t)max_hist_nodes * hist_node));
   HC(hipMalloc(&d_tot, sizeof(float2) * max_level_nodes));
@@ -503,9 +536,12 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   HC(hipMemcpy(d_fold, fold_h, sizeof(int) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_nb, nbins_h, sizeof(int) * F, hipMemcpyHostToDevice));
   double base = P[11];
-  if (obj != 0) { const double b = std::min(1 - 1e-7, std::max(1e-7, P[11])); base = std::log(b / (1 - b)); }
+  if (objective == 1 || objective == 2) {   // engine.cpp: logit base margin for the logistic objectives only
+    const double b = std::min(1 - 1e-7, std::max(1e-7, P[11]));
+    base = std::log(b / (1 - b));
+  }
   {
-    std::vector<float> m((size_t)n * nfold, (float)base);
+    std::vector<float> m((size_t)n * nfold * K, (float)base);
     HC(hipMemcpy(d_margin, m.data(), sizeof(float) * m.size(), hipMemcpyHostToDevice));
   }
   DevParams dp{(float)P[1], (float)P[8], (float)P[9], (float)P[4]};
@@ -542,192 +578,208 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
     return std::chrono::duration<double>(now() - t).count();
   };
   for (int round = 0; round < num_boost_round; ++round) {
-    double trv[64], tev[64];
+    std::vector<double> trv((size_t)nfold * n_metrics), tev((size_t)nfold * n_metrics);
     for (int k = 0; k < nfold; ++k) {
       auto t0 = now();
       // same splitmix stream and draw order as the CPU engine (engine.cpp round_fold / build_tree)
       uint64_t rs = smix(seed ^ smix((uint64_t)k * 1000003ull + (uint64_t)round * 7919ull + 17));
       auto next = [&]() { rs = smix(rs); return rs; };
       auto uni = [&]() { return (next() >> 11) * (1.0 / 9007199254740992.0); };
-      const unsigned long long row_key = P[5] < 1.0 ? next() : 0ull;   // engine.cpp: one draw keys the rows
-      HC(hipMemsetAsync(d_count, 0, sizeof(int), 0));
-      hipLaunchKernelGGL(root_rows_kernel, dim3(blocks), dim3(256), 0, 0, d_fold, k, n, row_key, P[5], d_rows[0],
-                         d_count);
-      int nroot = 0;
-      HC(hipMemcpy(&nroot, d_count, sizeof(int), hipMemcpyDeviceToHost));
-      ph[0] += since(t0);
-      ph[5] += 1;
-      // colsample_bytree
-      std::vector<int> feats(F);
-      for (int f = 0; f < F; ++f) feats[f] = f;
-      if (P[6] < 1.0) {
-        const int kk = std::max(1, (int)std::floor(P[6] * F + 1e-9));
-        for (int i = 0; i < F; ++i) std::swap(feats[i], feats[i + (int)(next() % (uint64_t)(F - i))]);
-        feats.resize(kk);
-        std::sort(feats.begin(), feats.end());
-      }
-      float* margin = d_margin + (size_t)k * n;
-      hipLaunchKernelGGL(grad_kernel, dim3(blocks), dim3(256), 0, 0, margin, d_y, d_gh, n, obj, (float)P[10]);
-      HC(hipMemsetAsync(d_mx, 0, 2 * sizeof(unsigned int), 0));
-      hipLaunchKernelGGL(gh_max_kernel, dim3(std::min(blocks, 512)), dim3(256), 0, 0, d_gh, n, d_mx);
-      std::vector<int4> tree(1, make_int4(-1, 0, 0, 0));
-      std::vector<float> leaf(1, 0.f);
-      std::vector<Node> level(1, Node{0, 0, nroot, -1, 0.f, 0.f, true});
-      int rb = 0;                   // row-list buffer holding this level's segments
-      int hb = 0;                   // histogram buffer of this level
-      for (int depth = 0; depth <= max_depth && !level.empty(); ++depth) {
-        const int L = (int)level.size();
-        if (depth == max_depth && depth > 0) {   // deepest level: leaves only, totals from the parent splits
-          for (const Node& nd : level) leaf[nd.gnode] = (float)(h_weight(P, nd.G, nd.H) * P[0]);
-          break;
+      float* margin = d_margin + (size_t)k * n * K;
+      for (int c = 0; c < K; ++c) {     // one tree per class (engine.cpp round_fold), margins updated in turn
+        const unsigned long long row_key = P[5] < 1.0 ? next() : 0ull;   // engine.cpp: one draw keys the rows
+        HC(hipMemsetAsync(d_count, 0, sizeof(int), 0));
+        hipLaunchKernelGGL(root_rows_kernel, dim3(blocks), dim3(256), 0, 0, d_fold, k, n, row_key, P[5], d_rows[0],
+                           d_count);
+        int nroot = 0;
+        HC(hipMemcpy(&nroot, d_count, sizeof(int), hipMemcpyDeviceToHost));
+        ph[0] += since(t0);
+        ph[5] += 1;
+        // colsample_bytree
+        std::vector<int> feats(F);
+        for (int f = 0; f < F; ++f) feats[f] = f;
+        if (P[6] < 1.0) {
+          const int kk = std::max(1, (int)std::floor(P[6] * F + 1e-9));
+          for (int i = 0; i < F; ++i) std::swap(feats[i], feats[i + (int)(next() % (uint64_t)(F - i))]);
+          feats.resize(kk);
+          std::sort(feats.begin(), feats.end());
         }
-        // ---- histograms: built children over their rows, siblings by subtraction
-        auto t1 = now();
-        float2* hcur = d_hist[hb];
-        chunks.clear(); pairs.clear(); reds.clear();
-        long long built_rows = 0;
-        for (const Node& nd : level) if (nd.built) built_rows += nd.count;
-        const int R = std::max(2048, (int)((built_rows + 63) / 64));
-        int nslots = 0;
-        for (int j = 0; j < L; ++j) {
-          const Node& nd = level[j];
-          if (!nd.built) {
-            pairs.push_back(make_int4(j, nd.parent, j ^ 1, 0));   // siblings are adjacent (2i, 2i+1)
-          } else if (nd.count <= R) {                             // one chunk: written in place
-            chunks.push_back(make_int4(j, nd.start, nd.count, -1));
-          } else {                                                // partial slots + reduction
-            const int first = nslots;
-            for (int o = 0; o < nd.count; o += R)
-              chunks.push_back(make_int4(j, nd.start + o, std::min(R, nd.count - o), nslots++));
-            reds.push_back(make_int4(j, first, nslots - first, 0));
+        if (multi)
+          hipLaunchKernelGGL(grad_multi_kernel, dim3(blocks), dim3(256), 0, 0, margin, d_y, d_gh, n, K, c);
+        else
+          hipLaunchKernelGGL(grad_kernel, dim3(blocks), dim3(256), 0, 0, margin, d_y, d_gh, n, obj, (float)P[10]);
+        HC(hipMemsetAsync(d_mx, 0, 2 * sizeof(unsigned int), 0));
+        hipLaunchKernelGGL(gh_max_kernel, dim3(std::min(blocks, 512)), dim3(256), 0, 0, d_gh, n, d_mx);
+        std::vector<int4> tree(1, make_int4(-1, 0, 0, 0));
+        std::vector<float> leaf(1, 0.f);
+        std::vector<Node> level(1, Node{0, 0, nroot, -1, 0.f, 0.f, true});
+        int rb = 0;                   // row-list buffer holding this level's segments
+        int hb = 0;                   // histogram buffer of this level
+        for (int depth = 0; depth <= max_depth && !level.empty(); ++depth) {
+          const int L = (int)level.size();
+          if (depth == max_depth && depth > 0) {   // deepest level: leaves only, totals from the parent splits
+            for (const Node& nd : level) leaf[nd.gnode] = (float)(h_weight(P, nd.G, nd.H) * P[0]);
+            break;
           }
-        }
-        if ((int)chunks.size() > max_chunks || (int)reds.size() > max_chunks) return -3;
-        if (nslots > part_cap) {
-          if (d_part) (void)hipFree(d_part);
-          part_cap = std::max(nslots, 2 * part_cap);
-          HC(hipMalloc(&d_part, sizeof(unsigned long long) * 2 * (size_t)part_cap * hist_node));
-        }
-        if (!chunks.empty()) {
+          // ---- histograms: built children over their rows, siblings by subtraction
+          auto t1 = now();
+          float2* hcur = d_hist[hb];
+          chunks.clear(); pairs.clear(); reds.clear();
+          long long built_rows = 0;
+          for (const Node& nd : level) if (nd.built) built_rows += nd.count;
+          const int R = std::max(2048, (int)((built_rows + 63) / 64));
+          int nslots = 0;
+          for (int j = 0; j < L; ++j) {
+            const Node& nd = level[j];
+            if (!nd.built) {
+              pairs.push_back(make_int4(j, nd.parent, j ^ 1, 0));   // siblings are adjacent (2i, 2i+1)
+            } else if (nd.count <= R) {                             // one chunk: written in place
+              chunks.push_back(make_int4(j, nd.start, nd.count, -1));
+            } else {                                                // partial slots + reduction
+              const int first = nslots;
+              for (int o = 0; o < nd.count; o += R)
+                chunks.push_back(make_int4(j, nd.start + o, std::min(R, nd.count - o), nslots++));
+              reds.push_back(make_int4(j, first, nslots - first, 0));
+            }
+          }
+          if ((int)chunks.size() > max_chunks || (int)reds.size() > max_chunks) return -3;
+          if (nslots > part_cap) {
+            if (d_part) (void)hipFree(d_part);
+            part_cap = std::max(nslots, 2 * part_cap);
+            HC(hipMalloc(&d_part, sizeof(unsigned long long) * 2 * (size_t)part_cap * hist_node));
+          }
+          if (!chunks.empty()) {
+            HC(hipMemcpy(d_chunks, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(hist_kernel, dim3((unsigned)chunks.size(), nfb), dim3(HB_T), 0, 0, d_bins, Fs, F,
+                               d_rows[rb], d_gh, d_chunks, hcur, d_part, d_mx, lg_n);
+          }
+          if (!reds.empty()) {
+            HC(hipMemcpy(d_reds, reds.data(), sizeof(int4) * reds.size(), hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)reds.size(), std::max(1, (int)(hist_node * 2 / 4096))),
+                               dim3(256), 0, 0, d_part, reinterpret_cast<float*>(hcur), d_reds, F, d_mx, lg_n);
+          }
+          if (!pairs.empty()) {
+            HC(hipMemcpy(d_pairs, pairs.data(), sizeof(int4) * pairs.size(), hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(subtract_kernel, dim3((unsigned)pairs.size(), std::max(1, (int)(hist_node / 2048))),
+                               dim3(256), 0, 0, d_hist[hb ^ 1], hcur, d_pairs, F);
+          }
+          // ---- node totals: root from its histogram, children from the parent's split
+          if (depth == 0) {
+            hipLaunchKernelGGL(totals_kernel, dim3(1), dim3(64), 0, 0, hcur, d_tot, F);
+            float2 t0;
+            HC(hipMemcpy(&t0, d_tot, sizeof(float2), hipMemcpyDeviceToHost));
+            level[0].G = t0.x; level[0].H = t0.y;
+          } else {
+            tot.resize(L);
+            for (int j = 0; j < L; ++j) tot[j] = make_float2(level[j].G, level[j].H);
+            HC(hipMemcpy(d_tot, tot.data(), sizeof(float2) * L, hipMemcpyHostToDevice));
+          }
+          if (timing) { HC(hipDeviceSynchronize()); ph[1] += since(t1); t1 = now(); }
+          // ---- split search (colsample_bylevel draw as in the CPU engine)
+          std::fill(fok.begin(), fok.end(), 0);
+          std::vector<int> lf = feats;
+          if (P[7] < 1.0 && lf.size() > 1) {
+            const int m = (int)lf.size();
+            const int kk = std::max(1, (int)std::floor(P[7] * m + 1e-9));
+            for (int i = 0; i < m; ++i) std::swap(lf[i], lf[i + (int)(next() % (uint64_t)(m - i))]);
+            lf.resize(kk);
+          }
+          for (int f : lf) fok[f] = 1;
+          HC(hipMemcpy(d_fok, fok.data(), F, hipMemcpyHostToDevice));
+          hipLaunchKernelGGL(split_kernel, dim3(F, L), dim3(64), 0, 0, hcur, d_nb, d_fok, d_tot, d_cand, F, dp);
+          hipLaunchKernelGGL(best_kernel, dim3(L), dim3(256), 0, 0, d_cand, d_best, F);
+          HC(hipMemcpy(best.data(), d_best, sizeof(NodeBest) * L, hipMemcpyDeviceToHost));
+          if (timing) { ph[2] += since(t1); t1 = now(); }
+          // ---- host: leaves, gamma pruning, next level layout
+          split.assign(L, make_int2(-1, 0));
+          cur.assign(L, make_int2(0, 0));
+          chunks.clear();
+          std::vector<Node> nextl;
+          std::vector<int> split_of;       // level node -> index of its left child in nextl (or -1)
+          split_of.assign(L, -1);
+          for (int j = 0; j < L; ++j) {
+            Node& nd = level[j];
+            leaf[nd.gnode] = (float)(h_weight(P, nd.G, nd.H) * P[0]);
+            const NodeBest& b = best[j];
+            if (depth >= max_depth || b.feature < 0 || b.bin < 0 || b.gain < P[3] || b.gain <= 1e-12f ||
+                nd.count <= 0)
+              continue;
+            const int li = (int)tree.size();
+            tree.push_back(make_int4(-1, 0, 0, 0));
+            tree.push_back(make_int4(-1, 0, 0, 0));
+            leaf.push_back(0.f);
+            leaf.push_back(0.f);
+            tree[nd.gnode] = make_int4(b.feature, b.bin, li, li + 1);
+            split[j] = make_int2(b.feature, b.bin);
+            cur[j] = make_int2(nd.start, nd.start + nd.count);
+            split_of[j] = (int)nextl.size();
+            nextl.push_back(Node{li, nd.start, 0, j, b.GL, b.HL, false});
+            nextl.push_back(Node{li + 1, 0, 0, j, nd.G - b.GL, nd.H - b.HL, false});
+            add_chunks(chunks, j, nd.start, nd.count, 4096);
+          }
+          if (nextl.empty()) break;
+          if ((int)chunks.size() > max_chunks) return -3;
+          // ---- partition the split nodes' rows into the other row buffer
+          const int ob = (rb == 1) ? 2 : 1;
+          HC(hipMemcpy(d_split, split.data(), sizeof(int2) * L, hipMemcpyHostToDevice));
+          HC(hipMemcpy(d_cur, cur.data(), sizeof(int2) * L, hipMemcpyHostToDevice));
           HC(hipMemcpy(d_chunks, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice));
-          hipLaunchKernelGGL(hist_kernel, dim3((unsigned)chunks.size(), nfb), dim3(HB_T), 0, 0, d_bins, Fs, F,
-                             d_rows[rb], d_gh, d_chunks, hcur, d_part, d_mx, lg_n);
+          hipLaunchKernelGGL(partition_kernel, dim3((unsigned)chunks.size()), dim3(256), 0, 0, d_bins, Fs,
+                             d_rows[rb], d_rows[ob], d_chunks, d_split, d_cur);
+          HC(hipMemcpy(cur.data(), d_cur, sizeof(int2) * L, hipMemcpyDeviceToHost));
+          for (int j = 0; j < L; ++j) {
+            if (split_of[j] < 0) continue;
+            const Node& nd = level[j];
+            const int lc = cur[j].x - nd.start;
+            Node& l = nextl[split_of[j]];
+            Node& r = nextl[split_of[j] + 1];
+            l.count = lc;
+            r.start = nd.start + lc; r.count = nd.count - lc;
+            l.parent = r.parent = j;
+            (l.count <= r.count ? l : r).built = true;     // smaller child: histogram; sibling: subtraction
+          }
+          if (timing) ph[3] += since(t1);
+          level.swap(nextl);
+          rb = ob;
+          hb ^= 1;
         }
-        if (!reds.empty()) {
-          HC(hipMemcpy(d_reds, reds.data(), sizeof(int4) * reds.size(), hipMemcpyHostToDevice));
-          hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)reds.size(), std::max(1, (int)(hist_node * 2 / 4096))),
-                             dim3(256), 0, 0, d_part, reinterpret_cast<float*>(hcur), d_reds, F, d_mx, lg_n);
-        }
-        if (!pairs.empty()) {
-          HC(hipMemcpy(d_pairs, pairs.data(), sizeof(int4) * pairs.size(), hipMemcpyHostToDevice));
-          hipLaunchKernelGGL(subtract_kernel, dim3((unsigned)pairs.size(), std::max(1, (int)(hist_node / 2048))),
-                             dim3(256), 0, 0, d_hist[hb ^ 1], hcur, d_pairs, F);
-        }
-        // ---- node totals: root from its histogram, children from the parent's split
-        if (depth == 0) {
-          hipLaunchKernelGGL(totals_kernel, dim3(1), dim3(64), 0, 0, hcur, d_tot, F);
-          float2 t0;
-          HC(hipMemcpy(&t0, d_tot, sizeof(float2), hipMemcpyDeviceToHost));
-          level[0].G = t0.x; level[0].H = t0.y;
-        } else {
-          tot.resize(L);
-          for (int j = 0; j < L; ++j) tot[j] = make_float2(level[j].G, level[j].H);
-          HC(hipMemcpy(d_tot, tot.data(), sizeof(float2) * L, hipMemcpyHostToDevice));
-        }
-        if (timing) { HC(hipDeviceSynchronize()); ph[1] += since(t1); t1 = now(); }
-        // ---- split search (colsample_bylevel draw as in the CPU engine)
-        std::fill(fok.begin(), fok.end(), 0);
-        std::vector<int> lf = feats;
-        if (P[7] < 1.0 && lf.size() > 1) {
-          const int m = (int)lf.size();
-          const int kk = std::max(1, (int)std::floor(P[7] * m + 1e-9));
-          for (int i = 0; i < m; ++i) std::swap(lf[i], lf[i + (int)(next() % (uint64_t)(m - i))]);
-          lf.resize(kk);
-        }
-        for (int f : lf) fok[f] = 1;
-        HC(hipMemcpy(d_fok, fok.data(), F, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(split_kernel, dim3(F, L), dim3(64), 0, 0, hcur, d_nb, d_fok, d_tot, d_cand, F, dp);
-        hipLaunchKernelGGL(best_kernel, dim3(L), dim3(256), 0, 0, d_cand, d_best, F);
-        HC(hipMemcpy(best.data(), d_best, sizeof(NodeBest) * L, hipMemcpyDeviceToHost));
-        if (timing) { ph[2] += since(t1); t1 = now(); }
-        // ---- host: leaves, gamma pruning, next level layout
-        split.assign(L, make_int2(-1, 0));
-        cur.assign(L, make_int2(0, 0));
-        chunks.clear();
-        std::vector<Node> nextl;
-        std::vector<int> split_of;       // level node -> index of its left child in nextl (or -1)
-        split_of.assign(L, -1);
-        for (int j = 0; j < L; ++j) {
-          Node& nd = level[j];
-          leaf[nd.gnode] = (float)(h_weight(P, nd.G, nd.H) * P[0]);
-          const NodeBest& b = best[j];
-          if (depth >= max_depth || b.feature < 0 || b.bin < 0 || b.gain < P[3] || b.gain <= 1e-12f ||
-              nd.count <= 0)
-            continue;
-          const int li = (int)tree.size();
-          tree.push_back(make_int4(-1, 0, 0, 0));
-          tree.push_back(make_int4(-1, 0, 0, 0));
-          leaf.push_back(0.f);
-          leaf.push_back(0.f);
-          tree[nd.gnode] = make_int4(b.feature, b.bin, li, li + 1);
-          split[j] = make_int2(b.feature, b.bin);
-          cur[j] = make_int2(nd.start, nd.start + nd.count);
-          split_of[j] = (int)nextl.size();
-          nextl.push_back(Node{li, nd.start, 0, j, b.GL, b.HL, false});
-          nextl.push_back(Node{li + 1, 0, 0, j, nd.G - b.GL, nd.H - b.HL, false});
-          add_chunks(chunks, j, nd.start, nd.count, 4096);
-        }
-        if (nextl.empty()) break;
-        if ((int)chunks.size() > max_chunks) return -3;
-        // ---- partition the split nodes' rows into the other row buffer
-        const int ob = (rb == 1) ? 2 : 1;
-        HC(hipMemcpy(d_split, split.data(), sizeof(int2) * L, hipMemcpyHostToDevice));
-        HC(hipMemcpy(d_cur, cur.data(), sizeof(int2) * L, hipMemcpyHostToDevice));
-        HC(hipMemcpy(d_chunks, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(partition_kernel, dim3((unsigned)chunks.size()), dim3(256), 0, 0, d_bins, Fs,
-                           d_rows[rb], d_rows[ob], d_chunks, d_split, d_cur);
-        HC(hipMemcpy(cur.data(), d_cur, sizeof(int2) * L, hipMemcpyDeviceToHost));
-        for (int j = 0; j < L; ++j) {
-          if (split_of[j] < 0) continue;
-          const Node& nd = level[j];
-          const int lc = cur[j].x - nd.start;
-          Node& l = nextl[split_of[j]];
-          Node& r = nextl[split_of[j] + 1];
-          l.count = lc;
-          r.start = nd.start + lc; r.count = nd.count - lc;
-          l.parent = r.parent = j;
-          (l.count <= r.count ? l : r).built = true;     // smaller child: histogram; sibling: subtraction
-        }
-        if (timing) ph[3] += since(t1);
-        level.swap(nextl);
-        rb = ob;
-        hb ^= 1;
+        auto t4 = now();
+        HC(hipMemcpy(d_tree, tree.data(), sizeof(int4) * tree.size(), hipMemcpyHostToDevice));
+        HC(hipMemcpy(d_leaf, leaf.data(), sizeof(float) * leaf.size(), hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(predict_kernel, dim3(blocks), dim3(256), 0, 0, d_bins, Fs, d_tree, d_leaf, margin, n, K, c);
       }
       auto t4 = now();
-      HC(hipMemcpy(d_tree, tree.data(), sizeof(int4) * tree.size(), hipMemcpyHostToDevice));
-      HC(hipMemcpy(d_leaf, leaf.data(), sizeof(float) * leaf.size(), hipMemcpyHostToDevice));
-      hipLaunchKernelGGL(predict_kernel, dim3(blocks), dim3(256), 0, 0, d_bins, Fs, d_tree, d_leaf, margin, n);
       const int mblocks = std::min(blocks, 1024);
-      hipLaunchKernelGGL(metric_kernel, dim3(mblocks), dim3(256), 0, 0, margin, d_y, d_fold, k, n, metric, obj,
-                         d_met);
       std::vector<double> mpart((size_t)mblocks * 4);
-      HC(hipMemcpy(mpart.data(), d_met, sizeof(double) * mpart.size(), hipMemcpyDeviceToHost));
-      double met[4] = {0, 0, 0, 0};
-      for (int b = 0; b < mblocks; ++b)
-        for (int q = 0; q < 4; ++q) met[q] += mpart[(size_t)b * 4 + q];
-      double tr = met[0] / std::max(1.0, met[1]), te = met[2] / std::max(1.0, met[3]);
-      if (metric == 0) { tr = std::sqrt(tr); te = std::sqrt(te); }
-      trv[k] = tr; tev[k] = te;
+      for (int mi = 0; mi < n_metrics; ++mi) {
+        const int metric = metrics[mi];
+        hipLaunchKernelGGL(metric_kernel, dim3(mblocks), dim3(256), 0, 0, margin, d_y, d_fold, k, n, metric,
+                           objective, K, d_met);
+        HC(hipMemcpy(mpart.data(), d_met, sizeof(double) * mpart.size(), hipMemcpyDeviceToHost));
+        double met[4] = {0, 0, 0, 0};
+        for (int b = 0; b < mblocks; ++b)
+          for (int q = 0; q < 4; ++q) met[q] += mpart[(size_t)b * 4 + q];
+        double tr = met[0] / std::max(1.0, met[1]), te = met[2] / std::max(1.0, met[3]);
+        if (metric == 0) { tr = std::sqrt(tr); te = std::sqrt(te); }
+        trv[k * n_metrics + mi] = tr; tev[k * n_metrics + mi] = te;
+      }
       ph[4] += since(t4);
     }
-    double trm = 0, tem = 0, trs = 0, tes = 0;
-    for (int k = 0; k < nfold; ++k) { trm += trv[k]; tem += tev[k]; }
-    trm /= nfold; tem /= nfold;
-    for (int k = 0; k < nfold; ++k) { trs += (trv[k] - trm) * (trv[k] - trm); tes += (tev[k] - tem) * (tev[k] - tem); }
-    double* o = &out_hist[(size_t)round * 4];
-    o[0] = trm; o[1] = std::sqrt(trs / nfold); o[2] = tem; o[3] = std::sqrt(tes / nfold);
+    double tem_last = 0;
+    for (int mi = 0; mi < n_metrics; ++mi) {
+      double trm = 0, tem = 0, trs = 0, tes = 0;
+      for (int k = 0; k < nfold; ++k) { trm += trv[k * n_metrics + mi]; tem += tev[k * n_metrics + mi]; }
+      trm /= nfold; tem /= nfold;
+      for (int k = 0; k < nfold; ++k) {
+        const double a = trv[k * n_metrics + mi] - trm, b = tev[k * n_metrics + mi] - tem;
+        trs += a * a; tes += b * b;
+      }
+      double* o = &out_hist[((size_t)round * n_metrics + mi) * 4];
+      o[0] = trm; o[1] = std::sqrt(trs / nfold); o[2] = tem; o[3] = std::sqrt(tes / nfold);
+      tem_last = tem;                  // early stopping on the last metric (engine.cpp)
+    }
     rounds_done = round + 1;
-    if (lower_better ? tem < best_score : tem > best_score) { best_score = tem; best_round = round; }
+    if (lower_better ? tem_last < best_score : tem_last > best_score) { best_score = tem_last; best_round = round; }
     if (early_stopping_rounds > 0 && round - best_round >= early_stopping_rounds) break;
   }
   if (timing)

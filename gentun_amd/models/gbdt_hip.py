@@ -2,9 +2,8 @@
 predict kernels on the GPU (csrc/hip/gbdt_hist.hip: row-major bins, per-node
 row segments, smaller-child histograms + subtraction). Used by
 :func:`gentun_amd.models.gbdt.cv` when ``device`` is a CUDA/HIP device;
-objectives reg:linear/squarederror, reg:logistic, binary:logistic and the
-rmse/mae/logloss/error metrics run on the GPU, anything else falls back to
-the CPU engine."""
+every objective (regression, logistic, binary, multi-class) and every metric
+but auc run on the GPU; auc falls back to the CPU engine."""
 
 import ctypes
 
@@ -12,12 +11,12 @@ import numpy as np
 
 from ..ops import _lib
 
-GPU_OBJECTIVES = (0, 1, 2)
-GPU_METRICS = (0, 1, 2, 3)
+GPU_OBJECTIVES = (0, 1, 2, 3, 4, 5)      # every objective of models/gbdt.py OBJECTIVES
+GPU_METRICS = (0, 1, 2, 3, 5, 6)         # all but auc (a sort per fold: CPU engine)
 
 
 def supported(obj, metrics):
-    return obj in GPU_OBJECTIVES and len(metrics) == 1 and int(metrics[0]) in GPU_METRICS
+    return obj in GPU_OBJECTIVES and len(metrics) >= 1 and all(int(m) in GPU_METRICS for m in metrics)
 
 
 def _fn():
@@ -26,8 +25,8 @@ def _fn():
     if not getattr(f, "_typed", False):
         c = ctypes
         f.argtypes = [c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_void_p, c.c_int,
-                      c.c_void_p, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_ulonglong, c.c_longlong,
-                      c.c_void_p]
+                      c.c_void_p, c.c_int, c.c_int, c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_ulonglong,
+                      c.c_longlong, c.c_void_p]
         f.restype = c.c_int
         f._typed = True
     return f
@@ -69,6 +68,7 @@ def cv(x, y, fold_of, nfold, parr, obj, num_class, marr, nrounds, esr, seed, his
     y = np.ascontiguousarray(y.astype(np.float32))
     marr = np.ascontiguousarray(marr.astype(np.int32))
     kept = _fn()(bins.ctypes.data, bins.shape[1], nb.ctypes.data, x.shape[0], x.shape[1], y.ctypes.data,
-                 fold_of.ctypes.data, int(nfold), parr.ctypes.data, int(obj), marr.ctypes.data, len(marr),
+                 fold_of.ctypes.data, int(nfold), parr.ctypes.data, int(obj), int(num_class), marr.ctypes.data,
+                 len(marr),
                  int(nrounds), int(esr), ctypes.c_ulonglong(seed & 0xFFFFFFFFFFFFFFFF), key, hist.ctypes.data)
     return kept

@@ -65,3 +65,31 @@ def test_hip_bins_cache_reused_and_bitwise_deterministic():
     second = gbdt.cv(p, x, y, num_boost_round=10, nfold=2, seed=0, device="cuda:0")
     assert gbdt_hip.quantize_rm(x)[2] == gbdt_hip.quantize_rm(x)[2]
     assert first == second
+
+
+@pytest.mark.parametrize("obj", ["multi:softprob", "multi:softmax"])
+def test_hip_multiclass_matches_cpu(obj):
+    """One tree per class per round on the GPU (K softmax gradients), merror
+    and mlogloss reported together, early stopping on the last metric."""
+    x, y = load_iris_xy()
+    p = {'objective': obj, 'num_class': 3, 'eval_metric': ['merror', 'mlogloss'], 'max_depth': 3, 'eta': 0.3}
+    cpu = gbdt.cv(p, x, y, num_boost_round=60, nfold=5, early_stopping_rounds=10, seed=0)
+    gpu = gbdt.cv(p, x, y, num_boost_round=60, nfold=5, early_stopping_rounds=10, seed=0, device="cuda:0")
+    assert set(gpu) == set(cpu)
+    assert abs(cpu['test-mlogloss-mean'][-1] - gpu['test-mlogloss-mean'][-1]) < 0.03
+    assert abs(cpu['test-merror-mean'][-1] - gpu['test-merror-mean'][-1]) < 0.03
+    assert gpu['test-mlogloss-mean'][-1] == min(gpu['test-mlogloss-mean'])
+
+
+def test_hip_logitraw_and_metric_semantics():
+    """binary:logitraw (margin threshold 0 for error, raw margin for rmse) and
+    logloss on a squared-error model, as the CPU engine defines them."""
+    x, y = load_iris_xy()
+    yb = (y == 1).astype(np.float64)
+    for p in ({'objective': 'binary:logitraw', 'eval_metric': ['rmse', 'error'], 'max_depth': 2},
+              {'objective': 'reg:linear', 'eval_metric': ['mae', 'logloss'], 'max_depth': 3}):
+        cpu = gbdt.cv(p, x, yb, num_boost_round=20, nfold=3, seed=0)
+        gpu = gbdt.cv(p, x, yb, num_boost_round=20, nfold=3, seed=0, device="cuda:0")
+        for k in cpu:
+            a, b = np.array(cpu[k]), np.array(gpu[k])
+            assert np.max(np.abs(a - b)) < 0.02 + 0.02 * np.max(np.abs(a)), (p, k, a[-3:], b[-3:])
