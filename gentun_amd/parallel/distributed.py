@@ -147,6 +147,7 @@ def evaluate_units(units, evaluator, nfold, rank, generation):
     for ui, u in source:
         t0 = time.perf_counter()
         try:
+            _localize_device(u.ind, evaluator)
             u.ind.evaluate_fitness()
             scores = u.ind.fold_scores or []
             rows[ui] = _row(ST_OK, u.ind.fitness, time.perf_counter() - t0, scores, nfold, u.fold_ids)
@@ -520,6 +521,16 @@ def _comm_from_args(host, port):
     if port != 5672:
         os.environ.setdefault("MASTER_PORT", str(port))
     return from_env()
+
+
+def _localize_device(ind, evaluator):
+    """A GPU-requesting individual (e.g. ``XgboostIndividual(device='cuda:0')``,
+    whose additional parameters come from rank 0's broadcast) runs on the GPU
+    of the rank evaluating it, not on rank 0's device."""
+    dev = getattr(evaluator, "device", None)
+    want = getattr(ind, "device", None)
+    if dev is not None and want is not None and str(want).startswith("cuda") and str(dev).startswith("cuda"):
+        ind.device = str(dev)
 
 
 def _device_sync(evaluator):

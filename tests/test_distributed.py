@@ -242,3 +242,20 @@ def test_auto_schedule_follows_the_evaluator():
     mk = lambda ev: DistributedPopulation(BitIndividual, None, None, size=6, comm=LocalComm(), evaluator=ev)
     assert mk(LocalBatchEvaluator(device=torch.device("cpu"), pop_batch=16)).schedule == "lpt"
     assert mk(SequentialEvaluator()).schedule == "dynamic"
+
+
+def test_gpu_individual_runs_on_evaluating_rank_device():
+    """Additional parameters come from rank 0's broadcast, so an XGB
+    individual asking for 'cuda:0' must be moved to the evaluating rank's GPU."""
+    from types import SimpleNamespace
+    from gentun_amd.parallel.distributed import _localize_device
+    ev = SimpleNamespace(device="cuda:3")
+    ind = SimpleNamespace(device="cuda:0")
+    _localize_device(ind, ev)
+    assert ind.device == "cuda:3"
+    cpu_ind = SimpleNamespace(device=None)
+    _localize_device(cpu_ind, ev)
+    assert cpu_ind.device is None
+    ind2 = SimpleNamespace(device="cuda:0")
+    _localize_device(ind2, SimpleNamespace(device="cpu"))
+    assert ind2.device == "cuda:0"
