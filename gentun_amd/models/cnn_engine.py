@@ -268,9 +268,15 @@ class FoldJob(object):
     def launch(self):
         use_graph = self.cfg.use_graph and self.device.type == "cuda" and getattr(self, "capture_ok", True)
         ctx = torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
+        timed = self.device.type == "cuda"
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
         with ctx:
+            if timed:
+                ev[0].record()
             self.init_params()
             graph = self._capture() if use_graph else None
+            if timed:
+                ev[1].record()
             for epochs, lr in zip(self.cfg.epochs, self.cfg.learning_rate):
                 self.reset_optimizer(lr)
                 for _ in range(epochs):
@@ -280,17 +286,29 @@ class FoldJob(object):
                             graph.replay()
                         else:
                             self.train_step()
+            if timed:
+                ev[2].record()
             self._graph = graph
             self._eval = self.evaluate()
+            if timed:
+                ev[3].record()
             if self.stream is not None:
                 self._done = torch.cuda.Event()
                 self._done.record(self.stream)
+        self._phase_events = ev
         return self
 
     def finish(self):
         if getattr(self, "_done", None) is not None:
             self._done.synchronize()
         loss, binc, catc = (t.detach().float().cpu().numpy() for t in self._eval)
+        ev = getattr(self, "_phase_events", None)
+        if ev is not None:
+            # device time per phase (HIP events on the job's stream)
+            ev[3].synchronize()
+            self.phase_ms = {"init_capture": ev[0].elapsed_time(ev[1]), "train": ev[1].elapsed_time(ev[2]),
+                             "eval": ev[2].elapsed_time(ev[3])}
+            self._phase_events = None
         nval = np.asarray(self.nval, np.float64)
         per = {
             "val_loss": (loss / nval).tolist(),

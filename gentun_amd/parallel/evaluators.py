@@ -54,7 +54,8 @@ class SequentialEvaluator(object):
     def _log(self, ind, wall):
         if self.event_log is not None:
             self.event_log.write("evaluation", genes=ind.get_genes(), fitness=ind.fitness,
-                                 fold_scores=ind.fold_scores, wall_s=wall)
+                                 fold_scores=ind.fold_scores, wall_s=wall,
+                                 phase_ms=getattr(ind, "phase_ms", None))
 
 
 class LocalBatchEvaluator(SequentialEvaluator):
@@ -141,7 +142,9 @@ def run_cnn_units(units, evaluator, done):
         res = job.finish()
         res = res if multi else [res]
         wall = time.perf_counter() - t0
+        phase = getattr(job, "phase_ms", None) or _merge_phases(getattr(job, "jobs", ()))
         for (ind, model, tag), r in zip(items, res):
+            ind.phase_ms = phase            # device ms per phase of the (shared) job
             done(ind, model, r, wall, tag)
 
     pending = []
@@ -198,6 +201,14 @@ def run_cnn_units(units, evaluator, done):
             window.append((_MultiJob(jobs), [(ind, model, tag)], t0, False))
     for entry in window:
         retire(entry)
+
+
+def _merge_phases(jobs):
+    out = {}
+    for j in jobs:
+        for k, v in (getattr(j, "phase_ms", None) or {}).items():
+            out[k] = out.get(k, 0.0) + v
+    return out or None
 
 
 class _MultiJob(object):

@@ -90,3 +90,16 @@ def test_population_batch_invariance():
     for i in range(3):
         assert pop[i] == alone[i], (i, pop[i], alone[i])
     assert pop[3]["val_loss"] == [alone[3]["val_loss"][2], alone[3]["val_loss"][0]]
+
+
+def test_job_phase_timers():
+    """HIP events around init/capture, training and evaluation of a job
+    (SURVEY.md §5.1 per-phase device timers)."""
+    from gentun_amd.models import cnn_engine as E
+    x, y, folds, plan = _setup(n=300)
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce")
+    job = E.make_job("hip", plan, x, y, folds, cfg, torch.device("cuda", 0))
+    job.launch()
+    job.finish()
+    assert set(job.phase_ms) == {"init_capture", "train", "eval"}
+    assert job.phase_ms["train"] > 0 and job.phase_ms["eval"] > 0
