@@ -149,7 +149,8 @@ def run(args):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (CIFAR-10-shaped 10k x 32x32x3 coloured stroke glyphs + clutter + noise; random-init weights)",
+        "data": "synthetic (CIFAR-10-shaped {}k x 32x32x3 coloured stroke glyphs + clutter + noise; "
+                "random-init weights)".format(args.samples // 1000),
         "config": {"model": "Genetic-CNN {} dense 500".format(space), "global_batch": 32 * args.nfold,
                    "seq_len": None, "parallelism": "population-dp{}".format(comm.world_size),
                    "candidates_per_step": P, "per_gpu": args.per_gpu, "nfold": args.nfold,
