@@ -36,6 +36,8 @@
 #include <mutex>
 #include <vector>
 
+#include "gbdt_cache.h"
+
 #define GB_BINS 256
 #define HB_F 16          // features per histogram workgroup
 #define HB_STRIDE 514    // int64 per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
@@ -465,12 +467,21 @@ uint64_t smix(uint64_t x) {
 
 }  // namespace
 
+namespace gbdt_cache {
+uint8_t* bins = nullptr;
+long long key = 0;
+size_t bytes = 0;
+std::mutex mu;
+}  // namespace gbdt_cache
+
 extern "C" {
 
 // Same contract as gbdt_cv (csrc/gbdt/engine.cpp) for every objective
 // (reg:linear/squarederror, reg:logistic, binary:logistic/logitraw,
 // multi:softmax/softprob: one tree per class) and every metric but auc
-// (rmse, mae, logloss, error, merror, mlogloss; early stopping on the last). bins: ROW-major [n][Fs] uint8 (Fs >= F,
+// (rmse, mae, logloss, error, merror, mlogloss; early stopping on the last).
+// bins_h may be null when gbdt_quantize_hip already left the dataset's bins
+// on the device under cache_key (returns -7 if they were evicted). bins: ROW-major [n][Fs] uint8 (Fs >= F,
 // Fs % 4 == 0), precomputed on the host. cache_key != 0 keeps the device copy
 // of the bins across calls for the same key (one dataset, many candidates).
 int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F, const float* y_h,
@@ -484,21 +495,18 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   const int K = multi ? std::max(2, num_class) : 1;
   const int obj = objective == 0 ? 0 : (objective == 1 ? 1 : 2);
   const int max_depth = std::max(0, std::min((int)P[2], 12));
-  static std::mutex mu;                    // one cv at a time per process (device bins cache)
-  std::lock_guard<std::mutex> lock(mu);
+  std::lock_guard<std::mutex> lock(gbdt_cache::mu);   // one GBDT call at a time per process (bins cache)
   // ---- device buffers
-  static uint8_t* c_bins = nullptr;        // cached bins (cache_key)
-  static long long c_key = 0;
-  static size_t c_bytes = 0;
   const size_t nbytes = (size_t)n * Fs;
-  if (cache_key == 0 || cache_key != c_key || c_bytes != nbytes || c_bins == nullptr) {
-    if (c_bins) (void)hipFree(c_bins);
-    c_bins = nullptr; c_key = 0; c_bytes = 0;
-    HC(hipMalloc(&c_bins, nbytes));
-    HC(hipMemcpy(c_bins, bins_h, nbytes, hipMemcpyHostToDevice));
-    c_key = cache_key; c_bytes = nbytes;
+  if (cache_key == 0 || cache_key != gbdt_cache::key || gbdt_cache::bytes != nbytes || gbdt_cache::bins == nullptr) {
+    if (bins_h == nullptr) return -7;      // device copy evicted: the caller quantises again
+    if (gbdt_cache::bins) (void)hipFree(gbdt_cache::bins);
+    gbdt_cache::bins = nullptr; gbdt_cache::key = 0; gbdt_cache::bytes = 0;
+    HC(hipMalloc(&gbdt_cache::bins, nbytes));
+    HC(hipMemcpy(gbdt_cache::bins, bins_h, nbytes, hipMemcpyHostToDevice));
+    gbdt_cache::key = cache_key; gbdt_cache::bytes = nbytes;
   }
-  const uint8_t* d_bins = c_bins;
+  const uint8_t* d_bins = gbdt_cache::bins;
   float *d_y, *d_margin, *d_leaf;
   int *d_fold, *d_nb, *d_rows[3];
   float2 *d_gh, *d_hist[2], *d_tot;

@@ -60,15 +60,71 @@ def quantize_rm(x):
     return b, nb, _KEYS[0]
 
 
+_DCACHE = []      # (x object, shape, nbins, key): datasets quantised on the device (G1 kernels)
+
+
+def _qfn():
+    L = _lib.hip()
+    f = L.gbdt_quantize_hip
+    if not getattr(f, "_typed", False):
+        c = ctypes
+        f.argtypes = [c.c_void_p, c.c_int, c.c_int, c.c_int, c.c_longlong, c.c_void_p]
+        f.restype = c.c_int
+        L.gbdt_bins_hip_copy.argtypes = [c.c_longlong, c.c_void_p, c.c_size_t]
+        L.gbdt_bins_hip_copy.restype = c.c_int
+        f._typed = True
+    return f
+
+
+def quantize_device(x, force=False, ident=None):
+    """Quantise ``x`` on the GPU (gbdt_quant.hip: transpose, segmented radix
+    sort, cuts, binary-search binning; bit-identical to the CPU engine) into
+    the device bins cache. Returns ``(nbins, key, Fs)``; cached per dataset
+    object (``ident``, default ``x``)."""
+    ident = x if ident is None else ident
+    if not force:
+        for ent in _DCACHE:
+            if ent[0] is ident and ent[1] == x.shape:
+                return ent[2], ent[3], ent[4]
+    xc = np.ascontiguousarray(x, dtype=np.float32)
+    n, f = xc.shape
+    fs = (f + 3) // 4 * 4
+    nb = np.zeros(f, np.int32)
+    _KEYS[0] += 1
+    key = _KEYS[0]
+    rc = _qfn()(xc.ctypes.data, n, f, fs, key, nb.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("gbdt_quantize_hip failed ({})".format(rc))
+    _DCACHE[:] = [e for e in _DCACHE if not (e[0] is ident)]
+    _DCACHE.append((ident, x.shape, nb, key, fs))
+    while len(_DCACHE) > 2:
+        _DCACHE.pop(0)
+    return nb, key, fs
+
+
+def device_bins(x, key, fs):
+    """Copy of the device-resident bins of ``key`` (tests / debugging)."""
+    out = np.zeros((x.shape[0], fs), np.uint8)
+    _qfn()
+    rc = _lib.hip().gbdt_bins_hip_copy(key, out.ctypes.data, out.nbytes)
+    if rc != 0:
+        raise RuntimeError("bins of key {} not resident ({})".format(key, rc))
+    return out
+
+
 def cv(x, y, fold_of, nfold, parr, obj, num_class, marr, nrounds, esr, seed, hist, x_key=None):
     if not supported(obj, marr):
         return None
-    bins, nb, key = quantize_rm(x if x_key is None else x_key)
+    xk = x if x_key is None else x_key
     fold_of = np.ascontiguousarray(fold_of.astype(np.int32))
     y = np.ascontiguousarray(y.astype(np.float32))
     marr = np.ascontiguousarray(marr.astype(np.int32))
-    kept = _fn()(bins.ctypes.data, bins.shape[1], nb.ctypes.data, x.shape[0], x.shape[1], y.ctypes.data,
-                 fold_of.ctypes.data, int(nfold), parr.ctypes.data, int(obj), int(num_class), marr.ctypes.data,
-                 len(marr),
-                 int(nrounds), int(esr), ctypes.c_ulonglong(seed & 0xFFFFFFFFFFFFFFFF), key, hist.ctypes.data)
+    for attempt in (0, 1):
+        nb, key, fs = quantize_device(x, force=attempt > 0, ident=xk)
+        kept = _fn()(None, fs, nb.ctypes.data, x.shape[0], x.shape[1], y.ctypes.data,
+                     fold_of.ctypes.data, int(nfold), parr.ctypes.data, int(obj), int(num_class), marr.ctypes.data,
+                     len(marr), int(nrounds), int(esr), ctypes.c_ulonglong(seed & 0xFFFFFFFFFFFFFFFF), key,
+                     hist.ctypes.data)
+        if kept != -7:                       # -7: another dataset evicted the device bins
+            return kept
     return kept

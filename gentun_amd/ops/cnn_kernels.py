@@ -171,6 +171,8 @@ def wgrad_blocks(kdim, with_bias=True):
 
 WGRAD_TARGET_BLOCKS = int(__import__("os").environ.get("GENTUN_WGRAD_TARGET", "50"))
 WGRAD_FAST_SPLITS = int(__import__("os").environ.get("GENTUN_WGRAD_SPLITS", "0"))   # 0: per-shape default
+WGRAD_SPLITS_BY_WIDTH = {int(k): int(v) for k, v in (kv.split(":") for kv in
+                         __import__("os").environ.get("GENTUN_WGRAD_SPLITS_W", "").split(",") if kv)}
 
 
 def wgrad_band(KH, KW, cinp, coutp, H, W):
@@ -181,7 +183,10 @@ def wgrad_band(KH, KW, cinp, coutp, H, W):
         L.gt_conv_set_fast(0)
         return 0, 0
     band = int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W))
-    return band, (int(L.gt_wgrad_fast_splits(KH, KW, cinp, coutp, H, W)) if band else 0)
+    splits = int(L.gt_wgrad_fast_splits(KH, KW, cinp, coutp, H, W)) if band else 0
+    if band and W in WGRAD_SPLITS_BY_WIDTH:
+        splits = WGRAD_SPLITS_BY_WIDTH[W]      # tuning override (GENTUN_WGRAD_SPLITS_W="16:8,32:16")
+    return band, splits
 
 
 def wgrad_split(npix, kdim, coutp, G=None, target_blocks=None, band=0):

@@ -93,3 +93,25 @@ def test_hip_logitraw_and_metric_semantics():
         for k in cpu:
             a, b = np.array(cpu[k]), np.array(gpu[k])
             assert np.max(np.abs(a - b)) < 0.02 + 0.02 * np.max(np.abs(a)), (p, k, a[-3:], b[-3:])
+
+
+def test_device_quantisation_bit_identical_to_cpu_engine():
+    """G1 on the GPU (transpose + segmented radix sort + cuts + binning) gives
+    exactly the CPU engine's bins: NaN -> lowest bin, few-valued columns,
+    signed zeros, a constant column, > 256 distinct values (quantile cuts)."""
+    from gentun_amd.models import gbdt_hip
+    rng = np.random.default_rng(11)
+    n = 5003
+    x = rng.standard_normal((n, 9)).astype(np.float32)
+    x[:, 1] = np.round(x[:, 1] * 2)                       # few distinct values
+    x[rng.random(n) < 0.05, 2] = np.nan
+    x[:, 3] = 0.0
+    x[::2, 3] = -0.0                                     # signed zeros, one value
+    x[:, 4] = 7.0                                        # constant
+    x[:, 5] = rng.integers(0, 300, n)                    # 300 distinct -> quantile cuts
+    b_cpu, nb_cpu = gbdt.quantize(x)
+    nb, key, fs = gbdt_hip.quantize_device(x, force=True)
+    b_gpu = gbdt_hip.device_bins(x, key, fs)
+    assert fs == 12 and not b_gpu[:, 9:].any()
+    np.testing.assert_array_equal(nb, nb_cpu)
+    np.testing.assert_array_equal(b_gpu[:, :9], b_cpu)

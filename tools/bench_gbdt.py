@@ -42,7 +42,7 @@ t_prep = 0.0
 if args.device != "cpu":
     # per-dataset quantisation (cached for every later candidate): timed inside eval_s, also reported alone
     from gentun_amd.models import gbdt_hip  # noqa: E402
-    gbdt_hip.quantize_rm(x)
+    gbdt_hip.quantize_device(x)
     t_prep = time.perf_counter() - t0
 best = pop.get_fittest()
 dt = time.perf_counter() - t0

@@ -15,7 +15,7 @@ depth = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 rounds = int(sys.argv[4]) if len(sys.argv) > 4 else 5
 sub = float(sys.argv[5]) if len(sys.argv) > 5 else 1.0
 x, y = make_regression(n=n, f=f, seed=0)
-gbdt_hip.quantize_rm(x)
+gbdt_hip.quantize_device(x)
 p = {'objective': 'reg:linear', 'eta': 0.3, 'max_depth': depth, 'subsample': sub, 'min_child_weight': 1}
 gbdt.cv(p, x, y, num_boost_round=1, nfold=5, seed=0, device="cuda:0")          # warm-up
 t0 = time.perf_counter()
