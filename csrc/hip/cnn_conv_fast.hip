@@ -59,7 +59,7 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int NKS = (NCH + 3) / 4;                // k-steps (32 k each)
   constexpr int TP = TH * W;                        // tile pixels
   constexpr int NPG = TP / 16;                      // pixel groups
-  constexpr int CT = NT >= 2 ? 2 : 1;               // co tiles per wave
+  constexpr int CT = (NT >= 2 && NT % 2 == 0) ? 2 : 1;   // co tiles per wave (odd NT: one per wave)
   constexpr int WC = NT / CT;                       // waves along co
   constexpr int WP = NWV / WC;                        // waves along pixels
   constexpr int PG = NPG / WP;                      // pixel groups per wave
@@ -362,6 +362,10 @@ extern "C" int gt_conv_set_nwv(int n) {
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 4)                                            \
   }
 
+// odd tile counts (104 channels = 7 x 16): one co tile per wave, NT waves
+#define CONV_FAST_CASE_NW(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                      \
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)
+
 extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
   // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
@@ -370,6 +374,10 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   CONV_FAST_CASE2(5, 5, 3, 16, 16, 4, 7, 4)  // s2 input conv (20 -> 50)
   CONV_FAST_CASE2(3, 3, 7, 16, 16, 4, 7, 8)  // s2 nodes / output conv, and their dgrad (50 -> 50)
   CONV_FAST_CASE2(5, 5, 7, 16, 16, 2, 3, 4)  // s2 input conv dgrad (50 -> 20)
+  // deep S=(3,4,5) space, kernels (20, 50, 100): stage 3 at 8x8 (one image per workgroup)
+  CONV_FAST_CASE_NW(5, 5, 7, 8, 8, 7, 13, 7)    // s3 input conv (50 -> 100)
+  CONV_FAST_CASE_NW(3, 3, 13, 8, 8, 7, 13, 7)   // s3 nodes / output conv, and their dgrad (100 -> 100)
+  CONV_FAST_CASE2(5, 5, 13, 8, 8, 4, 7, 4)      // s3 input conv dgrad (100 -> 50)
   return -100;
 }
 

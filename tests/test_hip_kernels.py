@@ -517,7 +517,10 @@ def test_glorot_init_kernel():
 @pytest.mark.parametrize("H,cin,cout,k,nin,dgrad", [(32, 3, 20, 5, 1, False), (32, 20, 20, 3, 2, False),
                                                     (16, 20, 50, 5, 1, False), (16, 50, 50, 3, 3, False),
                                                     (32, 20, 20, 3, 1, True), (16, 50, 50, 3, 1, True),
-                                                    (16, 50, 20, 5, 1, True)])
+                                                    (16, 50, 20, 5, 1, True),
+                                                    # deep S=(3,4,5) stage 3 (8x8, 100 channels: 7 co tiles)
+                                                    (8, 50, 100, 5, 1, False), (8, 100, 100, 3, 3, False),
+                                                    (8, 100, 100, 3, 1, True), (8, 100, 50, 5, 1, True)])
 def test_conv_fast_equals_generic(H, cin, cout, k, nin, dgrad):
     """The shape-specialised kernels (cnn_conv_fast.hip) walk the reduction in
     the generic kernel's chunk order: outputs are bit-identical, in group-table
