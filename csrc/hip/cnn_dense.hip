@@ -290,32 +290,38 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
 // ---------------------------------------------------------------------------
 struct DenseDgradArgs {
   const float* dH;     // [G][B][Up]
-  const float* w1;     // [G][Fp][Up] fp32 master
+  const uint16_t* wt;  // [G][Up][Fp] bf16 transposed copy of W1 (the values dense_fwd multiplied by)
   uint16_t* dx;        // [G][B][Fp]
   int G, B, Fp, Up;
 };
 
-// grid (Fp/64, ceil(B/32), G): D[row = f][col = b], K = units
+// grid (Fp/64, ceil(B/32), G): D[row = f][col = b], K = units.
+// W1 is read from the bf16 transposed copy (half the bytes of the fp32 master
+// this kernel used to read, on the critical path): each 32-unit x 64-feature
+// tile is one coalesced 16-byte load per thread, transposed through LDS so every
+// lane gets its 8 consecutive units as one 16-byte LDS read. The bf16 values are
+// the RNE roundings the old pack8(fp32) produced, so dx is bit-identical.
 __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t tl[64][40];    // [feature][unit], 80-byte rows
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
   const int g = blockIdx.z;
-  const int f_t = blockIdx.x * 64 + wave * 16;
+  const int fb = blockIdx.x * 64;
+  const int f_t = fb + wave * 16;
   const int b0 = blockIdx.y * 32;
-  const float* w1 = a.w1 + (long)g * a.Fp * a.Up;
+  const uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
   const float* dH = a.dH + (long)g * a.B * a.Up;
-  const int frow = f_t + l16;
+  const int lu = tid >> 3, lf = (tid & 7) * 8;       // staging: unit row lu, features lf .. lf+7
+  const bool fok = fb + lf < a.Fp;                   // Fp % 8 == 0: all 8 or none
   const int br0 = b0 + l16, br1 = b0 + 16 + l16;
   f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   const int nchunks = a.Up >> 3;
   for (int ks = 0; ks < nchunks; ks += 4) {
+    const int u = ks * 8 + lu;
+    uint4 q = {0u, 0u, 0u, 0u};
+    if (fok && u < a.Up) q = *reinterpret_cast<const uint4*>(wt + (long)u * a.Fp + fb + lf);
     const int c = ks + kq;
-    float fa[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float f0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (c < nchunks) {
-      if (frow < a.Fp) {
-        const float4* p = reinterpret_cast<const float4*>(w1 + (long)frow * a.Up + c * 8);
-        const float4 q0 = p[0], q1 = p[1];
-        fa[0] = q0.x; fa[1] = q0.y; fa[2] = q0.z; fa[3] = q0.w; fa[4] = q1.x; fa[5] = q1.y; fa[6] = q1.z; fa[7] = q1.w;
-      }
       if (br0 < a.B) {
         const float4* p = reinterpret_cast<const float4*>(dH + (long)br0 * a.Up + c * 8);
         const float4 q0 = p[0], q1 = p[1];
@@ -327,7 +333,16 @@ __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
         f1[0] = q0.x; f1[1] = q0.y; f1[2] = q0.z; f1[3] = q0.w; f1[4] = q1.x; f1[5] = q1.y; f1[6] = q1.z; f1[7] = q1.w;
       }
     }
-    const uint4 af = pack8(fa), b0f = pack8(f0), b1f = pack8(f1);
+    __syncthreads();                                 // previous tile fully read
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tl[lf + 2 * j][lu] = (uint16_t)(w[j] & 0xffffu);
+      tl[lf + 2 * j + 1][lu] = (uint16_t)(w[j] >> 16);
+    }
+    __syncthreads();
+    const uint4 af = *reinterpret_cast<const uint4*>(&tl[wave * 16 + l16][kq * 8]);
+    const uint4 b0f = pack8(f0), b1f = pack8(f1);
     acc[0] = mfma16(af, b0f, acc[0]);
     acc[1] = mfma16(af, b1f, acc[1]);
   }

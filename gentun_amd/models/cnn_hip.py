@@ -296,7 +296,7 @@ class HipPopJob(FoldJob):
         hd.eval = 0
         self.head_args = hd
         dd = K.DenseDgradArgs()
-        dd.dH, dd.w1, dd.dx = self.dH.data_ptr(), self.views["W1"][0].data_ptr(), self.grad[self.last].data_ptr()
+        dd.dH, dd.wt, dd.dx = self.dH.data_ptr(), self.w1t_bf.data_ptr(), self.grad[self.last].data_ptr()
         dd.G, dd.B, dd.Fp, dd.Up = Q, B, self.Fp, self.Up
         self.dense_dgrad_args = dd
         dw = K.DenseWgradAdamArgs()
@@ -445,7 +445,7 @@ class HipPopJob(FoldJob):
         self._run_fwd(s, self.fwd_ops)
         K.check(L.gt_dense_fwd(self.dense_fwd_args, s), "dense_fwd")
         K.check(L.gt_head(self.head_args, s), "head")
-        K.check(L.gt_dense_dgrad(self.dense_dgrad_args, s), "dense_dgrad")   # reads W1 before its update
+        K.check(L.gt_dense_dgrad(self.dense_dgrad_args, s), "dense_dgrad")   # reads the bf16 W1 copy before its update
         side = self.side if self.overlap else main
         side2 = (self.side2 if self.w1_stream else side) if self.overlap else main
         ss = side.cuda_stream

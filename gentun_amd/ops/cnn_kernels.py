@@ -52,7 +52,7 @@ class HeadArgs(C.Structure):
 
 
 class DenseDgradArgs(C.Structure):
-    _fields_ = [("dH", P), ("w1", P), ("dx", P), ("G", I), ("B", I), ("Fp", I), ("Up", I)]
+    _fields_ = [("dH", P), ("wt", P), ("dx", P), ("G", I), ("B", I), ("Fp", I), ("Up", I)]
 
 
 class DenseWgradAdamArgs(C.Structure):

@@ -321,7 +321,7 @@ def test_dense_fwd_dgrad():
     dH = torch.randn(G, B, Up, device=DEV)
     dx = torch.zeros(G, B, Fp, dtype=torch.bfloat16, device=DEV)
     d = Km.DenseDgradArgs()
-    d.dH, d.w1, d.dx, d.G, d.B, d.Fp, d.Up = dH.data_ptr(), w1.data_ptr(), dx.data_ptr(), G, B, Fp, Up
+    d.dH, d.wt, d.dx, d.G, d.B, d.Fp, d.Up = dH.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Fp, Up
     Km.check(Km.lib().gt_dense_dgrad(d, stream()), "dgrad")
     torch.cuda.synchronize()
     assert (out.float() - ref).abs().max().item() < 2e-2 * ref.abs().max().item()
