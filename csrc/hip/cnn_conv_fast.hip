@@ -608,10 +608,13 @@ extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, in
 
 // Preferred splits per group (measured, profiles/wgrad_splits.txt): many small
 // workgroups for the 32-wide stage (single LDS buffer, 4+ per CU), few large
-// ones for the 16-wide stage (double-buffered, fewer partials for Adam).
+// ones for the 16-wide stage (double-buffered: 128 KB of LDS, one workgroup per
+// CU). 3 splits x 80 groups of a 16-candidate population = 240 workgroups, one
+// round on 256 CUs; 4 splits left a 64-workgroup second round (population step
+// 2-3 % slower, same-box sweep).
 extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, int W) {
   (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H;
-  return W >= 32 ? 16 : 4;
+  return W >= 32 ? 16 : 3;
 }
 
 extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
