@@ -454,7 +454,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 
 __global__ void pool_fwd_kernel(const uint16_t* __restrict__ x0, const uint16_t* __restrict__ x1,
                                 const int* __restrict__ sel, uint16_t* __restrict__ y, int NB, int B, int H, int W,
-                                int Cp) {
+                                int Cp, uint8_t* __restrict__ mask) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
   const uint32_t total = (uint32_t)NB * Ho * Wo * ncb;       // < 2^31 (host-checked): 32-bit index math
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
@@ -466,14 +466,26 @@ __global__ void pool_fwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
     const uint16_t* x = (sel && sel[n / B]) ? x1 : x0;
     const uint16_t* base = x + ((n * H + 2 * ho) * W + 2 * wo) * Cp + cb * 8;
     float m[8], t[8];
+    int arg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unpack8(*reinterpret_cast<const uint4*>(base), m);
     const long offs[3] = {(long)Cp, (long)W * Cp, (long)W * Cp + Cp};
     for (int q = 0; q < 3; ++q) {
       unpack8(*reinterpret_cast<const uint4*>(base + offs[q]), t);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) m[j] = fmaxf(m[j], t[j]);
+      for (int j = 0; j < 8; ++j)
+        if (t[j] > m[j]) { m[j] = t[j]; arg[j] = q + 1; }      // first strict maximum, as pool_bwd_kernel
     }
-    *reinterpret_cast<uint4*>(y + ((n * Ho + ho) * Wo + wo) * Cp + cb * 8) = pack8(m);
+    const long o = ((n * Ho + ho) * Wo + wo) * Cp + cb * 8;
+    *reinterpret_cast<uint4*>(y + o) = pack8(m);
+    if (mask) {
+      // per channel: bits 0-1 = which of the 4 cell pixels holds the maximum, bit 2 = maximum > 0
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lo |= (uint32_t)(arg[j] | (m[j] > 0.f ? 4 : 0)) << (8 * j);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hi |= (uint32_t)(arg[4 + j] | (m[4 + j] > 0.f ? 4 : 0)) << (8 * j);
+      *reinterpret_cast<uint2*>(mask + o) = make_uint2(lo, hi);
+    }
   }
 }
 
@@ -512,6 +524,40 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
         float m = v[0][j];
         for (int q = 1; q < 4; ++q) if (v[q][j] > m) { m = v[q][j]; arg = q; }
         out[j] = (arg == me && (!relu_mask || m > 0.f)) ? g[j] : 0.f;
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + ((n * H + h) * W + w) * Cp + cb * 8) = pack8(out);
+  }
+}
+
+// Backward scatter from the forward's argmax mask (1 byte per pooled channel
+// instead of re-reading the 4 bf16 cell inputs: the pool_bwd traffic drops from
+// x + dy + dx to mask + dy + dx). Same first-maximum rule, so dx is identical
+// to pool_bwd_kernel's.
+__global__ void pool_bwd_mask_kernel(const uint8_t* __restrict__ mask, const int* __restrict__ sel,
+                                     const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx0,
+                                     uint16_t* __restrict__ dx1, int NB, int B, int H, int W, int Cp, int relu_mask) {
+  const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
+  const uint32_t total = (uint32_t)NB * H * W * ncb;         // < 2^31 (host-checked): 32-bit index math
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int cb = (int)(i % ncb);
+    uint32_t r = i / ncb;
+    const int w = (int)(r % W); r /= W;
+    const int h = (int)(r % H);
+    const long n = r / H;
+    uint16_t* dx = (sel && sel[n / B]) ? dx1 : dx0;
+    float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int ho = h >> 1, wo = w >> 1;
+    if (ho < Ho && wo < Wo) {
+      const long o = ((n * Ho + ho) * Wo + wo) * Cp + cb * 8;
+      const uint2 mk = *reinterpret_cast<const uint2*>(mask + o);
+      float g[8];
+      unpack8(*reinterpret_cast<const uint4*>(dy + o), g);
+      const uint32_t me = (uint32_t)((h & 1) * 2 + (w & 1));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t b = ((j < 4 ? mk.x : mk.y) >> (8 * (j & 3))) & 0xffu;
+        out[j] = ((b & 3u) == me && (!relu_mask || (b & 4u))) ? g[j] : 0.f;
       }
     }
     *reinterpret_cast<uint4*>(dx + ((n * H + h) * W + w) * Cp + cb * 8) = pack8(out);
@@ -601,7 +647,30 @@ int gt_pool_fwd(const uint16_t* x0, const uint16_t* x1, const int* sel, uint16_t
   const long total = (long)NB * (H / 2) * (W / 2) * (Cp / 8);
   if ((long)NB * H * W * (Cp / 8) >= (1L << 31)) return -4;
   const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, y, NB, B, H, W, Cp);
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, y, NB, B, H, W, Cp,
+                     (uint8_t*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// training forward: also writes the argmax mask [NB][H/2][W/2][Cp] (uint8) for gt_pool_bwd_mask
+int gt_pool_fwd_mask(const uint16_t* x0, const uint16_t* x1, const int* sel, uint16_t* y, int NB, int B, int H,
+                     int W, int Cp, uint8_t* mask, hipStream_t stream) {
+  const long total = (long)NB * (H / 2) * (W / 2) * (Cp / 8);
+  if ((long)NB * H * W * (Cp / 8) >= (1L << 31)) return -4;
+  if (Cp % 8 || mask == nullptr) return -1;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, y, NB, B, H, W, Cp, mask);
+  return (int)hipGetLastError();
+}
+
+int gt_pool_bwd_mask(const uint8_t* mask, const int* sel, const uint16_t* dy, uint16_t* dx0, uint16_t* dx1, int NB,
+                     int B, int H, int W, int Cp, int relu_mask, hipStream_t stream) {
+  const long total = (long)NB * H * W * (Cp / 8);
+  if (total >= (1L << 31)) return -4;
+  if (Cp % 8 || mask == nullptr) return -1;
+  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(pool_bwd_mask_kernel, dim3(blocks), dim3(256), 0, stream, mask, sel, dy, dx0, dx1, NB, B, H, W,
+                     Cp, relu_mask);
   return (int)hipGetLastError();
 }
 

@@ -272,8 +272,11 @@ class HipPopJob(FoldJob):
             x1 = self.act[self.sched.pool_x1(st)]
             hh, ww, cc = self.shapes[st.inp]
             st.sel = sel
+            # argmax mask of the training forward (1 byte per pooled channel): pool_bwd reads it
+            # instead of the 4 bf16 inputs of every cell
+            st.pmask = torch.zeros((Q * B, hh // 2, ww // 2, cc), dtype=torch.uint8, device=self.device)
             self.fwd_ops.append(("pool", (self.act[st.inp].data_ptr(), x1.data_ptr(), sel.data_ptr(),
-                                          self.act[st.pool].data_ptr(), Q * B, B, hh, ww, cc), None))
+                                          self.act[st.pool].data_ptr(), Q * B, B, hh, ww, cc), st.pmask.data_ptr()))
         # ---- head
         df = K.DenseFwdArgs()
         df.x, df.wt, df.bias, df.out = (self.act[self.last].data_ptr(), self.w1t_bf.data_ptr(),
@@ -314,7 +317,7 @@ class HipPopJob(FoldJob):
                 st = rec[1]
                 hh, ww, cc = self.shapes[st.inp]
                 x1 = self.sched.pool_x1(st)
-                self.bwd_ops.append(("pool_bwd", (self.act[st.inp].data_ptr(), self.act[x1].data_ptr(),
+                self.bwd_ops.append(("pool_bwd", (st.pmask.data_ptr(),
                                                   st.sel.data_ptr(), self.grad[st.pool].data_ptr(),
                                                   self.grad[st.inp].data_ptr(), self.grad[x1].data_ptr(),
                                                   Q * B, B, hh, ww, cc, 1), None))
@@ -431,9 +434,11 @@ class HipPopJob(FoldJob):
 
     def _run_fwd(self, s, ops):
         L = self.L
-        for kind, a, _ in ops:
+        for kind, a, mk in ops:
             if kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_fwd")
+            elif mk is not None:
+                K.check(L.gt_pool_fwd_mask(*a, mk, s), "pool_fwd")
             else:
                 K.check(L.gt_pool_fwd(*a, s), "pool_fwd")
 
@@ -468,7 +473,7 @@ class HipPopJob(FoldJob):
             elif kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
             else:
-                K.check(L.gt_pool_bwd(*a, s), "pool_bwd")
+                K.check(L.gt_pool_bwd_mask(*a, s), "pool_bwd")
         for stream in (side, side2):
             if stream is not main:
                 ev = torch.cuda.Event()
@@ -499,7 +504,7 @@ class HipPopJob(FoldJob):
                 b.xsum = 0
                 ops.append((kind, b, Lr))
             else:
-                ops.append((kind, a, Lr))
+                ops.append((kind, a, None))          # no argmax mask in evaluation
         df = K.DenseFwdArgs.from_buffer_copy(self.dense_fwd_args)
         df.train = 0
         hd = K.HeadArgs.from_buffer_copy(self.head_args)

@@ -111,6 +111,10 @@ def lib():
         L.gt_pool_fwd.restype = I
         L.gt_pool_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P]
         L.gt_pool_bwd.restype = I
+        L.gt_pool_fwd_mask.argtypes = [P, P, P, P, I, I, I, I, I, P, P]
+        L.gt_pool_fwd_mask.restype = I
+        L.gt_pool_bwd_mask.argtypes = [P, P, P, P, P, I, I, I, I, I, I, P]
+        L.gt_pool_bwd_mask.restype = I
         L.gt_wgrad_set_nb.argtypes = [I]
         L.gt_wgrad_set_nb.restype = I
         L.gt_wgrad_fast_band.argtypes = [I, I, I, I, I, I]

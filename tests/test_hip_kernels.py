@@ -214,6 +214,36 @@ def test_pool_group_select():
         assert torch.all((dx0 if sel[g] else dx1)[g] == 5.0)
 
 
+@pytest.mark.parametrize("H,W,relu", [(8, 8, 1), (7, 7, 1), (14, 14, 0), (16, 16, 1)])
+def test_pool_argmax_mask(H, W, relu):
+    """Training-forward argmax mask + mask backward: bit-identical to the
+    recomputing pool_bwd (ties, zeros, negative maxima, odd sizes included)."""
+    Km = K()
+    torch.manual_seed(9)
+    Q, B, cp = 3, 2, 16
+    # coarse values: many ties and exact zeros inside the 2x2 cells
+    x0 = bf(torch.randint(-2, 3, (Q, B, H, W, cp), device=DEV).float())
+    x1 = bf(torch.randint(-2, 3, (Q, B, H, W, cp), device=DEV).float())
+    sel = torch.tensor([1, 0, 1], dtype=torch.int32, device=DEV)
+    args = (x0.data_ptr(), x1.data_ptr(), sel.data_ptr())
+    y_ref = torch.zeros(Q, B, H // 2, W // 2, cp, dtype=torch.bfloat16, device=DEV)
+    y = torch.zeros_like(y_ref)
+    mask = torch.full((Q * B, H // 2, W // 2, cp), 255, dtype=torch.uint8, device=DEV)
+    Km.check(Km.lib().gt_pool_fwd(*args, y_ref.data_ptr(), Q * B, B, H, W, cp, stream()), "pool")
+    Km.check(Km.lib().gt_pool_fwd_mask(*args, y.data_ptr(), Q * B, B, H, W, cp, mask.data_ptr(), stream()), "poolm")
+    dy = bf(torch.randn_like(y.float()))
+    dx_ref = [torch.full_like(x0, 5.0), torch.full_like(x1, 5.0)]
+    dx = [torch.full_like(x0, 5.0), torch.full_like(x1, 5.0)]
+    Km.check(Km.lib().gt_pool_bwd(*args, dy.data_ptr(), dx_ref[0].data_ptr(), dx_ref[1].data_ptr(), Q * B, B, H, W,
+                                  cp, relu, stream()), "poolb")
+    Km.check(Km.lib().gt_pool_bwd_mask(mask.data_ptr(), sel.data_ptr(), dy.data_ptr(), dx[0].data_ptr(),
+                                       dx[1].data_ptr(), Q * B, B, H, W, cp, relu, stream()), "poolbm")
+    torch.cuda.synchronize()
+    assert torch.equal(y.float(), y_ref.float())
+    assert int(mask.max()) <= 7
+    assert torch.equal(dx[0], dx_ref[0]) and torch.equal(dx[1], dx_ref[1])
+
+
 @pytest.mark.parametrize("H,W,cin,cout,k,nin,first", [(32, 32, 3, 20, 5, 1, True), (16, 16, 50, 50, 3, 2, False),
                                                       (32, 32, 20, 20, 3, 1, False), (8, 8, 64, 128, 3, 1, False)])
 def test_conv_wgrad(H, W, cin, cout, k, nin, first):
