@@ -259,3 +259,52 @@ def test_gpu_individual_runs_on_evaluating_rank_device():
     ind2 = SimpleNamespace(device="cuda:0")
     _localize_device(ind2, SimpleNamespace(device="cpu"))
     assert ind2.device == "cuda:0"
+
+
+def _rccl_proc(port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": "0",
+                       "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
+    import sys
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from fake_species import BitIndividual as Bit
+    from gentun_amd.parallel import DistComm
+    from gentun_amd.parallel.distributed import DistributedPopulation as DP
+    from gentun_amd.parallel.evaluators import SequentialEvaluator as SE
+    from gentun_amd import RussianRouletteGA as RR
+    from gentun_amd.utils import rng as r
+    torch.cuda.set_device(0)
+    comm = DistComm(backend="nccl", timeout_s=60, device=torch.device("cuda", 0))
+    assert comm.backend == "nccl" and comm.device.type == "cuda"
+    arrays = [np.arange(12, dtype=np.float32).reshape(3, 4), np.array([1, -2, 3], np.int64),
+              np.frombuffer(b"genome", np.uint8).copy(), np.zeros((0,), np.float64)]
+    for a in arrays:
+        b = comm.broadcast_array(a)
+        assert b.dtype == a.dtype and b.shape == a.shape and np.array_equal(a, b)
+    g = comm.all_gather_array(np.array([0.5, np.nan], np.float32))
+    assert len(g) == 1 and g[0][0] == 0.5 and np.isnan(g[0][1])
+    comm.barrier()
+    r.seed(77)
+    pop = DP(Bit, None, None, size=10, comm=comm, evaluator=SE())
+    ga = RR(pop, verbose=False)
+    ga.run(4)
+    pop = ga.population
+    pop.sync_ranks()
+    pop.shutdown()
+    q.put([(h["best_fitness"], h["evals"], tuple(sorted(h["best_genes"].items()))) for h in ga.history])
+    comm.destroy()
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_matches_local_run():
+    """The RCCL (backend "nccl") communicator on one GPU: typed broadcast /
+    all_gather round trips and a distributed GA identical to the local run."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_proc, args=(_free_port(), q))
+    p.start()
+    hist = q.get(timeout=100)
+    p.join(timeout=30)
+    assert p.exitcode == 0
+    assert hist == _local(BitIndividual, RussianRouletteGA, 4, seed=77, size=10)
