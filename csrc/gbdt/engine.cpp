@@ -363,6 +363,12 @@ bool higher_better(int metric) { return metric == M_AUC; }
 
 extern "C" {
 
+#ifndef GT_SRC_HASH
+#define GT_SRC_HASH "unhashed"
+#endif
+// content hash of the sources this library was compiled from (tools/build_native.py)
+const char* gt_build_hash() { return GT_SRC_HASH; }
+
 // params: eta, min_child_weight, max_depth, gamma, max_delta_step, subsample,
 //         colsample_bytree, colsample_bylevel, lambda, alpha, scale_pos_weight, base_score
 // out_hist: [num_boost_round][n_metrics][4] = train-mean, train-std, test-mean, test-std

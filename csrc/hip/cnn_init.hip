@@ -53,6 +53,12 @@ extern "C" {
 
 size_t gt_sizeof_init_seg() { return sizeof(InitSeg); }
 
+#ifndef GT_SRC_HASH
+#define GT_SRC_HASH "unhashed"
+#endif
+// content hash of the sources this library was compiled from (tools/build_native.py)
+const char* gt_build_hash() { return GT_SRC_HASH; }
+
 int gt_glorot_init(const InitArgs* a, int nblocks, hipStream_t stream) {
   if (nblocks <= 0) return 0;
   hipLaunchKernelGGL(glorot_init_kernel, dim3(nblocks), dim3(256), 0, stream, *a);

@@ -22,14 +22,14 @@ if __name__ == "__main__":
     comm = from_env(device=device)
     evaluator = LocalBatchEvaluator(device=device, streams=4)
     if comm.rank == 0:
+        size, gens = (4, 2) if _common.SMALL else (20, 50)
         pop = DistributedPopulation(
-            GeneticCnnIndividual, x_train, y_train, size=20, crossover_rate=0.3, mutation_rate=0.1,
-            additional_parameters={
-                'nfold': 5, 'epochs': (20, 4, 1), 'learning_rate': (1e-3, 1e-4, 1e-5), 'batch_size': 32
-            }, maximize=True, comm=comm, evaluator=evaluator
+            GeneticCnnIndividual, x_train, y_train, size=size, crossover_rate=0.3, mutation_rate=0.1,
+            additional_parameters=dict(_common.cnn_schedule(), batch_size=32), maximize=True, comm=comm,
+            evaluator=evaluator
         )
         ga = RussianRouletteGA(pop, crossover_probability=0.2, mutation_probability=0.8)
-        ga.run(50)
+        ga.run(gens)
         pop.shutdown()
     else:
         GentunWorker(GeneticCnnIndividual, x_train, y_train, comm=comm, evaluator=evaluator).work()

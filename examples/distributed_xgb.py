@@ -13,8 +13,7 @@ if __name__ == "__main__":
     from gentun import DistributedPopulation, GeneticAlgorithm, GentunWorker, XgboostIndividual
     from gentun_amd.parallel import from_env
 
-    import os
-    small = os.environ.get("GENTUN_EXAMPLE_SMALL") == "1"   # CI-sized run
+    small = _common.SMALL                                      # CI-sized run
     size, gens = (10, 2) if small else (100, 10)
     extra = {'nfold': 3, 'num_boost_round': 40} if small else {'nfold': 3}
     x_train, y_train = _common.wine()

@@ -12,9 +12,12 @@ if __name__ == "__main__":
         'max_depth': range(3, 11),
         'colsample_bytree': [0.80, 0.85, 0.90, 0.95, 1.0],
     }
+    if _common.SMALL:
+        grid = {'eta': [0.1, 0.3], 'max_depth': [3, 4, 5]}
+    extra = {'nfold': 3, 'num_boost_round': 30} if _common.SMALL else {'nfold': 3}
     pop = GridPopulation(
         XgboostIndividual, x_train, y_train, genes_grid=grid,
-        additional_parameters={'nfold': 3}, maximize=False
+        additional_parameters=extra, maximize=False
     )
     ga = GeneticAlgorithm(pop)
-    ga.run(10)
+    ga.run(2 if _common.SMALL else 10)

@@ -10,12 +10,12 @@ if __name__ == "__main__":
     from gentun_amd import LocalBatchEvaluator
 
     x_train, y_train = _common.mnist_like()
+    size, gens = (4, 2) if _common.SMALL else (20, 50)
+    params = dict(_common.cnn_schedule(), batch_size=32)
     pop = Population(
-        GeneticCnnIndividual, x_train, y_train, size=20, crossover_rate=0.3, mutation_rate=0.1,
-        additional_parameters={
-            'nfold': 5, 'epochs': (20, 4, 1), 'learning_rate': (1e-3, 1e-4, 1e-5), 'batch_size': 32
-        }, maximize=True, evaluator=LocalBatchEvaluator(streams=4)
+        GeneticCnnIndividual, x_train, y_train, size=size, crossover_rate=0.3, mutation_rate=0.1,
+        additional_parameters=params, maximize=True, evaluator=LocalBatchEvaluator(streams=4)
     )
     ga = RussianRouletteGA(pop, crossover_probability=0.2, mutation_probability=0.8, seed=0,
-                           checkpoint_dir="ckpt_mnist")
-    ga.run(50)
+                           checkpoint_dir=None if _common.SMALL else "ckpt_mnist")
+    ga.run(gens)

@@ -7,8 +7,10 @@ if __name__ == "__main__":
     from gentun import GeneticAlgorithm, Population, XgboostIndividual
 
     x_train, y_train = _common.wine()
+    size, gens = (6, 2) if _common.SMALL else (100, 10)
+    extra = {'nfold': 3, 'num_boost_round': 30} if _common.SMALL else {'nfold': 3}
     pop = Population(
-        XgboostIndividual, x_train, y_train, size=100, additional_parameters={'nfold': 3}, maximize=False
+        XgboostIndividual, x_train, y_train, size=size, additional_parameters=extra, maximize=False
     )
     ga = GeneticAlgorithm(pop)
-    ga.run(10)
+    ga.run(gens)

@@ -14,6 +14,7 @@ log and atomic per-generation checkpoints (``checkpoint_dir=``) that
 ``resume()`` continues from.
 """
 
+import math
 import time
 
 from .utils import rng as _rng
@@ -25,7 +26,11 @@ class GeneticAlgorithm(object):
     def __init__(self, population, tournament_size=5, elitism=True, seed=None,
                  checkpoint_dir=None, event_log=None, verbose=True):
         if seed is not None:
-            _rng.seed(seed)
+            # the breeding stream is derived from the run seed, not the seed
+            # itself: a caller that seeded the stream with the same value to
+            # draw the initial population must not see those draws replayed
+            # by selection / crossover / mutation
+            _rng.seed(_rng.stable_hash(seed, "ga-breeding"))
         self.population = population
         self.x_train, self.y_train = population.get_data()
         self.tournament_size = tournament_size
@@ -149,8 +154,12 @@ class RussianRouletteGA(GeneticAlgorithm):
             w = list(fits)
         else:
             w = [1.0 / (f + eps) for f in fits]
-        floor = min(w)
-        w = [x - floor for x in w]
+        # a candidate whose evaluation failed twice carries the worst possible
+        # fitness (-inf when maximizing, +inf -> weight 0 when minimizing):
+        # it gets weight 0, and the floor is taken over the finite weights
+        finite = [x for x in w if math.isfinite(x)]
+        floor = min(finite) if finite else 0.0
+        w = [x - floor if math.isfinite(x) else 0.0 for x in w]
         if sum(w) == 0.0:
             w = [1.0] * len(w)
         return w

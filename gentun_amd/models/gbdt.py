@@ -39,12 +39,26 @@ def _as_arrays(x, y):
     return x, y
 
 
+# keys the engine accepts without using: xgboost plumbing / verbosity knobs
+IGNORED = {"silent", "verbosity", "nthread", "n_jobs", "seed", "random_state", "tree_method", "eval_metric",
+           "objective", "booster", "num_class", "disable_default_eval_metric"}
+
+
 def resolve_params(params):
+    """Engine parameters from an xgboost-style dict. Only ``booster='gbtree'``
+    exists here (the reference forwards ``booster`` to xgb.cv,
+    gentun/models/xgboost_models.py:16-22): gblinear / dart raise instead of
+    silently training trees, and unknown keys raise too."""
+    booster = params.get("booster", "gbtree")
+    if booster != "gbtree":
+        raise ValueError("booster {!r} is not supported: the native engine implements gbtree only".format(booster))
     p = dict(DEFAULTS)
     for k, v in params.items():
         k = ALIASES.get(k, k)
         if k in p:
             p[k] = float(v)
+        elif k not in IGNORED:
+            raise ValueError("unsupported GBDT parameter {!r}".format(k))
     obj = params.get("objective", "reg:linear")
     if obj not in OBJECTIVES:
         raise ValueError("unsupported objective {!r}".format(obj))

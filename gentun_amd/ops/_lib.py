@@ -46,8 +46,30 @@ def load(name):
         if not os.path.exists(path):
             raise RuntimeError("native library {} not found at {}".format(name, path))
         lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        _check_hash(name, lib)
         _LIBS[name] = lib
         return lib
+
+
+def _check_hash(name, lib):
+    """Refuse a library built from other sources than the tree's (a stale
+    binary must never run silently). Skipped when the sources are absent
+    (installed package)."""
+    import sys
+    root = os.path.dirname(os.path.dirname(_HERE))
+    if not os.path.isdir(os.path.join(root, "csrc")):
+        return
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    from tools import build_native
+    if name not in build_native.TARGETS:
+        return
+    fn = lib.gt_build_hash
+    fn.restype = ctypes.c_char_p
+    have, want = fn().decode(), build_native.source_hash(name)
+    if have != want:
+        raise RuntimeError("native library {} is stale (built from sources {}, tree is {}): run "
+                           "python tools/build_native.py".format(name, have, want))
 
 
 def gbdt():

@@ -153,10 +153,12 @@ def load_iris_xy():
 
 def load_wine_quality(path=None):
     """White wine quality (4,898 x 11 -> quality). ``path`` defaults to the
-    reference fixture (tests/data/winequality-white.csv, ';'-separated)."""
+    vendored copy of the public UCI fixture the reference ships
+    (tests/data/winequality-white.csv, ';'-separated)."""
     import pandas as pd
     if path is None:
-        path = os.environ.get("GENTUN_WINE_CSV", "/root/reference/tests/data/winequality-white.csv")
+        here = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        path = os.environ.get("GENTUN_WINE_CSV", os.path.join(here, "tests", "data", "winequality-white.csv"))
     df = pd.read_csv(path, sep=";")
     y = df.pop("quality").to_numpy(np.float64)
     return df.to_numpy(np.float64), y

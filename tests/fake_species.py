@@ -65,3 +65,16 @@ class NumIndividual(Individual):
 
     def get_additional_parameters(self):
         return {}
+
+
+class FlakyBitIndividual(BitIndividual):
+    """A BitIndividual whose evaluation ALWAYS raises when gene 'A' starts
+    with '11' (so the rank-0 re-evaluation fails too)."""
+
+    FAILS = [0]
+
+    def evaluate_fitness(self):
+        if self.genes['A'].startswith('11'):
+            FlakyBitIndividual.FAILS[0] += 1
+            raise RuntimeError("permanent evaluation failure")
+        super(FlakyBitIndividual, self).evaluate_fitness()

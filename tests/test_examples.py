@@ -25,6 +25,35 @@ def test_xgboost_model_example():
     assert 0.5 < rmse < 0.8
 
 
+SMALL = {"GENTUN_EXAMPLE_SMALL": "1", "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""}
+
+
+@pytest.mark.parametrize("script,expect", [("cnn_model.py", None), ("mnist_genetic_cnn.py", "Fitness value"),
+                                           ("wine_quality.py", "Fitness value"),
+                                           ("grid_wine_quality.py", "Fitness value")])
+def test_example_runs_small(script, expect):
+    """Every single-process example runs end to end (CI-sized: same code
+    path, smaller population / schedule; CPU executor)."""
+    r = _run(script, timeout=600, env=SMALL)
+    assert r.returncode == 0, r.stderr[-3000:]
+    if expect is None:
+        v = float(r.stdout.strip().splitlines()[-1])
+        assert 0.0 <= v <= 1.0
+    else:
+        assert expect in r.stdout, r.stdout[-2000:]
+
+
+def test_distributed_cnn_example_gloo():
+    """torchrun with 2 ranks on gloo: the Genetic-CNN master/worker pair."""
+    env = dict(os.environ, **SMALL)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29519",
+                        os.path.join(ROOT, "examples", "distributed_cnn.py")],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "Fitness value" in r.stdout, r.stdout[-2000:]
+
+
 def test_distributed_xgb_example_gloo():
     """torchrun with 2 ranks on gloo: rank 0 runs the GA, rank 1 is a worker."""
     env = dict(os.environ, GENTUN_EXAMPLE_SMALL="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")

@@ -121,3 +121,18 @@ def test_quantize_gpu_layout_matches_and_caches():
     xc = np.ascontiguousarray(x)
     _lib.gbdt().gbdt_quantize_fm(xc.ctypes.data, 3000, 7, bt.ctypes.data, nb3.ctypes.data)
     assert np.array_equal(b.T, bt)
+
+
+def test_unsupported_booster_and_unknown_params_raise():
+    """The reference forwards ``booster`` to xgb.cv; the engine only has
+    gbtree, so gblinear / dart must raise rather than silently train trees."""
+    import pytest
+    from gentun_amd.models import gbdt
+    x = np.random.default_rng(0).standard_normal((64, 3)).astype(np.float32)
+    y = x[:, 0].copy()
+    for booster in ("gblinear", "dart"):
+        with pytest.raises(ValueError, match="booster"):
+            gbdt.cv({"booster": booster}, x, y, num_boost_round=2, nfold=2)
+    with pytest.raises(ValueError, match="unsupported GBDT parameter"):
+        gbdt.cv({"max_leaves": 8}, x, y, num_boost_round=2, nfold=2)
+    gbdt.cv({"booster": "gbtree", "silent": 1, "eval_metric": "rmse"}, x, y, num_boost_round=2, nfold=2)

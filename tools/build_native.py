@@ -5,11 +5,17 @@
   (Genetic-CNN conv/pool/dense/loss/Adam + GBDT histogram/split), compiled
   with ``hipcc --offload-arch=gfx950``; cross-compiles on a CPU-only host.
 
-Rebuilds only when a source is newer than its library. Used by
-``__graft_entry__.build()`` and lazily by :mod:`gentun_amd.ops._lib`.
+Staleness is decided by CONTENT, not mtimes: every library is compiled with
+``-DGT_SRC_HASH=<sha256 of its sources, headers and compile command>`` and
+exports ``gt_build_hash()``; a library whose embedded hash differs from the
+current tree is rebuilt, and :mod:`gentun_amd.ops._lib` refuses to load one
+(so a stale binary can never run against newer sources, e.g. after a
+checkout). Used by ``__graft_entry__.build()`` and lazily by the loader.
 """
 
+import ctypes
 import glob
+import hashlib
 import os
 import shutil
 import subprocess
@@ -45,11 +51,56 @@ def _abs(p):
     return p if os.path.isabs(p) else os.path.join(ROOT, p)
 
 
-def _stale(lib, srcs):
+def source_hash(name):
+    """sha256 over the target's sources + headers (repo-relative paths and
+    bytes) and its compile flags: the value baked into the library."""
+    spec = TARGETS[name]
+    h = hashlib.sha256()
+    h.update(spec["kind"].encode())
+    h.update(" ".join(_flags(spec["kind"])).encode())
+    for f in sorted(set(_abs(x) for x in spec["sources"] + spec["deps"])):
+        h.update(os.path.relpath(f, ROOT).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:32]
+
+
+def library_hash(lib):
+    """The GT_SRC_HASH a built library carries (None if unreadable)."""
+    try:
+        handle = ctypes.CDLL(lib, mode=ctypes.RTLD_LOCAL)
+        fn = handle.gt_build_hash
+        fn.restype = ctypes.c_char_p
+        return fn().decode()
+    except (OSError, AttributeError):
+        return None
+
+
+def _stamp(lib):
+    return lib + ".srchash"
+
+
+def _stale(name, lib):
     if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(lib)
-    return any(os.path.getmtime(s) > t for s in srcs)
+    want = source_hash(name)
+    # the stamp file avoids dlopen()ing a multi-MB library just to compare
+    try:
+        with open(_stamp(lib)) as f:
+            if f.read().strip() != want:
+                return True
+    except OSError:
+        return True
+    return library_hash(lib) != want
+
+
+def _flags(kind):
+    if kind == "cxx":
+        return ["-O3", "-std=c++17", "-fPIC", "-shared", "-march=x86-64-v2", "-pthread"]
+    if kind == "cxx_asan":
+        return ["-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fno-omit-frame-pointer",
+                "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"]
+    return ["--offload-arch={}".format(ARCH), "-O3", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics"]
 
 
 def hipcc():
@@ -65,25 +116,41 @@ def build_target(name, verbose=False, force=False):
     if not srcs:
         return None
     lib = os.path.join(OUT, name)
-    if not force and not _stale(lib, srcs + [_abs(d) for d in spec["deps"]]):
+    if not force and not _stale(name, lib):
         return lib
     os.makedirs(OUT, exist_ok=True)
     tmp = lib + ".tmp.{}".format(os.getpid())
-    if spec["kind"] == "cxx":
-        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-march=x86-64-v2", "-pthread", "-o", tmp] + srcs
-    elif spec["kind"] == "cxx_asan":
-        cmd = ["g++", "-O1", "-g", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fno-omit-frame-pointer",
-               "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-o", tmp] + srcs
+    want = source_hash(name)
+    hflag = ['-DGT_SRC_HASH="{}"'.format(want)]
+    if spec["kind"] in ("cxx", "cxx_asan"):
+        cmd = ["g++"] + _flags(spec["kind"]) + hflag + ["-o", tmp] + srcs
     else:
         cc = hipcc()
         if cc is None:
             raise RuntimeError("hipcc not found; cannot build {}".format(name))
-        cmd = [cc, "--offload-arch={}".format(ARCH), "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-munsafe-fp-atomics", "-I", os.path.join(ROOT, "csrc", "hip"), "-o", tmp] + srcs
+        # one object per translation unit, compiled in parallel, then linked
+        objdir = os.path.join(ROOT, "build", "obj_" + name.split(".")[0])
+        os.makedirs(objdir, exist_ok=True)
+        comp = [cc] + [f for f in _flags("hip") if f != "-shared"] + hflag + ["-I", os.path.join(ROOT, "csrc", "hip")]
+        objs, cmds = [], []
+        for src in srcs:
+            obj = os.path.join(objdir, os.path.basename(src) + ".o")
+            objs.append(obj)
+            cmds.append(comp + ["-c", "-o", obj, src])
+        from concurrent.futures import ThreadPoolExecutor
+        jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "0")) or (os.cpu_count() or 4)))
+        with ThreadPoolExecutor(jobs) as ex:
+            for c in cmds:
+                if verbose:
+                    print("[build]", " ".join(c), flush=True)
+            list(ex.map(lambda c: subprocess.check_call(c, cwd=ROOT), cmds))
+        cmd = [cc, "--offload-arch={}".format(ARCH), "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=ROOT)
     os.replace(tmp, lib)
+    with open(_stamp(lib), "w") as f:
+        f.write(want + "\n")
     return lib
 
 
