@@ -21,28 +21,34 @@ struct GroupRec {
 
 #define GT_MAXSLOT 8
 
+// Activation / gradient tensors are bf16 (prec 0) or fp32 (prec 1) -- void
+// pointers here, typed by the kernel instantiation. Weights are always bf16
+// PLANES: one plane in prec 0; in prec 1 the exact 3-way split of the fp32
+// master (common.h split8), plane p at w + p * wps.
 struct ConvArgs {
-  const uint16_t* in[GT_MAXSLOT];   // input slot bases [Q][B][H][W][Cinp]
-  const uint16_t* mask;             // optional: staged value *= (mask > 0), same shape as in (legacy mode)
+  const void* in[GT_MAXSLOT];       // input slot bases [Q][B][H][W][Cinp]
+  const void* mask;                 // optional: staged value *= (mask > 0), same shape as in (legacy mode)
   const int64_t* gather;            // optional: image table [steps][Q][B]; in[0] is then the dataset
   const StepState* st;              // cur_step for the gather table
-  uint16_t* out[GT_MAXSLOT];        // output slot bases [Q][B][H][W][Coutp]
-  const uint16_t* out_mask[GT_MAXSLOT];  // per output slot: ReLU-mask source (that slot's activation)
-  const uint16_t* w;                // [Q][Coutp][KH][KW][Cinp] bf16
+  void* out[GT_MAXSLOT];            // output slot bases [Q][B][H][W][Coutp]
+  const void* out_mask[GT_MAXSLOT];  // per output slot: ReLU-mask source (that slot's activation)
+  const uint16_t* w;                // [planes][Q][Coutp][KH][KW][Cinp] bf16
   const float* bias;                // [Q][Coutp] or null
   const GroupRec* gtab;             // [grid.y] or null
   int n_in, n_out, acc_flags, relu;
   int G, B, H, W, Cinp, Coutp, KH, KW, TH;   // G = Q (group count of the slot tensors)
   int ngroups;                      // launch groups (rows of gtab); legacy mode: G
-  uint16_t* xsum;                   // optional [Q][B][H][W][Cinp]: groups summing >1 input slot write the sum
+  void* xsum;                       // optional [Q][B][H][W][Cinp]: groups summing >1 input slot write the sum
                                     // (the layer's wgrad then reads one tensor instead of re-summing)
   int dbg;                          // diagnostics only (0 in production): bit 0 skip MFMA, 1 skip stores, 2 skip loads
-  int epi_bf16;                     // 1: output tile staged in bf16 (forward launches: no accumulate / mask,
-                                    //    same bits, half the LDS); 0: fp32 tile (exact accumulate)
+  int epi_bf16;                     // 1: forward launch (no accumulate / mask; prec 0 stages the output tile in
+                                    //    bf16: same bits, half the LDS); 0: fp32 tile (exact accumulate)
+  int prec;                         // 0: bf16 tensors, bf16 MFMA; 1: fp32 tensors, split-fp32 MFMA (common.h)
+  long wps;                         // weight plane stride in elements (prec 1)
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,
-                                              const uint16_t* const* out_mask) {
+                                              const void* const* out_mask) {
   if (gtab) return gtab[y];
   GroupRec r;
   r.g = y;
@@ -57,15 +63,19 @@ __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n
 
 // Weight gradient (split-K, deterministic partials).
 struct WgradArgs {
-  const uint16_t* in[GT_MAXSLOT];   // input slots of the layer [Q][B][H][W][Cinp] (summed per group)
+  const void* in[GT_MAXSLOT];       // input slots of the layer [Q][B][H][W][Cinp] (summed per group)
   const int64_t* gather;     // optional dataset gather (first layer)
   const StepState* st;
-  const uint16_t* dz;        // ReLU-masked grad of the layer output [G][B][H][W][Coutp]
+  const void* dz;            // ReLU-masked grad of the layer output [G][B][H][W][Coutp]
   float* part_w;             // [S][G][Coutp][Kdim]
   float* part_b;             // [S][G][Coutp]
   const GroupRec* gtab;      // [n_groups] or null (legacy: all G groups, inputs 0..n_in-1)
   int n_in;
   int G, B, H, W, Cinp, Coutp, KH, KW, S, pps;  // pps = pixels per split (multiple of 64)
   int ngroups;
+  int prec;                  // 0: bf16 tensors; 1: fp32 tensors (split-fp32 MFMA)
 };
+
+// "> 0" on a stored activation: bf16 bits (sign clear, not +0) or fp32
+__device__ __forceinline__ bool pos_bits(uint32_t h) { return h != 0u && h < 0x8000u; }
 

@@ -37,8 +37,11 @@
 #define CF_WPE 5   // minimum waves per SIMD the register allocator must allow
 #endif
 
-template <int PXG>   // 16-pixel groups per wave (tile = 64 * PXG pixels)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG == 4 ? 3 : CF_WPE))) conv_fwd_kernel(ConvArgs a) {
+template <int PXG, int PREC>   // 16-pixel groups per wave (tile = 64 * PXG pixels); precision (cnn_args.h)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PREC ? 2 : (PXG == 4 ? 3 : CF_WPE))))
+conv_fwd_kernel(ConvArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   // tile = NI whole images (small images: the launcher passes TH = NI * H so
@@ -56,38 +59,45 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
   const int ncb = a.Cinp >> 3;
   const long img = (long)a.H * a.W * a.Cinp;
   const int pimg = PH * PW * ncb;                       // patch chunks per image
-  const int total = NI * pimg;
+  const int total = NI * pimg;                          // patch chunks per plane
   const int nchunks = a.KH * a.KW * ncb;
   const int Kdim = a.KH * a.KW * a.Cinp;
-  // LDS carve: [weight blocks: nbuf x wrows x CF_WLD][patch][chunk offset table].
+  // LDS carve: [weight blocks: NPL x nbuf x wrows x CF_WLD][patch: NPL x total][chunk offset table].
   // Only as many weight rows / buffers as this layer needs (occupancy).
   const int nkb = (nchunks + CF_KB - 1) / CF_KB;
   const int nbuf = nkb > 1 ? 2 : 1;
   const int wrows = ((min(64, a.Coutp) + 15) >> 4) << 4;
-  const size_t wbytes = (size_t)nbuf * wrows * CF_WLD * 2;
+  const int wplane = nbuf * wrows * CF_WLD;             // elements per weight plane
+  const size_t wbytes = (size_t)NPL * wplane * 2;
   uint16_t* wbuf = reinterpret_cast<uint16_t*>(smem);
   uint4* patch = reinterpret_cast<uint4*>(smem + wbytes);
-  int* coff = reinterpret_cast<int*>(smem + wbytes + (size_t)total * 16);
+  int* coff = reinterpret_cast<int*>(smem + wbytes + (size_t)NPL * total * 16);
   const uint16_t* wg = a.w + (long)g * a.Coutp * Kdim;
 
-  // weight-block staging role: row = tid >> 2 (up to 64 rows), 8 chunks per thread
+  // weight-block staging role: row = tid >> 2 (up to 64 rows), 4 chunks per thread and plane
   const int wr = tid >> 2, wq = (tid & 3) * (CF_KB / 4);
   const bool wrow_live = wr < wrows;
   const bool wrow_ok = co_blk + wr < a.Coutp;
   const uint16_t* wsrc = wg + (long)(co_blk + wr) * Kdim;
-  uint4 wreg[CF_KB / 4];
+  uint4 wreg[NPL][CF_KB / 4];
   auto load_wblock = [&](int kb) {
 #pragma unroll
-    for (int j = 0; j < CF_KB / 4; ++j) {
-      const int c = kb * CF_KB + wq + j;
-      wreg[j] = (wrow_ok && c < nchunks) ? *reinterpret_cast<const uint4*>(wsrc + c * 8) : make_uint4(0, 0, 0, 0);
-    }
+    for (int q = 0; q < NPL; ++q)
+#pragma unroll
+      for (int j = 0; j < CF_KB / 4; ++j) {
+        const int c = kb * CF_KB + wq + j;
+        wreg[q][j] = (wrow_ok && c < nchunks) ? *reinterpret_cast<const uint4*>(wsrc + q * a.wps + c * 8)
+                                              : make_uint4(0, 0, 0, 0);
+      }
   };
   auto store_wblock = [&](int buf) {
     if (!wrow_live) return;
-    uint16_t* dst = wbuf + buf * wrows * CF_WLD + wr * CF_WLD + wq * 8;
 #pragma unroll
-    for (int j = 0; j < CF_KB / 4; ++j) *reinterpret_cast<uint4*>(dst + j * 8) = wreg[j];
+    for (int q = 0; q < NPL; ++q) {
+      uint16_t* dst = wbuf + q * wplane + buf * wrows * CF_WLD + wr * CF_WLD + wq * 8;
+#pragma unroll
+      for (int j = 0; j < CF_KB / 4; ++j) *reinterpret_cast<uint4*>(dst + j * 8) = wreg[q][j];
+    }
   };
   load_wblock(0);
 
@@ -101,32 +111,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
     div_pw.divmod(pix, pr, pc);
     const int cb = (int)cbu, b = b0 + (int)im;
     const int hh = h0 - ph + (int)pr, ww = (int)pc - pw;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     uint4 v = make_uint4(0, 0, 0, 0);
+    bool raw = false;                                   // prec 0 single source: v holds the bf16 chunk as is
     if (b < a.B && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) {
       const long off = ((long)hh * a.W + ww) * a.Cinp + cb * 8;
       const long ioff = ((long)g * a.B + b) * img;
-      const uint16_t* msrc = a.mask ? a.mask + ioff : nullptr;
+      const AT* msrc = a.mask ? static_cast<const AT*>(a.mask) + ioff : nullptr;
       if (a.gather) {
-        v = *reinterpret_cast<const uint4*>(a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img + off);
+        const AT* src = static_cast<const AT*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img + off;
+        if (PREC) ld_chunk(src, acc); else { v = *reinterpret_cast<const uint4*>(src); raw = true; }
       } else if (n_src == 1 && !msrc) {
-        v = *reinterpret_cast<const uint4*>(a.in[__builtin_ctz(gr.in_mask | 0x100) & 7] + ioff + off);
+        const AT* src = static_cast<const AT*>(a.in[__builtin_ctz(gr.in_mask | 0x100) & 7]) + ioff + off;
+        if (PREC) ld_chunk(src, acc); else { v = *reinterpret_cast<const uint4*>(src); raw = true; }
       } else {
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, t[8];
+        float t[8];
         for (int k = 0; k < GT_MAXSLOT; ++k) {
           if (!((gr.in_mask >> k) & 1)) continue;
-          unpack8(*reinterpret_cast<const uint4*>(a.in[k] + ioff + off), t);
+          ld_chunk(static_cast<const AT*>(a.in[k]) + ioff + off, t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[j] += t[j];
         }
         if (msrc) {
-          unpack8(*reinterpret_cast<const uint4*>(msrc + off), t);
+          ld_chunk(msrc + off, t);
 #pragma unroll
           for (int j = 0; j < 8; ++j) acc[j] = t[j] > 0.f ? acc[j] : 0.f;
         }
-        v = pack8(acc);
       }
     }
-    patch[i] = v;
+    if (PREC) {
+      split8(acc, patch[i], patch[total + i], patch[2 * total + i]);
+    } else {
+      patch[i] = raw ? v : pack8(acc);
+    }
   }
   if (a.xsum && n_src > 1) {
     // the summed input of this tile (patch interiors) for the layer's wgrad
@@ -137,8 +154,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
       const int cb = q % ncb, pix = q / ncb;
       const int r = pix / a.W, cc = pix % a.W;
       if (b0 + im < a.B && h0 + r < a.H) {
-        uint16_t* xo = a.xsum + ((long)g * a.B + b0 + im) * img + (long)h0 * a.W * a.Cinp;
-        *reinterpret_cast<uint4*>(xo + (long)q * 8) = patch[im * pimg + ((r + ph) * PW + cc + pw) * ncb + cb];
+        AT* xo = static_cast<AT*>(a.xsum) + ((long)g * a.B + b0 + im) * img + (long)h0 * a.W * a.Cinp + (long)q * 8;
+        const int pi = im * pimg + ((r + ph) * PW + cc + pw) * ncb + cb;
+        if (PREC) {
+          float f[8];
+          join8(patch[pi], patch[total + pi], patch[2 * total + pi], f);
+          st_chunk(xo, f);
+        } else {
+          *reinterpret_cast<uint4*>(xo) = patch[pi];
+        }
       }
     }
   }
@@ -158,7 +182,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
   store_wblock(0);
   __syncthreads();
 
-  // ---- MFMA main loop: each wave = 32 pixels (2 B fragments) x all co tiles --
+  // ---- MFMA main loop: each wave = 16*PXG pixels x all co tiles --------------
   const int wave = tid >> 6, lane = tid & 63;
   const int kq = lane >> 4, l16 = lane & 15;
   const int ipx = THr * a.W;                            // tile pixels per image
@@ -191,16 +215,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
       const int c = kb * CF_KB + kk * 4 + kq;
       if (kb * CF_KB + kk * 4 >= nchunks) break;
       const int co_off = coff[c];
-      uint4 bfr[PXG];
+      uint4 bfr[PXG][NPL];
 #pragma unroll
       for (int h = 0; h < PXG; ++h)
-        bfr[h] = (co_off >= 0 && pvalid[h]) ? patch[pbase[h] + co_off] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < NPL; ++q)
+          bfr[h][q] = (co_off >= 0 && pvalid[h]) ? patch[q * total + pbase[h] + co_off] : make_uint4(0, 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (t < NT) {
-          const uint4 af = *reinterpret_cast<const uint4*>(wcur + (t * 16 + l16) * CF_WLD + (kk * 4 + kq) * 8);
+          uint4 af[NPL];
 #pragma unroll
-          for (int h = 0; h < PXG; ++h) acc[h][t] = mfma16(af, bfr[h], acc[h][t]);
+          for (int q = 0; q < NPL; ++q)
+            af[q] = *reinterpret_cast<const uint4*>(wcur + q * wplane + (t * 16 + l16) * CF_WLD + (kk * 4 + kq) * 8);
+#pragma unroll
+          for (int h = 0; h < PXG; ++h) acc[h][t] = mfma_np<NPL>(af, bfr[h], acc[h][t]);
         }
       }
     }
@@ -228,21 +257,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PXG ==
       }
       for (int k = 0; k < GT_MAXSLOT; ++k) {
         if (!((gr.out_mask >> k) & 1)) continue;
-        uint2* dst = reinterpret_cast<uint2*>(a.out[k] + obase + co0);
+        AT* dst = static_cast<AT*>(a.out[k]) + obase + co0;
         float sum[4] = {v[0], v[1], v[2], v[3]};
+        float o[4];
         if ((gr.out_mask >> (8 + k)) & 1) {
-          const uint2 old = *dst;
-          sum[0] += __uint_as_float(old.x << 16); sum[1] += __uint_as_float(old.x & 0xffff0000u);
-          sum[2] += __uint_as_float(old.y << 16); sum[3] += __uint_as_float(old.y & 0xffff0000u);
+          if (PREC) { const float4 q = *reinterpret_cast<const float4*>(dst); o[0] = q.x; o[1] = q.y; o[2] = q.z; o[3] = q.w; }
+          else { const uint2 q = *reinterpret_cast<const uint2*>(dst);
+                 o[0] = __uint_as_float(q.x << 16); o[1] = __uint_as_float(q.x & 0xffff0000u);
+                 o[2] = __uint_as_float(q.y << 16); o[3] = __uint_as_float(q.y & 0xffff0000u); }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sum[i] += o[i];
         }
         if ((gr.out_mask >> (16 + k)) & 1) {
-          const uint2 m = *reinterpret_cast<const uint2*>(a.out_mask[k] + obase + co0);
-          // bf16 > 0  <=>  sign bit clear and not +0
-          const uint32_t mw[4] = {m.x & 0xffffu, m.x >> 16, m.y & 0xffffu, m.y >> 16};
+          const AT* msrc = static_cast<const AT*>(a.out_mask[k]) + obase + co0;
+          if (PREC) { const float4 q = *reinterpret_cast<const float4*>(msrc); o[0] = q.x; o[1] = q.y; o[2] = q.z; o[3] = q.w; }
+          else { const uint2 q = *reinterpret_cast<const uint2*>(msrc);
+                 o[0] = __uint_as_float(q.x << 16); o[1] = __uint_as_float(q.x & 0xffff0000u);
+                 o[2] = __uint_as_float(q.y << 16); o[3] = __uint_as_float(q.y & 0xffff0000u); }
 #pragma unroll
-          for (int i = 0; i < 4; ++i) sum[i] = (mw[i] != 0u && mw[i] < 0x8000u) ? sum[i] : 0.f;
+          for (int i = 0; i < 4; ++i) sum[i] = o[i] > 0.f ? sum[i] : 0.f;
         }
-        *dst = pack4(sum);
+        if (PREC) *reinterpret_cast<float4*>(dst) = make_float4(sum[0], sum[1], sum[2], sum[3]);
+        else *reinterpret_cast<uint2*>(dst) = pack4(sum);
       }
     }
   }
@@ -279,12 +315,12 @@ __device__ __forceinline__ uint4 tr_frag(const uint16_t* tile, int col0, int lan
 //   im2col   [64 px][64 col]: slot i -> (col chunk i / 64 (wave-uniform), pixel
 //                             i % 64 = lane): a wave reads 64 consecutive
 //                             pixels at one (kh, kw, cb) shift.
-struct WgSlots {
-  uint4 dz[2], xs[2];
-};
-
+// PREC 1: the chunks are fp32, staged as three exact bf16 planes per tile.
+template <int PREC>
 __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[4 * WG_TILE];   // 2 buffers x (dz, im2col)
+  typedef typename ActT<PREC>::T AT;
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * NPL * WG_TILE];   // 2 buffers x (dz, im2col) x planes
   const int tid = threadIdx.x;
   const int nb = blockIdx.x;
   const int s = blockIdx.y;
@@ -302,6 +338,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   const int ndz = 64 * ncc;                                   // dz slots per K-step (<= 512)
   const int wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
   const FastDiv div_ncc(ncc), div_hw((uint32_t)HW), div_w(a.W), div_ncb(ncb), div_kw(a.KW);
+  auto tile = [&](int bf, int which, int q) { return lds + ((bf * 2 + which) * NPL + q) * WG_TILE; };
 
   // im2col roles: this thread stages column chunks (wave, wave + 4) of the block
   // column chunk Kdim/8 is the bias chunk: a column of ones, so dW and db come
@@ -317,11 +354,12 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
     if (c_ok[r]) { div_ncb.divmod((uint32_t)(col >> 3), kk, cb); div_kw.divmod(kk, kh, kw); }
     c_kh[r] = (int)kh - (a.KH >> 1); c_kw[r] = (int)kw - (a.KW >> 1); c_cb[r] = (int)cb;
   }
-  const uint16_t* fold_in[GT_MAXSLOT];
+  const AT* fold_in[GT_MAXSLOT];
   int n_src = 0;
   for (int k = 0; k < GT_MAXSLOT; ++k)
-    if ((gr.in_mask >> k) & 1) fold_in[n_src++] = a.in[k] + (long)g * a.B * HW * a.Cinp;
+    if ((gr.in_mask >> k) & 1) fold_in[n_src++] = static_cast<const AT*>(a.in[k]) + (long)g * a.B * HW * a.Cinp;
   const long fold_out = (long)g * npix * a.Coutp;
+  const AT* dzp = static_cast<const AT*>(a.dz);
 
   const int MT = (min(64, a.Coutp - co_blk) + 15) >> 4;
   const bool wave_live = nb * 64 + wave * 16 <= Kdim;
@@ -329,70 +367,79 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  WgSlots sl;
+  float dzf[2][8], xsf[2][8];
   auto load_step = [&](long p0) {
     // dz (masked by the layer's own ReLU output)
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int i = tid + 256 * r;
-      sl.dz[r] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dzf[r][e] = 0.f;
       if (i < ndz) {
         uint32_t px, cc;
         div_ncc.divmod((uint32_t)i, px, cc);
         const long p = p0 + px;
-        if (p < p_end) sl.dz[r] = *reinterpret_cast<const uint4*>(a.dz + fold_out + p * a.Coutp + co_blk + cc * 8);
+        if (p < p_end) ld_chunk(dzp + fold_out + p * a.Coutp + co_blk + cc * 8, dzf[r]);
       }
     }
     // im2col: lane = pixel
     const long p = p0 + lane;
     uint32_t bq = 0, rem = 0, hq = 0, wq = 0;
     if (p < p_end) { div_hw.divmod((uint32_t)p, bq, rem); div_w.divmod(rem, hq, wq); }
-    const uint16_t* gimg = nullptr;
+    const AT* gimg = nullptr;
     if (a.gather && p < p_end)
-      gimg = a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + bq] * HW * a.Cinp;
+      gimg = static_cast<const AT*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + g) * a.B + bq] * HW * a.Cinp;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      sl.xs[r] = make_uint4(0, 0, 0, 0);
-      if (c_one[r] && p < p_end) sl.xs[r].x = 0x3f80u;          // bf16 1.0 in element 0
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xsf[r][e] = 0.f;
+      if (c_one[r] && p < p_end) xsf[r][0] = 1.f;              // 1.0 in element 0 (exact in every plane split)
       const int ih = (int)hq + c_kh[r], iw = (int)wq + c_kw[r];
       if (p < p_end && c_ok[r] && ih >= 0 && ih < a.H && iw >= 0 && iw < a.W) {
         const long pix_off = ((long)ih * a.W + iw) * a.Cinp + c_cb[r] * 8;
         if (gimg) {
-          sl.xs[r] = *reinterpret_cast<const uint4*>(gimg + pix_off);
-        } else if (n_src == 1) {
-          sl.xs[r] = *reinterpret_cast<const uint4*>(fold_in[0] + (long)bq * HW * a.Cinp + pix_off);
+          ld_chunk(gimg + pix_off, xsf[r]);
         } else {
-          float xsum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t[8];
+          float t[8];
           for (int k = 0; k < n_src; ++k) {
-            unpack8(*reinterpret_cast<const uint4*>(fold_in[k] + (long)bq * HW * a.Cinp + pix_off), t);
+            ld_chunk(fold_in[k] + (long)bq * HW * a.Cinp + pix_off, t);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) xsum[j] += t[j];
+            for (int j = 0; j < 8; ++j) xsf[r][j] += t[j];
           }
-          sl.xs[r] = pack8(xsum);
         }
       }
     }
   };
+  auto put = [&](uint16_t* t0, int off, const float* f) {
+    if (PREC) {
+      uint4 p0, p1, p2;
+      split8(f, p0, p1, p2);
+      *reinterpret_cast<uint4*>(t0 + off) = p0;
+      *reinterpret_cast<uint4*>(t0 + WG_TILE + off) = p1;
+      *reinterpret_cast<uint4*>(t0 + 2 * WG_TILE + off) = p2;
+    } else {
+      *reinterpret_cast<uint4*>(t0 + off) = pack8(f);
+    }
+  };
   auto store_step = [&](int bf) {
-    uint16_t* dzT = lds + bf * 2 * WG_TILE;
-    uint16_t* colT = dzT + WG_TILE;
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int i = tid + 256 * r;
       if (i < ndz) {
         uint32_t px, cc;
         div_ncc.divmod((uint32_t)i, px, cc);
-        *reinterpret_cast<uint4*>(&dzT[px * WG_LD + cc * 8]) = sl.dz[r];
+        put(tile(bf, 0, 0), px * WG_LD + cc * 8, dzf[r]);
       }
-      *reinterpret_cast<uint4*>(&colT[lane * WG_LD + (wave + 4 * r) * 8]) = sl.xs[r];
+      put(tile(bf, 1, 0), lane * WG_LD + (wave + 4 * r) * 8, xsf[r]);
     }
   };
   // dz columns beyond this block's channels must read as zero
   if (ncc < 8) {
-    for (int i = tid; i < 2 * 64 * (8 - ncc); i += 256) {
-      const int bf = i / (64 * (8 - ncc)), rem = i % (64 * (8 - ncc));
+    for (int i = tid; i < 2 * NPL * 64 * (8 - ncc); i += 256) {
+      const int per = 64 * (8 - ncc);
+      const int bq = i / per, rem = i % per;          // bq = buffer * NPL + plane
       const int px = rem / (8 - ncc), cc = ncc + rem % (8 - ncc);
-      *reinterpret_cast<uint4*>(&lds[bf * 2 * WG_TILE + px * WG_LD + cc * 8]) = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(tile(bq / NPL, 0, bq % NPL) + px * WG_LD + cc * 8) = make_uint4(0, 0, 0, 0);
     }
   }
   load_step(p_begin);
@@ -402,17 +449,19 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
   for (long p0 = p_begin; p0 < p_end; p0 += 64) {
     const bool more = p0 + 64 < p_end;
     if (more) load_step(p0 + 64);
-    const uint16_t* dzT = lds + buf * 2 * WG_TILE;
-    const uint16_t* colT = dzT + WG_TILE;
     if (wave_live) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const uint4 bfrag = tr_frag(colT + h * 32 * WG_LD, wave * 16, lane);
+        uint4 bfrag[NPL];
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) bfrag[q] = tr_frag(tile(buf, 1, q) + h * 32 * WG_LD, wave * 16, lane);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           if (t < MT) {
-            const uint4 afrag = tr_frag(dzT + h * 32 * WG_LD, t * 16, lane);
-            acc[t] = mfma16(afrag, bfrag, acc[t]);
+            uint4 afrag[NPL];
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) afrag[q] = tr_frag(tile(buf, 0, q) + h * 32 * WG_LD, t * 16, lane);
+            acc[t] = mfma_np<NPL>(afrag, bfrag, acc[t]);
           }
         }
       }
@@ -449,11 +498,12 @@ __global__ void __launch_bounds__(256) conv_wgrad_kernel(WgradArgs a) {
 // ---------------------------------------------------------------------------
 // 2x2/2 max-pool (floor) and its backward scatter. Per group the source slot
 // is x0 or x1 (sel[g]): a stage without a DAG pools its input conv, a stage
-// with one pools its output conv.
+// with one pools its output conv. AT = bf16 (uint16_t) or fp32 storage.
 // ---------------------------------------------------------------------------
 
-__global__ void pool_fwd_kernel(const uint16_t* __restrict__ x0, const uint16_t* __restrict__ x1,
-                                const int* __restrict__ sel, uint16_t* __restrict__ y, int NB, int B, int H, int W,
+template <typename AT>
+__global__ void pool_fwd_kernel(const AT* __restrict__ x0, const AT* __restrict__ x1,
+                                const int* __restrict__ sel, AT* __restrict__ y, int NB, int B, int H, int W,
                                 int Cp, uint8_t* __restrict__ mask) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
   const uint32_t total = (uint32_t)NB * Ho * Wo * ncb;       // < 2^31 (host-checked): 32-bit index math
@@ -463,20 +513,20 @@ __global__ void pool_fwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
     const int wo = (int)(r % Wo); r /= Wo;
     const int ho = (int)(r % Ho);
     const long n = r / Ho;
-    const uint16_t* x = (sel && sel[n / B]) ? x1 : x0;
-    const uint16_t* base = x + ((n * H + 2 * ho) * W + 2 * wo) * Cp + cb * 8;
+    const AT* x = (sel && sel[n / B]) ? x1 : x0;
+    const AT* base = x + ((n * H + 2 * ho) * W + 2 * wo) * Cp + cb * 8;
     float m[8], t[8];
     int arg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unpack8(*reinterpret_cast<const uint4*>(base), m);
+    ld_chunk(base, m);
     const long offs[3] = {(long)Cp, (long)W * Cp, (long)W * Cp + Cp};
     for (int q = 0; q < 3; ++q) {
-      unpack8(*reinterpret_cast<const uint4*>(base + offs[q]), t);
+      ld_chunk(base + offs[q], t);
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (t[j] > m[j]) { m[j] = t[j]; arg[j] = q + 1; }      // first strict maximum, as pool_bwd_kernel
     }
     const long o = ((n * Ho + ho) * Wo + wo) * Cp + cb * 8;
-    *reinterpret_cast<uint4*>(y + o) = pack8(m);
+    st_chunk(y + o, m);
     if (mask) {
       // per channel: bits 0-1 = which of the 4 cell pixels holds the maximum, bit 2 = maximum > 0
       uint32_t lo = 0, hi = 0;
@@ -491,9 +541,10 @@ __global__ void pool_fwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
 
 // dx[pixel] = dy[pool cell] if pixel is the cell's first maximum (and, with
 // relu_mask, the maximum is > 0) else 0; dx / x slot chosen per group by sel
-__global__ void pool_bwd_kernel(const uint16_t* __restrict__ x0, const uint16_t* __restrict__ x1,
-                                const int* __restrict__ sel, const uint16_t* __restrict__ dy,
-                                uint16_t* __restrict__ dx0, uint16_t* __restrict__ dx1, int NB, int B, int H, int W,
+template <typename AT>
+__global__ void pool_bwd_kernel(const AT* __restrict__ x0, const AT* __restrict__ x1,
+                                const int* __restrict__ sel, const AT* __restrict__ dy,
+                                AT* __restrict__ dx0, AT* __restrict__ dx1, int NB, int B, int H, int W,
                                 int Cp, int relu_mask) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
   const uint32_t total = (uint32_t)NB * H * W * ncb;         // < 2^31 (host-checked): 32-bit index math
@@ -504,19 +555,19 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
     const int h = (int)(r % H);
     const long n = r / H;
     const bool s1 = sel && sel[n / B];
-    const uint16_t* x = s1 ? x1 : x0;
-    uint16_t* dx = s1 ? dx1 : dx0;
+    const AT* x = s1 ? x1 : x0;
+    AT* dx = s1 ? dx1 : dx0;
     float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int ho = h >> 1, wo = w >> 1;
     if (ho < Ho && wo < Wo) {
-      const uint16_t* base = x + ((n * H + 2 * ho) * W + 2 * wo) * Cp + cb * 8;
+      const AT* base = x + ((n * H + 2 * ho) * W + 2 * wo) * Cp + cb * 8;
       float v[4][8];
-      unpack8(*reinterpret_cast<const uint4*>(base), v[0]);
-      unpack8(*reinterpret_cast<const uint4*>(base + Cp), v[1]);
-      unpack8(*reinterpret_cast<const uint4*>(base + (long)W * Cp), v[2]);
-      unpack8(*reinterpret_cast<const uint4*>(base + (long)W * Cp + Cp), v[3]);
+      ld_chunk(base, v[0]);
+      ld_chunk(base + Cp, v[1]);
+      ld_chunk(base + (long)W * Cp, v[2]);
+      ld_chunk(base + (long)W * Cp + Cp, v[3]);
       float g[8];
-      unpack8(*reinterpret_cast<const uint4*>(dy + ((n * Ho + ho) * Wo + wo) * Cp + cb * 8), g);
+      ld_chunk(dy + ((n * Ho + ho) * Wo + wo) * Cp + cb * 8, g);
       const int me = (h & 1) * 2 + (w & 1);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -526,17 +577,18 @@ __global__ void pool_bwd_kernel(const uint16_t* __restrict__ x0, const uint16_t*
         out[j] = (arg == me && (!relu_mask || m > 0.f)) ? g[j] : 0.f;
       }
     }
-    *reinterpret_cast<uint4*>(dx + ((n * H + h) * W + w) * Cp + cb * 8) = pack8(out);
+    st_chunk(dx + ((n * H + h) * W + w) * Cp + cb * 8, out);
   }
 }
 
 // Backward scatter from the forward's argmax mask (1 byte per pooled channel
-// instead of re-reading the 4 bf16 cell inputs: the pool_bwd traffic drops from
+// instead of re-reading the 4 cell inputs: the pool_bwd traffic drops from
 // x + dy + dx to mask + dy + dx). Same first-maximum rule, so dx is identical
 // to pool_bwd_kernel's.
+template <typename AT>
 __global__ void pool_bwd_mask_kernel(const uint8_t* __restrict__ mask, const int* __restrict__ sel,
-                                     const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx0,
-                                     uint16_t* __restrict__ dx1, int NB, int B, int H, int W, int Cp, int relu_mask) {
+                                     const AT* __restrict__ dy, AT* __restrict__ dx0,
+                                     AT* __restrict__ dx1, int NB, int B, int H, int W, int Cp, int relu_mask) {
   const int Ho = H >> 1, Wo = W >> 1, ncb = Cp >> 3;
   const uint32_t total = (uint32_t)NB * H * W * ncb;         // < 2^31 (host-checked): 32-bit index math
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
@@ -545,14 +597,14 @@ __global__ void pool_bwd_mask_kernel(const uint8_t* __restrict__ mask, const int
     const int w = (int)(r % W); r /= W;
     const int h = (int)(r % H);
     const long n = r / H;
-    uint16_t* dx = (sel && sel[n / B]) ? dx1 : dx0;
+    AT* dx = (sel && sel[n / B]) ? dx1 : dx0;
     float out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const int ho = h >> 1, wo = w >> 1;
     if (ho < Ho && wo < Wo) {
       const long o = ((n * Ho + ho) * Wo + wo) * Cp + cb * 8;
       const uint2 mk = *reinterpret_cast<const uint2*>(mask + o);
       float g[8];
-      unpack8(*reinterpret_cast<const uint4*>(dy + o), g);
+      ld_chunk(dy + o, g);
       const uint32_t me = (uint32_t)((h & 1) * 2 + (w & 1));
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -560,7 +612,7 @@ __global__ void pool_bwd_mask_kernel(const uint8_t* __restrict__ mask, const int
         out[j] = ((b & 3u) == me && (!relu_mask || (b & 4u))) ? g[j] : 0.f;
       }
     }
-    *reinterpret_cast<uint4*>(dx + ((n * H + h) * W + w) * Cp + cb * 8) = pack8(out);
+    st_chunk(dx + ((n * H + h) * W + w) * Cp + cb * 8, out);
   }
 }
 
@@ -571,10 +623,56 @@ __global__ void pool_bwd_mask_kernel(const uint8_t* __restrict__ mask, const int
 extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream);
 extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream);
 
-extern "C" {
-
 static int g_conv_fast = 1;   // shape-specialised kernels (cnn_conv_fast.hip) where one matches
 static int g_conv_imgs = 2;   // max whole small images per generic-conv workgroup (2: measured best, deep space)
+
+template <typename F>
+static void set_lds_limit(F* fn, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)bytes);
+}
+
+template <int PREC>
+static int conv_fwd_generic(const ConvArgs* a, hipStream_t stream) {
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
+  const int nchunks = a->KH * a->KW * (a->Cinp / 8);
+  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
+  const int wrows = ((std::min(64, a->Coutp) + 15) / 16) * 16;
+  auto lds_of = [&](int ni, int th) {
+    const size_t total = (size_t)ni * (th + a->KH - 1) * (a->W + a->KW - 1) * (a->Cinp / 8);
+    return (size_t)NPL * ((size_t)(nkb > 1 ? 2 : 1) * wrows * CF_WLD * 2 + total * 16) + 4 * ((size_t)nchunks + 4);
+  };
+  // small images: several whole images per workgroup (up to 256 pixels), so
+  // one staged weight block serves 4x the pixels (8x8 stages: weight traffic
+  // per image was 6x the patch's)
+  int ni = 1;
+  if (a->TH == a->H && 2 * a->H * a->W <= 256) {
+    ni = std::min(g_conv_imgs, 256 / (a->H * a->W));
+    while (ni > 1 && lds_of(ni, a->H) > 160 * 1024) --ni;
+  }
+  ConvArgs t = *a;
+  // fp32 planes triple the patch: shrink the row band until it fits
+  while (ni == 1 && lds_of(1, t.TH) > 160 * 1024 && t.TH > 1) t.TH = (t.TH + 1) / 2;
+  if (lds_of(ni, t.TH) > 160 * 1024) return -3;
+  if (ni > 1) t.TH = ni * a->H;                      // kernel: TH > H = ni whole images per tile
+  const int nth = ni > 1 ? 1 : (a->H + t.TH - 1) / t.TH;
+  const int tile = ni > 1 ? ni * a->H * a->W : t.TH * a->W;
+  const size_t lds = lds_of(ni, ni > 1 ? a->H : t.TH);
+  dim3 grid(((a->B + ni - 1) / ni) * nth, a->ngroups, (a->Coutp + 63) / 64);
+  if (tile > 128) {
+    set_lds_limit(conv_fwd_kernel<4, PREC>, lds);
+    hipLaunchKernelGGL((conv_fwd_kernel<4, PREC>), grid, dim3(256), lds, stream, t);
+  } else if (tile > 64) {
+    set_lds_limit(conv_fwd_kernel<2, PREC>, lds);
+    hipLaunchKernelGGL((conv_fwd_kernel<2, PREC>), grid, dim3(256), lds, stream, t);
+  } else {
+    set_lds_limit(conv_fwd_kernel<1, PREC>, lds);
+    hipLaunchKernelGGL((conv_fwd_kernel<1, PREC>), grid, dim3(256), lds, stream, t);
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" {
 
 int gt_conv_set_imgs(int n) {
   const int old = g_conv_imgs;
@@ -590,6 +688,7 @@ int gt_conv_set_fast(int on) {
 
 int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   if (a->Cinp % 8 || a->Coutp % 8) return -1;
+  if (a->prec != 0 && a->prec != 1) return -1;
   if (g_conv_fast && a->ngroups >= 1) {
     const int rc = gt_conv_fast(a, stream);
     if (rc != -100) return rc;
@@ -597,39 +696,12 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
   if (!a->gtab && (a->n_in < 1 || a->n_in > GT_MAXSLOT || a->n_out < 1 || a->n_out > GT_MAXSLOT)) return -1;
   if (a->TH * a->W > 256 || a->TH < 1 || a->TH > a->H) return -2;
   if (a->ngroups < 1) return 0;
-  const int nchunks = a->KH * a->KW * (a->Cinp / 8);
-  const int nkb = (nchunks + CF_KB - 1) / CF_KB;
-  const int wrows = ((std::min(64, a->Coutp) + 15) / 16) * 16;
-  auto lds_of = [&](int ni, int th) {
-    const size_t total = (size_t)ni * (th + a->KH - 1) * (a->W + a->KW - 1) * (a->Cinp / 8);
-    return (size_t)(nkb > 1 ? 2 : 1) * wrows * CF_WLD * 2 + total * 16 + 4 * ((size_t)nchunks + 4);
-  };
-  // small images: several whole images per workgroup (up to 256 pixels), so
-  // one staged weight block serves 4x the pixels (8x8 stages: weight traffic
-  // per image was 6x the patch's)
-  int ni = 1;
-  if (a->TH == a->H && 2 * a->H * a->W <= 256) {
-    ni = std::min(g_conv_imgs, 256 / (a->H * a->W));
-    while (ni > 1 && lds_of(ni, a->H) > 160 * 1024) --ni;
-  }
-  if (lds_of(ni, a->TH) > 160 * 1024) return -3;
-  ConvArgs t = *a;
-  if (ni > 1) t.TH = ni * a->H;                      // kernel: TH > H = ni whole images per tile
-  const int nth = ni > 1 ? 1 : (a->H + a->TH - 1) / a->TH;
-  const int tile = ni > 1 ? ni * a->H * a->W : a->TH * a->W;
-  const size_t lds = lds_of(ni, ni > 1 ? a->H : a->TH);
-  dim3 grid(((a->B + ni - 1) / ni) * nth, a->ngroups, (a->Coutp + 63) / 64);
-  if (tile > 128)
-    hipLaunchKernelGGL(conv_fwd_kernel<4>, grid, dim3(256), lds, stream, t);
-  else if (tile > 64)
-    hipLaunchKernelGGL(conv_fwd_kernel<2>, grid, dim3(256), lds, stream, t);
-  else
-    hipLaunchKernelGGL(conv_fwd_kernel<1>, grid, dim3(256), lds, stream, t);
-  return (int)hipGetLastError();
+  return a->prec ? conv_fwd_generic<1>(a, stream) : conv_fwd_generic<0>(a, stream);
 }
 
 int gt_conv_wgrad(const WgradArgs* a, hipStream_t stream) {
   if (a->Cinp % 8 || a->Coutp % 8 || a->pps % 64) return -1;
+  if (a->prec != 0 && a->prec != 1) return -1;
   if (!a->gtab && (a->n_in < 1 || a->n_in > GT_MAXSLOT)) return -1;
   if (a->ngroups < 1) return 0;
   if (g_conv_fast) {
@@ -638,49 +710,69 @@ int gt_conv_wgrad(const WgradArgs* a, hipStream_t stream) {
   }
   const int Kdim = a->KH * a->KW * a->Cinp;
   dim3 grid((Kdim + (a->part_b ? 8 : 0) + 63) / 64, a->S, a->ngroups * ((a->Coutp + 63) / 64));
-  hipLaunchKernelGGL(conv_wgrad_kernel, grid, dim3(256), 0, stream, *a);
+  if (a->prec)
+    hipLaunchKernelGGL(conv_wgrad_kernel<1>, grid, dim3(256), 0, stream, *a);
+  else
+    hipLaunchKernelGGL(conv_wgrad_kernel<0>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 
-int gt_pool_fwd(const uint16_t* x0, const uint16_t* x1, const int* sel, uint16_t* y, int NB, int B, int H, int W,
-                int Cp, hipStream_t stream) {
+// pool launchers: prec 0 = bf16 tensors, 1 = fp32
+#define POOL_GRID(total) dim3((int)std::min<long>(((total) + 255) / 256, 16384))
+
+int gt_pool_fwd(const void* x0, const void* x1, const int* sel, void* y, int NB, int B, int H, int W, int Cp,
+                int prec, hipStream_t stream) {
   const long total = (long)NB * (H / 2) * (W / 2) * (Cp / 8);
   if ((long)NB * H * W * (Cp / 8) >= (1L << 31)) return -4;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, y, NB, B, H, W, Cp,
-                     (uint8_t*)nullptr);
+  if (prec)
+    hipLaunchKernelGGL(pool_fwd_kernel<float>, POOL_GRID(total), dim3(256), 0, stream, (const float*)x0,
+                       (const float*)x1, sel, (float*)y, NB, B, H, W, Cp, (uint8_t*)nullptr);
+  else
+    hipLaunchKernelGGL(pool_fwd_kernel<uint16_t>, POOL_GRID(total), dim3(256), 0, stream, (const uint16_t*)x0,
+                       (const uint16_t*)x1, sel, (uint16_t*)y, NB, B, H, W, Cp, (uint8_t*)nullptr);
   return (int)hipGetLastError();
 }
 
 // training forward: also writes the argmax mask [NB][H/2][W/2][Cp] (uint8) for gt_pool_bwd_mask
-int gt_pool_fwd_mask(const uint16_t* x0, const uint16_t* x1, const int* sel, uint16_t* y, int NB, int B, int H,
-                     int W, int Cp, uint8_t* mask, hipStream_t stream) {
+int gt_pool_fwd_mask(const void* x0, const void* x1, const int* sel, void* y, int NB, int B, int H, int W, int Cp,
+                     uint8_t* mask, int prec, hipStream_t stream) {
   const long total = (long)NB * (H / 2) * (W / 2) * (Cp / 8);
   if ((long)NB * H * W * (Cp / 8) >= (1L << 31)) return -4;
   if (Cp % 8 || mask == nullptr) return -1;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(pool_fwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, y, NB, B, H, W, Cp, mask);
+  if (prec)
+    hipLaunchKernelGGL(pool_fwd_kernel<float>, POOL_GRID(total), dim3(256), 0, stream, (const float*)x0,
+                       (const float*)x1, sel, (float*)y, NB, B, H, W, Cp, mask);
+  else
+    hipLaunchKernelGGL(pool_fwd_kernel<uint16_t>, POOL_GRID(total), dim3(256), 0, stream, (const uint16_t*)x0,
+                       (const uint16_t*)x1, sel, (uint16_t*)y, NB, B, H, W, Cp, mask);
   return (int)hipGetLastError();
 }
 
-int gt_pool_bwd_mask(const uint8_t* mask, const int* sel, const uint16_t* dy, uint16_t* dx0, uint16_t* dx1, int NB,
-                     int B, int H, int W, int Cp, int relu_mask, hipStream_t stream) {
+int gt_pool_bwd_mask(const uint8_t* mask, const int* sel, const void* dy, void* dx0, void* dx1, int NB, int B,
+                     int H, int W, int Cp, int relu_mask, int prec, hipStream_t stream) {
   const long total = (long)NB * H * W * (Cp / 8);
   if (total >= (1L << 31)) return -4;
   if (Cp % 8 || mask == nullptr) return -1;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(pool_bwd_mask_kernel, dim3(blocks), dim3(256), 0, stream, mask, sel, dy, dx0, dx1, NB, B, H, W,
-                     Cp, relu_mask);
+  if (prec)
+    hipLaunchKernelGGL(pool_bwd_mask_kernel<float>, POOL_GRID(total), dim3(256), 0, stream, mask, sel,
+                       (const float*)dy, (float*)dx0, (float*)dx1, NB, B, H, W, Cp, relu_mask);
+  else
+    hipLaunchKernelGGL(pool_bwd_mask_kernel<uint16_t>, POOL_GRID(total), dim3(256), 0, stream, mask, sel,
+                       (const uint16_t*)dy, (uint16_t*)dx0, (uint16_t*)dx1, NB, B, H, W, Cp, relu_mask);
   return (int)hipGetLastError();
 }
 
-int gt_pool_bwd(const uint16_t* x0, const uint16_t* x1, const int* sel, const uint16_t* dy, uint16_t* dx0,
-                uint16_t* dx1, int NB, int B, int H, int W, int Cp, int relu_mask, hipStream_t stream) {
+int gt_pool_bwd(const void* x0, const void* x1, const int* sel, const void* dy, void* dx0, void* dx1, int NB, int B,
+                int H, int W, int Cp, int relu_mask, int prec, hipStream_t stream) {
   const long total = (long)NB * H * W * (Cp / 8);
   if (total >= (1L << 31)) return -4;
-  const int blocks = (int)std::min<long>((total + 255) / 256, 16384);
-  hipLaunchKernelGGL(pool_bwd_kernel, dim3(blocks), dim3(256), 0, stream, x0, x1, sel, dy, dx0, dx1, NB, B, H, W,
-                     Cp, relu_mask);
+  if (prec)
+    hipLaunchKernelGGL(pool_bwd_kernel<float>, POOL_GRID(total), dim3(256), 0, stream, (const float*)x0,
+                       (const float*)x1, sel, (const float*)dy, (float*)dx0, (float*)dx1, NB, B, H, W, Cp, relu_mask);
+  else
+    hipLaunchKernelGGL(pool_bwd_kernel<uint16_t>, POOL_GRID(total), dim3(256), 0, stream, (const uint16_t*)x0,
+                       (const uint16_t*)x1, sel, (const uint16_t*)dy, (uint16_t*)dx0, (uint16_t*)dx1, NB, B, H, W,
+                       Cp, relu_mask);
   return (int)hipGetLastError();
 }
 

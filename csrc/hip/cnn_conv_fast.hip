@@ -26,18 +26,20 @@
 
 #include "cnn_args.h"
 
-// LDS bytes of one launch: the patch or the output tile (fp32, or bf16 for
-// forward launches -- measured 7-9 % faster: more workgroups per CU), whichever is larger
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO>
+// LDS bytes of one launch: the patch (NPL bf16 planes) or the output tile
+// (fp32, or bf16 for prec-0 forward launches -- measured 7-9 % faster: more
+// workgroups per CU), whichever is larger
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int PREC>
 struct FastCfg {
+  static constexpr int NPL = PREC ? GT_NPL_F32 : 1;
   static constexpr int PW = W + KW - 1;
   static constexpr int NP = (TH + KH - 1) * PW * NCBI;
   static constexpr int TP = TH * W;
   static constexpr int OROW = NT * 16 + 4;          // fp32 tile row (floats; conflict-free float4 writes)
   static constexpr int OROWB = NT * 16 + 8;         // bf16 tile row (elements; conflict-free 8-byte writes)
-  static size_t lds(bool bf16) {
-    const size_t p = (size_t)NP * 16;
-    const size_t o = bf16 ? (size_t)TP * OROWB * 2 : (size_t)TP * OROW * 4;
+  static size_t lds(bool fwd) {
+    const size_t p = (size_t)NP * 16 * NPL;
+    const size_t o = (fwd && !PREC) ? (size_t)TP * OROWB * 2 : (size_t)TP * OROW * 4;
     return p > o ? p : o;
   }
 };
@@ -46,14 +48,18 @@ struct FastCfg {
 // (<= 128 registers) for 32-channel output tiles, 3 for the 5x5 64-channel
 // tile; the 3x3 56-channel-input tile spills at 3 and keeps 2
 // tile; NWV = 8 waves per workgroup: half the pixels per wave (fewer
-// registers, 4 waves / SIMD) for the same 256-pixel tile
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4>
+// registers, 4 waves / SIMD) for the same 256-pixel tile. PREC 1 (fp32
+// tensors, six-term split MFMA): three operand planes per fragment, LDS-bound
+// at 2-3 workgroups per CU -> 2 waves / SIMD.
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0>
 __global__ void __launch_bounds__(NWV * 64)
-__attribute__((amdgpu_waves_per_eu(NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4))))
+__attribute__((amdgpu_waves_per_eu(PREC ? 2 : (NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))))
 conv_fast_kernel(ConvArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
   constexpr int NTH = NWV * 64;                     // threads
   constexpr int PH = TH + KH - 1, PW = W + KW - 1;
-  constexpr int NP = PH * PW * NCBI;                // patch chunks (16 B)
+  constexpr int NP = PH * PW * NCBI;                // patch chunks (8 channels) per plane
   constexpr int NPT = (NP + NTH - 1) / NTH;             // patch chunks per thread
   constexpr int NCH = KH * KW * NCBI;               // reduction chunks
   constexpr int NKS = (NCH + 3) / 4;                // k-steps (32 k each)
@@ -63,13 +69,14 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int WC = NT / CT;                       // waves along co
   constexpr int WP = NWV / WC;                        // waves along pixels
   constexpr int PG = NPG / WP;                      // pixel groups per wave
-  constexpr int PF = NKS < 4 ? NKS : 4;             // weight prefetch depth (k-steps)
+  constexpr int PFM = PREC ? 2 : 4;                 // weight prefetch depth (k-steps; 3 planes each in prec 1)
+  constexpr int PF = NKS < PFM ? NKS : PFM;
   static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == NWV, "tile shape");
   static_assert(W % 16 == 0 || 16 % W == 0, "pixel groups must tile image rows");
 
-  using FC = FastCfg<KH, KW, NCBI, W, TH, NT, NCO>;
+  using FC = FastCfg<KH, KW, NCBI, W, TH, NT, NCO, PREC>;
   constexpr int OROW = FC::OROW, OROWB = FC::OROWB;
-  extern __shared__ __attribute__((aligned(16))) uint4 smem[];   // patch, then the output tile
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];   // patch planes, then the output tile
   uint4* patch = smem;
   __shared__ int coff[NKS * 4];
 
@@ -99,19 +106,22 @@ conv_fast_kernel(ConvArgs a) {
     wok[t] = co < NCO * 8;
     wrow[t] = a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8);
   }
-  uint4 areg[PF][CT];
-  auto load_a = [&](int s, uint4* dst) {
+  uint4 areg[PF][CT][NPL];
+  auto load_a = [&](int s, uint4 (*dst)[NPL]) {
     const int c = s * 4 + kq;
 #pragma unroll
     for (int t = 0; t < CT; ++t)
-      dst[t] = (wok[t] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[t] + c * 8) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int p = 0; p < NPL; ++p)
+        dst[t][p] = (wok[t] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[t] + p * a.wps + c * 8)
+                                         : make_uint4(0, 0, 0, 0);
   };
 
   // ---- patch: summed inputs (or gathered dataset image), zero halo --------
   const long gimg = ((long)g * a.B + b) * img;
   const int n_src = a.gather ? 1 : __builtin_popcount(gr.in_mask);
-  const uint16_t* src0 = a.gather ? a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img
-                                  : a.in[__builtin_ctz(gr.in_mask | 0x100) & 7] + gimg;
+  const AT* src0 = a.gather ? static_cast<const AT*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img
+                            : static_cast<const AT*>(a.in[__builtin_ctz(gr.in_mask | 0x100) & 7]) + gimg;
   long poff[NPT];
   bool pok[NPT];
 #pragma unroll
@@ -126,8 +136,10 @@ conv_fast_kernel(ConvArgs a) {
   if (a.dbg & 4) {
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
-      if (tid + NTH * j < NP) patch[tid + NTH * j] = make_uint4(0, 0, 0, 0);
-  } else if (n_src == 1) {
+#pragma unroll
+      for (int p = 0; p < NPL; ++p)
+        if (tid + NTH * j < NP) patch[p * NP + tid + NTH * j] = make_uint4(0, 0, 0, 0);
+  } else if (!PREC && n_src == 1) {
     uint4 v[NPT];
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
@@ -136,8 +148,9 @@ conv_fast_kernel(ConvArgs a) {
     for (int j = 0; j < NPT; ++j)
       if (tid + NTH * j < NP) patch[tid + NTH * j] = v[j];
   } else {
-    // N-ary DAG input: chunks in batches of JB; per slot, the batch's loads are
-    // all in flight, then an fp32 accumulate (one rounding to bf16 at the end)
+    // chunks in batches of JB with the batch's loads in flight; N-ary DAG
+    // input summed in fp32 (prec 0: one rounding to bf16 at the end; prec 1:
+    // exact split of the fp32 sum into the three planes)
     constexpr int JB = NPT < 5 ? NPT : 5;
 #pragma unroll
     for (int j0 = 0; j0 < NPT; j0 += JB) {
@@ -146,37 +159,60 @@ conv_fast_kernel(ConvArgs a) {
       for (int j = 0; j < JB; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc8[j][e] = 0.f;
-#pragma unroll
-      for (int k = 0; k < GT_MAXSLOT; ++k) {
-        if (!((gr.in_mask >> k) & 1)) continue;
-        const uint16_t* sk = a.in[k] + gimg;
-        uint4 v[JB];
+      if (n_src == 1) {
 #pragma unroll
         for (int j = 0; j < JB; ++j)
-          v[j] = (j0 + j < NPT && pok[j0 + j]) ? *reinterpret_cast<const uint4*>(sk + poff[j0 + j])
-                                                : make_uint4(0, 0, 0, 0);
+          if (j0 + j < NPT && pok[j0 + j]) ld_chunk(src0 + poff[j0 + j], acc8[j]);
+      } else {
 #pragma unroll
-        for (int j = 0; j < JB; ++j) {
-          float t8[8];
-          unpack8(v[j], t8);
+        for (int k = 0; k < GT_MAXSLOT; ++k) {
+          if (!((gr.in_mask >> k) & 1)) continue;
+          const AT* sk = static_cast<const AT*>(a.in[k]) + gimg;
+          float t8[JB][8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc8[j][e] += t8[e];
+          for (int j = 0; j < JB; ++j) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t8[j][e] = 0.f;
+            if (j0 + j < NPT && pok[j0 + j]) ld_chunk(sk + poff[j0 + j], t8[j]);
+          }
+#pragma unroll
+          for (int j = 0; j < JB; ++j)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc8[j][e] += t8[j][e];
         }
       }
 #pragma unroll
-      for (int j = 0; j < JB; ++j)
-        if (j0 + j < NPT && tid + NTH * (j0 + j) < NP) patch[tid + NTH * (j0 + j)] = pack8(acc8[j]);
+      for (int j = 0; j < JB; ++j) {
+        const int i = tid + NTH * (j0 + j);
+        if (j0 + j >= NPT || i >= NP) continue;
+        if (PREC) {
+          uint4 p0, p1, p2;
+          split8(acc8[j], p0, p1, p2);
+          patch[i] = p0;
+          patch[NP + i] = p1;
+          patch[2 * NP + i] = p2;
+        } else {
+          patch[i] = pack8(acc8[j]);
+        }
+      }
     }
   }
   if (a.xsum && n_src > 1) {
     // the summed input of this band (interior of the patch) for the layer's wgrad
     __syncthreads();
-    uint16_t* xo = a.xsum + ((long)g * a.B + b) * img + (long)h0 * W * NCBI * 8;
+    AT* xo = static_cast<AT*>(a.xsum) + ((long)g * a.B + b) * img + (long)h0 * W * NCBI * 8;
     for (int i = tid; i < TH * W * NCBI; i += NTH) {
       const int cb = i % NCBI, pix = i / NCBI;
       const int r = pix / W, c = pix % W;
-      if (h0 + r < a.H)
-        *reinterpret_cast<uint4*>(xo + (long)i * 8) = patch[((r + KH / 2) * PW + c + KW / 2) * NCBI + cb];
+      if (h0 + r >= a.H) continue;
+      const int pi = ((r + KH / 2) * PW + c + KW / 2) * NCBI + cb;
+      if (PREC) {
+        float f[8];
+        join8(patch[pi], patch[NP + pi], patch[2 * NP + pi], f);   // exact: the fp32 sum
+        st_chunk(xo + (long)i * 8, f);
+      } else {
+        *reinterpret_cast<uint4*>(xo + (long)i * 8) = patch[pi];
+      }
     }
   }
   // chunk c -> patch offset of its (kh, kw, cb) relative to the output pixel
@@ -217,24 +253,25 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
   for (int s = 0; s < NKS; ++s) {
     const uint4* pb = patch + lbase + gbase + coff[s * 4 + kq];
-    uint4 bfr[PG];
+    uint4 bfr[PG][NPL];
 #pragma unroll
     for (int h = 0; h < PG; ++h) {
       const int p = h * 16;                        // relative to the wave's first group
-      bfr[h] = pb[((p / W) * PW + (p % W)) * NCBI];
+#pragma unroll
+      for (int q = 0; q < NPL; ++q) bfr[h][q] = pb[q * NP + ((p / W) * PW + (p % W)) * NCBI];
     }
 #pragma unroll
     for (int t = 0; t < CT; ++t)
 #pragma unroll
-      for (int h = 0; h < PG; ++h) acc[t][h] = mfma16(areg[s % PF][t], bfr[h], acc[t][h]);
+      for (int h = 0; h < PG; ++h) acc[t][h] = mfma_np<NPL>(areg[s % PF][t], bfr[h], acc[t][h]);
     if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
   }
 
-  // ---- epilogue: accumulators -> fp32 tile in LDS -> 16-byte row stores ------
+  // ---- epilogue: accumulators -> tile in LDS -> 16-byte row stores ---------
   // (a lane holds 4 channels of one pixel per tile: 8-byte scattered stores
-  // are store-issue bound; through LDS every store is a contiguous 16 B of the
-  // band, which is one contiguous range of the NHWC output)
-  if (a.epi_bf16) {
+  // are store-issue bound; through LDS every store is a contiguous chunk of
+  // the band, which is one contiguous range of the NHWC output)
+  if (a.epi_bf16 && !PREC) {
     // forward launches: values rounded once to bf16 in an LDS tile, copied out
     // as contiguous 16-byte chunks of the band (one contiguous NHWC range)
     __syncthreads();                                 // everyone is done with the patch
@@ -265,12 +302,13 @@ conv_fast_kernel(ConvArgs a) {
       const uint4 val = *reinterpret_cast<const uint4*>(ot + p * OROWB + cb * 8);
 #pragma unroll
       for (int k = 0; k < GT_MAXSLOT; ++k)
-        if ((gr.out_mask >> k) & 1) *reinterpret_cast<uint4*>(a.out[k] + obase + (long)i * 8) = val;
+        if ((gr.out_mask >> k) & 1) *reinterpret_cast<uint4*>(static_cast<uint16_t*>(a.out[k]) + obase + (long)i * 8) = val;
     }
     return;
   }
-  // data gradient (DAG fan-out: several output slots, accumulate, ReLU masks):
-  // fp32 tile in LDS, then contiguous 16-byte read-modify-write per slot
+  // fp32 tile in LDS, then one contiguous chunk per thread and slot: plain
+  // store (forward), or the data gradient's DAG fan-out (several output
+  // slots, accumulate, ReLU masks) as a read-modify-write
   __syncthreads();                                   // everyone is done with the patch
   float* otile = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -302,26 +340,23 @@ conv_fast_kernel(ConvArgs a) {
     const long off = obase + (long)i * 8;
     for (int k = 0; k < GT_MAXSLOT; ++k) {
       if (!((gr.out_mask >> k) & 1)) continue;
-      uint4* dst = reinterpret_cast<uint4*>(a.out[k] + off);
+      AT* dst = static_cast<AT*>(a.out[k]) + off;
       float sum[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) sum[e] = v[e];
       if ((gr.out_mask >> (8 + k)) & 1) {
         float o[8];
-        unpack8(*dst, o);
+        ld_chunk(dst, o);
 #pragma unroll
         for (int e = 0; e < 8; ++e) sum[e] += o[e];
       }
       if ((gr.out_mask >> (16 + k)) & 1) {
-        const uint4 m = *reinterpret_cast<const uint4*>(a.out_mask[k] + off);
-        const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+        float m[8];
+        ld_chunk(static_cast<const AT*>(a.out_mask[k]) + off, m);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t hbits = (e & 1) ? (mw[e >> 1] >> 16) : (mw[e >> 1] & 0xffffu);
-          sum[e] = (hbits != 0u && hbits < 0x8000u) ? sum[e] : 0.f;   // bf16 > 0
-        }
+        for (int e = 0; e < 8; ++e) sum[e] = m[e] > 0.f ? sum[e] : 0.f;
       }
-      *dst = pack8(sum);
+      st_chunk(dst, sum);
     }
   }
 }
@@ -339,12 +374,20 @@ extern "C" int gt_conv_set_nwv(int n) {
   return old;
 }
 
-#define CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                      \
+// dynamic LDS above 64 KiB: raise the per-function limit once (gfx950 has 160 KiB per CU)
+template <typename F>
+static void lds_limit(F* fn, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)bytes);
+}
+
+#define CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_)                               \
   {                                                                                                     \
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
-    const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_>::lds(a->epi_bf16 != 0);             \
-    hipLaunchKernelGGL((conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_>), grid, dim3(NWV_ * 64), lds, \
-                       stream, *a);                                                                     \
+    const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, PREC_>::lds(a->epi_bf16 != 0);      \
+    auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_>;                      \
+    lds_limit(fn, lds);                                                                                 \
+    hipLaunchKernelGGL(fn, grid, dim3(NWV_ * 64), lds, stream, *a);                                     \
     return (int)hipGetLastError();                                                                      \
   }
 
@@ -353,21 +396,35 @@ extern "C" int gt_conv_set_nwv(int n) {
    (NCO_ * 8 + 15) / 16 == NT_ && a->H % TH_ == 0)
 
 #define CONV_FAST_CASE(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)                                              \
-  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 4)
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 4, 0)
 
 // shapes with an 8-wave instantiation: `def_` waves unless overridden
 #define CONV_FAST_CASE2(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, def_)                                       \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
-    if ((g_conv_nwv ? g_conv_nwv : def_) == 8) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 8)  \
-    CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 4)                                            \
+    if ((g_conv_nwv ? g_conv_nwv : def_) == 8) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 8, 0) \
+    CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 4, 0)                                         \
   }
 
 // odd tile counts (104 channels = 7 x 16): one co tile per wave, NT waves
 #define CONV_FAST_CASE_NW(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                      \
-  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 0)
+
+// fp32 tensors (prec 1): 3-plane patch -> bands of 8 rows (LDS), 4 waves
+#define CONV_FAST_CASE_F32(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                     \
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)
 
 extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
+  if (a->prec == 1) {
+    // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
+    CONV_FAST_CASE_F32(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
+    CONV_FAST_CASE_F32(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
+    CONV_FAST_CASE_F32(5, 5, 3, 16, 8, 4, 7, 4)   // s2 input conv (20 -> 50)
+    CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
+    CONV_FAST_CASE_F32(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
+    return -100;
+  }
+  if (a->prec != 0) return -1;
   // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
   CONV_FAST_CASE2(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
   CONV_FAST_CASE2(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
@@ -461,8 +518,9 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
 
   auto issue = [&](int band, int buf) {
     const int b = band / nbi, h0 = (band - b * nbi) * R;
-    const uint16_t* src0 = a.gather ? a.in[0] + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img_in
-                                    : a.in[first_in & 7] + fold_off + (long)b * img_in;
+    const uint16_t* src0 = a.gather ? static_cast<const uint16_t*>(a.in[0]) +
+                                          a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img_in
+                                    : static_cast<const uint16_t*>(a.in[first_in & 7]) + fold_off + (long)b * img_in;
 #pragma unroll
     for (int j = 0; j < XT; ++j) {
       const int i = tid + NT_ * j;
@@ -480,7 +538,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
 #pragma unroll
           for (int k = 0; k < GT_MAXSLOT; ++k) {
             if (!((gr.in_mask >> k) & 1)) continue;
-            unpack8(*reinterpret_cast<const uint4*>(a.in[k] + fold_off + (long)b * img_in + off), t8);
+            unpack8(*reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(a.in[k]) + fold_off +
+                                                    (long)b * img_in + off), t8);
 #pragma unroll
             for (int e = 0; e < 8; ++e) sum[e] += t8[e];
           }
@@ -488,8 +547,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
         xs[buf][i] = pack8(sum);
       }
     }
-    const char* dsrc = reinterpret_cast<const char*>(a.dz + (long)g * a.B * img_out + (long)b * img_out +
-                                                     (long)h0 * W * NCBO * 8);
+    const char* dsrc = reinterpret_cast<const char*>(static_cast<const uint16_t*>(a.dz) + (long)g * a.B * img_out +
+                                                     (long)b * img_out + (long)h0 * W * NCBO * 8);
 #pragma unroll
     for (int j = 0; j < DT; ++j) {
       const int i = tid + NT_ * j;
@@ -577,6 +636,186 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 tensors (prec 1): the same workgroup shape, but the band is staged
+// through registers -- each 32-byte fp32 chunk is loaded (DAG inputs summed),
+// split exactly into three bf16 planes (common.h split8) and written to
+// plane-major LDS images that the same ds_read_b64_tr_b16 operand reads walk;
+// every (dz tile, input tile) pair is then the six-term split product. The
+// next band's global loads are issued before the current band's MFMAs and
+// written to LDS after them (async-STAGE split).
+// ---------------------------------------------------------------------------
+template <int KH, int KW, int NCBI, int NCBO, int W, int R, int NW, int NB>
+__global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
+  constexpr int NPL = GT_NPL_F32;
+  constexpr int NT_ = NW * 64;                     // threads
+  constexpr int PW = W + KW - 1, PR = R + KH - 1;
+  constexpr int NCH = KH * KW * NCBI;              // weight chunks (8 input channels each)
+  constexpr int NKT = (NCH + 1 + 1) / 2;           // 16-column tiles incl. the bias chunk
+  constexpr int MT = (NCBO * 8 + 15) / 16;         // output-channel tiles
+  constexpr int TPW = (NKT + NW - 1) / NW;         // k-column tiles per wave
+  constexpr int KS = R * W / 32;                   // K-steps per band
+  constexpr int XCH = PR * PW * NCBI;              // staged input chunks per band (per plane)
+  constexpr int DCH = R * W * NCBO;                // staged dz chunks per band (per plane)
+  constexpr int XT = (XCH + NT_ - 1) / NT_, DT = (DCH + NT_ - 1) / NT_;
+  constexpr int XROW = NCBI * 16, DROW = NCBO * 16;   // LDS bytes per pixel (one plane)
+  static_assert(R * W % 32 == 0 && (W == 16 || W == 32), "bands must be whole 32-pixel K-steps");
+
+  __shared__ __attribute__((aligned(16))) uint4 xs[NB][NPL][XCH];
+  __shared__ __attribute__((aligned(16))) uint4 ds[NB][NPL][DCH];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int s = blockIdx.x;
+  const GroupRec gr = group_rec(a.gtab, blockIdx.y, a.n_in, 0, 0, nullptr);
+  const int g = gr.g;
+  const int nbi = a.H / R;                                     // bands per image
+  const int bps = a.pps / (R * W);                             // bands per split
+  const int band0 = s * bps;
+  const int band1 = min(band0 + bps, a.B * nbi);
+  const long img_in = (long)a.H * W * NCBI * 8, img_out = (long)a.H * W * NCBO * 8;
+  const long fold_off = (long)g * a.B * img_in;
+  const int n_src = a.gather ? 1 : __builtin_popcount(gr.in_mask);
+  const float* in0 = static_cast<const float*>(a.in[__builtin_ctz(gr.in_mask | 0x100) & 7]);
+
+  float xr[XT][8], dr[DT][8];
+  auto load = [&](int band) {
+    const int b = band / nbi, h0 = (band - b * nbi) * R;
+    const long boff = fold_off + (long)b * img_in;
+    const float* src0 = a.gather ? static_cast<const float*>(a.in[0]) +
+                                       a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img_in
+                                 : in0 + boff;
+#pragma unroll
+    for (int j = 0; j < XT; ++j) {
+      const int i = tid + NT_ * j;
+      const int cb = i % NCBI, pix = i / NCBI;
+      const int hh = h0 - KH / 2 + pix / PW, ww = pix % PW - KW / 2;
+      const bool ok = i < XCH && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
+      const long off = ((long)hh * W + ww) * (NCBI * 8) + cb * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
+      if (!ok) continue;
+      if (n_src == 1) {
+        load8f(src0 + off, xr[j]);
+      } else {
+        for (int k = 0; k < GT_MAXSLOT; ++k) {
+          if (!((gr.in_mask >> k) & 1)) continue;
+          float t8[8];
+          load8f(static_cast<const float*>(a.in[k]) + boff + off, t8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xr[j][e] += t8[e];
+        }
+      }
+    }
+    const float* dsrc = static_cast<const float*>(a.dz) + (long)g * a.B * img_out + (long)b * img_out +
+                        (long)h0 * W * NCBO * 8;
+#pragma unroll
+    for (int j = 0; j < DT; ++j) {
+      const int i = tid + NT_ * j;
+      if (i < DCH) load8f(dsrc + (long)i * 8, dr[j]);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < XT; ++j) {
+      const int i = tid + NT_ * j;
+      if (i < XCH) split8(xr[j], xs[buf][0][i], xs[buf][1][i], xs[buf][2][i]);
+    }
+#pragma unroll
+    for (int j = 0; j < DT; ++j) {
+      const int i = tid + NT_ * j;
+      if (i < DCH) split8(dr[j], ds[buf][0][i], ds[buf][1][i], ds[buf][2][i]);
+    }
+  };
+
+  // ---- per-lane operand addresses (fixed for the whole kernel) -------------
+  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3, l16 = lane & 15;
+  const int px0 = 8 * gq + q;                                  // lane's first K row (pixel of a K-step)
+  const int prow = px0 / W, pcol = px0 % W;                    // its position inside the band
+  const int xlane = (prow * PW + pcol) * XROW;
+  const int dlane = px0 * DROW + p * 8;
+  int xoff[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int n = wave + NW * t;
+    int c = 2 * n + (p >> 1);
+    if (c >= NCH) c = 0;                                       // bias / padding columns: any valid row
+    const int kk = c / NCBI, cb = c % NCBI;
+    xoff[t] = xlane + ((kk / KW) * PW + (kk % KW)) * XROW + cb * 16 + (p & 1) * 8;
+  }
+  const bool ones_lane = l16 == (NCH & 1) * 8;                 // the bias column inside its tile
+
+  f32x4_t acc[MT][TPW];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[m][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  if (band0 < band1) {
+    load(band0);
+    store(0);
+  }
+  int cur = 0;
+  for (int band = band0; band < band1; ++band, cur ^= (NB - 1)) {
+    __syncthreads();                      // band `cur` staged everywhere; the other buffer no longer read
+    const bool more = band + 1 < band1;
+    if (more) load(band + 1);             // global loads in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int xrow_off = ((ks * 32) / W) * PW * XROW;        // compile-time after unrolling
+      uint4 afr[MT][NPL];
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) {
+          const char* d0 = reinterpret_cast<const char*>(ds[cur][pl]) + dlane + ks * 32 * DROW + m * 32;
+          afr[m][pl] = tr_pair(d0, d0 + 4 * DROW);
+        }
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int n = wave + NW * t;
+        if (n >= NKT) continue;
+        uint4 bfr[NPL];
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) {
+          const char* x0 = reinterpret_cast<const char*>(xs[cur][pl]) + xrow_off + xoff[t];
+          bfr[pl] = tr_pair(x0, x0 + 4 * XROW);
+        }
+        if (n == NCH / 2 && ones_lane) {                       // exact 1.0 = (1, 0, 0)
+          bfr[0] = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);
+          bfr[1] = bfr[2] = make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][t] = mfma_np<NPL>(afr[m], bfr, acc[m][t]);
+      }
+    }
+    if (more) {
+      if (NB == 1) __syncthreads();       // every wave is done reading the single buffer
+      store(cur ^ (NB - 1));
+    }
+  }
+
+  // ---- partial out: lane holds rows 4*kq..+3 (co) of column l16 (k col) ------
+  const int kq = lane >> 4;
+  constexpr int Kdim = NCH * 8;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int n = wave + NW * t;
+    if (n >= NKT) continue;
+    const int col = n * 16 + l16;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = m * 16 + kq * 4 + i;
+        if (co >= a.Coutp) continue;
+        if (col < Kdim)
+          a.part_w[(((long)s * a.G + g) * a.Coutp + co) * Kdim + col] = acc[m][t][i];
+        else if (col == Kdim && a.part_b)
+          a.part_b[((long)s * a.G + g) * a.Coutp + co] = acc[m][t][i];
+      }
+  }
+}
+
 static int g_wgrad_nb = 0;   // 0: per-shape default, 1 / 2: force band buffers (A/B switch)
 
 extern "C" int gt_wgrad_set_nb(int nb) {
@@ -596,14 +835,35 @@ extern "C" int gt_wgrad_set_nb(int nb) {
     return (int)hipGetLastError();                                                                       \
   }
 
-// 1 if a specialised wgrad exists for this geometry (the host then sizes the
-// split in whole bands: pps multiple of R*W)
-extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, int W) {
-  if (KH == 5 && KW == 5 && Cinp == 8 && Coutp == 24 && W == 32 && H % 8 == 0) return 8 * 32;
-  if (KH == 3 && KW == 3 && Cinp == 24 && Coutp == 24 && W == 32 && H % 8 == 0) return 8 * 32;
-  if (KH == 5 && KW == 5 && Cinp == 24 && Coutp == 56 && W == 16 && H % 16 == 0) return 16 * 16;
-  if (KH == 3 && KW == 3 && Cinp == 56 && Coutp == 56 && W == 16 && H % 16 == 0) return 16 * 16;
+#define WGRAD_FAST_CASE_F32(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_)                                     \
+  if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->Coutp == NCBO_ * 8 && a->W == W_ &&     \
+      a->H % R_ == 0 && a->pps % (R_ * W_) == 0) {                                                        \
+    dim3 grid(a->S, a->ngroups);                                                                         \
+    hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_>), grid, dim3(NW_ * 64), 0, \
+                       stream, *a);                                                                      \
+    return (int)hipGetLastError();                                                                       \
+  }
+
+// band rows of the specialised wgrad per precision (the host sizes the split
+// in whole bands: pps multiple of R*W); 0 = generic kernel
+static int wgrad_rows(int KH, int KW, int Cinp, int Coutp, int H, int W, int prec) {
+  if (prec == 1) {
+    if (KH == 5 && KW == 5 && Cinp == 8 && Coutp == 24 && W == 32 && H % 8 == 0) return 8;
+    if (KH == 3 && KW == 3 && Cinp == 24 && Coutp == 24 && W == 32 && H % 4 == 0) return 4;
+    if (KH == 5 && KW == 5 && Cinp == 24 && Coutp == 56 && W == 16 && H % 4 == 0) return 4;
+    if (KH == 3 && KW == 3 && Cinp == 56 && Coutp == 56 && W == 16 && H % 4 == 0) return 4;
+    return 0;
+  }
+  if (KH == 5 && KW == 5 && Cinp == 8 && Coutp == 24 && W == 32 && H % 8 == 0) return 8;
+  if (KH == 3 && KW == 3 && Cinp == 24 && Coutp == 24 && W == 32 && H % 8 == 0) return 8;
+  if (KH == 5 && KW == 5 && Cinp == 24 && Coutp == 56 && W == 16 && H % 16 == 0) return 16;
+  if (KH == 3 && KW == 3 && Cinp == 56 && Coutp == 56 && W == 16 && H % 16 == 0) return 16;
   return 0;
+}
+
+// pixels per band of the specialised wgrad for this geometry, or 0
+extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, int W, int prec) {
+  return wgrad_rows(KH, KW, Cinp, Coutp, H, W, prec) * W;
 }
 
 // Preferred splits per group (measured, profiles/wgrad_splits.txt): many small
@@ -612,12 +872,20 @@ extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, in
 // CU). 3 splits x 80 groups of a 16-candidate population = 240 workgroups, one
 // round on 256 CUs; 4 splits left a 64-workgroup second round (population step
 // 2-3 % slower, same-box sweep).
-extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, int W) {
-  (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H;
+extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, int W, int prec) {
+  (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H; (void)prec;
   return W >= 32 ? 16 : 3;
 }
 
 extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
+  if (a->prec == 1) {
+    WGRAD_FAST_CASE_F32(5, 5, 1, 3, 32, 8, 4, 1)      // s1 input conv (3 -> 20)
+    WGRAD_FAST_CASE_F32(3, 3, 3, 3, 32, 4, 4, 1)      // s1 nodes / output conv (20 -> 20)
+    WGRAD_FAST_CASE_F32(5, 5, 3, 7, 16, 4, 8, 2)      // s2 input conv (20 -> 50)
+    WGRAD_FAST_CASE_F32(3, 3, 7, 7, 16, 4, 8, 2)      // s2 nodes / output conv (50 -> 50)
+    return -100;
+  }
+  if (a->prec != 0) return -1;
   WGRAD_FAST_CASE(5, 5, 1, 3, 32, 8, 4, 1)      // s1 input conv (3 -> 20)
   WGRAD_FAST_CASE(3, 3, 3, 3, 32, 8, 4, 1)      // s1 nodes / output conv (20 -> 20)
   WGRAD_FAST_CASE(5, 5, 3, 7, 16, 16, 8, 2)     // s2 input conv (20 -> 50)

@@ -41,10 +41,10 @@ __global__ void step_begin_kernel(StepState* s) {
 
 // ---------------------------------------------------------------------------
 struct DenseFwdArgs {
-  const uint16_t* x;       // [G][B][Fp] (pooled features, NHWC flatten)
-  const uint16_t* wt;      // [G][Up][Fp] bf16 (transposed copy of W1)
+  const void* x;           // [G][B][Fp] (pooled features, NHWC flatten), bf16 or fp32 (prec)
+  const uint16_t* wt;      // [planes][G][Up][Fp] bf16 (transposed copy of W1; prec 1: 3 exact planes)
   const float* bias;       // [G][Up]
-  uint16_t* out;           // [G][B][Up]
+  void* out;               // [G][B][Up] bf16 or fp32
   const float* w2;         // [G][Up][C] fp32: dense2 weights (fused partial logits)
   float* plog;             // [G][Up/16][B][C] partial logits of this 16-unit tile (fixed-order sum later)
   const StepState* st;
@@ -55,11 +55,28 @@ struct DenseFwdArgs {
   int train;
   unsigned seed;
   int C;
+  int prec;                // 0: bf16 tensors, bf16 MFMA; 1: fp32 tensors, split-fp32 MFMA (common.h)
+  long wps;                // plane stride of wt (elements)
 };
+
+// an MFMA B operand of 8 consecutive activations: bf16 as is, fp32 split into planes
+template <int PREC>
+__device__ __forceinline__ void act_frag(const void* base, long off, bool ok, uint4* f) {
+  if (PREC) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ok) load8f(static_cast<const float*>(base) + off, v);
+    split8(v, f[0], f[1], f[2]);
+  } else {
+    f[0] = ok ? *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(base) + off) : make_uint4(0, 0, 0, 0);
+  }
+}
 
 // grid (Up/16, ceil(B/32), G): one 16-unit x 32-row tile per workgroup, the
 // K (feature) loop split over the 4 waves and reduced through LDS.
+template <int PREC>
 __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
   __shared__ f32x4_t red[3][2][64];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
   const int g = blockIdx.z;
@@ -67,24 +84,22 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
   const int b0 = blockIdx.y * 32;
   const int nchunks = a.Fp >> 3;
   const uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
-  const uint16_t* x = a.x + (long)g * a.B * a.Fp;
+  const long xg = (long)g * a.B * a.Fp;
   f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   const int urow = u_t + l16;
   const int br0 = b0 + l16, br1 = b0 + 16 + l16;
   const uint16_t* pa = wt + (long)urow * a.Fp;
-  const uint16_t* pb0 = x + (long)br0 * a.Fp;
-  const uint16_t* pb1 = x + (long)br1 * a.Fp;
   const bool ua = urow < a.Up, b0ok = br0 < a.B, b1ok = br1 < a.B;
   for (int ks = wave * 4; ks < nchunks; ks += 16) {
     const int c = ks + kq;
-    uint4 af = make_uint4(0, 0, 0, 0), bf0 = make_uint4(0, 0, 0, 0), bf1 = make_uint4(0, 0, 0, 0);
-    if (c < nchunks) {
-      if (ua) af = *reinterpret_cast<const uint4*>(pa + c * 8);
-      if (b0ok) bf0 = *reinterpret_cast<const uint4*>(pb0 + c * 8);
-      if (b1ok) bf1 = *reinterpret_cast<const uint4*>(pb1 + c * 8);
-    }
-    acc[0] = mfma16(af, bf0, acc[0]);
-    acc[1] = mfma16(af, bf1, acc[1]);
+    uint4 af[NPL], bf0[NPL], bf1[NPL];
+#pragma unroll
+    for (int q = 0; q < NPL; ++q)
+      af[q] = (c < nchunks && ua) ? *reinterpret_cast<const uint4*>(pa + q * a.wps + c * 8) : make_uint4(0, 0, 0, 0);
+    act_frag<PREC>(a.x, xg + (long)br0 * a.Fp + c * 8, c < nchunks && b0ok, bf0);
+    act_frag<PREC>(a.x, xg + (long)br1 * a.Fp + c * 8, c < nchunks && b1ok, bf1);
+    acc[0] = mfma_np<NPL>(af, bf0, acc[0]);
+    acc[1] = mfma_np<NPL>(af, bf1, acc[1]);
   }
   if (wave > 0) {
     red[wave - 1][0][lane] = acc[0];
@@ -117,9 +132,11 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
           const uint32_t r = hash4(seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)row, (uint32_t)(u0 + i));
           z = (r >= thr) ? z * keep_scale : 0.f;
         }
-        v[i] = bf2f(f2bf(z));      // the head sees exactly the stored bf16 activation
+        v[i] = PREC ? z : bf2f(f2bf(z));      // the head sees exactly the stored activation
       }
-      *reinterpret_cast<uint2*>(a.out + ((long)g * a.B + row) * a.Up + u0) = pack4(v);
+      AT* dst = static_cast<AT*>(a.out) + ((long)g * a.B + row) * a.Up + u0;
+      if (PREC) *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      else *reinterpret_cast<uint2*>(dst) = pack4(v);
     }
     if (a.plog == nullptr) continue;
     // partial logits of this 16-unit tile: 4 units per lane, reduced over the 4 lane groups
@@ -144,7 +161,7 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
 
 // ---------------------------------------------------------------------------
 struct HeadArgs {
-  const uint16_t* h;       // [G][B][Up] (post-dropout activations)
+  const void* h;           // [G][B][Up] (post-dropout activations), bf16 or fp32 (prec)
   const float* w2;         // [G][Up][C] fp32 master
   const float* b2;         // [G][C]
   const int64_t* labels;   // [N]
@@ -161,6 +178,7 @@ struct HeadArgs {
   int loss_ce;             // 0 = bce_compat, 1 = ce
   float drop_scale;        // 1/(1-p)
   int eval;
+  int prec;
 };
 
 #define HEAD_MAXB 64
@@ -253,7 +271,9 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
   }
   for (int i = tid; i < B * 64; i += 256) {
     const int b = i >> 6, j = i & 63;
-    hsl[b][j] = (u0 + j < Up) ? bf2f(a.h[((long)g * B + b) * Up + u0 + j]) : 0.f;
+    const long hi = ((long)g * B + b) * Up + u0 + j;
+    hsl[b][j] = (u0 + j < Up) ? (a.prec ? static_cast<const float*>(a.h)[hi] : bf2f(static_cast<const uint16_t*>(a.h)[hi]))
+                              : 0.f;
   }
   __syncthreads();
   // dH and gb1: thread = (unit j, row quarter)
@@ -290,9 +310,11 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
 // ---------------------------------------------------------------------------
 struct DenseDgradArgs {
   const float* dH;     // [G][B][Up]
-  const uint16_t* wt;  // [G][Up][Fp] bf16 transposed copy of W1 (the values dense_fwd multiplied by)
-  uint16_t* dx;        // [G][B][Fp]
+  const uint16_t* wt;  // [planes][G][Up][Fp] bf16 transposed copy of W1 (the values dense_fwd multiplied by)
+  void* dx;            // [G][B][Fp] bf16 or fp32 (prec)
   int G, B, Fp, Up;
+  int prec;
+  long wps;            // plane stride of wt (elements)
 };
 
 // grid (Fp/64, ceil(B/32), G): D[row = f][col = b], K = units.
@@ -301,8 +323,11 @@ struct DenseDgradArgs {
 // tile is one coalesced 16-byte load per thread, transposed through LDS so every
 // lane gets its 8 consecutive units as one 16-byte LDS read. The bf16 values are
 // the RNE roundings the old pack8(fp32) produced, so dx is bit-identical.
+template <int PREC>
 __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t tl[64][40];    // [feature][unit], 80-byte rows
+  typedef typename ActT<PREC>::T AT;
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t tl[NPL][64][40];    // [plane][feature][unit], 80-byte rows
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
   const int g = blockIdx.z;
   const int fb = blockIdx.x * 64;
@@ -317,8 +342,11 @@ __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
   const int nchunks = a.Up >> 3;
   for (int ks = 0; ks < nchunks; ks += 4) {
     const int u = ks * 8 + lu;
-    uint4 q = {0u, 0u, 0u, 0u};
-    if (fok && u < a.Up) q = *reinterpret_cast<const uint4*>(wt + (long)u * a.Fp + fb + lf);
+    uint4 qv[NPL];
+#pragma unroll
+    for (int pl = 0; pl < NPL; ++pl)
+      qv[pl] = (fok && u < a.Up) ? *reinterpret_cast<const uint4*>(wt + pl * a.wps + (long)u * a.Fp + fb + lf)
+                                 : make_uint4(0, 0, 0, 0);
     const int c = ks + kq;
     float f0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (c < nchunks) {
@@ -334,17 +362,28 @@ __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
       }
     }
     __syncthreads();                                 // previous tile fully read
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      tl[lf + 2 * j][lu] = (uint16_t)(w[j] & 0xffffu);
-      tl[lf + 2 * j + 1][lu] = (uint16_t)(w[j] >> 16);
+    for (int pl = 0; pl < NPL; ++pl) {
+      const uint32_t w[4] = {qv[pl].x, qv[pl].y, qv[pl].z, qv[pl].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        tl[pl][lf + 2 * j][lu] = (uint16_t)(w[j] & 0xffffu);
+        tl[pl][lf + 2 * j + 1][lu] = (uint16_t)(w[j] >> 16);
+      }
     }
     __syncthreads();
-    const uint4 af = *reinterpret_cast<const uint4*>(&tl[wave * 16 + l16][kq * 8]);
-    const uint4 b0f = pack8(f0), b1f = pack8(f1);
-    acc[0] = mfma16(af, b0f, acc[0]);
-    acc[1] = mfma16(af, b1f, acc[1]);
+    uint4 af[NPL], b0f[NPL], b1f[NPL];
+#pragma unroll
+    for (int pl = 0; pl < NPL; ++pl) af[pl] = *reinterpret_cast<const uint4*>(&tl[pl][wave * 16 + l16][kq * 8]);
+    if constexpr (PREC != 0) {
+      split8(f0, b0f[0], b0f[1], b0f[2]);
+      split8(f1, b1f[0], b1f[1], b1f[2]);
+    } else {
+      b0f[0] = pack8(f0);
+      b1f[0] = pack8(f1);
+    }
+    acc[0] = mfma_np<NPL>(af, b0f, acc[0]);
+    acc[1] = mfma_np<NPL>(af, b1f, acc[1]);
   }
   const int fo = f_t + kq * 4;
   if (fo >= a.Fp) return;
@@ -353,31 +392,45 @@ __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
     const int row = b0 + h * 16 + l16;
     if (row >= a.B) continue;
     float v[4] = {acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
-    *reinterpret_cast<uint2*>(a.dx + ((long)g * a.B + row) * a.Fp + fo) = pack4(v);
+    AT* dst = static_cast<AT*>(a.dx) + ((long)g * a.B + row) * a.Fp + fo;
+    if (PREC) *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    else *reinterpret_cast<uint2*>(dst) = pack4(v);
   }
 }
 
 // ---------------------------------------------------------------------------
 struct DenseWgradAdamArgs {
-  const uint16_t* x;   // [G][B][Fp]
+  const void* x;       // [G][B][Fp] bf16 or fp32 (prec)
   const float* dH;     // [G][B][Up]
   float* p; float* m; float* v;   // [G][Fp][Up]
-  uint16_t* wt;        // [G][Up][Fp] bf16 copy (transposed)
+  uint16_t* wt;        // [planes][G][Up][Fp] bf16 copy (transposed; prec 1: exact 3-plane split)
   const StepState* st;
   int G, B, Fp, Up;
   int Cp, Cr, Ur;      // feature = pixel * Cp + channel; channels >= Cr and units >= Ur are padding
-};                     // (zero forever: skipped, 13 % of the layer's optimizer traffic)
+                       // (zero forever: skipped, 13 % of the layer's optimizer traffic)
+  int prec;
+  long wps;            // plane stride of wt (elements)
+};
 
 // grid (Fp/16, G), 256 threads. Thread: unit quad q (4 units), rows fr, fr+2, ..., fr+14.
+template <int PREC>
 __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* xs = reinterpret_cast<float*>(smem);                       // [B][16]
-  uint16_t* tt = reinterpret_cast<uint16_t*>(xs + a.B * 16);        // [Up][16] transposed bf16 tile
+  uint16_t* tt = reinterpret_cast<uint16_t*>(xs + a.B * 16);        // [NPL][Up][16] transposed bf16 planes
+  const int tplane = a.Up * 16;
   const int g = blockIdx.y, f0 = blockIdx.x * 16, tid = threadIdx.x;
-  const uint16_t* x = a.x + (long)g * a.B * a.Fp;
+  const AT* x = static_cast<const AT*>(a.x) + (long)g * a.B * a.Fp;
   for (int i = tid; i < a.B * 16; i += 256) {
     const int b = i >> 4, j = i & 15;
-    xs[i] = (f0 + j < a.Fp) ? bf2f(x[(long)b * a.Fp + f0 + j]) : 0.f;
+    float xv = 0.f;
+    if (f0 + j < a.Fp) {
+      if (PREC) xv = static_cast<const float*>(static_cast<const void*>(x))[(long)b * a.Fp + f0 + j];
+      else xv = bf2f(static_cast<const uint16_t*>(static_cast<const void*>(x))[(long)b * a.Fp + f0 + j]);
+    }
+    xs[i] = xv;
   }
   __syncthreads();
   const float lr_t = a.st->lr_t;
@@ -403,7 +456,9 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
       if (f >= a.Fp) continue;
       if (a.Cp > 0 && f % a.Cp >= a.Cr) {      // padded channel: weights stay 0, only the bf16 tile
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) tt[pl * tplane + (u0 + i) * 16 + fr + 2 * r] = 0;
         continue;
       }
       const long off = ((long)g * a.Fp + f) * a.Up + u0;
@@ -414,7 +469,14 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         P[i] = opt_update(a.st, P[i], acc[r][i], M[i], V[i], lr_t);
-        tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
+        const uint16_t h0 = f2bf(P[i]);
+        tt[(u0 + i) * 16 + fr + 2 * r] = h0;
+        if (PREC) {                              // exact 3-plane split of the fp32 master
+          const float r1 = P[i] - bf2f(h0);
+          const uint16_t h1 = f2bf(r1);
+          tt[tplane + (u0 + i) * 16 + fr + 2 * r] = h1;
+          tt[2 * tplane + (u0 + i) * 16 + fr + 2 * r] = f2bf(r1 - bf2f(h1));
+        }
       }
       *reinterpret_cast<float4*>(a.p + off) = pp;
       *reinterpret_cast<float4*>(a.m + off) = mm;
@@ -423,16 +485,20 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
   }
   __syncthreads();
   // transposed bf16 copy: wt[u][f0 .. f0+15] (32 contiguous bytes per unit)
-  uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
   const int nu = a.Ur > 0 ? ((a.Ur + 3) >> 2) << 2 : a.Up;
-  for (int i = tid; i < nu * 2; i += 256) {
-    const int u = i >> 1, half = i & 1;
-    if (f0 + half * 8 + 8 <= a.Fp) {
-      *reinterpret_cast<uint4*>(wt + (long)u * a.Fp + f0 + half * 8) =
-          *reinterpret_cast<const uint4*>(&tt[u * 16 + half * 8]);
-    } else {
-      for (int j = 0; j < 8; ++j)
-        if (f0 + half * 8 + j < a.Fp) wt[(long)u * a.Fp + f0 + half * 8 + j] = tt[u * 16 + half * 8 + j];
+#pragma unroll
+  for (int pl = 0; pl < NPL; ++pl) {
+    uint16_t* wt = a.wt + pl * a.wps + (long)g * a.Up * a.Fp;
+    const uint16_t* tp = tt + pl * tplane;
+    for (int i = tid; i < nu * 2; i += 256) {
+      const int u = i >> 1, half = i & 1;
+      if (f0 + half * 8 + 8 <= a.Fp) {
+        *reinterpret_cast<uint4*>(wt + (long)u * a.Fp + f0 + half * 8) =
+            *reinterpret_cast<const uint4*>(&tp[u * 16 + half * 8]);
+      } else {
+        for (int j = 0; j < 8; ++j)
+          if (f0 + half * 8 + j < a.Fp) wt[(long)u * a.Fp + f0 + half * 8 + j] = tp[u * 16 + half * 8 + j];
+      }
     }
   }
 }
@@ -446,7 +512,17 @@ struct AdamSeg {
   long n, gstride;
   int S, tG, tCo, tKH, tKW, tCi;
   int tiled;             // 1: blocks are (group, 64-column) tiles of a [Co][KH*KW*Ci] weight (Co <= 128)
+  int npl;               // bf16 planes of bf / bfT: 1, or 3 (exact split of the fp32 master, prec 1)
+  long pstride_bf, pstride_bfT;   // plane strides (elements)
 };
+
+// plane q (0..2) of the exact split of p (q = 0: the bf16 rounding)
+__device__ __forceinline__ void split3(float p, uint16_t* h) {
+  h[0] = f2bf(p);
+  const float r1 = p - bf2f(h[0]);
+  h[1] = f2bf(r1);
+  h[2] = f2bf(r1 - bf2f(h[1]));
+}
 
 #define ADAM_TK 64
 
@@ -459,13 +535,14 @@ struct AdamArgs {
 __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
   const int2 blk = a.blocks[blockIdx.x];
   const AdamSeg sg = a.segs[blk.x];
+  const int npl = sg.npl > 1 ? GT_NPL_F32 : 1;
   if (sg.tiled) {
     // conv weight tile: Co rows x ADAM_TK reduction columns (row-contiguous
     // reads of p/m/v/partials), bf16 values staged in LDS, then the flipped /
     // transposed dgrad copy written as 16-byte runs along co -- one element per
     // thread scattered 2-byte stores over a 1-2 KB stride instead (every store
     // its own L2 transaction: the kernel's old bottleneck)
-    __shared__ __attribute__((aligned(16))) uint16_t tile[ADAM_TK][128 + 8];
+    __shared__ __attribute__((aligned(16))) uint16_t tile[GT_NPL_F32][ADAM_TK][128 + 8];
     const int Co = sg.tCo, Ci = sg.tCi, KH = sg.tKH, KW = sg.tKW;
     const int Kd = KH * KW * Ci;
     const int nkt = (Kd + ADAM_TK - 1) / ADAM_TK;
@@ -481,9 +558,12 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
       float m = sg.m[i], v = sg.v[i];
       const float p = opt_update(a.st, sg.p[i], gr, m, v, lr_t);
       sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
-      const uint16_t pb = f2bf(p);
-      if (sg.bf) sg.bf[i] = pb;
-      tile[kk][co] = pb;
+      uint16_t h[3];
+      split3(p, h);
+      for (int q = 0; q < npl; ++q) {
+        if (sg.bf) sg.bf[q * sg.pstride_bf + i] = h[q];
+        tile[q][kk][co] = h[q];
+      }
     }
     __syncthreads();
     const int nc8 = Co >> 3;
@@ -492,7 +572,8 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
       if (k >= Kd) continue;
       const int ci = k % Ci, r = k / Ci, kw = r % KW, kh = r / KW;
       const long o = ((((long)gg * Ci + ci) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * Co + c8 * 8;
-      *reinterpret_cast<uint4*>(sg.bfT + o) = *reinterpret_cast<const uint4*>(&tile[kk][c8 * 8]);
+      for (int q = 0; q < npl; ++q)
+        *reinterpret_cast<uint4*>(sg.bfT + q * sg.pstride_bfT + o) = *reinterpret_cast<const uint4*>(&tile[q][kk][c8 * 8]);
     }
     return;
   }
@@ -504,8 +585,10 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
   float m = sg.m[i], v = sg.v[i];
   const float p = opt_update(a.st, sg.p[i], gr, m, v, lr_t);
   sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
-  const uint16_t pb = f2bf(p);
-  if (sg.bf) sg.bf[i] = pb;
+  uint16_t h[3];
+  split3(p, h);
+  if (sg.bf)
+    for (int q = 0; q < npl; ++q) sg.bf[q * sg.pstride_bf + i] = h[q];
   if (sg.bfT) {
     // flipped / transposed dgrad copy: 32-bit index math (64-bit division is
     // a long software sequence on the GPU)
@@ -516,7 +599,7 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
     const uint32_t co = r % (uint32_t)sg.tCo;
     const uint32_t gg = r / (uint32_t)sg.tCo;
     const long o = ((((long)gg * sg.tCi + ci) * sg.tKH + (sg.tKH - 1 - kh)) * sg.tKW + (sg.tKW - 1 - kw)) * sg.tCo + co;
-    sg.bfT[o] = pb;
+    for (int q = 0; q < npl; ++q) sg.bfT[q * sg.pstride_bfT + o] = h[q];
   }
 }
 
@@ -529,9 +612,10 @@ int gt_step_begin(StepState* s, hipStream_t stream) {
 }
 
 int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
-  if (a->Fp % 8 || a->Up % 64 || a->C > HEAD_MAXC_FWD) return -1;
+  if (a->Fp % 8 || a->Up % 64 || a->C > HEAD_MAXC_FWD || (a->prec != 0 && a->prec != 1)) return -1;
   dim3 grid(a->Up / 16, (a->B + 31) / 32, a->G);
-  hipLaunchKernelGGL(dense_fwd_kernel, grid, dim3(256), 0, stream, *a);
+  if (a->prec) hipLaunchKernelGGL(dense_fwd_kernel<1>, grid, dim3(256), 0, stream, *a);
+  else hipLaunchKernelGGL(dense_fwd_kernel<0>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 
@@ -546,17 +630,26 @@ int gt_head(const HeadArgs* a, hipStream_t stream) {
 int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
   if (a->Fp % 64 && a->Fp % 8) return -1;
   if (a->Up % 8) return -1;
+  if (a->prec != 0 && a->prec != 1) return -1;
   dim3 grid((a->Fp + 63) / 64, (a->B + 31) / 32, a->G);
-  hipLaunchKernelGGL(dense_dgrad_kernel, grid, dim3(256), 0, stream, *a);
+  if (a->prec) hipLaunchKernelGGL(dense_dgrad_kernel<1>, grid, dim3(256), 0, stream, *a);
+  else hipLaunchKernelGGL(dense_dgrad_kernel<0>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 
 int gt_dense_wgrad_adam(const DenseWgradAdamArgs* a, hipStream_t stream) {
-  if (a->Up % 4) return -1;
-  const size_t lds = sizeof(float) * (size_t)a->B * 16 + 2 * (size_t)a->Up * 16;
+  if (a->Up % 4 || (a->prec != 0 && a->prec != 1)) return -1;
+  const size_t npl = a->prec ? GT_NPL_F32 : 1;
+  const size_t lds = sizeof(float) * (size_t)a->B * 16 + npl * 2 * (size_t)a->Up * 16;
   if (lds > 160 * 1024) return -2;
   dim3 grid((a->Fp + 15) / 16, a->G);
-  hipLaunchKernelGGL(dense_wgrad_adam_kernel, grid, dim3(256), lds, stream, *a);
+  if (a->prec) {
+    if (lds > 65536) (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dense_wgrad_adam_kernel<1>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(dense_wgrad_adam_kernel<1>, grid, dim3(256), lds, stream, *a);
+  } else {
+    hipLaunchKernelGGL(dense_wgrad_adam_kernel<0>, grid, dim3(256), lds, stream, *a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -566,5 +659,9 @@ int gt_adam_segments(const AdamArgs* a, int nblocks, hipStream_t stream) {
 }
 
 size_t gt_sizeof_adam_seg() { return sizeof(AdamSeg); }
+size_t gt_sizeof_dense_fwd_args() { return sizeof(DenseFwdArgs); }
+size_t gt_sizeof_head_args() { return sizeof(HeadArgs); }
+size_t gt_sizeof_dense_dgrad_args() { return sizeof(DenseDgradArgs); }
+size_t gt_sizeof_dense_wgrad_args() { return sizeof(DenseWgradAdamArgs); }
 
 }  // extern "C"

@@ -81,6 +81,88 @@ __device__ __forceinline__ f32x4_t mfma16(const uint4& a, const uint4& b, f32x4_
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_frag(a), as_frag(b), c, 0, 0, 0);
 }
 
+// ---------------------------------------------------------------------------
+// fp32 precision on bf16 matrix cores: exact 3-way split ("bf16x6")
+//
+// Every fp32 value a (24-bit significand) is the EXACT sum of three bf16
+// values a = a0 + a1 + a2: a0 = rne(a), a1 = rne(a - a0), a2 = a - a0 - a1
+// (each residual is exact in fp32; the last has <= 8 significant bits, so it
+// is a bf16 -- valid while a2 does not underflow, |a| > ~1e-33). A product
+//   a*b = sum_{i+j<=2} ai*bj  +  (a1 b2 + a2 b1 + a2 b2)
+// keeps six terms; every ai*bj is exact in fp32 (8x8-bit significands) and
+// the MFMA accumulates in fp32, so the only error beyond fp32 accumulation is
+// the three dropped terms: |a1 b2 + a2 b1 + a2 b2| <= (2^-24 + 2^-24 + 2^-32)|ab|
+// ~= 2^-23 |ab| = 2 fp32 ulps of the product -- fp32-level by construction
+// (tests/test_hip_fp32.py measures it against an fp64 oracle next to torch's
+// own fp32). Cost: 6 v_mfma_f32_16x16x32_bf16 per 32-deep k-step, i.e. 2.7x
+// cheaper than the native v_mfma_f32_16x16x4_f32 (8 x 32 cycles vs 6 x 16).
+// ---------------------------------------------------------------------------
+#define GT_NPL_F32 3     // bf16 planes of an fp32 operand
+
+// bf16 / fp32 storage type of a precision (0 / 1)
+template <int PREC> struct ActT { typedef uint16_t T; };
+template <> struct ActT<1> { typedef float T; };
+
+// 8 fp32 -> three bf16x8 planes with f = p0 + p1 + p2 exactly
+__device__ __forceinline__ void split8(const float* f, uint4& p0, uint4& p1, uint4& p2) {
+  float t[8], r[8];
+  p0 = pack8(f);
+  unpack8(p0, t);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = f[e] - t[e];
+  p1 = pack8(r);
+  unpack8(p1, t);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = r[e] - t[e];
+  p2 = pack8(r);
+}
+
+// the fp32 value of three planes (exact: the inverse of split8)
+__device__ __forceinline__ void join8(const uint4& p0, const uint4& p1, const uint4& p2, float* f) {
+  float t[8];
+  unpack8(p0, f);
+  unpack8(p1, t);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] += t[e];
+  unpack8(p2, t);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] += t[e];
+}
+
+// 8 consecutive fp32 (one 32-byte chunk of an fp32 activation)
+__device__ __forceinline__ void load8f(const float* p, float* f) {
+  const float4 q0 = reinterpret_cast<const float4*>(p)[0];
+  const float4 q1 = reinterpret_cast<const float4*>(p)[1];
+  f[0] = q0.x; f[1] = q0.y; f[2] = q0.z; f[3] = q0.w;
+  f[4] = q1.x; f[5] = q1.y; f[6] = q1.z; f[7] = q1.w;
+}
+
+__device__ __forceinline__ void store8f(float* p, const float* f) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+// one 16x16 x 32-deep k-step of a split-precision product: A and B each in
+// NPL bf16 planes (NPL = 1: plain bf16 MFMA; 3: the six-term fp32 product,
+// smallest terms first)
+template <int NPL>
+__device__ __forceinline__ f32x4_t mfma_np(const uint4* a, const uint4* b, f32x4_t c) {
+  if (NPL == 1) return mfma16(a[0], b[0], c);
+  c = mfma16(a[2], b[0], c);
+  c = mfma16(a[1], b[1], c);
+  c = mfma16(a[0], b[2], c);
+  c = mfma16(a[1], b[0], c);
+  c = mfma16(a[0], b[1], c);
+  return mfma16(a[0], b[0], c);
+}
+
+// element loads/stores of an activation chunk (8 channels) in either storage
+// type: bf16 (uint16_t) or fp32 (float)
+__device__ __forceinline__ void ld_chunk(const uint16_t* p, float* f) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
+__device__ __forceinline__ void ld_chunk(const float* p, float* f) { load8f(p, f); }
+__device__ __forceinline__ void st_chunk(uint16_t* p, const float* f) { *reinterpret_cast<uint4*>(p) = pack8(f); }
+__device__ __forceinline__ void st_chunk(float* p, const float* f) { store8f(p, f); }
+
 // Counter-based hash -> uniform in [0,1): keyed dropout (deterministic per
 // (seed, fold, step, row, col), independent of launch geometry).
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {

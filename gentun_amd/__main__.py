@@ -49,7 +49,7 @@ def _common(ap):
 def _config(args):
     from .config import RunConfig
     return RunConfig(seed=args.seed, checkpoint_dir=args.checkpoint_dir, events=args.events,
-                     collective_timeout_s=args.collective_timeout, dtype=getattr(args, "dtype", "bf16"),
+                     collective_timeout_s=args.collective_timeout, dtype=getattr(args, "dtype", "fp32"),
                      loss=getattr(args, "loss", "bce_compat"), pairing=args.pairing, streams=args.streams,
                      pop_batch=args.pop_batch, schedule=args.schedule, backend=args.backend)
 
@@ -177,7 +177,7 @@ def main(argv=None):
     c.add_argument("--batch", type=int, default=32)
     c.add_argument("--loss", choices=("bce_compat", "ce"), default=_env_default("loss"))
     c.add_argument("--dtype", choices=("bf16", "fp32"), default=_env_default("dtype"),
-                   help="bf16 MFMA with fp32 master weights (HIP path), or fp32 (PyTorch path)")
+                   help="fp32 (reference precision; HIP: exact split-fp32 MFMA) or bf16 (fast mode)")
     c.add_argument("--optimizer", choices=("adam", "sgd"), default="adam")
     c.add_argument("--momentum", type=float, default=0.9, help="SGD momentum")
     c.set_defaults(fn=cmd_cnn)

@@ -22,7 +22,7 @@ class RunConfig(object):
     checkpoint_dir: str = None          # one JSON checkpoint per generation (checkpoint.py)
     events: str = None                  # JSONL event log (metrics.py)
     collective_timeout_s: int = 1800    # RCCL / gloo collective timeout (a dead rank fails the run)
-    dtype: str = "bf16"                 # CNN compute: 'bf16' MFMA (fp32 master weights) or 'fp32'
+    dtype: str = "fp32"                 # CNN compute: fp32 (reference precision; exact split MFMA) or bf16 (fast)
     loss: str = "bce_compat"            # 'bce_compat' (reference: softmax + binary_crossentropy) or 'ce'
     pairing: str = "reference"          # RussianRouletteGA pairs: 'reference' (overlapping) or 'disjoint'
     streams: int = 1                    # concurrent population jobs per GPU

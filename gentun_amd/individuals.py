@@ -260,7 +260,8 @@ class GeneticCnnIndividual(Individual):
 
     Extra keyword arguments beyond the reference signature (all optional):
     ``loss`` ('bce_compat' = Keras softmax+binary_crossentropy parity, or 'ce'),
-    ``dtype`` ('bf16' MFMA with fp32 master weights, or 'fp32'), ``seed``
+    ``dtype`` ('fp32', the reference precision: fp32 tensors, exact split-fp32 MFMA on
+    MI355X; or 'bf16', the fast mode: bf16 tensors and MFMA, fp32 master weights), ``seed``
     (run seed; fitness is a pure function of (genes, seed, fold)),
     ``backend`` ('hip' -- MI355X kernels, default on GPU -- or 'torch' oracle),
     ``device``, and ``optimizer`` ('adam' = the reference's Keras Adam, or
@@ -271,7 +272,7 @@ class GeneticCnnIndividual(Individual):
                  nodes=(3, 5), input_shape=(28, 28, 1), kernels_per_layer=(20, 50),
                  kernel_sizes=((5, 5), (5, 5)), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
-                 loss='bce_compat', dtype='bf16', seed=0, backend=None, device=None, optimizer='adam',
+                 loss='bce_compat', dtype='fp32', seed=0, backend=None, device=None, optimizer='adam',
                  momentum=0.9):
         if genome is None:
             genome = {'S_{}'.format(i + 1): k * (k - 1) // 2 for i, k in enumerate(nodes)}

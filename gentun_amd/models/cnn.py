@@ -27,7 +27,7 @@ class GeneticCnnModel(GentunModel):
 
     def __init__(self, x_train, y_train, genes, nodes, input_shape, kernels_per_layer, kernel_sizes, dense_units,
                  dropout_probability, classes, nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
-                 loss="bce_compat", dtype="bf16", seed=0, backend=None, device=None, fold_parallel=True,
+                 loss="bce_compat", dtype="fp32", seed=0, backend=None, device=None, fold_parallel=True,
                  optimizer="adam", momentum=0.9):
         super(GeneticCnnModel, self).__init__(x_train, y_train)
         self.genes = dict(genes)

@@ -48,7 +48,7 @@ CLIP_EPS = 1e-7
 
 class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
-                 dtype="bf16", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9):
+                 dtype="fp32", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9):
         if isinstance(epochs, int):
             epochs = (epochs,)
         if isinstance(learning_rate, (int, float)):
@@ -96,13 +96,15 @@ class DeviceData(object):
         xt = torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32))
         if layout == "nchw":
             self.x = xt.permute(0, 3, 1, 2).contiguous().to(device)
-        elif layout == "nhwc8":
-            # channels padded to a multiple of 8 so one 16-byte load = 8 channels
+        elif layout in ("nhwc8", "nhwc8f"):
+            # channels padded to a multiple of 8 so one chunk = 8 channels
+            # (nhwc8: bf16 tensors of the bf16 mode; nhwc8f: fp32)
             c = xt.shape[-1]
             cp = (c + 7) // 8 * 8
             pad = torch.zeros(xt.shape[:-1] + (cp,), dtype=torch.float32)
             pad[..., :c] = xt
-            self.x = pad.to(device=device, dtype=torch.bfloat16).contiguous()
+            dt = torch.float32 if layout == "nhwc8f" else torch.bfloat16
+            self.x = pad.to(device=device, dtype=dt).contiguous()
         else:
             raise ValueError(layout)
         self.labels = torch.from_numpy(self.labels_np).to(device)

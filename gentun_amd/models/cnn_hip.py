@@ -26,9 +26,20 @@ Step (one HIP graph, replayed epochs x steps times):
   weights, DAG gradient fan-out accumulation and ReLU masks fused per group)
   -> adam_segments (reduces the partials in fixed order).
 
-Layouts: activations NHWC bf16 with channels padded to 8; fp32 master weights
-in padded layouts whose padding is zero and stays zero; bf16 weight copies
-written by the optimizer. Groups are member-major, fold-minor.
+Precision (``cfg.dtype``):
+
+* ``fp32`` (default, the reference's TF/Keras float32): activations and
+  gradients are fp32 tensors; every matrix product runs on the bf16 matrix
+  cores as the exact 3-way split of its fp32 operands (six MFMA terms per
+  product, error <= 2 fp32 ulps of each product before fp32 accumulation --
+  csrc/hip/common.h, measured in tests/test_hip_fp32.py); the optimizer
+  writes the three bf16 planes of every weight;
+* ``bf16``: bf16 activations, one bf16 MFMA per product (fast mode).
+
+Layouts: activations NHWC with channels padded to 8; fp32 master weights in
+padded layouts whose padding is zero and stays zero; bf16 weight planes
+(``[planes][...]``) written by the optimizer. Groups are member-major,
+fold-minor.
 """
 
 import math
@@ -51,16 +62,30 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
-class HipPopJob(FoldJob):
-    layout = "nhwc8"
+def split_planes(w, npl):
+    """``[npl][...]`` bf16 planes of an fp32 tensor: the exact split of
+    csrc/hip/common.h (plane 0 = the RNE bf16 rounding; w = sum of planes)."""
+    out = torch.empty((npl,) + tuple(w.shape), dtype=torch.bfloat16, device=w.device)
+    r = w.float()
+    for q in range(npl):
+        out[q] = r.to(torch.bfloat16)
+        r = r - out[q].float()
+    return out
 
-    def __init__(self, *a, **kw):
-        super(HipPopJob, self).__init__(*a, **kw)
+
+class HipPopJob(FoldJob):
+
+    def __init__(self, plan, x, y, folds, cfg, device, **kw):
+        if cfg.dtype not in K.PREC:
+            raise ValueError("HIP backend precision must be one of {}".format(sorted(K.PREC)))
+        self.layout = "nhwc8f" if cfg.dtype == "fp32" else "nhwc8"
+        super(HipPopJob, self).__init__(plan, x, y, folds, cfg, device, **kw)
         if self.device.type != "cuda":
             raise RuntimeError("the HIP backend needs a GPU device")
         self.L = K.lib()
-        if self.cfg.dtype != "bf16":
-            raise ValueError("HIP backend computes in bf16 MFMA with fp32 master weights (dtype='bf16')")
+        self.prec = K.PREC[cfg.dtype]
+        self.npl = K.NPL[cfg.dtype]
+        self.adt = torch.float32 if self.prec else torch.bfloat16      # activation / gradient storage
         p0 = self.plan
         Q, B, dev = self.G, self.B, self.device
         self.Q = Q
@@ -109,7 +134,7 @@ class HipPopJob(FoldJob):
             L.Kdim = L.KH * L.KW * L.cinp
             L.TH = K.conv_tile_rows(L.H, L.W)
             L.pps, L.S = K.wgrad_split(self.B * L.H * L.W, L.Kdim, L.coutp,
-                                       band=K.wgrad_band(L.KH, L.KW, L.cinp, L.coutp, L.H, L.W))
+                                       band=K.wgrad_band(L.KH, L.KW, L.cinp, L.coutp, L.H, L.W, self.prec))
         self.last = self.sched.last
         hs, ws = h0 >> len(p0.kernels_per_layer), w0 >> len(p0.kernels_per_layer)
         if hs < 1 or ws < 1:
@@ -127,17 +152,17 @@ class HipPopJob(FoldJob):
             self.shapes[st.pool] = (st.H // 2, st.W // 2, pad8(p0.kernels_per_layer[st.s]))
         self.act, self.grad = {}, {}
         for name, (hh, ww, cc) in self.shapes.items():
-            self.act[name] = torch.zeros((Q, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
-            self.grad[name] = torch.zeros((Q, B, hh, ww, cc), dtype=torch.bfloat16, device=dev)
+            self.act[name] = torch.zeros((Q, B, hh, ww, cc), dtype=self.adt, device=dev)
+            self.grad[name] = torch.zeros((Q, B, hh, ww, cc), dtype=self.adt, device=dev)
         # layers where some group sums >1 input: the forward conv writes that
         # sum once ("<layer>_xin") and the layer's wgrad reads it as one slot
         for L in self.layers:
             if L.xin is not None:
-                self.act[L.xin] = torch.zeros((Q, B, L.H, L.W, L.cinp), dtype=torch.bfloat16, device=dev)
+                self.act[L.xin] = torch.zeros((Q, B, L.H, L.W, L.cinp), dtype=self.adt, device=dev)
         hs, ws = self.final_hw
         self.Fp = hs * ws * self.final_cp
         self.Up = round_up(p0.dense_units, 64)
-        self.hdrop = torch.zeros((Q, B, self.Up), dtype=torch.bfloat16, device=dev)
+        self.hdrop = torch.zeros((Q, B, self.Up), dtype=self.adt, device=dev)
         self.dH = torch.zeros((Q, B, self.Up), dtype=torch.float32, device=dev)
         self.dz_head = torch.zeros((Q, B, self.classes), dtype=torch.float32, device=dev)
         self.plog = torch.zeros((Q, self.Up // 16, B, self.classes), dtype=torch.float32, device=dev)
@@ -164,12 +189,13 @@ class HipPopJob(FoldJob):
             else:
                 self.views[kind] = view
             off += n
+        npl = self.npl
         for L in self.layers:
-            L.w_bf = torch.zeros((Q, L.coutp, L.KH, L.KW, L.cinp), dtype=torch.bfloat16, device=dev)
-            L.wT_bf = torch.zeros((Q, L.cinp, L.KH, L.KW, L.coutp), dtype=torch.bfloat16, device=dev)
+            L.w_bf = torch.zeros((npl, Q, L.coutp, L.KH, L.KW, L.cinp), dtype=torch.bfloat16, device=dev)
+            L.wT_bf = torch.zeros((npl, Q, L.cinp, L.KH, L.KW, L.coutp), dtype=torch.bfloat16, device=dev)
             L.part_w = torch.zeros((L.S, Q, L.coutp, L.Kdim), dtype=torch.float32, device=dev)   # split-K partials
             L.part_b = torch.zeros((L.S, Q, L.coutp), dtype=torch.float32, device=dev)
-        self.w1t_bf = torch.zeros((Q, self.Up, self.Fp), dtype=torch.bfloat16, device=dev)
+        self.w1t_bf = torch.zeros((npl, Q, self.Up, self.Fp), dtype=torch.bfloat16, device=dev)
         self.gW2 = torch.zeros((Q, self.Up, self.classes), dtype=torch.float32, device=dev)
         self.gb2 = torch.zeros((Q, self.classes), dtype=torch.float32, device=dev)
         self.gb1 = torch.zeros((Q, self.Up), dtype=torch.float32, device=dev)
@@ -187,11 +213,13 @@ class HipPopJob(FoldJob):
     def _build_adam_table(self):
         segs, blocks = [], []
 
-        def add(p, m, v, g, S, gstride, bf=None, bfT=None, tdims=None):
+        def add(p, m, v, g, S, gstride, bf=None, bfT=None, tdims=None, pstrides=(0, 0)):
             sg = K.AdamSeg()
             sg.p, sg.m, sg.v, sg.g = p.data_ptr(), m.data_ptr(), v.data_ptr(), g.data_ptr()
             sg.bf = bf.data_ptr() if bf is not None else 0
             sg.bfT = bfT.data_ptr() if bfT is not None else 0
+            sg.npl = self.npl
+            sg.pstride_bf, sg.pstride_bfT = pstrides
             sg.n = p.numel()
             sg.gstride = gstride
             sg.S = S
@@ -212,8 +240,8 @@ class HipPopJob(FoldJob):
         for L in self.layers:
             for q, _ in L.rows:
                 p, m, v = (t[q] for t in L.w)
-                add(p, m, v, L.part_w[0, q], L.S, L.part_w[0].numel(), bf=L.w_bf[q], bfT=L.wT_bf[q],
-                    tdims=(1, L.coutp, L.KH, L.KW, L.cinp))
+                add(p, m, v, L.part_w[0, q], L.S, L.part_w[0].numel(), bf=L.w_bf[0, q], bfT=L.wT_bf[0, q],
+                    tdims=(1, L.coutp, L.KH, L.KW, L.cinp), pstrides=(L.w_bf[0].numel(), L.wT_bf[0].numel()))
                 p, m, v = (t[q] for t in L.b)
                 add(p, m, v, L.part_b[0, q], L.S, L.part_b[0].numel())
         for name, g in (("b1", self.gb1), ("W2", self.gW2), ("b2", self.gb2)):
@@ -244,6 +272,8 @@ class HipPopJob(FoldJob):
         a.Cinp = L.cinp if Cinp is None else Cinp
         a.Coutp = L.coutp if Coutp is None else Coutp
         a.KH, a.KW, a.TH = L.KH, L.KW, L.TH
+        a.prec = self.prec
+        a.wps = w[0].numel()                 # weights are [planes][...]
         return a
 
     def _slot_ptr(self, name, grad=False):
@@ -277,6 +307,7 @@ class HipPopJob(FoldJob):
             st.pmask = torch.zeros((Q * B, hh // 2, ww // 2, cc), dtype=torch.uint8, device=self.device)
             self.fwd_ops.append(("pool", (self.act[st.inp].data_ptr(), x1.data_ptr(), sel.data_ptr(),
                                           self.act[st.pool].data_ptr(), Q * B, B, hh, ww, cc), st.pmask.data_ptr()))
+        prec = self.prec
         # ---- head
         df = K.DenseFwdArgs()
         df.x, df.wt, df.bias, df.out = (self.act[self.last].data_ptr(), self.w1t_bf.data_ptr(),
@@ -285,6 +316,7 @@ class HipPopJob(FoldJob):
         df.G, df.B, df.Fp, df.Up = Q, B, self.Fp, self.Up
         df.drop_p, df.train, df.seed = self.cfg.dropout, 1, 0
         df.w2, df.plog, df.C = self.views["W2"][0].data_ptr(), self.plog.data_ptr(), self.classes
+        df.prec, df.wps = prec, self.w1t_bf[0].numel()
         self.dense_fwd_args = df
         hd = K.HeadArgs()
         hd.h, hd.w2, hd.b2 = self.hdrop.data_ptr(), self.views["W2"][0].data_ptr(), self.views["b2"][0].data_ptr()
@@ -297,10 +329,12 @@ class HipPopJob(FoldJob):
         hd.loss_ce = 1 if self.cfg.loss == "ce" else 0
         hd.drop_scale = 1.0 / (1.0 - self.cfg.dropout) if self.cfg.dropout < 1 else 0.0
         hd.eval = 0
+        hd.prec = prec
         self.head_args = hd
         dd = K.DenseDgradArgs()
         dd.dH, dd.wt, dd.dx = self.dH.data_ptr(), self.w1t_bf.data_ptr(), self.grad[self.last].data_ptr()
         dd.G, dd.B, dd.Fp, dd.Up = Q, B, self.Fp, self.Up
+        dd.prec, dd.wps = prec, self.w1t_bf[0].numel()
         self.dense_dgrad_args = dd
         dw = K.DenseWgradAdamArgs()
         p, m, v = self.views["W1"]
@@ -309,6 +343,7 @@ class HipPopJob(FoldJob):
         dw.wt, dw.st = self.w1t_bf.data_ptr(), self.state.data_ptr()
         dw.G, dw.B, dw.Fp, dw.Up = Q, B, self.Fp, self.Up
         dw.Cp, dw.Cr, dw.Ur = self.final_cp, self.plan.kernels_per_layer[-1], self.plan.dense_units
+        dw.prec, dw.wps = prec, self.w1t_bf[0].numel()
         self.dense_wgrad_args = dw
         # ---- backward (records: models/pop_schedule.py PopulationSchedule.backward)
         self.bwd_ops = []
@@ -320,7 +355,7 @@ class HipPopJob(FoldJob):
                 self.bwd_ops.append(("pool_bwd", (st.pmask.data_ptr(),
                                                   st.sel.data_ptr(), self.grad[st.pool].data_ptr(),
                                                   self.grad[st.inp].data_ptr(), self.grad[x1].data_ptr(),
-                                                  Q * B, B, hh, ww, cc, 1), None))
+                                                  Q * B, B, hh, ww, cc, 1, prec), None))
                 continue
             kind, L, rows = rec
             first = L.slots == ["input"]
@@ -337,6 +372,7 @@ class HipPopJob(FoldJob):
                 wa.ngroups = len(rows)
                 wa.G, wa.B, wa.H, wa.W = Q, B, L.H, L.W
                 wa.Cinp, wa.Coutp, wa.KH, wa.KW, wa.S, wa.pps = L.cinp, L.coutp, L.KH, L.KW, L.S, L.pps
+                wa.prec = prec
                 self.bwd_ops.append(("wgrad", wa, L))
             else:
                 # dgrad = conv with flipped, transposed weights; per group the
@@ -405,11 +441,13 @@ class HipPopJob(FoldJob):
         self._refresh_copies()
 
     def _refresh_copies(self):
+        """bf16 weight planes from the fp32 masters (the optimizer kernels
+        keep them current afterwards)."""
         for L in self.layers:
             w = L.w[0]
-            L.w_bf.copy_(w)
-            L.wT_bf.copy_(w.flip(2, 3).permute(0, 4, 2, 3, 1))
-        self.w1t_bf.copy_(self.views["W1"][0].transpose(1, 2))
+            L.w_bf.copy_(split_planes(w, self.npl))
+            L.wT_bf.copy_(split_planes(w.flip(2, 3).permute(0, 4, 2, 3, 1), self.npl))
+        self.w1t_bf.copy_(split_planes(self.views["W1"][0].transpose(1, 2), self.npl))
 
     def reset_optimizer(self, lr):
         self.m.zero_()
@@ -438,9 +476,9 @@ class HipPopJob(FoldJob):
             if kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_fwd")
             elif mk is not None:
-                K.check(L.gt_pool_fwd_mask(*a, mk, s), "pool_fwd")
+                K.check(L.gt_pool_fwd_mask(*a, mk, self.prec, s), "pool_fwd")
             else:
-                K.check(L.gt_pool_fwd(*a, s), "pool_fwd")
+                K.check(L.gt_pool_fwd(*a, self.prec, s), "pool_fwd")
 
     def train_step(self):
         L = self.L

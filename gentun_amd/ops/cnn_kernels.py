@@ -16,6 +16,11 @@ I = C.c_int
 
 MAXSLOT = 8      # GT_MAXSLOT: input / output slots of one conv launch
 
+# precision codes of the kernels (csrc/hip/cnn_args.h ``prec``): activations /
+# gradients bf16 with bf16 MFMA, or fp32 with the exact 3-plane split MFMA
+PREC = {"bf16": 0, "fp32": 1}
+NPL = {"bf16": 1, "fp32": 3}     # bf16 weight planes per precision
+
 
 class GroupRec(C.Structure):
     """One group (candidate x fold replica) of a population launch:
@@ -30,40 +35,43 @@ class ConvArgs(C.Structure):
                 ("out_mask", P * MAXSLOT), ("w", P), ("bias", P), ("gtab", P),
                 ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
-                ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I)]
+                ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long)]
 
 
 class WgradArgs(C.Structure):
     _fields_ = [("inp", P * MAXSLOT), ("gather", P), ("st", P), ("dz", P), ("part_w", P),
                 ("part_b", P), ("gtab", P), ("n_in", I), ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I),
-                ("Coutp", I), ("KH", I), ("KW", I), ("S", I), ("pps", I), ("ngroups", I)]
+                ("Coutp", I), ("KH", I), ("KW", I), ("S", I), ("pps", I), ("ngroups", I), ("prec", I)]
 
 
 class DenseFwdArgs(C.Structure):
     _fields_ = [("x", P), ("wt", P), ("bias", P), ("out", P), ("w2", P), ("plog", P), ("st", P), ("fold_ids", P),
                 ("seeds", P), ("G", I), ("B", I), ("Fp", I), ("Up", I), ("drop_p", C.c_float), ("train", I),
-                ("seed", C.c_uint), ("C", I)]
+                ("seed", C.c_uint), ("C", I), ("prec", I), ("wps", C.c_long)]
 
 
 class HeadArgs(C.Structure):
     _fields_ = [("h", P), ("w2", P), ("b2", P), ("labels", P), ("gather", P), ("st", P), ("dH", P),
                 ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P), ("dz", P), ("plog", P),
-                ("G", I), ("B", I), ("Up", I), ("C", I), ("loss_ce", I), ("drop_scale", C.c_float), ("eval", I)]
+                ("G", I), ("B", I), ("Up", I), ("C", I), ("loss_ce", I), ("drop_scale", C.c_float), ("eval", I),
+                ("prec", I)]
 
 
 class DenseDgradArgs(C.Structure):
-    _fields_ = [("dH", P), ("wt", P), ("dx", P), ("G", I), ("B", I), ("Fp", I), ("Up", I)]
+    _fields_ = [("dH", P), ("wt", P), ("dx", P), ("G", I), ("B", I), ("Fp", I), ("Up", I), ("prec", I),
+                ("wps", C.c_long)]
 
 
 class DenseWgradAdamArgs(C.Structure):
     _fields_ = [("x", P), ("dH", P), ("p", P), ("m", P), ("v", P), ("wt", P), ("st", P),
-                ("G", I), ("B", I), ("Fp", I), ("Up", I), ("Cp", I), ("Cr", I), ("Ur", I)]
+                ("G", I), ("B", I), ("Fp", I), ("Up", I), ("Cp", I), ("Cr", I), ("Ur", I), ("prec", I),
+                ("wps", C.c_long)]
 
 
 class AdamSeg(C.Structure):
     _fields_ = [("p", P), ("m", P), ("v", P), ("g", P), ("bf", P), ("bfT", P), ("n", C.c_long),
                 ("gstride", C.c_long), ("S", I), ("tG", I), ("tCo", I), ("tKH", I), ("tKW", I), ("tCi", I),
-                ("tiled", I)]
+                ("tiled", I), ("npl", I), ("pstride_bf", C.c_long), ("pstride_bfT", C.c_long)]
 
 ADAM_TK = 64        # adam_segments transpose tiles: tCo rows x ADAM_TK reduction columns
 
@@ -107,18 +115,18 @@ def lib():
         L.gt_adam_segments.restype = I
         L.gt_step_begin.argtypes = [P, P]
         L.gt_step_begin.restype = I
-        L.gt_pool_fwd.argtypes = [P, P, P, P, I, I, I, I, I, P]
+        L.gt_pool_fwd.argtypes = [P, P, P, P, I, I, I, I, I, I, P]
         L.gt_pool_fwd.restype = I
-        L.gt_pool_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, P]
+        L.gt_pool_bwd.argtypes = [P, P, P, P, P, P, I, I, I, I, I, I, I, P]
         L.gt_pool_bwd.restype = I
-        L.gt_pool_fwd_mask.argtypes = [P, P, P, P, I, I, I, I, I, P, P]
+        L.gt_pool_fwd_mask.argtypes = [P, P, P, P, I, I, I, I, I, P, I, P]
         L.gt_pool_fwd_mask.restype = I
-        L.gt_pool_bwd_mask.argtypes = [P, P, P, P, P, I, I, I, I, I, I, P]
+        L.gt_pool_bwd_mask.argtypes = [P, P, P, P, P, I, I, I, I, I, I, I, P]
         L.gt_pool_bwd_mask.restype = I
         L.gt_wgrad_set_nb.argtypes = [I]
         L.gt_wgrad_set_nb.restype = I
-        L.gt_wgrad_fast_band.argtypes = [I, I, I, I, I, I]
-        L.gt_wgrad_fast_splits.argtypes = [I, I, I, I, I, I]
+        L.gt_wgrad_fast_band.argtypes = [I, I, I, I, I, I, I]
+        L.gt_wgrad_fast_splits.argtypes = [I, I, I, I, I, I, I]
         L.gt_wgrad_fast_splits.restype = I
         L.gt_wgrad_fast_band.restype = I
         L.gt_conv_set_fast.argtypes = [I]
@@ -135,12 +143,17 @@ def lib():
         L.gt_glorot_init.restype = I
         L.gt_glorot_ref.argtypes = [C.c_uint64, C.c_uint64, I, C.c_float]
         L.gt_glorot_ref.restype = C.c_float
-        for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg", "gt_sizeof_init_seg"):
+        for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg", "gt_sizeof_init_seg",
+                     "gt_sizeof_dense_fwd_args", "gt_sizeof_head_args", "gt_sizeof_dense_dgrad_args",
+                     "gt_sizeof_dense_wgrad_args"):
             getattr(L, name).restype = C.c_size_t
         assert L.gt_sizeof_conv_args() == C.sizeof(ConvArgs), "ConvArgs ABI mismatch"
         assert L.gt_sizeof_init_seg() == C.sizeof(InitSeg), "InitSeg ABI mismatch"
         assert L.gt_sizeof_wgrad_args() == C.sizeof(WgradArgs), "WgradArgs ABI mismatch"
         assert L.gt_sizeof_adam_seg() == C.sizeof(AdamSeg), "AdamSeg ABI mismatch"
+        for nm, st in (("dense_fwd_args", DenseFwdArgs), ("head_args", HeadArgs),
+                       ("dense_dgrad_args", DenseDgradArgs), ("dense_wgrad_args", DenseWgradAdamArgs)):
+            assert getattr(L, "gt_sizeof_" + nm)() == C.sizeof(st), nm + " ABI mismatch"
         _TYPED[id(L)] = True
     return L
 
@@ -179,15 +192,15 @@ WGRAD_SPLITS_BY_WIDTH = {int(k): int(v) for k, v in (kv.split(":") for kv in
                          __import__("os").environ.get("GENTUN_WGRAD_SPLITS_W", "").split(",") if kv)}
 
 
-def wgrad_band(KH, KW, cinp, coutp, H, W):
+def wgrad_band(KH, KW, cinp, coutp, H, W, prec=0):
     """``(pixels per band, preferred splits)`` of the shape-specialised wgrad
     kernel, or ``(0, 0)`` for the generic one."""
     L = lib()
     if not L.gt_conv_set_fast(1):       # probe + restore the fast-path switch
         L.gt_conv_set_fast(0)
         return 0, 0
-    band = int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W))
-    splits = int(L.gt_wgrad_fast_splits(KH, KW, cinp, coutp, H, W)) if band else 0
+    band = int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W, prec))
+    splits = int(L.gt_wgrad_fast_splits(KH, KW, cinp, coutp, H, W, prec)) if band else 0
     if band and W in WGRAD_SPLITS_BY_WIDTH:
         splits = WGRAD_SPLITS_BY_WIDTH[W]      # tuning override (GENTUN_WGRAD_SPLITS_W="16:8,32:16")
     return band, splits

@@ -8,7 +8,7 @@ from gentun_amd.config import RunConfig
 
 def test_defaults_match_reference_semantics():
     c = RunConfig()
-    assert (c.loss, c.pairing, c.dtype, c.schedule) == ("bce_compat", "reference", "bf16", "auto")
+    assert (c.loss, c.pairing, c.dtype, c.schedule) == ("bce_compat", "reference", "fp32", "auto")
     assert c.collective_timeout_s > 0 and c.backend is None
 
 

@@ -196,13 +196,13 @@ def test_pool_group_select():
     x1 = bf(torch.randn(Q, B, H, W, cp, device=DEV))
     sel = torch.tensor([0, 1, 0], dtype=torch.int32, device=DEV)
     y = torch.zeros(Q, B, H // 2, W // 2, cp, dtype=torch.bfloat16, device=DEV)
-    Km.check(Km.lib().gt_pool_fwd(x0.data_ptr(), x1.data_ptr(), sel.data_ptr(), y.data_ptr(), Q * B, B, H, W, cp,
+    Km.check(Km.lib().gt_pool_fwd(x0.data_ptr(), x1.data_ptr(), sel.data_ptr(), y.data_ptr(), Q * B, B, H, W, cp, 0,
                                   stream()), "pool")
     dy = bf(torch.randn_like(y.float()))
     dx0 = torch.full_like(x0, 5.0)
     dx1 = torch.full_like(x1, 5.0)
     Km.check(Km.lib().gt_pool_bwd(x0.data_ptr(), x1.data_ptr(), sel.data_ptr(), dy.data_ptr(), dx0.data_ptr(),
-                                  dx1.data_ptr(), Q * B, B, H, W, cp, 1, stream()), "poolb")
+                                  dx1.data_ptr(), Q * B, B, H, W, cp, 1, 0, stream()), "poolb")
     torch.cuda.synchronize()
     for g in range(Q):
         src = (x1 if sel[g] else x0)[g].float().permute(0, 3, 1, 2).clone().requires_grad_(True)
@@ -229,15 +229,16 @@ def test_pool_argmax_mask(H, W, relu):
     y_ref = torch.zeros(Q, B, H // 2, W // 2, cp, dtype=torch.bfloat16, device=DEV)
     y = torch.zeros_like(y_ref)
     mask = torch.full((Q * B, H // 2, W // 2, cp), 255, dtype=torch.uint8, device=DEV)
-    Km.check(Km.lib().gt_pool_fwd(*args, y_ref.data_ptr(), Q * B, B, H, W, cp, stream()), "pool")
-    Km.check(Km.lib().gt_pool_fwd_mask(*args, y.data_ptr(), Q * B, B, H, W, cp, mask.data_ptr(), stream()), "poolm")
+    Km.check(Km.lib().gt_pool_fwd(*args, y_ref.data_ptr(), Q * B, B, H, W, cp, 0, stream()), "pool")
+    Km.check(Km.lib().gt_pool_fwd_mask(*args, y.data_ptr(), Q * B, B, H, W, cp, mask.data_ptr(), 0, stream()),
+             "poolm")
     dy = bf(torch.randn_like(y.float()))
     dx_ref = [torch.full_like(x0, 5.0), torch.full_like(x1, 5.0)]
     dx = [torch.full_like(x0, 5.0), torch.full_like(x1, 5.0)]
     Km.check(Km.lib().gt_pool_bwd(*args, dy.data_ptr(), dx_ref[0].data_ptr(), dx_ref[1].data_ptr(), Q * B, B, H, W,
-                                  cp, relu, stream()), "poolb")
+                                  cp, relu, 0, stream()), "poolb")
     Km.check(Km.lib().gt_pool_bwd_mask(mask.data_ptr(), sel.data_ptr(), dy.data_ptr(), dx[0].data_ptr(),
-                                       dx[1].data_ptr(), Q * B, B, H, W, cp, relu, stream()), "poolbm")
+                                       dx[1].data_ptr(), Q * B, B, H, W, cp, relu, 0, stream()), "poolbm")
     torch.cuda.synchronize()
     assert torch.equal(y.float(), y_ref.float())
     assert int(mask.max()) <= 7
@@ -305,13 +306,13 @@ def test_pool_fwd_bwd(H, W):
     y.backward(dy)
     xp = nhwc_pad(x, cp).to(torch.bfloat16).contiguous()
     yp = torch.zeros(N, H // 2, W // 2, cp, dtype=torch.bfloat16, device=DEV)
-    Km.check(Km.lib().gt_pool_fwd(xp.data_ptr(), 0, 0, yp.data_ptr(), N, 1, H, W, cp, stream()), "pool")
+    Km.check(Km.lib().gt_pool_fwd(xp.data_ptr(), 0, 0, yp.data_ptr(), N, 1, H, W, cp, 0, stream()), "pool")
     dyp = nhwc_pad(dy, cp).to(torch.bfloat16).contiguous()
     dxp = torch.full((N, H, W, cp), 7.0, dtype=torch.bfloat16, device=DEV)
-    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), 0, 0, dyp.data_ptr(), dxp.data_ptr(), 0, N, 1, H, W, cp, 0,
+    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), 0, 0, dyp.data_ptr(), dxp.data_ptr(), 0, N, 1, H, W, cp, 0, 0,
                                   stream()), "poolb")
     dxm = torch.full((N, H, W, cp), 7.0, dtype=torch.bfloat16, device=DEV)
-    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), 0, 0, dyp.data_ptr(), dxm.data_ptr(), 0, N, 1, H, W, cp, 1,
+    Km.check(Km.lib().gt_pool_bwd(xp.data_ptr(), 0, 0, dyp.data_ptr(), dxm.data_ptr(), 0, N, 1, H, W, cp, 1, 0,
                                   stream()), "poolm")
     torch.cuda.synchronize()
     assert torch.equal(yp[..., :C].float().permute(0, 3, 1, 2), y.detach())
