@@ -119,6 +119,7 @@ class Individual(object):
         self.fitness = value
         if value is None:
             self.fold_scores = None
+            self.fold_metrics = None
 
     # --------------------------------------------------------------- operators
     def _spawn(self, genes):
@@ -171,6 +172,9 @@ class Individual(object):
         twin = self._spawn(dict(self.genes))
         twin.set_fitness(self.fitness)
         twin.fold_scores = None if self.fold_scores is None else list(self.fold_scores)
+        fm = getattr(self, "fold_metrics", None)
+        if fm:
+            twin.fold_metrics = {k: list(v) for k, v in fm.items()}
         return twin
 
     def genes_key(self):
@@ -330,6 +334,7 @@ class GeneticCnnIndividual(Individual):
         model = self.build_fitness_model()
         self.fitness = model.cross_validate()
         self.fold_scores = list(model.fold_scores)
+        self.fold_metrics = dict(model.fold_metrics or {})
 
     def get_additional_parameters(self):
         return {

@@ -452,12 +452,17 @@ class TorchFoldJob(FoldJob):
         h = torch.baddbmm(P["dense1.b"][:, None, :], feat, P["dense1.w"])
         h = F.relu(h)
         if train and self.cfg.dropout > 0:
-            # job-owned generator (not torch's global RNG): the oracle is deterministic
+            # job-owned generators (not torch's global RNG), one per fold keyed
+            # by (candidate seed, fold id): the oracle is deterministic and a
+            # fold's masks do not depend on which other folds share the job
             if self.drop_gen is None:
-                self.drop_gen = torch.Generator(device=self.device)
-                self.drop_gen.manual_seed(_rng.stable_hash(self.base_seed, "dropout") & 0x7FFFFFFF)
-            keep = torch.rand(h.shape, generator=self.drop_gen, device=self.device) >= self.cfg.dropout
-            h = h * keep.to(h.dtype) / (1.0 - self.cfg.dropout)
+                self.drop_gen = []
+                for g in range(G):
+                    gen = torch.Generator(device=self.device)
+                    gen.manual_seed(_rng.stable_hash(self.base_seed, "dropout", self.fold_ids[g]) & 0x7FFFFFFF)
+                    self.drop_gen.append(gen)
+            keep = torch.stack([torch.rand(h.shape[1:], generator=gen, device=self.device) for gen in self.drop_gen])
+            h = h * (keep >= self.cfg.dropout).to(h.dtype) / (1.0 - self.cfg.dropout)
         return torch.baddbmm(P["dense2.b"][:, None, :], h, P["dense2.w"])
 
     def _gather(self, idx):

@@ -13,8 +13,10 @@ per generation (collectives X2/X3 of SURVEY.md §2.6)
      fold mask, encoded genes) for the ``U`` work units;
   2. every rank evaluates the units it owns (several concurrently on its GPU,
      :class:`~gentun_amd.parallel.evaluators.LocalBatchEvaluator`);
-  3. one ``all_gather`` of ``float64[U, 3 + nfold]`` = (status, fitness,
-     wall_s, fold scores) -- < 2 KB, latency-bound on xGMI;
+  3. one ``all_gather`` of ``float64[U, 3 + 2 nfold]`` = (status, fitness,
+     wall_s, fold scores, secondary fold scores -- categorical accuracy of a
+     Genetic-CNN whose fitness is the reference's binary accuracy) -- a few
+     KB, latency-bound on xGMI;
   4. rank 0 merges fold groups per candidate, re-evaluates failed units
      locally once (worst fitness if that fails too) and breeds.
 
@@ -150,7 +152,8 @@ def evaluate_units(units, evaluator, nfold, rank, generation):
             _localize_device(u.ind, evaluator)
             u.ind.evaluate_fitness()
             scores = u.ind.fold_scores or []
-            rows[ui] = _row(ST_OK, u.ind.fitness, time.perf_counter() - t0, scores, nfold, u.fold_ids)
+            aux = (getattr(u.ind, "fold_metrics", None) or {}).get("categorical_accuracy")
+            rows[ui] = _row(ST_OK, u.ind.fitness, time.perf_counter() - t0, scores, nfold, u.fold_ids, aux=aux)
         except Exception as exc:     # noqa: BLE001 -- reported as a status code
             warnings.warn("evaluation failed on rank {}: {}".format(rank, exc))
             rows[ui] = _row(ST_ERR, np.nan, time.perf_counter() - t0, [], nfold, u.fold_ids)
@@ -225,7 +228,8 @@ def _evaluate_cnn_units(source, evaluator, nfold):
     def done(ind, model, res, wall, ui):
         scores = res[model.primary_metric()]
         u = units_by_index[ui]
-        rows[ui] = _row(ST_OK, float(np.mean(scores)), wall, scores, nfold, u.fold_ids)
+        rows[ui] = _row(ST_OK, float(np.mean(scores)), wall, scores, nfold, u.fold_ids,
+                        aux=res.get("categorical_accuracy"))
 
     units_by_index = {}
 
@@ -238,11 +242,17 @@ def _evaluate_cnn_units(source, evaluator, nfold):
     return rows
 
 
-def _row(status, fitness, wall, scores, nfold, fold_ids):
-    row = np.full(3 + nfold, np.nan, np.float64)
+def row_width(nfold):
+    return 3 + 2 * nfold
+
+
+def _row(status, fitness, wall, scores, nfold, fold_ids, aux=None):
+    row = np.full(row_width(nfold), np.nan, np.float64)
     row[0], row[1], row[2] = status, fitness, wall
     for j, f in enumerate(fold_ids[:len(scores)]):
         row[3 + f] = scores[j]
+    for j, f in enumerate(fold_ids[:len(aux or ())]):
+        row[3 + nfold + f] = aux[j]
     return row
 
 
@@ -307,9 +317,13 @@ class DistributedPopulation(Population):
     def evaluate_pending(self):
         return self.evaluate_in_parallel()
 
-    def evaluate_in_parallel(self):
-        """Dispatch pending individuals to every rank and collect fitness."""
+    def evaluate_in_parallel(self, limit=None):
+        """Dispatch pending individuals to every rank and collect fitness.
+        ``limit``: evaluate at most that many (in population order) -- one
+        evaluation *round*; the rest stay pending."""
         todo = self.pending()
+        if limit is not None:
+            todo = todo[:max(0, int(limit))]
         if not todo:
             return 0
         self.generation_counter += 1
@@ -318,7 +332,10 @@ class DistributedPopulation(Population):
         codec = GenomeCodec(todo[0].get_genome())
         costs = [float(ind.cost()) if hasattr(ind, "cost") else 1.0 for ind in todo]
         splittable = self.split_folds and hasattr(todo[0], "build_fitness_model")
-        units, ucost = make_units(costs, nfold, comm.world_size, splittable)
+        # population-batched evaluators take (candidate, fold) units: equal
+        # group counts per rank at any generation size
+        per_fold = splittable and getattr(self.local_evaluator, "pop_batch", 1) > 1
+        units, ucost = make_units(costs, nfold, comm.world_size, splittable, per_fold=per_fold)
         dynamic = self.schedule == "dynamic" and comm.world_size > 1
         if dynamic:
             # table order = claim order: most expensive first (on-line LPT)
@@ -352,14 +369,14 @@ class DistributedPopulation(Population):
         else:
             mine = [(k, make_unit(k)) for k in range(len(units)) if owner[k] == comm.rank]
         rows = evaluate_units(mine, self.local_evaluator, nfold, comm.rank, self.generation_counter)
-        local = np.zeros((len(units), 3 + nfold), np.float64)
+        local = np.zeros((len(units), row_width(nfold)), np.float64)
         for k, row in rows.items():
             local[k] = row
         gathered = comm.all_gather_array(local)
         merged = _merge(gathered, units, len(todo), nfold)
         retried = 0
         for slot, ind in enumerate(todo):
-            status, fitness, scores = merged[slot]
+            status, fitness, scores, aux = merged[slot]
             if status != ST_OK:
                 retried += 1
                 try:
@@ -371,6 +388,8 @@ class DistributedPopulation(Population):
             else:
                 ind.set_fitness(fitness)
                 ind.fold_scores = scores
+                if aux is not None:
+                    ind.fold_metrics = dict(getattr(ind, "fold_metrics", None) or {}, categorical_accuracy=aux)
         self.last_dispatch = {"units": len(units), "candidates": len(todo), "retried": retried,
                               "wall_s": time.perf_counter() - t0,
                               "schedule": "dynamic" if dynamic else "lpt",
@@ -398,7 +417,8 @@ def _clone(ind):
 
 def _merge(gathered, units, ncand, nfold):
     """Combine per-rank result tables into ``(status, fitness, fold_scores)`` per candidate."""
-    per = [{"status": ST_OK, "scores": [np.nan] * nfold, "fit": [], "n": 0} for _ in range(ncand)]
+    per = [{"status": ST_OK, "scores": [np.nan] * nfold, "aux": [np.nan] * nfold, "fit": [], "n": 0}
+           for _ in range(ncand)]
     have = [False] * len(units)
     rows = [None] * len(units)
     for table in gathered:
@@ -415,18 +435,20 @@ def _merge(gathered, units, ncand, nfold):
         p["fit"].append((row[1], len(fids)))
         for f in fids:
             p["scores"][f] = float(row[3 + f])
+            p["aux"][f] = float(row[3 + nfold + f])
     out = []
     for p in per:
         if p["status"] != ST_OK or not p["fit"]:
-            out.append((ST_ERR, None, None))
+            out.append((ST_ERR, None, None, None))
             continue
+        aux = [a for a in p["aux"] if not np.isnan(a)]
         scores = [s for s in p["scores"] if not np.isnan(s)]
         if scores and len(scores) == sum(n for _, n in p["fit"]):
             fit = float(np.mean(scores))
         else:
             tot = sum(n for _, n in p["fit"])
             fit = float(sum(f * n for f, n in p["fit"]) / tot)
-        out.append((ST_OK, fit, p["scores"] if scores else None))
+        out.append((ST_OK, fit, p["scores"] if scores else None, aux or None))
     return out
 
 
@@ -497,7 +519,7 @@ class GentunWorker(object):
         else:
             mine = [(k, make_unit(k)) for k in range(n_units) if int(table[k, 1]) == comm.rank]
         rows = evaluate_units(mine, self.evaluator, nfold, comm.rank, generation)
-        local = np.zeros((table.shape[0], 3 + nfold), np.float64)
+        local = np.zeros((table.shape[0], row_width(nfold)), np.float64)
         for k, row in rows.items():
             local[k] = row
         comm.all_gather_array(local)

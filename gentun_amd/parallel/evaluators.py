@@ -104,6 +104,7 @@ class LocalBatchEvaluator(SequentialEvaluator):
         def done(ind, model, res, wall, _tag):
             ind.set_fitness(model.collect([res]))
             ind.fold_scores = list(model.fold_scores)
+            ind.fold_metrics = dict(model.fold_metrics or {})
             self._store(ind)
             self._log(ind, wall)
 
@@ -121,6 +122,9 @@ def _chunks(units, nchunks):
         bins[k].append(u)
         load[k] += u[3]
     return [b for b in bins if b]
+
+
+
 
 
 def run_cnn_units(units, evaluator, done):
@@ -147,13 +151,18 @@ def run_cnn_units(units, evaluator, done):
             ind.phase_ms = phase            # device ms per phase of the (shared) job
             done(ind, model, r, wall, tag)
 
-    pending = []
+    pending = []          # (ind, model, fold_ids, cost, tag, groups)
     k = 0
     exhausted = False
+
+    def groups_of(entries):
+        return sum(e[5] for e in entries)
+
+    max_groups = None     # groups (candidate x fold pairs) per population job
     while True:
-        if not exhausted and len(pending) < pop_batch * len(streams):
-            # pull enough units to fill every stream with a batch
-            while len(pending) < pop_batch * len(streams):
+        if not exhausted and (max_groups is None or groups_of(pending) < max_groups * len(streams)):
+            # pull enough units to fill every stream with a batch of groups
+            while max_groups is None or groups_of(pending) < max_groups * len(streams):
                 nxt = next(it, None)
                 if nxt is None:
                     exhausted = True
@@ -162,7 +171,9 @@ def run_cnn_units(units, evaluator, done):
                 model = ind.build_fitness_model(device=device)
                 cost = float(ind.cost()) if hasattr(ind, "cost") else 1.0
                 nf = len(fold_ids) if fold_ids is not None else model.nfold
-                pending.append((ind, model, fold_ids, cost * nf, tag))
+                if max_groups is None:
+                    max_groups = pop_batch * model.nfold
+                pending.append((ind, model, fold_ids, cost * nf, tag, nf))
         if not pending:
             break
         if len(window) >= len(streams):
@@ -171,17 +182,23 @@ def run_cnn_units(units, evaluator, done):
         hip = all(e[1].backend == "hip" for e in pending) and pop_batch > 1
         if hip:
             free = len(streams) - len(window)
-            nchunks = min(free, max(1, -(-len(pending) // pop_batch))) if exhausted else 1
-            take = pending[:pop_batch * nchunks] if exhausted else pending[:pop_batch]
+            nchunks = min(free, max(1, -(-groups_of(pending) // max_groups))) if exhausted else 1
+            take, ng = [], 0
+            for e in pending:
+                if take and ng + e[5] > max_groups * nchunks:
+                    break
+                take.append(e)
+                ng += e[5]
             pending = pending[len(take):]
-            chunks = _chunks([(e[0], e[1], e[2], e[3], e[4]) for e in take], nchunks)
+            chunks = _chunks(take, nchunks)
             for ch in chunks:
                 if len(window) >= len(streams):
                     retire(window.pop(0))
                 stream = streams[k % len(streams)]
                 k += 1
+                _check_shared_settings(ch)
                 members, items = [], []
-                for ind, model, fold_ids, _c, tag in ch:
+                for ind, model, fold_ids, _c, tag, _g in ch:
                     members.append(model.member(fold_ids))
                     items.append((ind, model, tag))
                 m0 = ch[0][1]
@@ -191,7 +208,7 @@ def run_cnn_units(units, evaluator, done):
                 job.launch()
                 window.append((job, items, t0, True))
         else:
-            ind, model, fold_ids, _c, tag = pending.pop(0)
+            ind, model, fold_ids, _c, tag, _g = pending.pop(0)
             stream = streams[k % len(streams)]
             k += 1
             jobs = model.make_jobs(stream=stream, fold_ids=fold_ids)
@@ -201,6 +218,28 @@ def run_cnn_units(units, evaluator, done):
             window.append((_MultiJob(jobs), [(ind, model, tag)], t0, False))
     for entry in window:
         retire(entry)
+
+
+def _settings_key(model):
+    """Everything a population job takes from its first member and applies
+    to all (training config, dataset identity, search space)."""
+    c = model.cfg
+    return (id(model.x_train), id(model.y_train), model.backend, str(model.device), model.nfold,
+            c.epochs, c.learning_rate, c.batch_size, c.dropout, c.loss, c.dtype, c.seed, c.optimizer, c.momentum,
+            getattr(c, "reset", None), getattr(c, "batch_norm", None),
+            model.nodes, model.input_shape, model.kernels_per_layer, model.kernel_sizes, model.dense_units,
+            model.classes)
+
+
+def _check_shared_settings(chunk):
+    """A population job trains every member with the first member's settings:
+    refuse a batch that mixes settings instead of training some candidates
+    with another candidate's hyper-parameters."""
+    k0 = _settings_key(chunk[0][1])
+    for e in chunk[1:]:
+        if _settings_key(e[1]) != k0:
+            raise ValueError("population job members differ in training settings / dataset / search space; "
+                             "evaluate them in separate batches")
 
 
 def _merge_phases(jobs):

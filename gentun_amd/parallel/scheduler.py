@@ -5,11 +5,15 @@ The reference load-balances dynamically through a RabbitMQ pull queue with
 whole genome table, so an assignment computed on rank 0 from a cost model
 (forward FLOPs per sample, :meth:`Plan.forward_flops`) is broadcast with it.
 
-Work units are ``(candidate, fold-group)``. A candidate's folds stay
-together (one fold-batched launch) unless there are fewer candidates than
-ranks, in which case candidates are split into fold groups so every GPU gets
-work. Units are placed Longest-Processing-Time-first on the least-loaded
-rank; ties break on rank id, so the result is deterministic.
+Work units are ``(candidate, fold-group)``. With a population-batched
+evaluator (every (candidate, fold) pair of a rank's share is one group of
+shared kernel launches, models/cnn_hip.py) the unit is always ONE fold
+(``per_fold``): the ranks then get near-equal numbers of groups even when a
+generation re-evaluates only ~14 of 32 candidates on 8 GPUs (SURVEY.md §2.2;
+master.py:108-129 dispatches whole candidates). Otherwise a candidate's folds
+stay together (one fold-batched launch) unless there are fewer candidates
+than ranks. Units are placed Longest-Processing-Time-first on the
+least-loaded rank; ties break on rank id, so the result is deterministic.
 """
 
 import heapq
@@ -28,17 +32,20 @@ def lpt_assign(costs, world_size):
     return owner
 
 
-def make_units(costs, nfold, world_size, split_folds=True):
+def make_units(costs, nfold, world_size, split_folds=True, per_fold=False):
     """Units ``(candidate, fold_ids)`` with their costs.
 
-    Splits candidates into fold groups only while that helps fill the ranks:
-    the number of groups per candidate is ``min(nfold, ceil(world/ncand))``.
+    ``per_fold``: one unit per (candidate, fold). Otherwise candidates are
+    split into fold groups only while that helps fill the ranks: the number
+    of groups per candidate is ``min(nfold, ceil(world/ncand))``.
     """
     n = len(costs)
     if n == 0:
         return [], []
     groups = 1
-    if split_folds and nfold > 1 and n < world_size:
+    if split_folds and nfold > 1 and per_fold and world_size > 1:
+        groups = nfold
+    elif split_folds and nfold > 1 and n < world_size:
         groups = min(nfold, -(-world_size // n))
     units, ucost = [], []
     base, extra = divmod(nfold, groups)
