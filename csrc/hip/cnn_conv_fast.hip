@@ -872,8 +872,13 @@ extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, in
 // CU). 3 splits x 80 groups of a 16-candidate population = 240 workgroups, one
 // round on 256 CUs; 4 splits left a 64-workgroup second round (population step
 // 2-3 % slower, same-box sweep).
+// fp32 (prec 1): the band work is ~6x the bf16 one, and a bench round
+// trains only ~10 groups per launch: 8 / 32 splits keep >= 80 / 320
+// workgroups busy at 10 groups (3 splits left 30 workgroups on 256 CUs:
+// 199 us per call, 34 % of a 10-group step) for 2.7x the partial-sum bytes.
 extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, int W, int prec) {
-  (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H; (void)prec;
+  (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H;
+  if (prec == 1) return W >= 32 ? 32 : 8;
   return W >= 32 ? 16 : 3;
 }
 
