@@ -24,6 +24,8 @@
 // Epilogue = generic kernel's: bias + ReLU (forward) or per-group DAG
 // fan-out (accumulate, ReLU mask) for the data gradient.
 
+#include <algorithm>
+
 #include "cnn_args.h"
 
 // LDS bytes of one launch: the patch (NPL bf16 planes) or the output tile
@@ -362,6 +364,243 @@ conv_fast_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// fp32 (prec 1), persistent and software-pipelined. The tile kernel above
+// runs stage -> MFMA -> epilogue back to back, and with 2 workgroups per CU
+// (60 KB of 3-plane patch, ~180 VGPRs) its memory phases barely overlap the
+// matrix work (tools/bench_conv.py: time ~= skip-MFMA time + MFMA time).
+// Here a workgroup loops over tiles (tile = blockIdx.x + i * gridDim.x) and
+// issues the global loads of its NEXT tile's patch into registers before the
+// current tile's MFMA loop, splitting and writing them to LDS after it (the
+// async-STAGE split); the epilogue stores straight from the accumulators
+// (16 contiguous bytes = 4 fp32 channels per lane) instead of through an LDS
+// tile, so a tile costs one LDS refill and two barriers. Only the first input
+// slot is prefetched; further DAG inputs are added after the MFMA loop.
+// ---------------------------------------------------------------------------
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV>
+__global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2)))
+conv_f32p_kernel(ConvArgs a, int ntiles) {
+  constexpr int NPL = GT_NPL_F32;
+  constexpr int NTH = NWV * 64;
+  constexpr int PH = TH + KH - 1, PW = W + KW - 1;
+  constexpr int NP = PH * PW * NCBI;
+  constexpr int NPT = (NP + NTH - 1) / NTH;
+  constexpr int NCH = KH * KW * NCBI;
+  constexpr int NKS = (NCH + 3) / 4;
+  constexpr int TP = TH * W;
+  constexpr int NPG = TP / 16;
+  constexpr int CT = (NT >= 2 && NT % 2 == 0) ? 2 : 1;
+  constexpr int WC = NT / CT;
+  constexpr int WP = NWV / WC;
+  constexpr int PG = NPG / WP;
+  constexpr int PF = NKS < 2 ? NKS : 2;
+  static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == NWV, "tile shape");
+  static_assert(W % 16 == 0, "pixel groups must tile image rows");
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
+  uint4* patch = smem;                               // [NPL][NP]
+  __shared__ int coff[NKS * 4];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  const int nband = a.H / TH;
+  const int tiles_per_group = a.B * nband;
+  const long img = (long)a.H * W * NCBI * 8;
+  const long oimg = (long)a.H * W * NCO * 8;
+  for (int c = tid; c < NKS * 4; c += NTH) {
+    const int kk = c / NCBI, cb = c % NCBI;
+    coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
+  }
+  // per-thread patch chunk geometry (tile independent)
+  int pdh[NPT], pdw[NPT], pcb[NPT];
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) {
+    const int i = tid + NTH * j;
+    const int pix = i / NCBI;
+    pcb[j] = i % NCBI;
+    pdh[j] = pix / PW - KH / 2;
+    pdw[j] = pix % PW - KW / 2;
+  }
+  struct Tile { GroupRec gr; int b, h0; };
+  auto tile_of = [&](int t) {
+    Tile x;
+    const int q = t / tiles_per_group, r = t - q * tiles_per_group;
+    x.gr = group_rec(a.gtab, q, a.n_in, a.n_out, a.acc_flags, a.out_mask);
+    x.b = r / nband;
+    x.h0 = (r - x.b * nband) * TH;
+    return x;
+  };
+  float xr[NPT][8];
+  // loads of the first input slot (or the gathered dataset image) of tile x
+  auto load_first = [&](const Tile& x) {
+    const float* src = a.gather
+        ? static_cast<const float*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + x.gr.g) * a.B + x.b] * img
+        : static_cast<const float*>(a.in[__builtin_ctz(x.gr.in_mask | 0x100) & 7]) + ((long)x.gr.g * a.B + x.b) * img;
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int hh = x.h0 + pdh[j], ww = pdw[j];
+      const bool ok = tid + NTH * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
+      if (ok) load8f(src + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, xr[j]);
+    }
+  };
+  // remaining DAG input slots of tile x, added into xr; the split planes to
+  // LDS; the exact fp32 sum of N-ary tiles to xsum (interior chunks)
+  auto finish_stage = [&](const Tile& x) {
+    const int first = __builtin_ctz(x.gr.in_mask | 0x100) & 7;
+    const bool multi = !a.gather && __builtin_popcount(x.gr.in_mask) > 1;
+    if (multi) {
+      const long gimg = ((long)x.gr.g * a.B + x.b) * img;
+      for (int k = first + 1; k < GT_MAXSLOT; ++k) {
+        if (!((x.gr.in_mask >> k) & 1)) continue;
+        const float* sk = static_cast<const float*>(a.in[k]) + gimg;
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+          const int hh = x.h0 + pdh[j], ww = pdw[j];
+          if (tid + NTH * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W) {
+            float t8[8];
+            load8f(sk + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, t8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xr[j][e] += t8[e];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int i = tid + NTH * j;
+      if (i >= NP) continue;
+      split8(xr[j], patch[i], patch[NP + i], patch[2 * NP + i]);
+      if (multi && a.xsum) {
+        const int hh = x.h0 + pdh[j], ww = pdw[j];
+        if (pdh[j] >= 0 && pdh[j] < TH && hh < a.H && ww >= 0 && ww < W)     // band interior
+          store8f(static_cast<float*>(a.xsum) + ((long)x.gr.g * a.B + x.b) * img + ((long)hh * W + ww) * (NCBI * 8) +
+                      pcb[j] * 8, xr[j]);
+      }
+    }
+  };
+
+  const int wco = (wave % WC) * CT;
+  const int pgw = (wave / WC) * PG;
+  const int lbase = (l16 / W) * PW * NCBI + (l16 % W) * NCBI;
+  const int gbase = (((pgw * 16) / W) * PW + (pgw * 16) % W) * NCBI;
+
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  Tile cur = tile_of(t);
+  load_first(cur);
+  finish_stage(cur);
+  __syncthreads();
+  while (true) {
+    const int tn = t + gridDim.x;
+    const bool more = tn < ntiles;
+    Tile nxt;
+    if (more) {
+      nxt = tile_of(tn);
+      load_first(nxt);                                 // in flight during this tile's MFMAs
+    }
+    // ---- weights of this tile's group
+    const int g = cur.gr.g;
+    const uint16_t* wrow[CT];
+    bool wok[CT];
+#pragma unroll
+    for (int tt = 0; tt < CT; ++tt) {
+      const int co = (wco + tt) * 16 + l16;
+      wok[tt] = co < NCO * 8;
+      wrow[tt] = a.w + ((long)g * (NCO * 8) + (wok[tt] ? co : 0)) * (NCH * 8);
+    }
+    uint4 areg[PF][CT][NPL];
+    auto load_a = [&](int s, uint4 (*dst)[NPL]) {
+      const int c = s * 4 + kq;
+#pragma unroll
+      for (int tt = 0; tt < CT; ++tt)
+#pragma unroll
+        for (int p = 0; p < NPL; ++p)
+          dst[tt][p] = (wok[tt] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[tt] + p * a.wps + c * 8)
+                                             : make_uint4(0, 0, 0, 0);
+    };
+#pragma unroll
+    for (int s = 0; s < PF; ++s) load_a(s, areg[s]);
+    f32x4_t acc[CT][PG];
+#pragma unroll
+    for (int tt = 0; tt < CT; ++tt)
+#pragma unroll
+      for (int h = 0; h < PG; ++h) acc[tt][h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const uint4* pb = patch + lbase + gbase + coff[s * 4 + kq];
+      uint4 bfr[PG][NPL];
+#pragma unroll
+      for (int h = 0; h < PG; ++h) {
+        const int p = h * 16;
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) bfr[h][q] = pb[q * NP + ((p / W) * PW + (p % W)) * NCBI];
+      }
+#pragma unroll
+      for (int tt = 0; tt < CT; ++tt)
+#pragma unroll
+        for (int h = 0; h < PG; ++h) acc[tt][h] = mfma_np<NPL>(areg[s % PF][tt], bfr[h], acc[tt][h]);
+      if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
+    }
+    // ---- epilogue straight from the accumulators: lane = 4 channels of one pixel
+    const long obase = ((long)g * a.B + cur.b) * oimg + (long)cur.h0 * W * (NCO * 8);
+#pragma unroll
+    for (int tt = 0; tt < CT; ++tt) {
+      const int co0 = (wco + tt) * 16 + kq * 4;
+      if (co0 >= NCO * 8) continue;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.bias) {
+        const float4 q = *reinterpret_cast<const float4*>(a.bias + (long)g * (NCO * 8) + co0);
+        bv[0] = q.x; bv[1] = q.y; bv[2] = q.z; bv[3] = q.w;
+      }
+#pragma unroll
+      for (int h = 0; h < PG; ++h) {
+        const int p = (pgw + h) * 16 + l16;
+        const long off = obase + (long)p * (NCO * 8) + co0;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          v[i] = acc[tt][h][i] + bv[i];
+          if (a.relu) v[i] = fmaxf(v[i], 0.f);
+        }
+        for (int k = 0; k < GT_MAXSLOT; ++k) {
+          if (!((cur.gr.out_mask >> k) & 1)) continue;
+          float* dst = static_cast<float*>(a.out[k]) + off;
+          float4 o = make_float4(v[0], v[1], v[2], v[3]);
+          if ((cur.gr.out_mask >> (8 + k)) & 1) {
+            const float4 q = *reinterpret_cast<const float4*>(dst);
+            o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+          }
+          if ((cur.gr.out_mask >> (16 + k)) & 1) {
+            const float4 m = *reinterpret_cast<const float4*>(static_cast<const float*>(a.out_mask[k]) + off);
+            o.x = m.x > 0.f ? o.x : 0.f; o.y = m.y > 0.f ? o.y : 0.f;
+            o.z = m.z > 0.f ? o.z : 0.f; o.w = m.w > 0.f ? o.w : 0.f;
+          }
+          *reinterpret_cast<float4*>(dst) = o;
+        }
+      }
+    }
+    if (!more) break;
+    __syncthreads();                                   // every wave is done with this tile's patch
+    finish_stage(nxt);
+    __syncthreads();
+    cur = nxt;
+    t = tn;
+  }
+}
+
+// persistent pipelined fp32 conv: measured no faster than the tile kernel on
+// the S=(3,5) shapes (profiles/conv_f32_persistent_ab_r2.txt: the k loop, not
+// the staging, sets the time), so off by default; kept as the A/B switch
+static int g_f32_persistent = 0;
+static int g_f32_grid = 0;         // workgroups of the persistent kernel (0: 2 per CU)
+
+extern "C" int gt_conv_set_f32p(int on, int grid) {
+  const int old = g_f32_persistent;
+  g_f32_persistent = on;
+  g_f32_grid = grid;
+  return old;
+}
+
+// ---------------------------------------------------------------------------
 // dispatch: (KH, KW, Cinp, W, Coutp-tiles) -> instantiation; -100 = no match
 // (the caller then uses the generic kernel)
 // ---------------------------------------------------------------------------
@@ -409,9 +648,24 @@ static void lds_limit(F* fn, size_t bytes) {
 #define CONV_FAST_CASE_NW(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                      \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 0)
 
-// fp32 tensors (prec 1): 3-plane patch -> bands of 8 rows (LDS), 4 waves
+// fp32 tensors (prec 1): 3-plane patch -> bands of 8 rows (LDS), 4 waves;
+// the persistent pipelined kernel unless switched off
+#define CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                       \
+  {                                                                                                     \
+    const int ntiles = a->ngroups * a->B * (a->H / TH_);                                                \
+    const int grid = std::min(ntiles, g_f32_grid > 0 ? g_f32_grid : 512);                               \
+    const size_t lds = (size_t)(TH_ + KH_ - 1) * (W_ + KW_ - 1) * NCBI_ * 16 * GT_NPL_F32;              \
+    auto* fn = conv_f32p_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_>;                            \
+    lds_limit(fn, lds);                                                                                 \
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(NWV_ * 64), lds, stream, *a, ntiles);                       \
+    return (int)hipGetLastError();                                                                      \
+  }
+
 #define CONV_FAST_CASE_F32(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                     \
-  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
+    if (g_f32_persistent && (W_ % 16) == 0) CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)   \
+    CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
+  }
 
 extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
