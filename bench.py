@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--nfold", type=int, default=5)
     ap.add_argument("--dtype", default="fp32", choices=("fp32", "bf16"))
     ap.add_argument("--loss", default="bce_compat", choices=("bce_compat", "ce"))
+    ap.add_argument("--fold-reset", default="all", choices=("all", "kernels"),
+                    help="all: the 5 folds of a candidate train concurrently, each from fresh weights (fast mode); "
+                         "kernels: the reference's sequential folds with biases carried over")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--space", choices=("default", "deep"), default="default",
@@ -120,7 +123,7 @@ def run(args):
     extra = dict(nodes=nodes, input_shape=(32, 32, 3), kernels_per_layer=kernels,
                  kernel_sizes=((5, 5),) * len(nodes), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=args.nfold, epochs=epochs, learning_rate=lrs, batch_size=32, dtype=args.dtype,
-                 loss=args.loss, seed=args.seed, backend=args.backend)
+                 loss=args.loss, seed=args.seed, backend=args.backend, reset=args.fold_reset, batching="keras")
     evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch)
     N = comm.world_size
     round_size = per_gpu * N
@@ -195,6 +198,7 @@ def run(args):
                    "candidates_per_round": round_size, "per_gpu": per_gpu, "nfold": args.nfold,
                    "epochs": list(epochs), "learning_rate": list(lrs), "samples": args.samples,
                    "loss": args.loss, "backend": args.backend or ("hip" if device.type == "cuda" else "torch"),
+                   "fold_reset": args.fold_reset, "batching": "keras (8000 = 250 x 32: no short batch)",
                    "fp32_impl": "fp32 tensors, 3-way exact bf16 split x 6 MFMA terms per product"
                    if args.dtype == "fp32" else None,
                    "streams_per_gpu": args.streams, "pop_batch": args.pop_batch},

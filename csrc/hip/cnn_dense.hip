@@ -179,6 +179,7 @@ struct HeadArgs {
   float drop_scale;        // 1/(1-p)
   int eval;
   int prec;
+  const int* valid;        // [steps][G] real rows of each training batch (Keras short batch) or null = B
 };
 
 #define HEAD_MAXB 64
@@ -237,7 +238,9 @@ __global__ void __launch_bounds__(64) head_fwd_kernel(HeadArgs a) {
     return;
   }
   float* dz = a.dz + ((long)g * a.B + b) * C;
-  const float inv_b = 1.0f / a.B;
+  // mean over the batch's real rows; padding rows of a short batch: zero weight
+  const int nv = a.valid ? a.valid[(long)step * a.G + g] : a.B;
+  const float inv_b = (b < nv && nv > 0) ? 1.0f / nv : 0.f;
   if (a.loss_ce) {
     for (int c = 0; c < C; ++c) dz[c] = (p[c] - ((c == y) ? 1.f : 0.f)) * inv_b;
   } else {

@@ -32,7 +32,12 @@ def _common(ap):
     ap.add_argument("--algorithm", choices=("roulette", "tournament"), default="roulette")
     ap.add_argument("--seed", type=int, default=d.seed)
     ap.add_argument("--checkpoint-dir", default=d.checkpoint_dir)
-    ap.add_argument("--resume", default=None, help="checkpoint file or directory to continue from")
+    ap.add_argument("--resume", default=None,
+                    help="checkpoint file or directory to continue from; 'auto': <checkpoint-dir>/latest.json if "
+                         "it exists (restarted runs), else a fresh start")
+    ap.add_argument("--watchdog", default=os.environ.get("GENTUN_WATCHDOG", ""),
+                    help="per-generation deadline first_s[:factor[:min_s]]: a rank stuck past it (dead / hung "
+                         "peer) exits with code 75 so the launcher can restart the group from the checkpoint")
     ap.add_argument("--events", default=d.events, help="JSONL event log path")
     ap.add_argument("--streams", type=int, default=d.streams, help="concurrent population jobs per GPU")
     ap.add_argument("--pop-batch", type=int, default=d.pop_batch,
@@ -70,6 +75,11 @@ def _run_search(args, species, x, y, extra, maximize):
     from .parallel.distributed import DistributedPopulation, GentunWorker
     from .utils import rng
     cfg = _config(args)
+    if args.watchdog:
+        os.environ["GENTUN_WATCHDOG"] = args.watchdog
+    if args.resume == "auto":
+        latest = os.path.join(cfg.checkpoint_dir or "", "latest.json")
+        args.resume = latest if cfg.checkpoint_dir and os.path.exists(latest) else None
     device = _device()
     comm = from_env(backend=cfg.backend, timeout_s=cfg.collective_timeout_s, device=device)
     evaluator = LocalBatchEvaluator(device=device, streams=cfg.streams, pop_batch=cfg.pop_batch)
@@ -115,7 +125,8 @@ def cmd_cnn(args):
     extra = dict(nodes=nodes, input_shape=shape, kernels_per_layer=kernels, kernel_sizes=ks,
                  dense_units=args.dense, dropout_probability=args.dropout, classes=args.classes, nfold=args.nfold,
                  epochs=_ints(args.epochs), learning_rate=_floats(args.lr), batch_size=args.batch, loss=args.loss,
-                 seed=args.seed, optimizer=args.optimizer, momentum=args.momentum, dtype=args.dtype)
+                 seed=args.seed, optimizer=args.optimizer, momentum=args.momentum, dtype=args.dtype,
+                 reset=args.fold_reset, batching=args.batching)
     return _run_search(args, GeneticCnnIndividual, x, y, extra, maximize=True)
 
 
@@ -179,6 +190,10 @@ def main(argv=None):
     c.add_argument("--dtype", choices=("bf16", "fp32"), default=_env_default("dtype"),
                    help="fp32 (reference precision; HIP: exact split-fp32 MFMA) or bf16 (fast mode)")
     c.add_argument("--optimizer", choices=("adam", "sgd"), default="adam")
+    c.add_argument("--fold-reset", choices=("kernels", "all"), default="kernels",
+                   help="kernels: reference sequential folds (biases carried over); all: concurrent folds (fast)")
+    c.add_argument("--batching", choices=("keras", "wrap"), default="keras",
+                   help="keras: short last batch; wrap: the last batch wraps around the epoch permutation")
     c.add_argument("--momentum", type=float, default=0.9, help="SGD momentum")
     c.set_defaults(fn=cmd_cnn)
     x = sub.add_parser("xgb", help="GBDT (XGBoost-style) hyper-parameter search")

@@ -60,7 +60,8 @@ def atomic_write_json(path, obj):
 
 def _individual_record(i, ind):
     return {"i": i, "genes": _jsonable(ind.get_genes()), "fitness": ind.fitness,
-            "fold_scores": _jsonable(getattr(ind, "fold_scores", None))}
+            "fold_scores": _jsonable(getattr(ind, "fold_scores", None)),
+            "fold_metrics": _jsonable(getattr(ind, "fold_metrics", None))}
 
 
 def generation_state(ga):
@@ -109,6 +110,8 @@ def _rebuild(species, x_train, y_train, rec, extra):
     ind = species(x_train, y_train, genes=dict(rec["genes"]), **extra)
     ind.set_fitness(rec["fitness"])
     ind.fold_scores = rec.get("fold_scores")
+    if rec.get("fold_metrics"):
+        ind.fold_metrics = rec["fold_metrics"]
     return ind
 
 

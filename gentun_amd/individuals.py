@@ -268,8 +268,11 @@ class GeneticCnnIndividual(Individual):
     MI355X; or 'bf16', the fast mode: bf16 tensors and MFMA, fp32 master weights), ``seed``
     (run seed; fitness is a pure function of (genes, seed, fold)),
     ``backend`` ('hip' -- MI355X kernels, default on GPU -- or 'torch' oracle),
-    ``device``, and ``optimizer`` ('adam' = the reference's Keras Adam, or
-    'sgd' = Keras SGD with ``momentum``; both reset at every lr stage).
+    ``device``, ``optimizer`` ('adam' = the reference's Keras Adam, or
+    'sgd' = Keras SGD with ``momentum``; both reset at every lr stage),
+    ``reset`` ('kernels' = the reference's sequential folds that re-draw only
+    the kernels, or 'all' = concurrent folds from fresh weights) and
+    ``batching`` ('keras' = short last batch, or 'wrap').
     """
 
     def __init__(self, x_train, y_train, genome=None, genes=None, crossover_rate=0.3, mutation_rate=0.1,
@@ -277,7 +280,7 @@ class GeneticCnnIndividual(Individual):
                  kernel_sizes=((5, 5), (5, 5)), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
                  loss='bce_compat', dtype='fp32', seed=0, backend=None, device=None, optimizer='adam',
-                 momentum=0.9):
+                 momentum=0.9, reset='kernels', batching='keras'):
         if genome is None:
             genome = {'S_{}'.format(i + 1): k * (k - 1) // 2 for i, k in enumerate(nodes)}
         if genes is None:
@@ -306,6 +309,8 @@ class GeneticCnnIndividual(Individual):
         self.device = device
         self.optimizer = optimizer
         self.momentum = momentum
+        self.reset = reset
+        self.batching = batching
 
     @staticmethod
     def generate_random_genes(genome):
@@ -322,7 +327,8 @@ class GeneticCnnIndividual(Individual):
                                self.dropout_probability, self.classes, self.nfold, self.epochs,
                                self.learning_rate, self.batch_size, loss=self.loss, dtype=self.dtype,
                                seed=self.seed, backend=self.backend, device=device or self.device,
-                               optimizer=self.optimizer, momentum=self.momentum)
+                               optimizer=self.optimizer, momentum=self.momentum, reset=self.reset,
+                               batching=self.batching)
 
     def cost(self):
         """Relative training cost (forward FLOPs/sample); LPT scheduling key."""
@@ -356,6 +362,8 @@ class GeneticCnnIndividual(Individual):
             'device': self.device,
             'optimizer': self.optimizer,
             'momentum': self.momentum,
+            'reset': self.reset,
+            'batching': self.batching,
         }
 
     def mutate(self):

@@ -28,7 +28,7 @@ class GeneticCnnModel(GentunModel):
     def __init__(self, x_train, y_train, genes, nodes, input_shape, kernels_per_layer, kernel_sizes, dense_units,
                  dropout_probability, classes, nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
                  loss="bce_compat", dtype="fp32", seed=0, backend=None, device=None, fold_parallel=True,
-                 optimizer="adam", momentum=0.9):
+                 optimizer="adam", momentum=0.9, reset="kernels", batching="keras"):
         super(GeneticCnnModel, self).__init__(x_train, y_train)
         self.genes = dict(genes)
         self.name = '-'.join(self.genes[k] for k in sorted(self.genes))
@@ -57,7 +57,7 @@ class GeneticCnnModel(GentunModel):
         self.backend = backend or _eng.default_backend(self.device)
         self.cfg = _eng.TrainConfig(epochs=epochs, learning_rate=learning_rate, batch_size=batch_size,
                                     dropout=dropout_probability, loss=loss, dtype=dtype, seed=seed,
-                                    optimizer=optimizer, momentum=momentum)
+                                    optimizer=optimizer, momentum=momentum, reset=reset, batching=batching)
         self.fold_parallel = fold_parallel
         self.model = self.build_model(self.genes, self.nodes, self.input_shape, self.kernels_per_layer,
                                       self.kernel_sizes, self.dense_units, self.dropout_probability, self.classes)
@@ -87,9 +87,14 @@ class GeneticCnnModel(GentunModel):
         return body, " + ".join(names[i] for i in outputs)
 
     def reset_weights(self):
-        """Weights are re-initialised per fold inside the engine (Glorot
-        kernels, zero biases); kept for API compatibility."""
-        return None
+        """Per-fold re-initialisation policy of the engine (keras_models.py:
+        120-125): with ``reset="kernels"`` (default) each fold re-draws only
+        the Glorot kernels and keeps the biases of the previous fold
+        (models/cnn_engine.py SequentialFoldJob); ``reset="all"`` trains the
+        folds concurrently from fresh kernels and zero biases. Returns the
+        active policy (the engine applies it; there is no live Keras model
+        to mutate here)."""
+        return self.cfg.reset
 
     def plot(self, path=None):
         """Write the decoded topology as text (Keras' plot_model needs
@@ -113,7 +118,8 @@ class GeneticCnnModel(GentunModel):
     def make_jobs(self, stream=None, fold_ids=None):
         folds = self.make_folds()
         ids = list(range(self.nfold)) if fold_ids is None else list(fold_ids)
-        groups = [ids] if self.fold_parallel else [[i] for i in ids]
+        # sequential-fold semantics need every fold of the candidate in one job
+        groups = [ids] if (self.fold_parallel or self.cfg.reset == "kernels") else [[i] for i in ids]
         return [_eng.make_job(self.backend, self.model, self.x_train, self.y_train, [folds[i] for i in grp],
                               self.cfg, self.device, fold_ids=grp, stream=stream) for grp in groups]
 

@@ -13,10 +13,12 @@ concurrently (hard part 1: a single tiny candidate cannot fill 256 CUs).
 Training protocol (reference: gentun/models/keras_models.py:120-143, Keras
 2.2 semantics -- SURVEY.md §2.2):
 
-* per fold: fresh Glorot-uniform kernels, zero biases (the reference resets
-  kernels only and lets biases carry over between *sequential* folds; with
-  folds trained concurrently every fold starts from zero biases -- the
-  ``reset="all"`` variant of SURVEY.md Q6);
+* folds (``reset``): ``"kernels"`` (default, the reference:
+  folds run one after another and each re-draws only the Glorot kernels,
+  so the biases trained on fold k start fold k+1 -- keras_models.py:
+  120-125,135; :class:`SequentialFoldJob`), or ``"all"`` (folds train
+  CONCURRENTLY as groups of one job, each from fresh kernels and zero
+  biases -- the fast mode);
 * per ``(epochs_i, lr_i)`` stage a NEW Adam (m, v, t reset), beta1 0.9,
   beta2 0.999, eps 1e-7, Keras bias-corrected step size;
 * loss ``bce_compat`` = binary cross-entropy on the softmax output with
@@ -24,10 +26,12 @@ Training protocol (reference: gentun/models/keras_models.py:120-143, Keras
   (Keras' resolution of 'accuracy' for that loss), or ``ce`` = categorical
   cross-entropy with categorical accuracy;
 * dropout is inverted dropout on the dense layer;
-* each epoch visits every training sample once in a fresh random order;
-  an epoch is ``ceil(n_train / B)`` full batches and the last batch wraps
-  around to the start of the permutation (Keras would run one short
-  batch; fixed shapes keep the step graph-capturable).
+* each epoch visits every training sample once in a fresh random order in
+  ``ceil(n_train / B)`` steps (``batching``): ``"keras"`` (default) -- the
+  last step is Keras' short batch: the shapes stay fixed (graph capture),
+  the padding rows carry zero loss weight and the mean is over the real
+  rows; or ``"wrap"`` -- the last batch wraps around to the start of the
+  permutation.
 
 Backends: ``hip`` (MI355X kernels, :mod:`gentun_amd.models.cnn_hip`) and
 ``torch`` (autograd oracle / comparator path (a) of SURVEY.md §6).
@@ -48,7 +52,8 @@ CLIP_EPS = 1e-7
 
 class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
-                 dtype="fp32", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9):
+                 dtype="fp32", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9,
+                 reset="kernels", batching="keras"):
         if isinstance(epochs, int):
             epochs = (epochs,)
         if isinstance(learning_rate, (int, float)):
@@ -62,6 +67,12 @@ class TrainConfig(object):
             raise ValueError("dtype must be 'bf16' or 'fp32'")
         if optimizer not in ("adam", "sgd"):
             raise ValueError("optimizer must be 'adam' or 'sgd'")
+        if reset not in ("kernels", "all"):
+            raise ValueError("reset must be 'kernels' (reference: sequential folds, biases carried over) or 'all'")
+        if batching not in ("keras", "wrap"):
+            raise ValueError("batching must be 'keras' (short last batch) or 'wrap'")
+        self.reset = reset
+        self.batching = batching
         self.epochs = epochs
         self.learning_rate = learning_rate
         self.batch_size = int(batch_size)
@@ -200,6 +211,17 @@ class FoldJob(object):
             self.shuffle_gens.append(gen)
         self.epoch_idx = torch.zeros((self.steps_per_epoch, self.G, self.B), dtype=torch.int64,
                                      device=self.device)
+        # real rows of each (step, group) batch: B, except a Keras short last
+        # batch (batching="keras"); padding rows repeat real samples and carry
+        # zero loss weight
+        self.epoch_valid = torch.full((self.steps_per_epoch, self.G), self.B, dtype=torch.int32, device=self.device)
+        if cfg.batching == "keras":
+            v = np.zeros((self.steps_per_epoch, self.G), np.int32)
+            for g, n in enumerate(ntr):
+                for st in range(self.steps_per_epoch):
+                    v[st, g] = max(0, min(self.B, n - st * self.B))
+            self.epoch_valid.copy_(torch.from_numpy(v))
+        self.after_init = None        # callable run right after init_params (sequential folds)
         self.step_ctr = torch.zeros((1,), dtype=torch.int64, device=self.device)
         self.result = None
 
@@ -276,6 +298,8 @@ class FoldJob(object):
             if timed:
                 ev[0].record()
             self.init_params()
+            if self.after_init is not None:
+                self.after_init(self)
             graph = self._capture() if use_graph else None
             if timed:
                 ev[1].record()
@@ -324,6 +348,57 @@ class FoldJob(object):
         self._graph = None
         self.result = out if self.multi else out[0]
         return self.result
+
+
+class SequentialFoldJob(object):
+    """The reference's fold protocol (keras_models.py:127-143): the folds of
+    the job's candidates train ONE AFTER ANOTHER; fold k+1 re-draws only the
+    kernels (Glorot, keyed by fold id) and starts from the biases fold k
+    trained (``reset_weights`` re-runs kernel initialisers only,
+    keras_models.py:120-125). ``make(fold_index)`` builds the job of one
+    fold (all candidates, one group each); everything is enqueued on the
+    jobs' stream, so ``launch()`` does not block."""
+
+    def __init__(self, make, nfolds, multi):
+        self.make = make
+        self.nfolds = nfolds
+        self.multi = multi
+        self.jobs = []
+        self.phase_ms = None
+
+    def launch(self):
+        prev = None
+        for f in range(self.nfolds):
+            job = self.make(f)
+            if prev is not None:
+                job.after_init = _carry_biases(prev)
+            job.launch()
+            self.jobs.append(job)
+            prev = job
+        return self
+
+    def finish(self):
+        per_fold = [j.finish() for j in self.jobs]
+        self.phase_ms = _sum_phases(self.jobs)
+        keys = ("val_loss", "binary_accuracy", "categorical_accuracy")
+        if not self.multi:
+            return {k: [v for r in per_fold for v in r[k]] for k in keys}
+        nmem = len(per_fold[0])
+        return [{k: [v for r in per_fold for v in r[c][k]] for k in keys} for c in range(nmem)]
+
+
+def _carry_biases(prev):
+    def hook(job):
+        job.copy_biases_from(prev)
+    return hook
+
+
+def _sum_phases(jobs):
+    out = {}
+    for j in jobs:
+        for k, v in (getattr(j, "phase_ms", None) or {}).items():
+            out[k] = out.get(k, 0.0) + v
+    return out or None
 
 
 class _nullctx(object):
@@ -414,6 +489,14 @@ class TorchFoldJob(FoldJob):
     def snapshot(self):
         return (self.flat.detach().clone(), self.m.clone(), self.v.clone(), self.t.clone())
 
+    def copy_biases_from(self, other):
+        """Biases of every layer from ``other`` (same plan and folds count)."""
+        with torch.no_grad():
+            a, b = self._views(), other._views()
+            for name, _, kind, _ in self.shapes:
+                if kind == "zero":
+                    a[name].copy_(b[name])
+
     def restore(self, snap):
         with torch.no_grad():
             self.flat.copy_(snap[0])
@@ -474,6 +557,7 @@ class TorchFoldJob(FoldJob):
 
     def train_step(self):
         idx = self.epoch_idx.index_select(0, self.step_ctr).view(self.G, self.B)
+        nval = self.epoch_valid.index_select(0, self.step_ctr).view(self.G, 1).float()
         self.step_ctr.add_(1)
         xb = self._gather(idx)
         yb = self.data.onehot.index_select(0, idx.reshape(-1)).view(self.G, self.B, -1)
@@ -484,7 +568,10 @@ class TorchFoldJob(FoldJob):
         else:
             logits = self._forward(xb, True)
         per, _, _ = loss_and_metrics(logits, yb, self.cfg.loss)
-        per.mean(-1).sum().backward()
+        # mean over the real rows of each group's batch (Keras short batch)
+        rows = torch.arange(self.B, device=self.device)[None, :].float()
+        wt = (rows < nval).float() / nval.clamp_min(1.0)
+        (per * wt).sum().backward()
         with torch.no_grad():
             g = self.flat.grad
             self.t.add_(1.0)
@@ -522,7 +609,7 @@ class TorchFoldJob(FoldJob):
         return loss, binc, catc
 
 
-def make_job(backend, plan, x, y, folds, cfg, device, fold_ids=None, stream=None):
+def _one_job(backend, plan, x, y, folds, cfg, device, fold_ids, stream):
     if backend == "torch":
         return TorchFoldJob(plan, x, y, folds, cfg, device, fold_ids=fold_ids, stream=stream)
     if backend == "hip":
@@ -531,15 +618,36 @@ def make_job(backend, plan, x, y, folds, cfg, device, fold_ids=None, stream=None
     raise ValueError("unknown backend {!r}".format(backend))
 
 
+def make_job(backend, plan, x, y, folds, cfg, device, fold_ids=None, stream=None):
+    """Job training ``folds`` of one architecture: concurrent folds
+    (``cfg.reset == "all"``) or the reference's sequential folds with
+    carried-over biases (``"kernels"``)."""
+    ids = list(range(len(folds))) if fold_ids is None else list(fold_ids)
+    if cfg.reset == "all" or len(folds) == 1:
+        return _one_job(backend, plan, x, y, folds, cfg, device, ids, stream)
+    return SequentialFoldJob(lambda f: _one_job(backend, plan, x, y, [folds[f]], cfg, device, [ids[f]], stream),
+                             len(folds), multi=False)
+
+
 def make_population_job(backend, members, x, y, cfg, device, stream=None):
     """One job training several architectures at once: ``members`` is a list
     of ``(plan, folds, fold_ids)``; ``finish()`` returns one result dict per
-    member. The HIP executor batches them into shared launches; the torch
-    oracle has no such mode and is rejected."""
+    member. The HIP executor batches them into shared launches (with
+    ``reset="kernels"`` one launch set per fold position, folds in sequence);
+    the torch oracle has no such mode and is rejected."""
     if backend != "hip":
         raise ValueError("population batching needs the hip backend")
     from .cnn_hip import HipPopJob
-    return HipPopJob(None, x, y, None, cfg, device, stream=stream, members=members)
+    nf = {len(f) for _, f, _ in members}
+    if cfg.reset == "all" or nf == {1}:
+        return HipPopJob(None, x, y, None, cfg, device, stream=stream, members=members)
+    if len(nf) != 1:
+        raise ValueError("sequential-fold population jobs need the same number of folds per member")
+
+    def make(k):
+        return HipPopJob(None, x, y, None, cfg, device, stream=stream,
+                         members=[(p, [f[k]], [ids[k]]) for p, f, ids in members])
+    return SequentialFoldJob(make, nf.pop(), multi=True)
 
 
 def default_backend(device):

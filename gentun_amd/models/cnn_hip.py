@@ -321,6 +321,7 @@ class HipPopJob(FoldJob):
         hd = K.HeadArgs()
         hd.h, hd.w2, hd.b2 = self.hdrop.data_ptr(), self.views["W2"][0].data_ptr(), self.views["b2"][0].data_ptr()
         hd.labels, hd.gather, hd.st = self.data.labels.data_ptr(), gather_train, self.state.data_ptr()
+        hd.valid = self.epoch_valid.data_ptr()
         hd.dH, hd.gw2, hd.gb2, hd.gb1 = self.dH.data_ptr(), self.gW2.data_ptr(), self.gb2.data_ptr(), self.gb1.data_ptr()
         hd.eval_out = 0
         hd.dz = self.dz_head.data_ptr()
@@ -459,6 +460,16 @@ class HipPopJob(FoldJob):
 
     def snapshot(self):
         return (self.flat.clone(), self.m.clone(), self.v.clone(), self.state.clone())
+
+    def copy_biases_from(self, other):
+        """Conv / dense biases of every group from ``other`` (a job of the same
+        members at the previous fold: SequentialFoldJob)."""
+        mine = {L.name: L for L in self.layers}
+        for L in other.layers:
+            if L.name in mine:
+                mine[L.name].b[0].copy_(L.b[0])
+        for name in ("b1", "b2"):
+            self.views[name][0].copy_(other.views[name][0])
 
     def restore(self, snap):
         self.flat.copy_(snap[0])

@@ -54,7 +54,7 @@ class HeadArgs(C.Structure):
     _fields_ = [("h", P), ("w2", P), ("b2", P), ("labels", P), ("gather", P), ("st", P), ("dH", P),
                 ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P), ("dz", P), ("plog", P),
                 ("G", I), ("B", I), ("Up", I), ("C", I), ("loss_ce", I), ("drop_scale", C.c_float), ("eval", I),
-                ("prec", I)]
+                ("prec", I), ("valid", P)]
 
 
 class DenseDgradArgs(C.Structure):

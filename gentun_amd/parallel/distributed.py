@@ -20,9 +20,13 @@ per generation (collectives X2/X3 of SURVEY.md §2.6)
   4. rank 0 merges fold groups per candidate, re-evaluates failed units
      locally once (worst fitness if that fails too) and breeds.
 
-Failure handling: collective timeout from
-``init_process_group(timeout=...)``; per-unit status codes; fault injection
-via ``GENTUN_FAULT="rank:generation:kind"`` (kind = ``raise``).
+Failure handling (:mod:`gentun_amd.parallel.fault`):
+per-unit status codes with one local retry on rank 0; a per-rank watchdog
+(``GENTUN_WATCHDOG``) that turns a dead or hung peer into a clean process
+exit sized from measured generation times; restart of the whole group from
+the last generation checkpoint (``torchrun --max-restarts``, CLI
+``--resume auto``); fault injection ``GENTUN_FAULT="rank:generation:kind"``,
+kind = ``raise`` | ``exit`` | ``hang``.
 """
 
 import json
@@ -34,6 +38,7 @@ import numpy as np
 
 from ..populations import Population, GridPopulation
 from .comm import LocalComm, from_env
+from . import fault as _fault
 from .evaluators import LocalBatchEvaluator
 from .scheduler import lpt_assign, make_units
 
@@ -102,15 +107,7 @@ def _tuplify(v):
 
 
 def _fault_hook(rank, generation):
-    spec = os.environ.get("GENTUN_FAULT")
-    if not spec:
-        return
-    try:
-        r, g, kind = spec.split(":")
-    except ValueError:
-        return
-    if int(r) == rank and int(g) == generation and kind == "raise":
-        raise RuntimeError("injected fault on rank {} generation {}".format(rank, generation))
+    _fault.inject(rank, generation)
 
 
 class _Unit(object):
@@ -331,7 +328,11 @@ class DistributedPopulation(Population):
         nfold = int(getattr(todo[0], "nfold", 1) or 1)
         codec = GenomeCodec(todo[0].get_genome())
         costs = [float(ind.cost()) if hasattr(ind, "cost") else 1.0 for ind in todo]
-        splittable = self.split_folds and hasattr(todo[0], "build_fitness_model")
+        # a candidate's folds may be split over units only when they train
+        # independently (reset="all"); the reference's sequential folds carry
+        # biases from fold to fold and stay one unit
+        splittable = self.split_folds and hasattr(todo[0], "build_fitness_model") and \
+            getattr(todo[0], "reset", "all") == "all"
         # population-batched evaluators take (candidate, fold) units: equal
         # group counts per rank at any generation size
         per_fold = splittable and getattr(self.local_evaluator, "pop_batch", 1) > 1
@@ -351,6 +352,9 @@ class DistributedPopulation(Population):
             table[k, 1] = owner[k]
             table[k, 2] = sum(1 << f for f in fids)
             table[k, 3:] = codec.encode(todo[slot].get_genes())
+        wd = _fault.watchdog()
+        if wd is not None:
+            wd.arm("generation {} (rank 0)".format(self.generation_counter))
         extra = _jsonable(todo[0].get_additional_parameters())
         genome = {k: (list(v) if isinstance(v, tuple) else v) for k, v in todo[0].get_genome().items()}
         blob = np.frombuffer(json.dumps({"species": self.species.__name__, "extra": extra,
@@ -373,6 +377,8 @@ class DistributedPopulation(Population):
         for k, row in rows.items():
             local[k] = row
         gathered = comm.all_gather_array(local)
+        if wd is not None:
+            wd.disarm()
         merged = _merge(gathered, units, len(todo), nfold)
         retried = 0
         for slot, ind in enumerate(todo):
@@ -489,13 +495,20 @@ class GentunWorker(object):
     def serve_one(self):
         """Handle one broadcast; returns False on STOP."""
         comm = self.comm
+        wd = _fault.watchdog()
+        if wd is not None:
+            wd.arm("evaluator rank {} waiting / evaluating".format(comm.rank))
         hdr = comm.broadcast_array(None)
         cmd, generation, _ncand, nfold = (int(v) for v in hdr)
         if cmd == CMD_STOP:
+            if wd is not None:
+                wd.disarm()
             return False
         if cmd == CMD_SYNC:
             _device_sync(self.evaluator)
             comm.barrier()
+            if wd is not None:
+                wd.disarm()
             return True
         blob = comm.broadcast_array(None)
         meta = json.loads(bytes(blob.astype(np.uint8)).decode())
@@ -523,6 +536,8 @@ class GentunWorker(object):
         for k, row in rows.items():
             local[k] = row
         comm.all_gather_array(local)
+        if wd is not None:
+            wd.disarm()
         self.served += len(rows)
         return True
 

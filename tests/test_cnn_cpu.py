@@ -59,7 +59,8 @@ def test_fold_results_independent_of_grouping():
     plan = make_plan({'S_1': '100', 'S_2': '0000000000'}, (3, 5), (16, 16, 1), (8, 16), ((3, 3), (3, 3)), 32, 4)
     # dropout off: the torch oracle draws dropout masks from torch's global RNG
     # (the HIP path keys them by fold id; tests/test_hip_train.py checks that)
-    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=16, dtype="fp32", loss="ce", dropout=0.0)
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=16, dtype="fp32", loss="ce", dropout=0.0,
+                        reset="all")
     together = E.make_job("torch", plan, x, y, folds, cfg, "cpu", fold_ids=[0, 1]).launch().finish()
     alone = E.make_job("torch", plan, x, y, [folds[1]], cfg, "cpu", fold_ids=[1]).launch().finish()
     assert abs(together["val_loss"][1] - alone["val_loss"][0]) < 1e-4
@@ -103,7 +104,7 @@ def test_sgd_momentum_update_rule():
     folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
     plan = make_plan({'S_1': '000', 'S_2': '0000000000'}, (3, 5), (16, 16, 1), (4, 4), ((3, 3), (3, 3)), 8, 4)
     cfg = E.TrainConfig(epochs=(1,), learning_rate=(0.1,), batch_size=8, dtype="fp32", loss="ce", dropout=0.0,
-                        optimizer="sgd", momentum=0.5)
+                        optimizer="sgd", momentum=0.5, reset="all")
     job = E.make_job("torch", plan, x, y, folds, cfg, "cpu")
     job.init_params()
     job.reset_optimizer(0.1)
@@ -139,4 +140,73 @@ def test_bench_contract_two_ranks_gloo():
     assert len(lines) == 1, out.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["timed_candidates"] == 2 and rec["value"] > 0
-    assert rec["config"]["parallelism"] == "population-dp2"
+    assert rec["config"]["parallelism"].startswith("population-dp2")
+    assert rec["metric"].startswith("candidates/hour + best val-acc@genN") and rec["dtype"] == "fp32"
+
+
+def test_reference_sequential_folds_carry_biases():
+    """reset="kernels" (default, keras_models.py:120-125,135): folds run in
+    sequence; fold k+1 re-draws the kernels and starts from the biases fold k
+    trained."""
+    x, y = _data(200)
+    folds = stratified_kfold(np.argmax(y, 1), 3, seed=0)
+    plan = make_plan({'S_1': '101', 'S_2': '0000000000'}, (3, 5), (16, 16, 1), (8, 16), ((3, 3), (3, 3)), 32, 4)
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-2,), batch_size=16, dtype="fp32", loss="ce", dropout=0.0)
+    assert cfg.reset == "kernels" and cfg.batching == "keras"
+    job = E.make_job("torch", plan, x, y, folds, cfg, "cpu")
+    assert isinstance(job, E.SequentialFoldJob)
+    seen = []
+
+    def spy(orig):
+        def hook(j):
+            orig(j)
+            seen.append({n: t.detach().clone() for n, t in j._views().items()})
+        return hook
+
+    made = job.make
+
+    def make(f):
+        j = made(f)
+        j.after_init = None
+        return j
+    job.make = make
+    # run the folds by hand to look at the weights between them
+    prev = None
+    finals = []
+    for f in range(3):
+        j = job.make(f)
+        if prev is not None:
+            j.after_init = spy(E._carry_biases(prev))
+        j.launch()
+        j.finish()
+        finals.append({n: t.detach().clone() for n, t in j._views().items()})
+        prev = j
+    for f in (1, 2):
+        start = seen[f - 1]
+        for n in start:
+            if n.endswith(".b"):
+                assert torch.equal(start[n], finals[f - 1][n]), n          # biases carried over
+                assert not torch.equal(start[n], torch.zeros_like(start[n])) or n == "dense2.b"
+            else:
+                assert not torch.equal(start[n], finals[f - 1][n]), n      # kernels re-drawn
+    res = E.make_job("torch", plan, x, y, folds, cfg, "cpu").launch().finish()
+    assert len(res["val_loss"]) == 3
+
+
+def test_keras_short_last_batch_weights():
+    """batching="keras": 10 steps of 16 for 150 training rows, the last with
+    6 real rows; the torch oracle's loss is the mean over those rows only."""
+    x, y = _data(190)
+    fold = (np.arange(150), np.arange(150, 190))
+    plan = make_plan({'S_1': '000', 'S_2': '0000000000'}, (3, 5), (16, 16, 1), (4, 8), ((3, 3), (3, 3)), 16, 4)
+    k = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=16, dtype="fp32", loss="ce", dropout=0.0)
+    w = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=16, dtype="fp32", loss="ce", dropout=0.0,
+                      batching="wrap")
+    jk = E.make_job("torch", plan, x, y, [fold], k, "cpu")
+    jw = E.make_job("torch", plan, x, y, [fold], w, "cpu")
+    assert jk.steps_per_epoch == 10
+    assert jk.epoch_valid[:, 0].tolist() == [16] * 9 + [6]
+    assert jw.epoch_valid[:, 0].tolist() == [16] * 10
+    rk = jk.launch().finish()
+    rw = jw.launch().finish()
+    assert rk["val_loss"][0] != rw["val_loss"][0]

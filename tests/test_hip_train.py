@@ -65,7 +65,7 @@ def test_hip_fold_subset_equals_batched():
     from gentun_amd.models import cnn_engine as E
     x, y, folds, plan = _setup(n=600)
     dev = torch.device("cuda", 0)
-    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce")
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce", reset="all")
     full = E.make_job("hip", plan, x, y, folds, cfg, dev, fold_ids=[0, 1, 2]).launch().finish()
     one = E.make_job("hip", plan, x, y, [folds[1]], cfg, dev, fold_ids=[1]).launch().finish()
     assert one["val_loss"][0] == full["val_loss"][1]
@@ -79,7 +79,7 @@ def test_population_batch_invariance():
     from gentun_amd.models.genome import make_plan
     x, y, folds, _ = _setup(n=600)
     dev = torch.device("cuda", 0)
-    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce")
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce", reset="all")
     genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '000', 'S_2': '0000000000'},
              {'S_1': '111', 'S_2': '1111111111'}, {'S_1': '010', 'S_2': '1000000001'}]
     plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
@@ -103,3 +103,25 @@ def test_job_phase_timers():
     job.finish()
     assert set(job.phase_ms) == {"init_capture", "train", "eval"}
     assert job.phase_ms["train"] > 0 and job.phase_ms["eval"] > 0
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_sequential_folds_population_invariance(dtype):
+    """Reference fold semantics (reset="kernels", default): folds in
+    sequence, biases carried over; a candidate's result is the same alone or
+    in a population job, and differs from the concurrent fast mode."""
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.genome import make_plan
+    x, y, folds, _ = _setup(n=600)
+    dev = torch.device("cuda", 0)
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype=dtype, loss="ce")
+    assert cfg.reset == "kernels"
+    genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '111', 'S_2': '1111111111'}]
+    plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
+    alone = [E.make_job("hip", p, x, y, folds, cfg, dev).launch().finish() for p in plans]
+    pop = E.make_population_job("hip", [(p, folds, [0, 1, 2]) for p in plans], x, y, cfg, dev).launch().finish()
+    assert pop == alone
+    fast = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype=dtype, loss="ce", reset="all")
+    conc = E.make_job("hip", plans[0], x, y, folds, fast, dev).launch().finish()
+    assert conc["val_loss"][0] == alone[0]["val_loss"][0]          # fold 0 starts from scratch either way
+    assert conc["val_loss"][1:] != alone[0]["val_loss"][1:]        # later folds start from carried biases

@@ -16,7 +16,7 @@ from gentun_amd.utils.data import make_image_classification
 
 TINY = dict(nodes=(3, 3), input_shape=(8, 8, 1), kernels_per_layer=(2, 3), kernel_sizes=((3, 3), (3, 3)),
             dense_units=8, dropout_probability=0.5, classes=3, nfold=5, epochs=(1,), learning_rate=(1e-3,),
-            batch_size=16, backend="torch", device="cpu", seed=3)
+            batch_size=16, backend="torch", device="cpu", seed=3, reset="all")
 
 
 def _rr_generation_sizes(pop=32, gens=30, seed=0):
@@ -82,3 +82,23 @@ def test_rounds_with_per_fold_units_match_a_single_process_run():
         local.append((twin.get_fitness(), twin.fold_metrics["categorical_accuracy"]))
     for (fd, cd), (fl, cl) in zip(dist, local):
         assert abs(fd - fl) < 1e-6 and np.allclose(cd, cl)
+
+
+def test_sequential_fold_candidates_are_never_split():
+    """reset="kernels" (the reference's fold protocol) chains the folds of a
+    candidate, so the distributed evaluator keeps each candidate one unit."""
+    x, y = make_image_classification(n=60, shape=(8, 8, 1), classes=3, seed=1)
+    comms = ThreadComm.group(2)
+    evs = [LocalBatchEvaluator(device="cpu", streams=1, pop_batch=4) for _ in range(2)]
+    t = threading.Thread(target=lambda: GentunWorker(GeneticCnnIndividual, x, y, comm=comms[1],
+                                                     evaluator=evs[1]).work(), daemon=True)
+    t.start()
+    rng.seed(6)
+    params = dict(TINY, reset="kernels", nfold=3)
+    pop = DistributedPopulation(GeneticCnnIndividual, x, y, size=2, additional_parameters=params, comm=comms[0],
+                                evaluator=evs[0])
+    pop.evaluate_in_parallel()
+    assert pop.last_dispatch["units"] == 2
+    assert all(len(ind.fold_scores) == 3 for ind in pop)
+    pop.shutdown()
+    t.join(timeout=60)
