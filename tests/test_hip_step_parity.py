@@ -191,7 +191,7 @@ def test_fifty_steps_track_the_torch_fp32_oracle(gi):
     genes = GENES[gi]
     x, y, fold, plan = _setup(genes, n=2000, ntrain=1600)
     dev = torch.device("cuda", 0)
-    cfg = E.TrainConfig(epochs=(1,), learning_rate=(0.01,), batch_size=32, dropout=0.0, loss="ce", dtype="fp32",
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(0.003,), batch_size=32, dropout=0.0, loss="ce", dtype="fp32",
                         use_graph=False, optimizer="sgd", momentum=0.9)
     hip = HipPopJob(plan, x, y, [fold], cfg, dev, fold_ids=[0])
     tg = E.TorchFoldJob(plan, x, y, [fold], cfg, dev, fold_ids=[0])
@@ -201,7 +201,7 @@ def test_fifty_steps_track_the_torch_fp32_oracle(gi):
     _copy_into_torch_job(tg, w)
     _copy_into_torch_job(tc, w)
     for job in (hip, tg, tc):
-        job.reset_optimizer(0.01)
+        job.reset_optimizer(0.003)
         job._new_epoch_order()
     tc.epoch_idx.copy_(hip.epoch_idx.cpu())         # the CPU generator draws another order: use the same batches
     assert torch.equal(hip.epoch_idx.cpu(), tg.epoch_idx.cpu())

@@ -3,10 +3,10 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export GENTUN_NO_AUTOBUILD=1
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
-rc=$?; tail -4 gpurun_out/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
+true
+true
 out=gpurun_out/probe_reset.log; : > $out
-for cfg in "2 all" "2 kernels" "16 all" "16 kernels"; do
+for cfg in ${RCFGS:-"2 all" "2 kernels" "16 all" "16 kernels"}; do
   set -- $cfg
   echo "== P=$1 RESET=$2" >> $out
   RESET=$2 timeout -k 10 300 python -u tools/probe_pop.py $1 $1 1 1 >> $out 2>&1 || exit $?

@@ -52,7 +52,10 @@ tl = time.perf_counter()
 res = [r for j in jobs for r in j.finish()]
 torch.cuda.synchronize()
 dt = time.perf_counter() - t
-steps = jobs[0].steps_per_epoch * epochs
+# one "step" = one optimizer step of every fold of every candidate (the
+# sequential-fold job runs its folds' steps one fold at a time)
+j0 = jobs[0]
+steps = (j0.steps_per_epoch if hasattr(j0, "steps_per_epoch") else j0.jobs[0].steps_per_epoch) * epochs
 print(json.dumps({"P": P, "pop_batch": pb, "streams": ns, "steps": steps, "s": round(dt, 3),
                   "build_s": round(tb - t, 3), "enqueue_s": round(tl - tb, 3),
                   "ms_per_step": round(1000 * dt / steps, 3), "ms_per_cand_step": round(1000 * dt / steps / P, 4),
