@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--per-gpu", type=int, default=None,
-                    help="candidates per GPU per round (default: 2 fp32 / 4 bf16)")
+                    help="candidates per GPU per round (default: 3 fp32 / 6 bf16)")
     ap.add_argument("--pop-per-gpu", type=int, default=32, help="GA population per GPU")
     ap.add_argument("--streams", type=int, default=1, help="concurrent population jobs per GPU")
     ap.add_argument("--pop-batch", type=int, default=16, help="candidates (x folds) per population job")
@@ -114,7 +114,7 @@ def run(args):
 
     epochs = tuple(int(e) for e in args.epochs.split(","))
     lrs = tuple(float(x) for x in args.lr.split(","))
-    per_gpu = args.per_gpu or (2 if args.dtype == "fp32" else 4)
+    per_gpu = args.per_gpu or (3 if args.dtype == "fp32" else 6)
     x, y = make_cifar_like(n=args.samples, seed=0)
     nodes, kernels = ((3, 4, 5), (20, 50, 100)) if args.space == "deep" else ((3, 5), (20, 50))
     if args.kernels:
