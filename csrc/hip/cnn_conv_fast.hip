@@ -25,6 +25,7 @@
 // fan-out (accumulate, ReLU mask) for the data gradient.
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "cnn_args.h"
 
@@ -1093,8 +1094,12 @@ extern "C" int gt_wgrad_set_nb(int nb) {
   if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->Coutp == NCBO_ * 8 && a->W == W_ &&     \
       a->H % R_ == 0 && a->pps % (R_ * W_) == 0) {                                                        \
     dim3 grid(a->S, a->ngroups);                                                                         \
-    hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_>), grid, dim3(NW_ * 64), 0, \
-                       stream, *a);                                                                      \
+    if ((g_wgrad_nb ? g_wgrad_nb : NB_) == 1)                                                            \
+      hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1>), grid, dim3(NW_ * 64), 0, \
+                         stream, *a);                                                                    \
+    else                                                                                                 \
+      hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 2>), grid, dim3(NW_ * 64), 0, \
+                         stream, *a);                                                                    \
     return (int)hipGetLastError();                                                                       \
   }
 
@@ -1132,7 +1137,10 @@ extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, in
 // 199 us per call, 34 % of a 10-group step) for 2.7x the partial-sum bytes.
 extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, int W, int prec) {
   (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H;
-  if (prec == 1) return W >= 32 ? 32 : 8;
+  if (prec == 1) {
+    const char* e = getenv("GENTUN_F32_SPLITS16");     // A/B: splits of the 16-wide stage
+    return W >= 32 ? 32 : (e ? atoi(e) : 8);
+  }
   return W >= 32 ? 16 : 3;
 }
 

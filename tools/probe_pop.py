@@ -23,6 +23,9 @@ ns = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 epochs = int(sys.argv[4]) if len(sys.argv) > 4 else 1
 n = int(sys.argv[5]) if len(sys.argv) > 5 else 10000
 dev = torch.device("cuda", 0)
+if os.environ.get("GENTUN_WGRAD_NB"):                 # A/B: force the wgrad band buffers
+    from gentun_amd.ops import cnn_kernels as K
+    K.lib().gt_wgrad_set_nb(int(os.environ["GENTUN_WGRAD_NB"]))
 x, y = make_cifar_like(n=n, seed=0)
 folds = stratified_kfold(np.argmax(y, 1), 5, seed=0)
 rnd = random.Random(0)
