@@ -1,0 +1,298 @@
+// Optional BatchNorm of the Genetic-CNN node convs (TrainConfig.batch_norm,
+// off by default: the reference network has none, keras_models.py:97-118).
+//
+//   conv (bias, no ReLU) -> z  ->  y = relu(gamma * (z - mean) * rstd + beta)
+//
+// Per group (candidate x fold replica) and channel, statistics over the
+// batch's real rows (B, or the short last batch of batching="keras") and all
+// pixels; running mean / unbiased variance with Keras' momentum (0.99) and
+// epsilon (1e-3) for evaluation. Population-batched like the convs: a launch
+// covers the groups of a GroupRec table, the grid is (chunks, groups).
+//
+// Two kernels per direction, both deterministic (fixed chunk geometry per
+// layer shape, fixed-order reductions: a group's result does not depend on
+// which other groups share the launch):
+//   forward  : bn_stats  -> per-chunk shifted sums S1 = sum(z - k), S2 = sum((z - k)^2)
+//              bn_apply  -> reduce the chunk partials, save (mean, rstd), update
+//                           the running stats (chunk 0), write y (ReLU fused)
+//   backward : bn_bwd_stats -> per-chunk sum(g), sum(g * xhat) of the ReLU-masked
+//                              output gradient g (the consumers' dgrad applied the mask)
+//              bn_bwd_apply -> dgamma / dbeta (chunk 0) and, in place,
+//                              dz = gamma rstd (g - sum g / N - xhat sum(g xhat) / N)
+//                              (0 on padding rows of a short batch)
+// The shift k = z at pixel 0 of the group keeps S2 / N - (S1 / N)^2 free of
+// cancellation when |mean| >> std.
+#include "common.h"
+#include "cnn_args.h"
+
+struct BnArgs {
+  void* z;                  // [Q][B][H][W][Cp] pre-activation (conv output with bias)
+  void* y;                  // fwd: [Q][B][H][W][Cp] relu(bn(z)) out; bwd: ReLU-masked grad in, dz out (in place)
+  const float* gamma;       // [Q][Cp]
+  const float* beta;        // [Q][Cp]
+  float* stat;              // [Q][2][Cp] saved mean, rstd of the training forward
+  float* run;               // [2][Q][Cp] running mean, running (unbiased) variance
+  float* part;              // [Q][nchunk][2][Cp] chunk partials
+  float* ggamma;            // [Q][Cp] (bwd)
+  float* gbeta;             // [Q][Cp] (bwd)
+  const GroupRec* gtab;     // [ngroups]
+  const int* valid;         // [steps][Q] real rows per training batch, or null = B
+  const StepState* st;
+  int ngroups, G, B, HW, Cp, nchunk, chunk_px;
+  float momentum, eps;
+  int train;                // 1: batch statistics (training forward); 0: running statistics
+  int prec;
+};
+
+#define BN_THREADS 256
+
+__device__ __forceinline__ int bn_rows(const BnArgs& a, int g) {
+  if (!a.train || !a.valid) return a.B;
+  const int step = a.st ? a.st->cur_step : 0;
+  const int nv = a.valid[(long)step * a.G + g];
+  return nv < 0 ? 0 : (nv > a.B ? a.B : nv);
+}
+
+// Two per-channel sums over a pixel range, reduced in a fixed order: threads
+// t < nact own channel chunk t % nc8 and pixels (t / nc8) + k * (nact / nc8).
+// acc[0..7] / acc[8..15] are the two sums of the thread's 8 channels; the
+// result for channel c lands in out[0][c], out[1][c] (threads c < Cp).
+__device__ __forceinline__ void bn_block_reduce(float (*red)[17], const float* acc, int nc8, int nact,
+                                                float* out0, float* out1, int Cp) {
+  const int t = threadIdx.x;
+  if (t < nact) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[t][e] = acc[e];
+  }
+  __syncthreads();
+  if (t < Cp) {
+    const int c8 = t >> 3, e = t & 7, np = nact / nc8;
+    float s0 = 0.f, s1 = 0.f;
+    for (int p = 0; p < np; ++p) {
+      s0 += red[p * nc8 + c8][e];
+      s1 += red[p * nc8 + c8][8 + e];
+    }
+    out0[t] = s0;
+    out1[t] = s1;
+  }
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(BnArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  __shared__ float red[BN_THREADS][17];
+  const GroupRec r = a.gtab[blockIdx.y];
+  const int g = r.g, Cp = a.Cp, nc8 = Cp >> 3;
+  const int nact = (BN_THREADS / nc8) * nc8, t = threadIdx.x;
+  const long npx = (long)bn_rows(a, g) * a.HW;
+  const long p0 = (long)blockIdx.x * a.chunk_px;
+  const long p1 = p0 + a.chunk_px < npx ? p0 + a.chunk_px : npx;
+  const AT* z = reinterpret_cast<const AT*>(a.z) + (long)g * a.B * a.HW * Cp;
+  float acc[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  if (t < nact) {
+    const int c8 = t % nc8;
+    float k[8], v[8];
+    ld_chunk(z + c8 * 8, k);                       // shift: the group's pixel 0
+    for (long p = p0 + t / nc8; p < p1; p += nact / nc8) {
+      ld_chunk(z + p * Cp + c8 * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float d = v[e] - k[e];
+        acc[e] += d;
+        acc[8 + e] += d * d;
+      }
+    }
+  }
+  float* part = a.part + ((long)g * a.nchunk + blockIdx.x) * 2 * Cp;
+  bn_block_reduce(red, acc, nc8, nact, part, part + Cp, Cp);
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(BnArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  __shared__ float sc[256], sh[256];
+  const GroupRec r = a.gtab[blockIdx.y];
+  const int g = r.g, Cp = a.Cp, nc8 = Cp >> 3, t = threadIdx.x;
+  const AT* z = reinterpret_cast<const AT*>(a.z) + (long)g * a.B * a.HW * Cp;
+  AT* y = reinterpret_cast<AT*>(a.y) + (long)g * a.B * a.HW * Cp;
+  if (t < Cp) {
+    const float gm = a.gamma[(long)g * Cp + t], bt = a.beta[(long)g * Cp + t];
+    float mean, rstd;
+    if (a.train) {
+      const long npx = (long)bn_rows(a, g) * a.HW;
+      const int nch = (int)((npx + a.chunk_px - 1) / a.chunk_px);
+      const float* part = a.part + (long)g * a.nchunk * 2 * Cp;
+      float s1 = 0.f, s2 = 0.f;
+      for (int c = 0; c < nch; ++c) {
+        s1 += part[(long)c * 2 * Cp + t];
+        s2 += part[(long)c * 2 * Cp + Cp + t];
+      }
+      const float n = npx > 0 ? (float)npx : 1.f;
+      const float m1 = s1 / n;
+      const float var = fmaxf(s2 / n - m1 * m1, 0.f);
+      float k;                                     // the shift of bn_stats: the group's pixel 0
+      if constexpr (PREC) k = z[t]; else k = bf2f(z[t]);
+      mean = k + m1;
+      rstd = rsqrtf(var + a.eps);
+      if (blockIdx.x == 0 && npx > 0) {
+        a.stat[(long)g * 2 * Cp + t] = mean;
+        a.stat[(long)g * 2 * Cp + Cp + t] = rstd;
+        float* rm = a.run + (long)g * Cp + t;
+        float* rv = a.run + (long)a.G * Cp + (long)g * Cp + t;
+        const float unb = npx > 1 ? var * n / (n - 1.f) : var;
+        *rm = a.momentum * *rm + (1.f - a.momentum) * mean;
+        *rv = a.momentum * *rv + (1.f - a.momentum) * unb;
+      }
+    } else {
+      mean = a.run[(long)g * Cp + t];
+      rstd = rsqrtf(a.run[(long)a.G * Cp + (long)g * Cp + t] + a.eps);
+    }
+    sc[t] = gm * rstd;
+    sh[t] = bt - mean * gm * rstd;
+  }
+  __syncthreads();
+  const long npx = (long)a.B * a.HW;              // every row (padding rows too: finite values, zero loss weight)
+  const long p0 = (long)blockIdx.x * a.chunk_px;
+  const long p1 = p0 + a.chunk_px < npx ? p0 + a.chunk_px : npx;
+  const long n8 = (p1 - p0) * nc8;
+  for (long i = t; i < n8; i += BN_THREADS) {
+    const long p = p0 + i / nc8;
+    const int c8 = (int)(i % nc8);
+    float v[8];
+    ld_chunk(z + p * Cp + c8 * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[c8 * 8 + e] + sh[c8 * 8 + e], 0.f);
+    st_chunk(y + p * Cp + c8 * 8, v);
+  }
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(BN_THREADS) bn_bwd_stats_kernel(BnArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  __shared__ float red[BN_THREADS][17];
+  const GroupRec r = a.gtab[blockIdx.y];
+  const int g = r.g, Cp = a.Cp, nc8 = Cp >> 3;
+  const int nact = (BN_THREADS / nc8) * nc8, t = threadIdx.x;
+  const long npx = (long)bn_rows(a, g) * a.HW;
+  const long p0 = (long)blockIdx.x * a.chunk_px;
+  const long p1 = p0 + a.chunk_px < npx ? p0 + a.chunk_px : npx;
+  const AT* z = reinterpret_cast<const AT*>(a.z) + (long)g * a.B * a.HW * Cp;
+  const AT* gy = reinterpret_cast<const AT*>(a.y) + (long)g * a.B * a.HW * Cp;
+  const float* stat = a.stat + (long)g * 2 * Cp;
+  float acc[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+  if (t < nact) {
+    const int c8 = t % nc8;
+    float mean[8], rstd[8], v[8], d[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      mean[e] = stat[c8 * 8 + e];
+      rstd[e] = stat[Cp + c8 * 8 + e];
+    }
+    for (long p = p0 + t / nc8; p < p1; p += nact / nc8) {
+      ld_chunk(z + p * Cp + c8 * 8, v);
+      ld_chunk(gy + p * Cp + c8 * 8, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        acc[e] += d[e];
+        acc[8 + e] += d[e] * ((v[e] - mean[e]) * rstd[e]);
+      }
+    }
+  }
+  float* part = a.part + ((long)g * a.nchunk + blockIdx.x) * 2 * Cp;
+  bn_block_reduce(red, acc, nc8, nact, part, part + Cp, Cp);
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(BnArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  __shared__ float cg[256], cm[256], cx[256], mu[256], rs[256];
+  const GroupRec r = a.gtab[blockIdx.y];
+  const int g = r.g, Cp = a.Cp, nc8 = Cp >> 3, t = threadIdx.x;
+  const long nvpx = (long)bn_rows(a, g) * a.HW;
+  const AT* z = reinterpret_cast<const AT*>(a.z) + (long)g * a.B * a.HW * Cp;
+  AT* gy = reinterpret_cast<AT*>(a.y) + (long)g * a.B * a.HW * Cp;
+  if (t < Cp) {
+    const int nch = (int)((nvpx + a.chunk_px - 1) / a.chunk_px);
+    const float* part = a.part + (long)g * a.nchunk * 2 * Cp;
+    float sg = 0.f, sgx = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      sg += part[(long)c * 2 * Cp + t];
+      sgx += part[(long)c * 2 * Cp + Cp + t];
+    }
+    if (blockIdx.x == 0) {
+      a.gbeta[(long)g * Cp + t] = sg;
+      a.ggamma[(long)g * Cp + t] = sgx;
+    }
+    const float inv_n = nvpx > 0 ? 1.f / (float)nvpx : 0.f;
+    const float rstd = a.stat[(long)g * 2 * Cp + Cp + t];
+    cg[t] = a.gamma[(long)g * Cp + t] * rstd;
+    cm[t] = sg * inv_n;
+    cx[t] = sgx * inv_n;
+    mu[t] = a.stat[(long)g * 2 * Cp + t];
+    rs[t] = rstd;
+  }
+  __syncthreads();
+  const long npx = (long)a.B * a.HW;
+  const long p0 = (long)blockIdx.x * a.chunk_px;
+  const long p1 = p0 + a.chunk_px < npx ? p0 + a.chunk_px : npx;
+  const long n8 = (p1 - p0) * nc8;
+  for (long i = t; i < n8; i += BN_THREADS) {
+    const long p = p0 + i / nc8;
+    const int c8 = (int)(i % nc8);
+    float v[8], d[8];
+    if (p < nvpx) {
+      ld_chunk(z + p * Cp + c8 * 8, v);
+      ld_chunk(gy + p * Cp + c8 * 8, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int c = c8 * 8 + e;
+        const float xh = (v[e] - mu[c]) * rs[c];
+        d[e] = cg[c] * (d[e] - cm[c] - xh * cx[c]);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = 0.f;
+    }
+    st_chunk(gy + p * Cp + c8 * 8, d);
+  }
+}
+
+static bool bn_shape_ok(const BnArgs* a) {
+  return a->Cp > 0 && a->Cp % 8 == 0 && a->Cp <= 256 && a->ngroups > 0 && a->nchunk > 0 && a->chunk_px > 0 &&
+         (long)a->nchunk * a->chunk_px >= (long)a->B * a->HW && a->gtab && a->part;
+}
+
+extern "C" {
+
+int gt_bn_fwd(const BnArgs* a, hipStream_t s) {
+  if (!bn_shape_ok(a)) return (int)hipErrorInvalidValue;
+  const dim3 grid(a->nchunk, a->ngroups);
+  if (a->train) {
+    if (a->prec) hipLaunchKernelGGL(bn_stats_kernel<1>, grid, dim3(BN_THREADS), 0, s, *a);
+    else hipLaunchKernelGGL(bn_stats_kernel<0>, grid, dim3(BN_THREADS), 0, s, *a);
+  }
+  if (a->prec) hipLaunchKernelGGL(bn_apply_kernel<1>, grid, dim3(BN_THREADS), 0, s, *a);
+  else hipLaunchKernelGGL(bn_apply_kernel<0>, grid, dim3(BN_THREADS), 0, s, *a);
+  return (int)hipGetLastError();
+}
+
+int gt_bn_bwd(const BnArgs* a, hipStream_t s) {
+  if (!bn_shape_ok(a) || !a->ggamma || !a->gbeta) return (int)hipErrorInvalidValue;
+  const dim3 grid(a->nchunk, a->ngroups);
+  if (a->prec) {
+    hipLaunchKernelGGL(bn_bwd_stats_kernel<1>, grid, dim3(BN_THREADS), 0, s, *a);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid, dim3(BN_THREADS), 0, s, *a);
+  } else {
+    hipLaunchKernelGGL(bn_bwd_stats_kernel<0>, grid, dim3(BN_THREADS), 0, s, *a);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<0>, grid, dim3(BN_THREADS), 0, s, *a);
+  }
+  return (int)hipGetLastError();
+}
+
+size_t gt_sizeof_bn_args() { return sizeof(BnArgs); }
+
+}  // extern "C"

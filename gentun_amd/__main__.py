@@ -126,7 +126,7 @@ def cmd_cnn(args):
                  dense_units=args.dense, dropout_probability=args.dropout, classes=args.classes, nfold=args.nfold,
                  epochs=_ints(args.epochs), learning_rate=_floats(args.lr), batch_size=args.batch, loss=args.loss,
                  seed=args.seed, optimizer=args.optimizer, momentum=args.momentum, dtype=args.dtype,
-                 reset=args.fold_reset, batching=args.batching)
+                 reset=args.fold_reset, batching=args.batching, batch_norm=args.batch_norm)
     return _run_search(args, GeneticCnnIndividual, x, y, extra, maximize=True)
 
 
@@ -195,6 +195,8 @@ def main(argv=None):
     c.add_argument("--batching", choices=("keras", "wrap"), default="keras",
                    help="keras: short last batch; wrap: the last batch wraps around the epoch permutation")
     c.add_argument("--momentum", type=float, default=0.9, help="SGD momentum")
+    c.add_argument("--batch-norm", action="store_true",
+                   help="conv -> BatchNorm -> ReLU in every node (not in the reference network; off by default)")
     c.set_defaults(fn=cmd_cnn)
     x = sub.add_parser("xgb", help="GBDT (XGBoost-style) hyper-parameter search")
     _common(x)

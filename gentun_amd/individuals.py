@@ -272,7 +272,9 @@ class GeneticCnnIndividual(Individual):
     'sgd' = Keras SGD with ``momentum``; both reset at every lr stage),
     ``reset`` ('kernels' = the reference's sequential folds that re-draw only
     the kernels, or 'all' = concurrent folds from fresh weights) and
-    ``batching`` ('keras' = short last batch, or 'wrap').
+    ``batching`` ('keras' = short last batch, or 'wrap') and ``batch_norm``
+    (False = the reference network; True = conv -> BatchNorm -> ReLU in every
+    node, Keras BatchNormalization defaults).
     """
 
     def __init__(self, x_train, y_train, genome=None, genes=None, crossover_rate=0.3, mutation_rate=0.1,
@@ -280,7 +282,7 @@ class GeneticCnnIndividual(Individual):
                  kernel_sizes=((5, 5), (5, 5)), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
                  loss='bce_compat', dtype='fp32', seed=0, backend=None, device=None, optimizer='adam',
-                 momentum=0.9, reset='kernels', batching='keras'):
+                 momentum=0.9, reset='kernels', batching='keras', batch_norm=False):
         if genome is None:
             genome = {'S_{}'.format(i + 1): k * (k - 1) // 2 for i, k in enumerate(nodes)}
         if genes is None:
@@ -311,6 +313,7 @@ class GeneticCnnIndividual(Individual):
         self.momentum = momentum
         self.reset = reset
         self.batching = batching
+        self.batch_norm = batch_norm
 
     @staticmethod
     def generate_random_genes(genome):
@@ -328,7 +331,7 @@ class GeneticCnnIndividual(Individual):
                                self.learning_rate, self.batch_size, loss=self.loss, dtype=self.dtype,
                                seed=self.seed, backend=self.backend, device=device or self.device,
                                optimizer=self.optimizer, momentum=self.momentum, reset=self.reset,
-                               batching=self.batching)
+                               batching=self.batching, batch_norm=self.batch_norm)
 
     def cost(self):
         """Relative training cost (forward FLOPs/sample); LPT scheduling key."""
@@ -364,6 +367,7 @@ class GeneticCnnIndividual(Individual):
             'momentum': self.momentum,
             'reset': self.reset,
             'batching': self.batching,
+            'batch_norm': self.batch_norm,
         }
 
     def mutate(self):

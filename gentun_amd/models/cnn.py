@@ -28,7 +28,7 @@ class GeneticCnnModel(GentunModel):
     def __init__(self, x_train, y_train, genes, nodes, input_shape, kernels_per_layer, kernel_sizes, dense_units,
                  dropout_probability, classes, nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
                  loss="bce_compat", dtype="fp32", seed=0, backend=None, device=None, fold_parallel=True,
-                 optimizer="adam", momentum=0.9, reset="kernels", batching="keras"):
+                 optimizer="adam", momentum=0.9, reset="kernels", batching="keras", batch_norm=False):
         super(GeneticCnnModel, self).__init__(x_train, y_train)
         self.genes = dict(genes)
         self.name = '-'.join(self.genes[k] for k in sorted(self.genes))
@@ -57,7 +57,8 @@ class GeneticCnnModel(GentunModel):
         self.backend = backend or _eng.default_backend(self.device)
         self.cfg = _eng.TrainConfig(epochs=epochs, learning_rate=learning_rate, batch_size=batch_size,
                                     dropout=dropout_probability, loss=loss, dtype=dtype, seed=seed,
-                                    optimizer=optimizer, momentum=momentum, reset=reset, batching=batching)
+                                    optimizer=optimizer, momentum=momentum, reset=reset, batching=batching,
+                                    batch_norm=batch_norm)
         self.fold_parallel = fold_parallel
         self.model = self.build_model(self.genes, self.nodes, self.input_shape, self.kernels_per_layer,
                                       self.kernel_sizes, self.dense_units, self.dropout_probability, self.classes)

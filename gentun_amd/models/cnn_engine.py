@@ -53,7 +53,7 @@ CLIP_EPS = 1e-7
 class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
                  dtype="fp32", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9,
-                 reset="kernels", batching="keras"):
+                 reset="kernels", batching="keras", batch_norm=False, bn_momentum=0.99, bn_eps=1e-3):
         if isinstance(epochs, int):
             epochs = (epochs,)
         if isinstance(learning_rate, (int, float)):
@@ -73,6 +73,11 @@ class TrainConfig(object):
             raise ValueError("batching must be 'keras' (short last batch) or 'wrap'")
         self.reset = reset
         self.batching = batching
+        # optional BatchNorm after every conv (conv -> BN -> ReLU; not in the
+        # reference network, off by default); Keras BatchNormalization defaults
+        self.batch_norm = bool(batch_norm)
+        self.bn_momentum = float(bn_momentum)
+        self.bn_eps = float(bn_eps)
         self.epochs = epochs
         self.learning_rate = learning_rate
         self.batch_size = int(batch_size)
@@ -445,6 +450,9 @@ class TorchFoldJob(FoldJob):
             shapes.append((st.name + ".w", (G, st.cout, st.cin, st.k[0], st.k[1]), "glorot",
                            (st.cin * st.k[0] * st.k[1], st.cout * st.k[0] * st.k[1])))
             shapes.append((st.name + ".b", (G, st.cout), "zero", None))
+            if self.cfg.batch_norm:
+                shapes.append((st.name + ".gamma", (G, st.cout), "one", None))
+                shapes.append((st.name + ".beta", (G, st.cout), "zero", None))
         shapes.append(("dense1.w", (G, plan.flatten, plan.dense_units), "glorot", (plan.flatten, plan.dense_units)))
         shapes.append(("dense1.b", (G, plan.dense_units), "zero", None))
         shapes.append(("dense2.w", (G, plan.dense_units, plan.classes), "glorot", (plan.dense_units, plan.classes)))
@@ -463,6 +471,9 @@ class TorchFoldJob(FoldJob):
         self.capture_ok = os.environ.get("GENTUN_TORCH_GRAPH") == "1"
         self.amp = (self.cfg.dtype == "bf16") and self.device.type == "cuda"
         self.drop_gen = None
+        # BatchNorm running statistics per conv: [2 (mean, var)][G][C]
+        self.bn_run = {st.name: torch.zeros((2, G, st.cout), device=self.device) for st in plan.convs()} \
+            if self.cfg.batch_norm else {}
 
     def init_params(self):
         with torch.no_grad():
@@ -478,7 +489,12 @@ class TorchFoldJob(FoldJob):
                         gen.manual_seed(_rng.stable_hash(self._fold_seed(g), name) & 0x7FFFFFFF)
                         vals = torch.rand(per, generator=gen, device=self.device) * (2 * limit) - limit
                         self.flat[off + g * per: off + (g + 1) * per].copy_(vals)
+                elif kind == "one":
+                    self.flat[off:off + n].fill_(1.0)
                 off += n
+            for r in self.bn_run.values():
+                r[0].zero_()
+                r[1].fill_(1.0)
 
     def reset_optimizer(self, lr):
         self.m.zero_()
@@ -487,15 +503,20 @@ class TorchFoldJob(FoldJob):
         self.lr.fill_(lr)
 
     def snapshot(self):
-        return (self.flat.detach().clone(), self.m.clone(), self.v.clone(), self.t.clone())
+        return (self.flat.detach().clone(), self.m.clone(), self.v.clone(), self.t.clone(),
+                {k: r.clone() for k, r in self.bn_run.items()})
 
     def copy_biases_from(self, other):
-        """Biases of every layer from ``other`` (same plan and folds count)."""
+        """Everything ``reset_weights`` keeps (keras_models.py:120-125 re-runs
+        kernel initialisers only): biases and, with BatchNorm, gamma / beta /
+        running statistics, from ``other`` (same plan and folds count)."""
         with torch.no_grad():
             a, b = self._views(), other._views()
             for name, _, kind, _ in self.shapes:
-                if kind == "zero":
+                if kind in ("zero", "one"):
                     a[name].copy_(b[name])
+            for k, r in self.bn_run.items():
+                r.copy_(other.bn_run[k])
 
     def restore(self, snap):
         with torch.no_grad():
@@ -503,6 +524,8 @@ class TorchFoldJob(FoldJob):
             self.m.copy_(snap[1])
             self.v.copy_(snap[2])
             self.t.copy_(snap[3])
+            for k, r in snap[4].items():
+                self.bn_run[k].copy_(r)
 
     def _views(self):
         # Views are rebuilt per call so their autograd nodes live on the
@@ -514,7 +537,35 @@ class TorchFoldJob(FoldJob):
             off += n
         return out
 
-    def _forward(self, xb, train):
+    def _bn(self, z, name, P, train, nval):
+        """BatchNorm of a grouped conv output z [B, G*C, H, W] per group and
+        channel; training statistics over the first ``nval[g]`` rows (the
+        real rows of a Keras short batch), running stats with Keras momentum
+        and the unbiased variance (torch.nn.BatchNorm2d's convention)."""
+        G = self.G
+        Bn, GC, H, W = z.shape
+        C = GC // G
+        zz = z.view(Bn, G, C, H, W)
+        run = self.bn_run[name]
+        if train:
+            rows = torch.arange(Bn, device=z.device)[:, None]
+            m = (rows < nval[None, :]).to(z.dtype)[:, :, None, None, None]          # [B, G, 1, 1, 1]
+            n = (nval.to(z.dtype) * (H * W)).clamp_min(1.0)[None, :, None, None, None]
+            mean = (zz * m).sum((0, 3, 4), keepdim=True) / n
+            var = ((zz - mean) ** 2 * m).sum((0, 3, 4), keepdim=True) / n
+            with torch.no_grad():
+                mo = self.cfg.bn_momentum
+                nn_ = n.view(1, G, 1)
+                run[0].mul_(mo).add_((1.0 - mo) * mean.view(G, C))
+                run[1].mul_(mo).add_((1.0 - mo) * (var.view(1, G, C) * nn_ / (nn_ - 1.0).clamp_min(1.0)).view(G, C))
+        else:
+            mean = run[0].view(1, G, C, 1, 1)
+            var = run[1].view(1, G, C, 1, 1)
+        xh = (zz - mean) * torch.rsqrt(var + self.cfg.bn_eps)
+        out = xh * P[name + ".gamma"].view(1, G, C, 1, 1) + P[name + ".beta"].view(1, G, C, 1, 1)
+        return out.reshape(Bn, GC, H, W)
+
+    def _forward(self, xb, train, nval=None):
         """xb: [B, G*C, H, W] -> logits [G, B, classes]."""
         G, plan, P = self.G, self.plan, self._views()
         acts = {"input": xb}
@@ -525,7 +576,12 @@ class TorchFoldJob(FoldJob):
                     inp = inp + acts[extra]
                 w = P[st.name + ".w"].reshape(G * st.cout, st.cin, st.k[0], st.k[1])
                 b = P[st.name + ".b"].reshape(G * st.cout)
-                acts[st.name] = F.relu(F.conv2d(inp, w, b, padding=(st.k[0] // 2, st.k[1] // 2), groups=G))
+                z = F.conv2d(inp, w, b, padding=(st.k[0] // 2, st.k[1] // 2), groups=G)
+                if self.cfg.batch_norm:
+                    if nval is None:
+                        nval = torch.full((G,), xb.shape[0], device=xb.device)
+                    z = self._bn(z, st.name, P, train, nval)
+                acts[st.name] = F.relu(z)
             else:
                 src = acts[st.srcs[0]]
                 acts[st.name] = F.max_pool2d(src, 2, 2)
@@ -564,9 +620,9 @@ class TorchFoldJob(FoldJob):
         self.flat.grad.zero_()
         if self.amp:
             with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
-                logits = self._forward(xb, True)
+                logits = self._forward(xb, True, nval.view(-1))
         else:
-            logits = self._forward(xb, True)
+            logits = self._forward(xb, True, nval.view(-1))
         per, _, _ = loss_and_metrics(logits, yb, self.cfg.loss)
         # mean over the real rows of each group's batch (Keras short batch)
         rows = torch.arange(self.B, device=self.device)[None, :].float()

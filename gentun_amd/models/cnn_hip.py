@@ -86,6 +86,7 @@ class HipPopJob(FoldJob):
         self.prec = K.PREC[cfg.dtype]
         self.npl = K.NPL[cfg.dtype]
         self.adt = torch.float32 if self.prec else torch.bfloat16      # activation / gradient storage
+        self.bn = bool(getattr(cfg, "batch_norm", False))
         p0 = self.plan
         Q, B, dev = self.G, self.B, self.device
         self.Q = Q
@@ -159,6 +160,19 @@ class HipPopJob(FoldJob):
         for L in self.layers:
             if L.xin is not None:
                 self.act[L.xin] = torch.zeros((Q, B, L.H, L.W, L.cinp), dtype=self.adt, device=dev)
+        # BatchNorm: the conv writes its pre-activation z, the BN kernels write
+        # relu(bn(z)) into the layer's activation slot
+        self.zpre = {}
+        if self.bn:
+            for L in self.layers:
+                self.zpre[L.name] = torch.zeros((Q, B, L.H, L.W, L.coutp), dtype=self.adt, device=dev)
+                L.bn_chunk = K.BN_CHUNK_PX
+                L.bn_nchunk = -(-(B * L.H * L.W) // L.bn_chunk)
+                L.bn_stat = torch.zeros((Q, 2, L.coutp), dtype=torch.float32, device=dev)
+                L.bn_run = torch.zeros((2, Q, L.coutp), dtype=torch.float32, device=dev)
+                L.bn_part = torch.zeros((Q, L.bn_nchunk, 2, L.coutp), dtype=torch.float32, device=dev)
+                L.g_gamma = torch.zeros((Q, L.coutp), dtype=torch.float32, device=dev)
+                L.g_beta = torch.zeros((Q, L.coutp), dtype=torch.float32, device=dev)
         hs, ws = self.final_hw
         self.Fp = hs * ws * self.final_cp
         self.Up = round_up(p0.dense_units, 64)
@@ -170,6 +184,9 @@ class HipPopJob(FoldJob):
         for L in self.layers:
             segs.append(("w", L, (Q, L.coutp, L.KH, L.KW, L.cinp)))
             segs.append(("b", L, (Q, L.coutp)))
+            if self.bn:
+                segs.append(("gamma", L, (Q, L.coutp)))
+                segs.append(("beta", L, (Q, L.coutp)))
         segs.append(("W1", None, (Q, self.Fp, self.Up)))
         segs.append(("b1", None, (Q, self.Up)))
         segs.append(("W2", None, (Q, self.Up, self.classes)))
@@ -244,6 +261,10 @@ class HipPopJob(FoldJob):
                     tdims=(1, L.coutp, L.KH, L.KW, L.cinp), pstrides=(L.w_bf[0].numel(), L.wT_bf[0].numel()))
                 p, m, v = (t[q] for t in L.b)
                 add(p, m, v, L.part_b[0, q], L.S, L.part_b[0].numel())
+                if self.bn:
+                    for t, g in ((L.gamma, L.g_gamma), (L.beta, L.g_beta)):
+                        p, m, v = (x[q] for x in t)
+                        add(p, m, v, g[q], 1, g[q].numel())
         for name, g in (("b1", self.gb1), ("W2", self.gW2), ("b2", self.gb2)):
             p, m, v = self.views[name]
             add(p, m, v, g, 1, g.numel())
@@ -276,6 +297,21 @@ class HipPopJob(FoldJob):
         a.wps = w[0].numel()                 # weights are [planes][...]
         return a
 
+    def _bn_args(self, L, train):
+        a = K.BnArgs()
+        a.z, a.y = self.zpre[L.name].data_ptr(), self.act[L.name].data_ptr()
+        a.gamma, a.beta = L.gamma[0].data_ptr(), L.beta[0].data_ptr()
+        a.stat, a.run, a.part = L.bn_stat.data_ptr(), L.bn_run.data_ptr(), L.bn_part.data_ptr()
+        a.ggamma, a.gbeta = L.g_gamma.data_ptr(), L.g_beta.data_ptr()
+        a.gtab = self._gtab([(q, 0, 0) for q, _ in L.rows]).data_ptr()
+        a.valid = self.epoch_valid.data_ptr()
+        a.st = self.state.data_ptr()
+        a.ngroups, a.G, a.B, a.HW, a.Cp = len(L.rows), self.Q, self.B, L.H * L.W, L.coutp
+        a.nchunk, a.chunk_px = L.bn_nchunk, L.bn_chunk
+        a.momentum, a.eps = self.cfg.bn_momentum, self.cfg.bn_eps
+        a.train, a.prec = train, self.prec
+        return a
+
     def _slot_ptr(self, name, grad=False):
         if name == "input":
             return self.data.x.data_ptr()
@@ -290,13 +326,16 @@ class HipPopJob(FoldJob):
         for st in self.stages:
             for L in st.layers:
                 first = L.slots == ["input"]
-                a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [self.act[L.name].data_ptr()], [],
-                                    L.w_bf, L.b[0], 1, [(q, im, 1) for q, im in L.rows],
+                out = self.zpre[L.name] if self.bn else self.act[L.name]
+                a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [out.data_ptr()], [],
+                                    L.w_bf, L.b[0], 0 if self.bn else 1, [(q, im, 1) for q, im in L.rows],
                                     gather=gather_train if first else None)
                 if L.xin is not None:
                     a.xsum = self.act[L.xin].data_ptr()
                 a.epi_bf16 = 1            # forward outputs never accumulate: bf16 output tile
                 self.fwd_ops.append(("conv", a, L))
+                if self.bn:
+                    self.fwd_ops.append(("bn", self._bn_args(L, 1), L))
             sel = torch.tensor(self.sched.pool_source(st), dtype=torch.int32, device=self.device)
             self._keep.append(sel)
             x1 = self.act[self.sched.pool_x1(st)]
@@ -348,6 +387,7 @@ class HipPopJob(FoldJob):
         self.dense_wgrad_args = dw
         # ---- backward (records: models/pop_schedule.py PopulationSchedule.backward)
         self.bwd_ops = []
+        bn_done = set()
         for rec in self.sched.backward():
             if rec[0] == "pool_bwd":
                 st = rec[1]
@@ -360,6 +400,13 @@ class HipPopJob(FoldJob):
                 continue
             kind, L, rows = rec
             first = L.slots == ["input"]
+            if self.bn and L.name not in bn_done:
+                # grad[L] is complete (every consumer's dgrad ran): BN backward
+                # turns it into dz in place before the layer's wgrad / dgrad
+                bn_done.add(L.name)
+                ba = self._bn_args(L, 1)
+                ba.y = self.grad[L.name].data_ptr()      # ReLU-masked grad in, dz out (in place)
+                self.bwd_ops.append(("bn_bwd", ba, L))
             if kind == "wgrad":
                 wa = K.WgradArgs()
                 wslots = L.slots + ([L.xin] if L.xin is not None else [])
@@ -439,6 +486,11 @@ class HipPopJob(FoldJob):
             self._build_init_table()
         self.flat.zero_()
         K.check(K.lib().gt_glorot_init(self.init_args, self.init_nblocks, self._stream()), "glorot_init")
+        if self.bn:
+            for L in self.layers:                # gamma 1 (padding channels stay 0), running stats (0, 1)
+                L.gamma[0][:, :L.cout].fill_(1.0)
+                L.bn_run[0].zero_()
+                L.bn_run[1].fill_(1.0)
         self._refresh_copies()
 
     def _refresh_copies(self):
@@ -459,15 +511,22 @@ class HipPopJob(FoldJob):
         self.state_f[7:8].fill_(float(self.cfg.momentum))                  # StepState.momentum
 
     def snapshot(self):
-        return (self.flat.clone(), self.m.clone(), self.v.clone(), self.state.clone())
+        return (self.flat.clone(), self.m.clone(), self.v.clone(), self.state.clone(),
+                [L.bn_run.clone() for L in self.layers] if self.bn else [])
 
     def copy_biases_from(self, other):
-        """Conv / dense biases of every group from ``other`` (a job of the same
-        members at the previous fold: SequentialFoldJob)."""
+        """Everything ``reset_weights`` keeps (keras_models.py:120-125 re-runs
+        kernel initialisers only): conv / dense biases and, with BatchNorm,
+        gamma / beta / running statistics of every group, from ``other`` (a job
+        of the same members at the previous fold: SequentialFoldJob)."""
         mine = {L.name: L for L in self.layers}
         for L in other.layers:
             if L.name in mine:
                 mine[L.name].b[0].copy_(L.b[0])
+                if self.bn and other.bn:
+                    mine[L.name].gamma[0].copy_(L.gamma[0])
+                    mine[L.name].beta[0].copy_(L.beta[0])
+                    mine[L.name].bn_run.copy_(L.bn_run)
         for name in ("b1", "b2"):
             self.views[name][0].copy_(other.views[name][0])
 
@@ -476,6 +535,8 @@ class HipPopJob(FoldJob):
         self.m.copy_(snap[1])
         self.v.copy_(snap[2])
         self.state.copy_(snap[3])
+        for L, r in zip(self.layers, snap[4]):
+            L.bn_run.copy_(r)
         self._refresh_copies()
 
     def _stream(self):
@@ -486,6 +547,8 @@ class HipPopJob(FoldJob):
         for kind, a, mk in ops:
             if kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_fwd")
+            elif kind == "bn":
+                K.check(L.gt_bn_fwd(a, s), "bn_fwd")
             elif mk is not None:
                 K.check(L.gt_pool_fwd_mask(*a, mk, self.prec, s), "pool_fwd")
             else:
@@ -521,6 +584,8 @@ class HipPopJob(FoldJob):
                 K.check(L.gt_conv_wgrad(a, ss), "conv_wgrad")
             elif kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
+            elif kind == "bn_bwd":
+                K.check(L.gt_bn_bwd(a, s), "bn_bwd")
             else:
                 K.check(L.gt_pool_bwd_mask(*a, s), "pool_bwd")
         for stream in (side, side2):
@@ -551,6 +616,10 @@ class HipPopJob(FoldJob):
                 b = K.ConvArgs.from_buffer_copy(a)
                 b.st = self.eval_state.data_ptr()
                 b.xsum = 0
+                ops.append((kind, b, Lr))
+            elif kind == "bn":
+                b = K.BnArgs.from_buffer_copy(a)
+                b.train = 0                          # running statistics
                 ops.append((kind, b, Lr))
             else:
                 ops.append((kind, a, None))          # no argmax mask in evaluation

@@ -85,6 +85,17 @@ def adam_tiles(tG, tCo, tKH, tKW, tCi):
     return tG * (-(-kd // ADAM_TK))
 
 
+class BnArgs(C.Structure):
+    """csrc/hip/cnn_bn.hip BnArgs (optional BatchNorm of the node convs)."""
+    _fields_ = [("z", P), ("y", P), ("gamma", P), ("beta", P), ("stat", P), ("run", P), ("part", P),
+                ("ggamma", P), ("gbeta", P), ("gtab", P), ("valid", P), ("st", P),
+                ("ngroups", I), ("G", I), ("B", I), ("HW", I), ("Cp", I), ("nchunk", I), ("chunk_px", I),
+                ("momentum", C.c_float), ("eps", C.c_float), ("train", I), ("prec", I)]
+
+
+BN_CHUNK_PX = 512     # pixels per BatchNorm workgroup (fixed per shape: batch-invariant sums)
+
+
 class AdamArgs(C.Structure):
     _fields_ = [("segs", P), ("blocks", P), ("st", P)]
 
@@ -110,6 +121,10 @@ def lib():
                            ("gt_dense_wgrad_adam", C.POINTER(DenseWgradAdamArgs))):
             fn = getattr(L, name)
             fn.argtypes = [argt, P]
+            fn.restype = I
+        for name in ("gt_bn_fwd", "gt_bn_bwd"):
+            fn = getattr(L, name)
+            fn.argtypes = [C.POINTER(BnArgs), P]
             fn.restype = I
         L.gt_adam_segments.argtypes = [C.POINTER(AdamArgs), I, P]
         L.gt_adam_segments.restype = I
@@ -145,12 +160,13 @@ def lib():
         L.gt_glorot_ref.restype = C.c_float
         for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg", "gt_sizeof_init_seg",
                      "gt_sizeof_dense_fwd_args", "gt_sizeof_head_args", "gt_sizeof_dense_dgrad_args",
-                     "gt_sizeof_dense_wgrad_args"):
+                     "gt_sizeof_dense_wgrad_args", "gt_sizeof_bn_args"):
             getattr(L, name).restype = C.c_size_t
         assert L.gt_sizeof_conv_args() == C.sizeof(ConvArgs), "ConvArgs ABI mismatch"
         assert L.gt_sizeof_init_seg() == C.sizeof(InitSeg), "InitSeg ABI mismatch"
         assert L.gt_sizeof_wgrad_args() == C.sizeof(WgradArgs), "WgradArgs ABI mismatch"
         assert L.gt_sizeof_adam_seg() == C.sizeof(AdamSeg), "AdamSeg ABI mismatch"
+        assert L.gt_sizeof_bn_args() == C.sizeof(BnArgs), "BnArgs ABI mismatch"
         for nm, st in (("dense_fwd_args", DenseFwdArgs), ("head_args", HeadArgs),
                        ("dense_dgrad_args", DenseDgradArgs), ("dense_wgrad_args", DenseWgradAdamArgs)):
             assert getattr(L, "gt_sizeof_" + nm)() == C.sizeof(st), nm + " ABI mismatch"

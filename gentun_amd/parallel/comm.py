@@ -72,6 +72,20 @@ class LocalComm(Communicator):
 _DTYPES = [np.float64, np.float32, np.int64, np.int32, np.uint8]
 
 
+def _attempt_store(timeout):
+    """Under torchrun's static rendezvous the agent's TCPStore outlives a
+    restart (``--max-restarts``): without a per-attempt key prefix a restarted
+    rank can read a dead peer's gloo / RCCL bootstrap address left over from
+    the previous attempt and fail to connect. Returns the agent store under
+    ``gentun/attempt_<TORCHELASTIC_RESTART_COUNT>`` (None outside torchrun)."""
+    import torch.distributed as dist
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") != "True" or "TORCHELASTIC_RESTART_COUNT" not in os.environ:
+        return None
+    base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]),
+                         int(os.environ["WORLD_SIZE"]), is_master=False, timeout=timeout)
+    return dist.PrefixStore("gentun/attempt_{}".format(os.environ["TORCHELASTIC_RESTART_COUNT"]), base)
+
+
 class DistComm(Communicator):
     """``torch.distributed`` collectives on small numpy arrays.
 
@@ -90,6 +104,9 @@ class DistComm(Communicator):
             kwargs = {"backend": backend, "timeout": datetime.timedelta(seconds=timeout_s)}
             if backend == "nccl" and device is not None:
                 kwargs["device_id"] = torch.device(device)
+            store = _attempt_store(kwargs["timeout"])
+            if store is not None:
+                kwargs.update(store=store, rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
             dist.init_process_group(**kwargs)
         self.backend = dist.get_backend()
         self.rank = dist.get_rank()

@@ -226,7 +226,7 @@ def _settings_key(model):
     c = model.cfg
     return (id(model.x_train), id(model.y_train), model.backend, str(model.device), model.nfold,
             c.epochs, c.learning_rate, c.batch_size, c.dropout, c.loss, c.dtype, c.seed, c.optimizer, c.momentum,
-            getattr(c, "reset", None), getattr(c, "batch_norm", None),
+            getattr(c, "reset", None), getattr(c, "batching", None), getattr(c, "batch_norm", None),
             model.nodes, model.input_shape, model.kernels_per_layer, model.kernel_sizes, model.dense_units,
             model.classes)
 

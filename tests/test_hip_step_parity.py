@@ -39,6 +39,8 @@ def _hip_weights(job):
     for L in job.layers:
         w = L.w[0][0][:L.cout, :, :, :L.cin].permute(0, 3, 1, 2)
         out[L.name] = (w.detach().clone(), L.b[0][0][:L.cout].detach().clone())
+        if job.bn:
+            out[L.name] += (L.gamma[0][0][:L.cout].detach().clone(), L.beta[0][0][:L.cout].detach().clone())
     hs, ws = job.final_hw
     cp, C, U = job.final_cp, job.plan.kernels_per_layer[-1], job.plan.dense_units
     W1 = job.views["W1"][0][0].view(hs, ws, cp, job.Up)[:, :, :C, :U]          # NHWC features
@@ -56,6 +58,8 @@ def _hip_grads(job):
     for L in job.layers:
         m = L.w[1][0][:L.cout, :, :, :L.cin].permute(0, 3, 1, 2)
         g[L.name] = (-m.detach().clone(), -L.b[1][0][:L.cout].detach().clone())
+        if job.bn:
+            g[L.name] += (-L.gamma[1][0][:L.cout].detach().clone(), -L.beta[1][0][:L.cout].detach().clone())
     hs, ws = job.final_hw
     cp, C, U = job.final_cp, job.plan.kernels_per_layer[-1], job.plan.dense_units
     M1 = job.views["W1"][1][0].view(hs, ws, cp, job.Up)[:, :, :C, :U].permute(2, 0, 1, 3).reshape(C * hs * ws, U)
@@ -66,8 +70,10 @@ def _hip_grads(job):
     return g
 
 
-def _reference_grads(plan, weights, xb, yb, loss, dtype=torch.float64):
-    """autograd through the plan (NCHW) on the CPU, mean loss over the batch."""
+def _reference_grads(plan, weights, xb, yb, loss, dtype=torch.float64, bn_eps=None, masks=None):
+    """autograd through the plan (NCHW) on the CPU, mean loss over the batch;
+    ``bn_eps``: conv -> BatchNorm (batch statistics) -> ReLU; ``masks``:
+    {layer: NCHW bool} ReLU decisions to use instead of the reference's own."""
     from gentun_amd.models.genome import ConvSpec
     P = {k: (tuple(t.to(dtype).cpu().requires_grad_(True) for t in v) if isinstance(v, tuple)
              else v.to(dtype).cpu().requires_grad_(True)) for k, v in weights.items()}
@@ -78,8 +84,14 @@ def _reference_grads(plan, weights, xb, yb, loss, dtype=torch.float64):
             inp = acts[st.inputs[0]]
             for extra in st.inputs[1:]:
                 inp = inp + acts[extra]
-            w, b = P[st.name]
-            acts[st.name] = F.relu(F.conv2d(inp, w, b, padding=(st.k[0] // 2, st.k[1] // 2)))
+            w, b = P[st.name][:2]
+            z = F.conv2d(inp, w, b, padding=(st.k[0] // 2, st.k[1] // 2))
+            if bn_eps is not None:
+                gm, bt = P[st.name][2:]
+                mean = z.mean((0, 2, 3), keepdim=True)
+                var = ((z - mean) ** 2).mean((0, 2, 3), keepdim=True)
+                z = (z - mean) / torch.sqrt(var + bn_eps) * gm.view(1, -1, 1, 1) + bt.view(1, -1, 1, 1)
+            acts[st.name] = z * masks[st.name].to(dtype) if masks is not None else F.relu(z)
         else:
             acts[st.name] = F.max_pool2d(acts[st.srcs[0]], 2, 2)
     feat = acts[plan.steps[-1].name].reshape(xb.shape[0], -1)
@@ -106,13 +118,24 @@ def _rel(a, b):
 @pytest.mark.parametrize("loss", ["ce", "bce_compat"])
 @pytest.mark.parametrize("gi", range(len(GENES)))
 def test_one_step_gradients_match_fp64_autograd(gi, loss):
+    _one_step_parity(gi, loss, bn=False)
+
+
+@pytest.mark.parametrize("gi", range(len(GENES)))
+def test_one_step_gradients_with_batchnorm(gi):
+    """The optional BatchNorm (conv -> BN -> ReLU, cnn_bn.hip) inside the
+    composed step: every conv / gamma / beta / dense gradient vs fp64."""
+    _one_step_parity(gi, "ce", bn=True)
+
+
+def _one_step_parity(gi, loss, bn):
     from gentun_amd.models import cnn_engine as E
     from gentun_amd.models.cnn_hip import HipPopJob
     genes = GENES[gi]
     x, y, fold, plan = _setup(genes)
     dev = torch.device("cuda", 0)
     cfg = E.TrainConfig(epochs=(1,), learning_rate=(1.0,), batch_size=32, dropout=0.0, loss=loss, dtype="fp32",
-                        optimizer="sgd", momentum=0.9, use_graph=False)
+                        optimizer="sgd", momentum=0.9, use_graph=False, batch_norm=bn)
     job = HipPopJob(plan, x, y, [fold], cfg, dev, fold_ids=[0])
     job.init_params()
     w0 = _hip_weights(job)
@@ -124,24 +147,36 @@ def test_one_step_gradients_match_fp64_autograd(gi, loss):
     got = _hip_grads(job)
     xb = torch.from_numpy(np.asarray(x)[idx.numpy()]).permute(0, 3, 1, 2)
     yb = torch.from_numpy(np.asarray(y)[idx.numpy()]).double()
-    ref = _reference_grads(plan, w0, xb, yb, loss)
-    r32 = _reference_grads(plan, w0, xb, yb, loss, torch.float32)    # torch's own fp32, same inputs
+    eps = cfg.bn_eps if bn else None
+    # BatchNorm rescales every pre-activation to O(1): a node's BN output lands
+    # within fp32 rounding of 0 at a few positions, and a ReLU decision that
+    # flips there moves that layer's gradient by O(1e-2). With BN the fp64
+    # reference therefore takes the HIP forward's ReLU decisions (the
+    # arithmetic is compared, not the tie-breaking).
+    masks = None
+    if bn:
+        masks = {L.name: (job.act[L.name][0][..., :L.cout] > 0).permute(0, 3, 1, 2).cpu() for L in job.layers}
+    ref = _reference_grads(plan, w0, xb, yb, loss, bn_eps=eps, masks=masks)
+    r32 = _reference_grads(plan, w0, xb, yb, loss, torch.float32, bn_eps=eps, masks=masks)    # torch fp32, same inputs
 
     def errs(g):
         out = {}
         for k, r in ref.items():
             if isinstance(r, tuple):
                 out[k + ".w"] = _rel(g[k][0], r[0])
-                if r[1].abs().max() > 0:
+                if r[1].abs().max() > 0 and not bn:         # with BN the conv bias gradient is 0 (+ rounding)
                     out[k + ".b"] = _rel(g[k][1], r[1])
+                if bn:
+                    out[k + ".gamma"] = _rel(g[k][2], r[2])
+                    out[k + ".beta"] = _rel(g[k][3], r[3])
             else:
                 out[k] = _rel(g[k], r)
         return out
 
     worst, worst32 = errs(got), errs(r32)
     kmax = max(worst, key=worst.get)
-    print("[parity] genes {} loss {}: worst rel grad err HIP {:.2e} ({}); torch fp32 there {:.2e}, worst {:.2e}"
-          .format(genes, loss, worst[kmax], kmax, worst32[kmax], max(worst32.values())))
+    print("[parity] genes {} loss {} bn {}: worst rel grad err HIP {:.2e} ({}); torch fp32 there {:.2e}, worst {:.2e}"
+          .format(genes, loss, bn, worst[kmax], kmax, worst32[kmax], max(worst32.values())))
     assert set(k.split(".")[0] for k in worst) >= set(L.name for L in job.layers)
     # fp32-level: within 2e-4 of the fp64 gradient, or no further than torch's
     # own fp32 CPU autograd (ReLU / max-pool decisions near ties flip in fp32)
@@ -167,7 +202,7 @@ def _named(w, name):
     base, kind = name.rsplit(".", 1)
     if base in ("dense1", "dense2"):
         return w[("W" if kind == "w" else "b") + base[-1]]
-    return w[base][0 if kind == "w" else 1]
+    return w[base][{"w": 0, "b": 1, "gamma": 2, "beta": 3}[kind]]
 
 
 def _torch_weights(tj, like):
@@ -179,8 +214,8 @@ def _torch_weights(tj, like):
     return out
 
 
-@pytest.mark.parametrize("gi", [0, 1])
-def test_fifty_steps_track_the_torch_fp32_oracle(gi):
+@pytest.mark.parametrize("gi,bn", [(0, False), (1, False), (0, True)])
+def test_fifty_steps_track_the_torch_fp32_oracle(gi, bn):
     """50 SGD-momentum steps (no dropout) from identical weights on identical
     batches. Two valid fp32 executions of a 50-step non-convex training run
     drift apart chaotically (ReLU / max-pool decisions near ties flip), so the
@@ -192,7 +227,7 @@ def test_fifty_steps_track_the_torch_fp32_oracle(gi):
     x, y, fold, plan = _setup(genes, n=2000, ntrain=1600)
     dev = torch.device("cuda", 0)
     cfg = E.TrainConfig(epochs=(1,), learning_rate=(0.003,), batch_size=32, dropout=0.0, loss="ce", dtype="fp32",
-                        use_graph=False, optimizer="sgd", momentum=0.9)
+                        use_graph=False, optimizer="sgd", momentum=0.9, batch_norm=bn)
     hip = HipPopJob(plan, x, y, [fold], cfg, dev, fold_ids=[0])
     tg = E.TorchFoldJob(plan, x, y, [fold], cfg, dev, fold_ids=[0])
     tc = E.TorchFoldJob(plan, x, y, [fold], cfg, torch.device("cpu"), fold_ids=[0])
@@ -213,13 +248,16 @@ def test_fifty_steps_track_the_torch_fp32_oracle(gi):
     wg, wc = _torch_weights(tg, w), _torch_weights(tc, w)
     d_hip, d_cpu = {}, {}
     for name in wg:
+        if bn and name.endswith(".b") and not name.startswith("dense"):
+            continue             # conv bias under BN: zero gradient, a free direction that only drifts with rounding
         scale = max(wg[name].abs().max().item(), 1e-12)
         d_hip[name] = (_named(wh, name).cpu() - wg[name]).abs().max().item() / scale
         d_cpu[name] = (wc[name] - wg[name]).abs().max().item() / scale
     vh, vg, vc = (float(j.evaluate()[0].sum()) / 400 for j in (hip, tg, tc))
     k = max(d_hip, key=d_hip.get)
-    print("[parity] 50 SGD steps genes {}: max |w_hip - w_torchGPU| / max|w| = {:.2e} ({}); torch CPU vs GPU: {:.2e} "
+    print("[parity] 50 SGD steps genes {} bn {}: max |w_hip - w_torchGPU| / max|w| = {:.2e} ({}); torch CPU vs GPU: {:.2e} "
           "(max {:.2e}); val loss hip {:.5f} torchGPU {:.5f} torchCPU {:.5f}".format(
-              genes, d_hip[k], k, d_cpu[k], max(d_cpu.values()), vh, vg, vc))
+              genes, bn, d_hip[k], k, d_cpu[k], max(d_cpu.values()), vh, vg, vc))
     assert max(d_hip.values()) <= 3 * max(d_cpu.values()) + 1e-5
-    assert abs(vh - vg) <= max(3 * abs(vc - vg), 0.1)
+    if not bn:       # with BN the evaluation uses running statistics that, after 50 steps, are still
+        assert abs(vh - vg) <= max(3 * abs(vc - vg), 0.1)      # 60% their (0, 1) start: no stable yardstick
