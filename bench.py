@@ -66,6 +66,8 @@ def parse():
                     help="default: S=(3,5) kernels (20,50) (headline); deep: BASELINE cfg 4, S=(3,4,5) kernels "
                          "(20,50,100) on 32x32 inputs")
     ap.add_argument("--kernels", default=None, help="override kernels per stage, e.g. 64,128,256")
+    ap.add_argument("--batch-norm", action="store_true",
+                    help="conv -> BatchNorm -> ReLU in every node (not in the reference network)")
     return ap.parse_args()
 
 
@@ -123,7 +125,8 @@ def run(args):
     extra = dict(nodes=nodes, input_shape=(32, 32, 3), kernels_per_layer=kernels,
                  kernel_sizes=((5, 5),) * len(nodes), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=args.nfold, epochs=epochs, learning_rate=lrs, batch_size=32, dtype=args.dtype,
-                 loss=args.loss, seed=args.seed, backend=args.backend, reset=args.fold_reset, batching="keras")
+                 loss=args.loss, seed=args.seed, backend=args.backend, reset=args.fold_reset, batching="keras",
+                 batch_norm=args.batch_norm)
     evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch)
     N = comm.world_size
     round_size = per_gpu * N
@@ -198,7 +201,7 @@ def run(args):
                    "candidates_per_round": round_size, "per_gpu": per_gpu, "nfold": args.nfold,
                    "epochs": list(epochs), "learning_rate": list(lrs), "samples": args.samples,
                    "loss": args.loss, "backend": args.backend or ("hip" if device.type == "cuda" else "torch"),
-                   "fold_reset": args.fold_reset, "batching": "keras (8000 = 250 x 32: no short batch)",
+                   "fold_reset": args.fold_reset, "batch_norm": args.batch_norm, "batching": "keras (8000 = 250 x 32: no short batch)",
                    "fp32_impl": "fp32 tensors, 3-way exact bf16 split x 6 MFMA terms per product"
                    if args.dtype == "fp32" else None,
                    "streams_per_gpu": args.streams, "pop_batch": args.pop_batch},

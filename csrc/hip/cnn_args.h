@@ -45,6 +45,8 @@ struct ConvArgs {
                                     //    bf16: same bits, half the LDS); 0: fp32 tile (exact accumulate)
   int prec;                         // 0: bf16 tensors, bf16 MFMA; 1: fp32 tensors, split-fp32 MFMA (common.h)
   long wps;                         // weight plane stride in elements (prec 1)
+  int cbb;                          // generic kernel, set by its launcher: input chunks (8 channels) per channel
+                                    // block (0: all at once). Wide fp32 layers stage the patch block by block.
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

@@ -56,16 +56,20 @@ conv_fwd_kernel(ConvArgs a) {
   const int co_blk = blockIdx.z * 64;
   const int ph = a.KH >> 1, pw = a.KW >> 1;
   const int PH = THr + a.KH - 1, PW = a.W + a.KW - 1;
-  const int ncb = a.Cinp >> 3;
+  const int ncb_all = a.Cinp >> 3;
+  // channel blocks: the patch holds ncb input chunks at a time (wide fp32
+  // layers whose whole patch does not fit in LDS); accumulators persist
+  const int ncb = a.cbb > 0 && a.cbb < ncb_all ? a.cbb : ncb_all;
+  const int ncblk = (ncb_all + ncb - 1) / ncb;
   const long img = (long)a.H * a.W * a.Cinp;
   const int pimg = PH * PW * ncb;                       // patch chunks per image
   const int total = NI * pimg;                          // patch chunks per plane
-  const int nchunks = a.KH * a.KW * ncb;
+  const int nchunks = a.KH * a.KW * ncb;                // k chunks per channel block
   const int Kdim = a.KH * a.KW * a.Cinp;
   // LDS carve: [weight blocks: NPL x nbuf x wrows x CF_WLD][patch: NPL x total][chunk offset table].
   // Only as many weight rows / buffers as this layer needs (occupancy).
   const int nkb = (nchunks + CF_KB - 1) / CF_KB;
-  const int nbuf = nkb > 1 ? 2 : 1;
+  const int nbuf = nkb > 1 || ncblk > 1 ? 2 : 1;
   const int wrows = ((min(64, a.Coutp) + 15) >> 4) << 4;
   const int wplane = nbuf * wrows * CF_WLD;             // elements per weight plane
   const size_t wbytes = (size_t)NPL * wplane * 2;
@@ -80,14 +84,20 @@ conv_fwd_kernel(ConvArgs a) {
   const bool wrow_ok = co_blk + wr < a.Coutp;
   const uint16_t* wsrc = wg + (long)(co_blk + wr) * Kdim;
   uint4 wreg[NPL][CF_KB / 4];
-  auto load_wblock = [&](int kb) {
+  const FastDiv div_ncb(ncb);
+  auto load_wblock = [&](int kb, int cb0) {
 #pragma unroll
     for (int q = 0; q < NPL; ++q)
 #pragma unroll
       for (int j = 0; j < CF_KB / 4; ++j) {
         const int c = kb * CF_KB + wq + j;
-        wreg[q][j] = (wrow_ok && c < nchunks) ? *reinterpret_cast<const uint4*>(wsrc + q * a.wps + c * 8)
-                                              : make_uint4(0, 0, 0, 0);
+        // block-local chunk (kh, kw, cb) -> the weight row's chunk (kh, kw, cb0 + cb)
+        uint32_t kk, cb;
+        div_ncb.divmod((uint32_t)c, kk, cb);
+        const int cg = (int)kk * ncb_all + cb0 + (int)cb;
+        wreg[q][j] = (wrow_ok && c < nchunks && cb0 + (int)cb < ncb_all)
+                         ? *reinterpret_cast<const uint4*>(wsrc + q * a.wps + (long)cg * 8)
+                         : make_uint4(0, 0, 0, 0);
       }
   };
   auto store_wblock = [&](int buf) {
@@ -99,22 +109,60 @@ conv_fwd_kernel(ConvArgs a) {
       for (int j = 0; j < CF_KB / 4; ++j) *reinterpret_cast<uint4*>(dst + j * 8) = wreg[q][j];
     }
   };
-  load_wblock(0);
+  const int n_src = a.gather ? 1 : __builtin_popcount(gr.in_mask);
+  const FastDiv div_pw(PW), div_pimg(pimg);
+  const int wave = tid >> 6, lane = tid & 63;
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int ipx = THr * a.W;                            // tile pixels per image
+  int pbase[PXG];
+  bool pvalid[PXG];
+  int pyy[PXG], pxx[PXG], pim[PXG];
+#pragma unroll
+  for (int h = 0; h < PXG; ++h) {
+    const int pl = wave * 16 * PXG + h * 16 + l16;
+    pim[h] = pl / ipx;
+    const int pp = pl - pim[h] * ipx;
+    pyy[h] = pp / a.W; pxx[h] = pp % a.W;
+    pvalid[h] = (pl < NI * ipx) && (h0 + pyy[h] < a.H) && (b0 + pim[h] < a.B);
+    pbase[h] = pim[h] * pimg + (pyy[h] * PW + pxx[h]) * ncb;
+  }
+  const int nco = min(64, a.Coutp - co_blk);
+  const int NT = (nco + 15) >> 4;
+  f32x4_t acc[PXG][4];
+#pragma unroll
+  for (int h = 0; h < PXG; ++h)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[h][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  {
+    const FastDiv div_kw(a.KW);
+    for (int c = tid; c < nchunks + 4; c += 256) {
+      if (c < nchunks) {
+        uint32_t kk, cb, kh, kw;
+        div_ncb.divmod((uint32_t)c, kk, cb);
+        div_kw.divmod(kk, kh, kw);
+        coff[c] = ((int)kh * PW + (int)kw) * ncb + (int)cb;
+      } else {
+        coff[c] = -1;
+      }
+    }
+  }
+
+  for (int blk = 0; blk < ncblk; ++blk) {
+  const int cb0 = blk * ncb;
+  load_wblock(0, cb0);
 
   // ---- stage the summed / masked input patch of every image ----------------
-  const int n_src = a.gather ? 1 : __builtin_popcount(gr.in_mask);
-  const FastDiv div_ncb(ncb), div_pw(PW), div_pimg(pimg);
   for (int i = tid; i < total; i += 256) {
     uint32_t im, r, pix, cbu, pr, pc;
     div_pimg.divmod((uint32_t)i, im, r);
     div_ncb.divmod(r, pix, cbu);
     div_pw.divmod(pix, pr, pc);
-    const int cb = (int)cbu, b = b0 + (int)im;
+    const int cb = cb0 + (int)cbu, b = b0 + (int)im;
     const int hh = h0 - ph + (int)pr, ww = (int)pc - pw;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     uint4 v = make_uint4(0, 0, 0, 0);
     bool raw = false;                                   // prec 0 single source: v holds the bf16 chunk as is
-    if (b < a.B && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W) {
+    if (b < a.B && hh >= 0 && hh < a.H && ww >= 0 && ww < a.W && cb < ncb_all) {
       const long off = ((long)hh * a.W + ww) * a.Cinp + cb * 8;
       const long ioff = ((long)g * a.B + b) * img;
       const AT* msrc = a.mask ? static_cast<const AT*>(a.mask) + ioff : nullptr;
@@ -153,8 +201,9 @@ conv_fwd_kernel(ConvArgs a) {
       const int im = i / per, q = i - im * per;
       const int cb = q % ncb, pix = q / ncb;
       const int r = pix / a.W, cc = pix % a.W;
-      if (b0 + im < a.B && h0 + r < a.H) {
-        AT* xo = static_cast<AT*>(a.xsum) + ((long)g * a.B + b0 + im) * img + (long)h0 * a.W * a.Cinp + (long)q * 8;
+      if (b0 + im < a.B && h0 + r < a.H && cb0 + cb < ncb_all) {
+        AT* xo = static_cast<AT*>(a.xsum) + ((long)g * a.B + b0 + im) * img +
+                 (((long)h0 * a.W + pix) * ncb_all + cb0 + cb) * 8;
         const int pi = im * pimg + ((r + ph) * PW + cc + pw) * ncb + cb;
         if (PREC) {
           float f[8];
@@ -166,49 +215,13 @@ conv_fwd_kernel(ConvArgs a) {
       }
     }
   }
-  {
-    const FastDiv div_kw(a.KW);
-    for (int c = tid; c < nchunks + 4; c += 256) {
-      if (c < nchunks) {
-        uint32_t kk, cb, kh, kw;
-        div_ncb.divmod((uint32_t)c, kk, cb);
-        div_kw.divmod(kk, kh, kw);
-        coff[c] = ((int)kh * PW + (int)kw) * ncb + (int)cb;
-      } else {
-        coff[c] = -1;
-      }
-    }
-  }
   store_wblock(0);
   __syncthreads();
 
   // ---- MFMA main loop: each wave = 16*PXG pixels x all co tiles --------------
-  const int wave = tid >> 6, lane = tid & 63;
-  const int kq = lane >> 4, l16 = lane & 15;
-  const int ipx = THr * a.W;                            // tile pixels per image
-  int pbase[PXG];
-  bool pvalid[PXG];
-  int pyy[PXG], pxx[PXG], pim[PXG];
-#pragma unroll
-  for (int h = 0; h < PXG; ++h) {
-    const int pl = wave * 16 * PXG + h * 16 + l16;
-    pim[h] = pl / ipx;
-    const int pp = pl - pim[h] * ipx;
-    pyy[h] = pp / a.W; pxx[h] = pp % a.W;
-    pvalid[h] = (pl < NI * ipx) && (h0 + pyy[h] < a.H) && (b0 + pim[h] < a.B);
-    pbase[h] = pim[h] * pimg + (pyy[h] * PW + pxx[h]) * ncb;
-  }
-  const int nco = min(64, a.Coutp - co_blk);
-  const int NT = (nco + 15) >> 4;
-  f32x4_t acc[PXG][4];
-#pragma unroll
-  for (int h = 0; h < PXG; ++h)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[h][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
   for (int kb = 0; kb < nkb; ++kb) {
     const bool more = kb + 1 < nkb;
-    if (more) load_wblock(kb + 1);
+    if (more) load_wblock(kb + 1, cb0);
     const uint16_t* wcur = wbuf + (kb & 1) * wrows * CF_WLD;
 #pragma unroll
     for (int kk = 0; kk < CF_KB / 4; ++kk) {
@@ -236,6 +249,7 @@ conv_fwd_kernel(ConvArgs a) {
     if (more) store_wblock((kb + 1) & 1);
     __syncthreads();
   }
+  }  // channel blocks
 
   // ---- epilogue: bias + relu, 4 channels per lane ---------------------------
 #pragma unroll
@@ -651,13 +665,28 @@ static int conv_fwd_generic(const ConvArgs* a, hipStream_t stream) {
     while (ni > 1 && lds_of(ni, a->H) > 160 * 1024) --ni;
   }
   ConvArgs t = *a;
-  // fp32 planes triple the patch: shrink the row band until it fits
-  while (ni == 1 && lds_of(1, t.TH) > 160 * 1024 && t.TH > 1) t.TH = (t.TH + 1) / 2;
-  if (lds_of(ni, t.TH) > 160 * 1024) return -3;
+  t.cbb = 0;
+  // fp32 planes triple the patch: shrink the row band to >= 128-pixel tiles,
+  // then stage the input channels block by block
+  while (ni == 1 && lds_of(1, t.TH) > 160 * 1024 && t.TH > 1 && (t.TH / 2) * a->W >= 128) t.TH = (t.TH + 1) / 2;
+  if (lds_of(ni, t.TH) > 160 * 1024) {
+    ni = 1;
+    t.TH = a->TH;
+    const int ncb = a->Cinp / 8;
+    for (int cbb : {16, 8, 4, 2, 1}) {
+      if (cbb >= ncb) continue;
+      const size_t w = (size_t)NPL * 2 * wrows * CF_WLD * 2;
+      const size_t p = (size_t)NPL * (t.TH + a->KH - 1) * (a->W + a->KW - 1) * cbb * 16;
+      if (w + p + 4 * ((size_t)a->KH * a->KW * cbb + 4) <= 160 * 1024) { t.cbb = cbb; break; }
+    }
+    if (!t.cbb) return -3;
+  }
   if (ni > 1) t.TH = ni * a->H;                      // kernel: TH > H = ni whole images per tile
   const int nth = ni > 1 ? 1 : (a->H + t.TH - 1) / t.TH;
   const int tile = ni > 1 ? ni * a->H * a->W : t.TH * a->W;
-  const size_t lds = lds_of(ni, ni > 1 ? a->H : t.TH);
+  size_t lds = lds_of(ni, ni > 1 ? a->H : t.TH);
+  if (t.cbb) lds = (size_t)NPL * (2 * wrows * CF_WLD * 2 + (size_t)(t.TH + a->KH - 1) * (a->W + a->KW - 1) * t.cbb * 16) +
+                   4 * ((size_t)a->KH * a->KW * t.cbb + 4);
   dim3 grid(((a->B + ni - 1) / ni) * nth, a->ngroups, (a->Coutp + 63) / 64);
   if (tile > 128) {
     set_lds_limit(conv_fwd_kernel<4, PREC>, lds);

@@ -35,7 +35,8 @@ class ConvArgs(C.Structure):
                 ("out_mask", P * MAXSLOT), ("w", P), ("bias", P), ("gtab", P),
                 ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
-                ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long)]
+                ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long),
+                ("cbb", I)]
 
 
 class WgradArgs(C.Structure):
