@@ -193,6 +193,10 @@ Tree build_tree(const Quantized& q, const std::vector<GH>& gh, std::vector<int>&
     feats.resize(k);
     std::sort(feats.begin(), feats.end());
   }
+  // colsample_bylevel: one draw keys the level streams (level d shuffles with
+  // its own stream), so the tree stream's draw count does not depend on how
+  // deep the tree grows -- the GPU engine precomputes every level's features
+  const uint64_t level_key = p.colsample_bylevel < 1.0 ? rng.next() : 0ull;
   struct Work { int node; int begin, end; std::vector<GH> hist; double G, H; };
   auto build_hist = [&](int b, int e, std::vector<GH>& hist) {
     hist.assign((size_t)F * kMaxBin, GH{0.0, 0.0});
@@ -221,7 +225,8 @@ Tree build_tree(const Quantized& q, const std::vector<GH>& gh, std::vector<int>&
     if (p.colsample_bylevel < 1.0 && (int)lfeats.size() > 1) {
       int m = (int)lfeats.size();
       int k = std::max(1, (int)std::floor(p.colsample_bylevel * m + 1e-9));
-      for (int i = 0; i < m; ++i) std::swap(lfeats[i], lfeats[i + (int)(rng.next() % (uint64_t)(m - i))]);
+      Rng lrng(splitmix(level_key ^ splitmix((uint64_t)depth + 1)));
+      for (int i = 0; i < m; ++i) std::swap(lfeats[i], lfeats[i + (int)(lrng.next() % (uint64_t)(m - i))]);
       lfeats.resize(k);
     }
     for (Work& w : level) {
@@ -400,8 +405,12 @@ int gbdt_cv(const float* X, int n, int F, const float* y, const int* fold_of, in
 
   auto round_fold = [&](int k, int round) {
     FoldState& fs = folds[k];
-    Rng rng(splitmix(seed ^ splitmix((uint64_t)k * 1000003ull + (uint64_t)round * 7919ull + 17)));
+    const uint64_t fold_round = splitmix(seed ^ splitmix((uint64_t)k * 1000003ull + (uint64_t)round * 7919ull + 17));
     for (int c = 0; c < K; ++c) {
+      // one stream per tree (class c of fold k, round): a fixed number of draws
+      // per tree (row key, colsample_bytree, level key), so the GPU engine
+      // (csrc/hip/gbdt_hist.hip) derives every tree's draws up front
+      Rng rng(c == 0 ? fold_round : splitmix(fold_round ^ splitmix((uint64_t)c * 0x51ED27ull + 3)));
       std::vector<GH> gh(n, GH{0.0, 0.0});
       for (int i : fs.train) {
         const double* m = &fs.margin[(size_t)i * K];

@@ -1,28 +1,48 @@
-// GBDT on MI355X: histogram / split / partition / predict kernels plus the
-// host driver that runs xgboost-style k-fold CV with them (SURVEY.md §2.4
-// G2-G8; reference call site gentun/models/xgboost_models.py:32-36).
+// GBDT on MI355X: xgboost-style k-fold CV with every fold's trees built
+// TOGETHER and every tree level decided ON THE DEVICE (SURVEY.md §2.4 G2-G8;
+// reference call site gentun/models/xgboost_models.py:32-36).
 //
-// Layout: ROW-major uint8 bins [n][Fs] (Fs = F rounded up to 4), so one row's
-// bins are a contiguous 32-byte run per 32-feature block. Each tree level keeps
-// the active rows grouped by node in an index list (one contiguous segment per
-// node, partitioned level by level), which gives the gpu_hist structure:
-//   * histograms are built only for the SMALLER child of every split (its own
-//     rows, gathered through the index list); the sibling is parent - built
-//     (subtraction trick), so a level touches <= n/2 rows, not n per 16 nodes;
-//   * a histogram workgroup = one row chunk of one node x 32 features: 8 lanes
-//     read a row's 32 bins as 4-byte words, LDS float atomics into a
-//     [32][257] float2 histogram (+1 float2 pad per feature spreads the banks),
-//     then one global float atomic per non-zero entry (Guideline 12);
-//   * the partition is one pass: left rows fill the parent's segment from its
-//     start, right rows from its end (workgroup ballot scans + one cursor
-//     atomic per wave side), so child segments need no count pre-pass.
-// Split search: one wave per (node, feature) scans the 256-bin prefix sums with
-// xgboost's CalcGain (lambda, alpha L1 soft-threshold, max_delta_step,
-// min_child_weight); a per-node reduction picks the best feature on the device
-// and the host only applies gamma pruning and lays out the next level.
-// Histogram float atomics make the last bits order-dependent (like xgboost's
-// gpu_hist); the CPU engine (csrc/gbdt/engine.cpp) is the bit-reproducible
-// reference.
+// Fold batching: the nfold boosters of a CV run advance in lock step; every
+// launch covers all folds (grid z / y = fold), so one level of one round is a
+// fixed sequence of ~8 launches whatever nfold is, and the launches are nfold
+// times larger (fills 256 CUs at small n).
+//
+// Device-resident level loop: the level structure of a depth-D tree is static
+// (level d has at most 2^d nodes, heap-indexed), so every grid is a host-known
+// upper bound and the device decides which nodes exist. Per level:
+//   hist      : histograms of the "built" nodes (the root; then the smaller
+//               child of every split) over their row segments, chunk lists
+//               written by the previous level's plan kernel (blocks past the
+//               fold's chunk count exit at once);
+//   reduce    : multi-chunk nodes: exact sum of their partial slots;
+//   subtract  : the sibling of every built node = parent - built (exact);
+//   split     : one wave per (node, feature): 256-bin prefix scan, xgboost's
+//               CalcGain (lambda, alpha L1 soft threshold, max_delta_step,
+//               min_child_weight) in fp64; best: per-node argmax;
+//   plan      : leaf weight (eta), gamma pruning, the split table, the tree
+//               arrays, the children's totals;
+//   partition : one pass over the level's row positions: left rows fill the
+//               parent's segment from its start, right rows from its end
+//               (wave-uniform ballot + one cursor atomic per side; per-lane
+//               atomics at segment boundaries);
+//   plan_next : children's segments, which child is built (the smaller, the
+//               CPU engine's rule), the next level's chunk / reduction lists.
+// No host round trip inside a round: the only blocking copy per round is the
+// metric read-back that early stopping needs. The per-tree random draws
+// (row-subsample key, colsample_bytree / _bylevel feature orders) do not
+// depend on the data, so the host derives them up front (same streams as the
+// CPU engine, csrc/gbdt/engine.cpp round_fold / build_tree) and uploads them
+// with one asynchronous copy per round.
+//
+// Histograms are fixed point: every row's (g, h) is scaled by a power of two
+// chosen from the fold's max |g|, |h| and the row count (no overflow for any
+// node) and summed with 64-bit integer LDS atomics. Sums, the subtraction
+// trick and the partial-slot reduction are exact and order independent, and
+// the split search reads the exact integers into fp64: the GPU run is bitwise
+// reproducible and follows the CPU engine (fp64 sums) to rounding level.
+//
+// Layout: ROW-major uint8 bins [n][Fs] (Fs = F rounded up to 4): a histogram
+// lane reads 4 features of a row as one 4-byte word.
 
 #include <hip/hip_runtime.h>
 
@@ -41,115 +61,189 @@
 #define GB_BINS 256
 #define HB_F 16          // features per histogram workgroup
 #define HB_STRIDE 514    // int64 per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
+#define HB_T 512
+#define HB_U 4
+#define GB_R 4096        // rows per histogram chunk
+#define GB_MAXD 12       // deepest supported tree
 
 namespace {
+typedef long long i64;
+typedef unsigned long long u64;
+
 struct DevParams {
-  float min_child_weight, lambda, alpha, max_delta_step;
+  double min_child_weight, lambda, alpha, max_delta_step, eta, gamma;
 };
 
-__device__ __forceinline__ float thr_l1(float g, float a) { return g > a ? g - a : (g < -a ? g + a : 0.f); }
+__device__ __forceinline__ double thr_l1(double g, double a) { return g > a ? g - a : (g < -a ? g + a : 0.0); }
 
-__device__ __forceinline__ float dev_weight(const DevParams& p, float G, float H) {
-  if (H < p.min_child_weight || H <= 0.f) return 0.f;
-  float w = -thr_l1(G, p.alpha) / (H + p.lambda);
-  if (p.max_delta_step != 0.f && fabsf(w) > p.max_delta_step) w = copysignf(p.max_delta_step, w);
+__device__ __forceinline__ double dev_weight(const DevParams& p, double G, double H) {
+  if (H < p.min_child_weight || H <= 0.0) return 0.0;
+  double w = -thr_l1(G, p.alpha) / (H + p.lambda);
+  if (p.max_delta_step != 0.0 && fabs(w) > p.max_delta_step) w = copysign(p.max_delta_step, w);
   return w;
 }
 
-__device__ __forceinline__ float dev_gain(const DevParams& p, float G, float H) {
-  if (H < p.min_child_weight || H <= 0.f) return 0.f;
-  if (p.max_delta_step == 0.f) {
-    const float t = thr_l1(G, p.alpha);
+__device__ __forceinline__ double dev_gain(const DevParams& p, double G, double H) {
+  if (H < p.min_child_weight || H <= 0.0) return 0.0;
+  if (p.max_delta_step == 0.0) {
+    const double t = thr_l1(G, p.alpha);
     return t * t / (H + p.lambda);
   }
-  const float w = dev_weight(p, G, H);
-  const float r = -(2.f * G * w + (H + p.lambda) * w * w);
-  return p.alpha == 0.f ? r : r + p.alpha * fabsf(w);
+  const double w = dev_weight(p, G, H);
+  const double r = -(2.0 * G * w + (H + p.lambda) * w * w);
+  return p.alpha == 0.0 ? r : r + p.alpha * fabs(w);
 }
 
-// ---- G2: gradients (all rows; only indexed rows are ever read) -------------
-// obj 0 squared error, 1 reg:logistic, 2 binary:logistic (scale_pos_weight)
-__global__ void grad_kernel(const float* __restrict__ margin, const float* __restrict__ y,
-                            float2* __restrict__ gh, int n, int obj, float spw) {
+// one node of a level (per fold): row segment [start, start + count) in the
+// level's row list; exact fixed-point totals; built = histogram from rows
+// (else parent - sibling). Segments of a level are ordered by node index and
+// (start + count) is non-decreasing: nodes that do not exist have count 0.
+struct LNode {
+  int start, count;
+  i64 G, H;
+  int exists, built, parent, pad;
+};
+struct Chunk { int node, start, count, slot; };      // slot -1: one chunk, written in place
+struct Red { int node, first, nslots, pad; };
+struct SplitOut { double gain; i64 GL, HL; int bin, order; };
+struct NodeBest { double gain; i64 GL, HL; int feature, bin; };
+
+// geometry of one CV call (kernel argument)
+struct Geo {
+  int n, F, Fs, nfold, K, max_depth;
+  int Lmax;      // nodes of the deepest level (2^max_depth)
+  int Lh;        // nodes with a histogram per level (2^(max_depth-1), >= 1)
+  int maxch;     // chunk records per fold
+  int maxslot;   // partial histogram slots per fold
+  int lg_n;
+};
+
+// ---- G2: gradients of every fold (all rows; only indexed rows are read) ----
+// obj 0 squared error, 1 reg:logistic, 2 binary:logistic (scale_pos_weight), 3 multi (class c of K)
+__global__ void grad_kernel(const float* __restrict__ margin, const float* __restrict__ y, float2* __restrict__ gh,
+                            int n, int K, int c, int obj, float spw) {
+  const int k = blockIdx.y;
+  const float* mk = margin + (size_t)k * n * K;
+  float2* gk = gh + (size_t)k * n;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     float g, h;
-    if (obj == 0) { g = margin[i] - y[i]; h = 1.f; }
-    else {
-      const float p = 1.f / (1.f + expf(-margin[i]));
+    if (obj == 0) {
+      g = mk[i] - y[i]; h = 1.f;
+    } else if (obj == 3) {
+      const float* m = mk + (size_t)i * K;
+      float mx = m[0];
+      for (int q = 1; q < K; ++q) mx = fmaxf(mx, m[q]);
+      float z = 0.f;
+      for (int q = 0; q < K; ++q) z += expf(m[q] - mx);
+      const float p = expf(m[c] - mx) / z;
+      g = p - ((int)y[i] == c ? 1.f : 0.f); h = fmaxf(2.f * p * (1.f - p), 1e-16f);
+    } else {
+      const float p = 1.f / (1.f + expf(-mk[i]));
       g = p - y[i]; h = fmaxf(p * (1.f - p), 1e-16f);
       if (obj == 2 && y[i] > 0.5f) { g *= spw; h *= spw; }
     }
-    gh[i] = make_float2(g, h);
+    gk[i] = make_float2(g, h);
   }
 }
 
-// multi:softmax / multi:softprob, class c of K: softmax over the row's K
-// margins (engine.cpp: g = p_c - [y == c], h = max(2 p_c (1 - p_c), 1e-16))
-__global__ void grad_multi_kernel(const float* __restrict__ margin, const float* __restrict__ y,
-                                  float2* __restrict__ gh, int n, int K, int c) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float* m = margin + (size_t)i * K;
-    float mx = m[0];
-    for (int k = 1; k < K; ++k) mx = fmaxf(mx, m[k]);
-    float z = 0.f;
-    for (int k = 0; k < K; ++k) z += expf(m[k] - mx);
-    const float p = expf(m[c] - mx) / z;
-    gh[i] = make_float2(p - ((int)y[i] == c ? 1.f : 0.f), fmaxf(2.f * p * (1.f - p), 1e-16f));
-  }
-}
-
-// ---- G3: histograms -----------------------------------------------------------
-// Fixed-point LDS accumulation: LDS float atomics measured 7x slower than the
-// same loop with plain adds (profiles/gbdt_probe_depth6_10.log), so every
-// row's (g, h) is scaled by a power of two chosen from the tree's max |g|,
-// |h| and the row count (no overflow for any node) and summed with 64-bit
-// integer LDS atomics: exact, order-independent sums -> the histograms (and
-// with the fixed-order partial reduction, the whole GPU boosting run) are
-// bitwise reproducible, unlike float atomics.
-
-// max |g|, max |h| over all rows (bit patterns of non-negative floats order as ints)
+// max |g|, max |h| per fold (bit patterns of non-negative floats order as ints)
 __global__ void gh_max_kernel(const float2* __restrict__ gh, int n, unsigned int* __restrict__ mx) {
+  const int k = blockIdx.y;
+  const float2* gk = gh + (size_t)k * n;
   unsigned int mg = 0, mh = 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float2 v = gh[i];
+    const float2 v = gk[i];
     mg = max(mg, __float_as_uint(fabsf(v.x)));
     mh = max(mh, __float_as_uint(fabsf(v.y)));
   }
   for (int o = 32; o > 0; o >>= 1) { mg = max(mg, __shfl_xor(mg, o)); mh = max(mh, __shfl_xor(mh, o)); }
-  if ((threadIdx.x & 63) == 0) { atomicMax(&mx[0], mg); atomicMax(&mx[1], mh); }
+  if ((threadIdx.x & 63) == 0) { atomicMax(&mx[2 * k], mg); atomicMax(&mx[2 * k + 1], mh); }
 }
 
-// scale exponent: max * 2^se * n < 2^62
+// fixed-point exponent: max * 2^se * n < 2^62
 __device__ __forceinline__ int fx_exp(unsigned int maxbits, int lg_n) {
   int e = 0;
   (void)frexpf(__uint_as_float(maxbits), &e);          // max < 2^e
   return min(100, 61 - e - lg_n);
 }
 
-// grid (chunks, feature blocks of HB_F), HB_T threads = HB_T/4 row lanes x 4 word
-// lanes (16 features = 4 x 4 bin bytes per row); each lane keeps HB_U rows' loads in flight
-#define HB_T 512
-#define HB_U 4
-__global__ void __launch_bounds__(HB_T) hist_kernel(const uint8_t* __restrict__ bins, int Fs, int F,
+// root rows of fold k: rows of the other folds, Bernoulli(subsample) by the
+// counter-based hash of the CPU engine (engine.cpp row_uniform) keyed by one
+// draw of the tree's stream; unordered compaction (ballot + one atomic per wave)
+__global__ void __launch_bounds__(256) root_rows_kernel(const int* __restrict__ fold_of, int n,
+                                                        const u64* __restrict__ keys, double subsample,
+                                                        int* __restrict__ rows, int* __restrict__ counts) {
+  const int k = blockIdx.y, lane = threadIdx.x & 63;
+  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const u64 key = keys[k];
+  int* rk = rows + (size_t)k * n;
+  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const int i = base + threadIdx.x;
+    bool keep = i < n && fold_of[i] != k;
+    if (keep && subsample < 1.0) {
+      u64 x = (u64)i + 0x9E3779B97F4A7C15ull;
+      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
+      x = (key ^ x) + 0x9E3779B97F4A7C15ull;
+      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
+      keep = (double)(x >> 11) * (1.0 / 9007199254740992.0) < subsample;
+    }
+    const u64 m = __ballot(keep);
+    int b0 = 0;
+    if (lane == 0 && m) b0 = atomicAdd(&counts[k], __popcll(m));
+    b0 = __shfl(b0, 0);
+    if (keep) rk[b0 + __popcll(m & below)] = i;
+  }
+}
+
+// chunk records of one built node (thread-serial; plan kernels)
+__device__ void emit_node(Chunk* ch, Red* rd, int& nch, int& nrd, int& nslot, int node, int start, int count) {
+  if (count <= GB_R) {
+    ch[nch++] = Chunk{node, start, count, -1};
+    return;
+  }
+  const int first = nslot;
+  for (int o = 0; o < count; o += GB_R) ch[nch++] = Chunk{node, start + o, min(GB_R, count - o), nslot++};
+  rd[nrd++] = Red{node, first, nslot - first, 0};
+}
+
+// level 0 of every fold: the root over all its rows
+__global__ void level0_kernel(Geo geo, const int* __restrict__ nroot, LNode* __restrict__ cur,
+                              Chunk* __restrict__ chunks, Red* __restrict__ reds, int* __restrict__ counts) {
+  const int k = blockIdx.x;
+  if (threadIdx.x != 0) return;
+  LNode r;
+  r.start = 0; r.count = nroot[k]; r.G = 0; r.H = 0; r.exists = 1; r.built = 1; r.parent = -1; r.pad = 0;
+  cur[(size_t)k * geo.Lmax] = r;
+  int nch = 0, nrd = 0, nslot = 0;
+  emit_node(chunks + (size_t)k * geo.maxch, reds + (size_t)k * geo.maxch, nch, nrd, nslot, 0, 0, r.count);
+  counts[2 * k] = nch;
+  counts[2 * k + 1] = nrd;
+}
+
+// ---- G3: histograms (grid: chunks x feature blocks x folds) -----------------
+__global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __restrict__ bins,
                                                     const int* __restrict__ rows, const float2* __restrict__ gh,
-                                                    const int4* __restrict__ chunks, float2* __restrict__ hist,
-                                                    unsigned long long* __restrict__ hist_part,
-                                                    const unsigned int* __restrict__ mx, int lg_n) {
-  __shared__ unsigned long long lh[HB_F * HB_STRIDE];
-  const int4 c = chunks[blockIdx.x];
+                                                    const Chunk* __restrict__ chunks, const int* __restrict__ counts,
+                                                    i64* __restrict__ hist, i64* __restrict__ part,
+                                                    const unsigned int* __restrict__ mx) {
+  const int k = blockIdx.z;
+  if ((int)blockIdx.x >= counts[2 * k]) return;
+  __shared__ u64 lh[HB_F * HB_STRIDE];
+  const Chunk c = chunks[(size_t)k * geo.maxch + blockIdx.x];
+  const int F = geo.F, Fs = geo.Fs;
   const int fb = blockIdx.y * HB_F, tid = threadIdx.x;
   constexpr int RL = HB_T / 4;                  // row lanes
   for (int i = tid; i < HB_F * HB_STRIDE; i += HB_T) lh[i] = 0ull;
-  const int seg = fx_exp(mx[0], lg_n), seh = fx_exp(mx[1], lg_n);
-  const float sg = ldexpf(1.f, seg), sh = ldexpf(1.f, seh);
+  const float sg = ldexpf(1.f, fx_exp(mx[2 * k], geo.lg_n)), sh = ldexpf(1.f, fx_exp(mx[2 * k + 1], geo.lg_n));
   __syncthreads();
   const int wl = tid & 3, rl = tid >> 2;
   const int f4 = fb + wl * 4;
+  const float2* gk = gh + (size_t)k * geo.n;
   if (f4 < F) {
-    const int* rp = rows + c.y;
-    unsigned long long* my = lh + wl * 4 * HB_STRIDE;
+    const int* rp = rows + (size_t)k * geo.n + c.start;
+    u64* my = lh + wl * 4 * HB_STRIDE;
     int i = rl;
-    for (; i + (HB_U - 1) * RL < c.z; i += HB_U * RL) {
+    for (; i + (HB_U - 1) * RL < c.count; i += HB_U * RL) {
       int r[HB_U];
       float2 g[HB_U];
       uint32_t w[HB_U];
@@ -157,261 +251,345 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(const uint8_t* __restrict__ 
       for (int u = 0; u < HB_U; ++u) r[u] = rp[i + RL * u];
 #pragma unroll
       for (int u = 0; u < HB_U; ++u) {
-        g[u] = gh[r[u]];
+        g[u] = gk[r[u]];
         w[u] = *reinterpret_cast<const uint32_t*>(bins + (size_t)r[u] * Fs + f4);
       }
 #pragma unroll
       for (int u = 0; u < HB_U; ++u) {
-        const unsigned long long qg = (unsigned long long)llrintf(g[u].x * sg);
-        const unsigned long long qh = (unsigned long long)llrintf(g[u].y * sh);
+        const u64 qg = (u64)llrintf(g[u].x * sg);
+        const u64 qh = (u64)llrintf(g[u].y * sh);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          unsigned long long* d = my + k * HB_STRIDE + 2 * ((w[u] >> (8 * k)) & 255u);
+        for (int q = 0; q < 4; ++q) {
+          u64* d = my + q * HB_STRIDE + 2 * ((w[u] >> (8 * q)) & 255u);
           atomicAdd(d, qg);
           atomicAdd(d + 1, qh);
         }
       }
     }
-    for (; i < c.z; i += RL) {
+    for (; i < c.count; i += RL) {
       const int r = rp[i];
-      const float2 g = gh[r];
+      const float2 g = gk[r];
       const uint32_t w = *reinterpret_cast<const uint32_t*>(bins + (size_t)r * Fs + f4);
-      const unsigned long long qg = (unsigned long long)llrintf(g.x * sg);
-      const unsigned long long qh = (unsigned long long)llrintf(g.y * sh);
+      const u64 qg = (u64)llrintf(g.x * sg);
+      const u64 qh = (u64)llrintf(g.y * sh);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        unsigned long long* d = my + k * HB_STRIDE + 2 * ((w >> (8 * k)) & 255u);
+      for (int q = 0; q < 4; ++q) {
+        u64* d = my + q * HB_STRIDE + 2 * ((w >> (8 * q)) & 255u);
         atomicAdd(d, qg);
         atomicAdd(d + 1, qh);
       }
     }
   }
   __syncthreads();
-  // flush with plain stores, no global atomics: a node that fits one chunk is
-  // written straight into its (float) histogram, otherwise its exact integer
-  // sums go to partial slot c.w (reduce_kernel adds a node's slots exactly,
-  // so the result does not depend on which rows a chunk got)
+  // exact integer sums: in place for a one-chunk node, else partial slot c.slot
   const int nf = min(HB_F, F - fb);
-  if (c.w < 0) {
-    float* dst = reinterpret_cast<float*>(hist + (size_t)c.x * F * GB_BINS) + (size_t)fb * 2 * GB_BINS;
-    const float ig = ldexpf(1.f, -seg), ih = ldexpf(1.f, -seh);
-    for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
-      const int fl = i >> 9, j = i & 511;
-      const long long v = (long long)lh[fl * HB_STRIDE + j];
-      dst[(size_t)fl * 2 * GB_BINS + j] = (float)v * ((j & 1) ? ih : ig);
-    }
-  } else {
-    unsigned long long* dst = hist_part + ((size_t)c.w * F + fb) * 2 * GB_BINS;
-    for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
-      const int fl = i >> 9, j = i & 511;
-      dst[(size_t)fl * 2 * GB_BINS + j] = lh[fl * HB_STRIDE + j];
-    }
+  i64* dst = c.slot < 0 ? hist + (((size_t)k * geo.Lh + c.node) * F + fb) * 2 * GB_BINS
+                        : part + (((size_t)k * geo.maxslot + c.slot) * F + fb) * 2 * GB_BINS;
+  for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
+    const int fl = i >> 9, j = i & 511;
+    dst[(size_t)fl * 2 * GB_BINS + j] = (i64)lh[fl * HB_STRIDE + j];
   }
 }
 
-// node histogram = sum of its partial slots; red = (node, first slot, slots)
-__global__ void __launch_bounds__(256) reduce_kernel(const unsigned long long* __restrict__ part,
-                                                     float* __restrict__ hist, const int4* __restrict__ red, int F,
-                                                     const unsigned int* __restrict__ mx, int lg_n) {
-  const int4 rd = red[blockIdx.x];
-  const size_t per = (size_t)F * 2 * GB_BINS;
-  const float ig = ldexpf(1.f, -fx_exp(mx[0], lg_n)), ih = ldexpf(1.f, -fx_exp(mx[1], lg_n));
+// node histogram = sum of its partial slots (grid: reductions x y x folds)
+__global__ void __launch_bounds__(256) reduce_kernel(Geo geo, const i64* __restrict__ part, i64* __restrict__ hist,
+                                                     const Red* __restrict__ reds, const int* __restrict__ counts) {
+  const int k = blockIdx.z;
+  if ((int)blockIdx.x >= counts[2 * k + 1]) return;
+  const Red rd = reds[(size_t)k * geo.maxch + blockIdx.x];
+  const size_t per = (size_t)geo.F * 2 * GB_BINS;
+  const i64* pk = part + (size_t)k * geo.maxslot * per;
+  i64* h = hist + ((size_t)k * geo.Lh + rd.node) * per;
   for (size_t e = threadIdx.x + (size_t)blockIdx.y * 256; e < per; e += (size_t)gridDim.y * 256) {
-    unsigned long long acc = 0;
-    for (int sl = 0; sl < rd.z; ++sl) acc += part[(size_t)(rd.y + sl) * per + e];
-    hist[(size_t)rd.x * per + e] = (float)(long long)acc * ((e & 1) ? ih : ig);
+    i64 acc = 0;
+    for (int sl = 0; sl < rd.nslots; ++sl) acc += pk[(size_t)(rd.first + sl) * per + e];
+    h[e] = acc;
   }
 }
 
-// root rows of fold k: rows of the other folds, Bernoulli(subsample) by a
-// counter-based hash keyed by one draw of the tree's stream (engine.cpp
-// row_uniform); unordered compaction (ballot + one counter atomic per wave)
-__global__ void __launch_bounds__(256) root_rows_kernel(const int* __restrict__ fold_of, int fold, int n,
-                                                        unsigned long long key, double subsample,
-                                                        int* __restrict__ rows, int* __restrict__ count) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-    const int i = base + threadIdx.x;
-    bool keep = i < n && fold_of[i] != fold;
-    if (keep && subsample < 1.0) {
-      unsigned long long x = (unsigned long long)i + 0x9E3779B97F4A7C15ull;
-      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
-      x = (key ^ x) + 0x9E3779B97F4A7C15ull;
-      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
-      keep = (double)(x >> 11) * (1.0 / 9007199254740992.0) < subsample;
-    }
-    const unsigned long long m = __ballot(keep);
-    int b0 = 0;
-    if (lane == 0 && m) b0 = atomicAdd(count, __popcll(m));
-    b0 = __shfl(b0, 0);
-    if (keep) rows[b0 + __popcll(m & below)] = i;
-  }
+// sibling = parent (previous level) - built child (grid: level nodes x y x folds)
+__global__ void __launch_bounds__(256) subtract_kernel(Geo geo, const LNode* __restrict__ cur,
+                                                       const i64* __restrict__ prev, i64* __restrict__ hist) {
+  const int k = blockIdx.z, j = blockIdx.x;
+  const LNode nd = cur[(size_t)k * geo.Lmax + j];
+  if (!nd.exists || nd.built) return;
+  const size_t per = (size_t)geo.F * 2 * GB_BINS;
+  const i64* P = prev + ((size_t)k * geo.Lh + nd.parent) * per;
+  const i64* B = hist + ((size_t)k * geo.Lh + (j ^ 1)) * per;
+  i64* O = hist + ((size_t)k * geo.Lh + j) * per;
+  for (size_t i = threadIdx.x + (size_t)blockIdx.y * 256; i < per; i += (size_t)gridDim.y * 256) O[i] = P[i] - B[i];
 }
 
-// sibling = parent (previous level) - built child; pairs (other, parent_prev, built)
-__global__ void __launch_bounds__(256) subtract_kernel(const float2* __restrict__ prev, float2* __restrict__ cur,
-                                                       const int4* __restrict__ pairs, int F) {
-  const int4 pr = pairs[blockIdx.x];
-  const size_t per = (size_t)F * GB_BINS;
-  const float2* P = prev + (size_t)pr.y * per;
-  const float2* B = cur + (size_t)pr.z * per;
-  float2* O = cur + (size_t)pr.x * per;
-  for (size_t i = threadIdx.x + (size_t)blockIdx.y * 256; i < per; i += (size_t)gridDim.y * 256) {
-    const float2 a = P[i], b = B[i];
-    O[i] = make_float2(a.x - b.x, a.y - b.y);
-  }
+// root totals: sum over the bins of feature 0 (exact)
+__global__ void root_totals_kernel(Geo geo, const i64* __restrict__ hist, LNode* __restrict__ cur) {
+  const int k = blockIdx.x, lane = threadIdx.x;
+  const i64* h = hist + (size_t)k * geo.Lh * geo.F * 2 * GB_BINS;
+  i64 g = 0, hh = 0;
+  for (int b = lane; b < GB_BINS; b += 64) { g += h[2 * b]; hh += h[2 * b + 1]; }
+  for (int o = 32; o > 0; o >>= 1) { g += __shfl_xor(g, o); hh += __shfl_xor(hh, o); }
+  if (lane == 0) { cur[(size_t)k * geo.Lmax].G = g; cur[(size_t)k * geo.Lmax].H = hh; }
 }
 
-// ---- G4: best split per (node, feature): one wave each -----------------------
-struct SplitOut { float gain; int bin; float GL, HL; };
+// the CPU engine's scan rule (build_tree): a candidate later in the scan
+// replaces an earlier one only if better by more than 1e-12
+__device__ __forceinline__ bool later_wins(double g_early, bool early_ok, double g_late, bool late_ok) {
+  if (!late_ok) return false;
+  if (!early_ok) return true;
+  return g_late > g_early + 1e-12;
+}
 
-__global__ void __launch_bounds__(64) split_kernel(const float2* __restrict__ hist, const int* __restrict__ nbins,
-                                                   const uint8_t* __restrict__ feat_ok, const float2* __restrict__ tot,
-                                                   SplitOut* __restrict__ out, int F, DevParams p) {
-  const int node = blockIdx.y, f = blockIdx.x, lane = threadIdx.x;
-  SplitOut best = {0.f, -1, 0.f, 0.f};
-  if (feat_ok[f]) {
-    const float2* h = hist + ((long)node * F + f) * GB_BINS;
-    // each lane owns 4 consecutive bins; wave prefix over lane sums
-    float2 v[4];
-    float sg = 0.f, sh = 0.f;
+// ---- G4: best split per (node, feature): one wave each (grid F x L x folds) --
+// order[(k * (D+1) + depth) * F + f] = position of f in the level's feature
+// scan (colsample_bytree / _bylevel), 0 = not sampled
+__global__ void __launch_bounds__(64) split_kernel(Geo geo, int depth, const i64* __restrict__ hist,
+                                                   const int* __restrict__ nbins, const int* __restrict__ order,
+                                                   const LNode* __restrict__ cur, const unsigned int* __restrict__ mx,
+                                                   SplitOut* __restrict__ out, DevParams p) {
+  const int f = blockIdx.x, j = blockIdx.y, k = blockIdx.z, lane = threadIdx.x, F = geo.F;
+  const LNode nd = cur[(size_t)k * geo.Lmax + j];
+  const int ord = order[((size_t)k * (geo.max_depth + 1) + depth) * F + f] - 1;
+  double bg = 0.0;
+  int bb = -1;
+  i64 bGL = 0, bHL = 0;
+  if (nd.exists && nd.count >= 2 && ord >= 0) {
+    const double ig = ldexp(1.0, -fx_exp(mx[2 * k], geo.lg_n)), ih = ldexp(1.0, -fx_exp(mx[2 * k + 1], geo.lg_n));
+    const i64* h = hist + (((size_t)k * geo.Lh + j) * F + f) * 2 * GB_BINS;
+    i64 vg[4], vh[4], sg = 0, sh = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { v[k] = h[lane * 4 + k]; sg += v[k].x; sh += v[k].y; }
-    float pg = sg, ph = sh;                       // inclusive scan across lanes
+    for (int q = 0; q < 4; ++q) { vg[q] = h[2 * (lane * 4 + q)]; vh[q] = h[2 * (lane * 4 + q) + 1]; sg += vg[q]; sh += vh[q]; }
+    i64 pg = sg, ph = sh;                       // inclusive scan across lanes (exact)
     for (int o = 1; o < 64; o <<= 1) {
-      const float tg = __shfl_up(pg, o), th = __shfl_up(ph, o);
+      const i64 tg = __shfl_up(pg, o), th = __shfl_up(ph, o);
       if (lane >= o) { pg += tg; ph += th; }
     }
-    float GL = pg - sg, HL = ph - sh;             // exclusive prefix
-    const float G = tot[node].x, H = tot[node].y;
-    const float parent = dev_gain(p, G, H);
+    i64 GLf = pg - sg, HLf = ph - sh;           // exclusive prefix
+    const double G = (double)nd.G * ig, H = (double)nd.H * ih;
+    const double parent = dev_gain(p, G, H);
     const int nb = nbins[f];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      GL += v[k].x; HL += v[k].y;
-      const int b = lane * 4 + k;
+    for (int q = 0; q < 4; ++q) {
+      GLf += vg[q]; HLf += vh[q];
+      const int b = lane * 4 + q;
       if (b + 1 >= nb) continue;
-      const float GR = G - GL, HR = H - HL;
-      if (HL < p.min_child_weight || HR < p.min_child_weight || HL <= 0.f || HR <= 0.f) continue;
-      const float chg = dev_gain(p, GL, HL) + dev_gain(p, GR, HR) - parent;
-      if (chg > best.gain) { best.gain = chg; best.bin = b; best.GL = GL; best.HL = HL; }
+      const double GL = (double)GLf * ig, HL = (double)HLf * ih;
+      const double GR = G - GL, HR = H - HL;
+      if (HL < p.min_child_weight || HR < p.min_child_weight || HL <= 0.0 || HR <= 0.0) continue;
+      const double chg = dev_gain(p, GL, HL) + dev_gain(p, GR, HR) - parent;
+      if (chg > bg + 1e-12 || (bb < 0 && chg > 1e-12)) { bg = chg; bb = b; bGL = GLf; bHL = HLf; }
     }
-    for (int o = 32; o > 0; o >>= 1) {           // argmax, ties -> lower bin
-      const float og = __shfl_xor(best.gain, o);
-      const int ob = __shfl_xor(best.bin, o);
-      const float oG = __shfl_xor(best.GL, o), oH = __shfl_xor(best.HL, o);
-      if (og > best.gain || (og == best.gain && ob >= 0 && (best.bin < 0 || ob < best.bin))) {
-        best.gain = og; best.bin = ob; best.GL = oG; best.HL = oH;
-      }
+    for (int o = 1; o < 64; o <<= 1) {          // combine lane groups in bin (scan) order
+      const double og = __shfl_xor(bg, o);
+      const int ob = __shfl_xor(bb, o);
+      const i64 oG = __shfl_xor(bGL, o), oH = __shfl_xor(bHL, o);
+      const bool partner_early = (lane & o) != 0;  // the partner holds the lower bins
+      const bool take = partner_early ? !later_wins(og, ob >= 0, bg, bb >= 0) && ob >= 0
+                                      : later_wins(bg, bb >= 0, og, ob >= 0);
+      if (take) { bg = og; bb = ob; bGL = oG; bHL = oH; }
     }
   }
-  if (lane == 0) out[(long)node * F + f] = best;
+  if (lane == 0) out[((size_t)k * geo.Lh + j) * F + f] = SplitOut{bg, bGL, bHL, bb, ord};
 }
 
-// per-node totals: sum of hist over bins of feature 0 (all features give the same sum)
-__global__ void totals_kernel(const float2* __restrict__ hist, float2* __restrict__ tot, int F) {
-  const int node = blockIdx.x, lane = threadIdx.x;
-  const float2* h = hist + (long)node * F * GB_BINS;
-  float g = 0.f, hh = 0.f;
-  for (int b = lane; b < GB_BINS; b += 64) { g += h[b].x; hh += h[b].y; }
-  for (int o = 32; o > 0; o >>= 1) { g += __shfl_xor(g, o); hh += __shfl_xor(hh, o); }
-  if (lane == 0) tot[node] = make_float2(g, hh);
-}
-
-// best feature per node: ties -> lower feature (the host scan order of the CPU engine)
-struct NodeBest { float gain; int bin; float GL, HL; int feature; int pad[3]; };
-
-__global__ void __launch_bounds__(256) best_kernel(const SplitOut* __restrict__ cand, NodeBest* __restrict__ out,
-                                                   int F) {
-  __shared__ float sg[256];
-  __shared__ int sf[256];
-  const int node = blockIdx.x, tid = threadIdx.x;
-  float bg = 0.f;
-  int bf = -1;
+// best feature per node, in the CPU engine's feature scan order (grid L x folds)
+__global__ void __launch_bounds__(256) best_kernel(Geo geo, const SplitOut* __restrict__ cand,
+                                                   NodeBest* __restrict__ out) {
+  __shared__ double sg[256];
+  __shared__ int so[256], sf[256];
+  const int j = blockIdx.x, k = blockIdx.y, tid = threadIdx.x, F = geo.F;
+  const SplitOut* c = cand + ((size_t)k * geo.Lh + j) * F;
+  // per thread: its features in scan order (sequential rule), then a tree over threads by order
+  double bg = 0.0;
+  int bo = -1, bf = -1;
   for (int f = tid; f < F; f += 256) {
-    const SplitOut& c = cand[(size_t)node * F + f];
-    if (c.bin >= 0 && c.gain > bg) { bg = c.gain; bf = f; }
+    const SplitOut s = c[f];
+    if (s.bin < 0 || s.order < 0) continue;
+    if (bf < 0 || (s.order < bo ? !(bg > s.gain + 1e-12) : s.gain > bg + 1e-12)) { bg = s.gain; bo = s.order; bf = f; }
   }
-  sg[tid] = bg; sf[tid] = bf;
+  sg[tid] = bg; so[tid] = bo; sf[tid] = bf;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) {
-      const float og = sg[tid + o];
-      const int of = sf[tid + o];
-      if (of >= 0 && (sf[tid] < 0 || og > sg[tid] || (og == sg[tid] && of < sf[tid]))) { sg[tid] = og; sf[tid] = of; }
+    if (tid < o && sf[tid + o] >= 0) {
+      const double og = sg[tid + o];
+      const int oo = so[tid + o];
+      bool take;
+      if (sf[tid] < 0) take = true;
+      else if (oo < so[tid]) take = !(sg[tid] > og + 1e-12);
+      else take = og > sg[tid] + 1e-12;
+      if (take) { sg[tid] = og; so[tid] = oo; sf[tid] = sf[tid + o]; }
     }
     __syncthreads();
   }
   if (tid == 0) {
-    NodeBest b = {0.f, -1, 0.f, 0.f, -1, {0, 0, 0}};
+    NodeBest b{0.0, 0, 0, -1, -1};
     if (sf[0] >= 0) {
-      const SplitOut& c = cand[(size_t)node * F + sf[0]];
-      b.gain = c.gain; b.bin = c.bin; b.GL = c.GL; b.HL = c.HL; b.feature = sf[0];
+      const SplitOut& s = c[sf[0]];
+      b = NodeBest{s.gain, s.GL, s.HL, sf[0], s.bin};
     }
-    out[node] = b;
+    out[(size_t)k * geo.Lh + j] = b;
   }
 }
 
-// ---- G5: partition ---------------------------------------------------------------
-// chunks of split nodes' rows: (node, first index, count); split[node] = (feature, bin);
-// cursors[node] = (next left slot, end of the right region); left grows up, right grows down
-__global__ void __launch_bounds__(256) partition_kernel(const uint8_t* __restrict__ bins, int Fs,
+// ---- plan: leaves, gamma pruning, split table, children totals (grid folds) --
+__global__ void __launch_bounds__(256) plan_split_kernel(Geo geo, int depth, const LNode* __restrict__ cur,
+                                                         const NodeBest* __restrict__ best,
+                                                         const unsigned int* __restrict__ mx, int2* __restrict__ tree,
+                                                         float* __restrict__ leaf, int2* __restrict__ splitv,
+                                                         int2* __restrict__ cursor, LNode* __restrict__ nxt,
+                                                         DevParams p) {
+  const int k = blockIdx.x, L = 1 << depth;
+  const int tsz = (2 << geo.max_depth) - 1;
+  const double ig = ldexp(1.0, -fx_exp(mx[2 * k], geo.lg_n)), ih = ldexp(1.0, -fx_exp(mx[2 * k + 1], geo.lg_n));
+  for (int j = threadIdx.x; j < L; j += blockDim.x) {
+    const LNode nd = cur[(size_t)k * geo.Lmax + j];
+    const int id = L - 1 + j;
+    bool split = false;
+    NodeBest b{0.0, 0, 0, -1, -1};
+    if (nd.exists) {
+      leaf[(size_t)k * tsz + id] = (float)(dev_weight(p, (double)nd.G * ig, (double)nd.H * ih) * p.eta);
+      tree[(size_t)k * tsz + id] = make_int2(-1, 0);
+      if (depth < geo.max_depth && nd.count >= 2) {
+        b = best[(size_t)k * geo.Lh + j];
+        split = b.feature >= 0 && b.bin >= 0 && b.gain >= p.gamma && b.gain > 1e-12;
+      }
+    }
+    splitv[(size_t)k * geo.Lmax + j] = split ? make_int2(b.feature, b.bin) : make_int2(-1, 0);
+    cursor[(size_t)k * geo.Lmax + j] = make_int2(nd.start, nd.start + nd.count);
+    if (split) tree[(size_t)k * tsz + id] = make_int2(b.feature, b.bin);
+    if (depth < geo.max_depth) {
+      const int end = nd.start + nd.count;
+      LNode l, r;
+      l.start = r.start = end; l.count = r.count = 0;
+      l.G = l.H = r.G = r.H = 0;
+      l.exists = r.exists = split ? 1 : 0;
+      l.built = r.built = 0;
+      l.parent = r.parent = j;
+      l.pad = r.pad = 0;
+      if (split) { l.G = b.GL; l.H = b.HL; r.G = nd.G - b.GL; r.H = nd.H - b.HL; }
+      nxt[(size_t)k * geo.Lmax + 2 * j] = l;
+      nxt[(size_t)k * geo.Lmax + 2 * j + 1] = r;
+    }
+  }
+}
+
+// ---- G5: partition of the level's row positions (grid: position blocks x folds)
+__global__ void __launch_bounds__(256) partition_kernel(Geo geo, int depth, const uint8_t* __restrict__ bins,
+                                                        const int* __restrict__ nroot, const LNode* __restrict__ cur,
+                                                        const int2* __restrict__ splitv,
                                                         const int* __restrict__ rows_in, int* __restrict__ rows_out,
-                                                        const int4* __restrict__ chunks,
-                                                        const int2* __restrict__ split, int2* __restrict__ cursors) {
-  __shared__ int wl_cnt[4], wr_cnt[4], wl_base[4], wr_base[4];
-  const int4 c = chunks[blockIdx.x];
-  const int2 sp = split[c.x];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int base = 0; base < c.z; base += 256) {
-    const int i = base + tid;
-    const bool valid = i < c.z;
-    const int r = valid ? rows_in[c.y + i] : 0;
-    const bool left = valid && bins[(size_t)r * Fs + sp.x] <= (uint8_t)sp.y;
-    const bool right = valid && !left;
-    const unsigned long long lm = __ballot(left), rm = __ballot(right);
-    if (lane == 0) { wl_cnt[wv] = __popcll(lm); wr_cnt[wv] = __popcll(rm); }
-    __syncthreads();
-    if (tid == 0) {
-      int tl = 0, tr = 0;
-      for (int w = 0; w < 4; ++w) { tl += wl_cnt[w]; tr += wr_cnt[w]; }
-      const int l0 = atomicAdd(&cursors[c.x].x, tl);
-      const int r0 = atomicSub(&cursors[c.x].y, tr) - tr;
-      int al = l0, ar = r0;
-      for (int w = 0; w < 4; ++w) { wl_base[w] = al; al += wl_cnt[w]; wr_base[w] = ar; ar += wr_cnt[w]; }
+                                                        int2* __restrict__ cursor) {
+  __shared__ int ends[1 << GB_MAXD];
+  const int k = blockIdx.y, L = 1 << depth, tid = threadIdx.x, lane = tid & 63;
+  const int p0 = blockIdx.x * 256;
+  if (p0 >= nroot[k]) return;
+  for (int j = tid; j < L; j += 256) {
+    const LNode nd = cur[(size_t)k * geo.Lmax + j];
+    ends[j] = nd.start + nd.count;
+  }
+  __syncthreads();
+  const int p = p0 + tid;
+  bool valid = p < nroot[k];
+  int j = -1;
+  if (valid) {                               // first node whose segment ends after p
+    int lo = 0, hi = L;
+    while (lo < hi) { const int mid = (lo + hi) >> 1; if (ends[mid] > p) hi = mid; else lo = mid + 1; }
+    j = lo;
+    valid = j < L && cur[(size_t)k * geo.Lmax + j].start <= p;
+  }
+  int2 sp = make_int2(-1, 0);
+  if (valid) sp = splitv[(size_t)k * geo.Lmax + j];
+  valid = valid && sp.x >= 0;
+  int r = 0;
+  bool left = false;
+  if (valid) {
+    r = rows_in[(size_t)k * geo.n + p];
+    left = bins[(size_t)r * geo.Fs + sp.x] <= (uint8_t)sp.y;
+  }
+  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const u64 vm = __ballot(valid);
+  if (!vm) return;
+  const int lead = __builtin_ctzll(vm);
+  const int j0 = __shfl(j, lead);
+  const bool uniform = __ballot(valid && j != j0) == 0ull;
+  int* out = rows_out + (size_t)k * geo.n;
+  if (uniform) {
+    const u64 lm = __ballot(valid && left), rm = __ballot(valid && !left);
+    int l0 = 0, r0 = 0;
+    if (lane == lead) {
+      int2* cu = cursor + (size_t)k * geo.Lmax + j0;
+      l0 = atomicAdd(&cu->x, __popcll(lm));
+      r0 = atomicSub(&cu->y, __popcll(rm)) - __popcll(rm);
     }
-    __syncthreads();
-    if (left) rows_out[wl_base[wv] + __popcll(lm & below)] = r;
-    if (right) rows_out[wr_base[wv] + __popcll(rm & below)] = r;
-    __syncthreads();
+    l0 = __shfl(l0, lead);
+    r0 = __shfl(r0, lead);
+    if (valid) out[left ? l0 + __popcll(lm & below) : r0 + __popcll(rm & below)] = r;
+  } else if (valid) {                        // segment boundary inside the wave
+    int2* cu = cursor + (size_t)k * geo.Lmax + j;
+    const int pos = left ? atomicAdd(&cu->x, 1) : atomicSub(&cu->y, 1) - 1;
+    out[pos] = r;
   }
 }
 
-// ---- G6: prediction update by tree traversal (all rows, train and test) -----
-__global__ void predict_kernel(const uint8_t* __restrict__ bins, int Fs, const int4* __restrict__ tree,
-                               const float* __restrict__ leaf, float* __restrict__ margin, int n, int K, int c) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    int k = 0;
-    int4 t = tree[0];
-    const uint8_t* row = bins + (size_t)i * Fs;
-    while (t.x >= 0) { k = (row[t.x] <= t.y) ? t.z : t.w; t = tree[k]; }
-    margin[(size_t)i * K + c] += leaf[k];
+// children segments, built flags, next level's chunk / reduction lists (grid folds)
+__global__ void __launch_bounds__(256) plan_next_kernel(Geo geo, int depth, const LNode* __restrict__ cur,
+                                                        const int2* __restrict__ splitv,
+                                                        const int2* __restrict__ cursor, LNode* __restrict__ nxt,
+                                                        Chunk* __restrict__ chunks, Red* __restrict__ reds,
+                                                        int* __restrict__ counts) {
+  const int k = blockIdx.x, L = 1 << depth;
+  for (int j = threadIdx.x; j < L; j += blockDim.x) {
+    if (splitv[(size_t)k * geo.Lmax + j].x < 0) continue;
+    const LNode nd = cur[(size_t)k * geo.Lmax + j];
+    const int lc = cursor[(size_t)k * geo.Lmax + j].x - nd.start;
+    LNode* l = nxt + (size_t)k * geo.Lmax + 2 * j;
+    LNode* r = l + 1;
+    l->start = nd.start; l->count = lc;
+    r->start = nd.start + lc; r->count = nd.count - lc;
+    l->built = lc <= nd.count - lc ? 1 : 0;     // smaller child (engine.cpp: left on ties)
+    r->built = 1 - l->built;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int nch = 0, nrd = 0, nslot = 0;
+  if (depth + 1 < geo.max_depth) {
+    Chunk* ch = chunks + (size_t)k * geo.maxch;
+    Red* rd = reds + (size_t)k * geo.maxch;
+    for (int j = 0; j < 2 * L; ++j) {
+      const LNode c = nxt[(size_t)k * geo.Lmax + j];
+      if (c.exists && c.built) emit_node(ch, rd, nch, nrd, nslot, j, c.start, c.count);
+    }
+  }
+  counts[2 * k] = nch;
+  counts[2 * k + 1] = nrd;
+}
+
+// ---- G6: prediction update by tree traversal (all rows of every fold) ------
+__global__ void predict_kernel(Geo geo, const uint8_t* __restrict__ bins, const int2* __restrict__ tree,
+                               const float* __restrict__ leaf, float* __restrict__ margin, int c) {
+  const int k = blockIdx.y, tsz = (2 << geo.max_depth) - 1;
+  const int2* tk = tree + (size_t)k * tsz;
+  const float* lk = leaf + (size_t)k * tsz;
+  float* mk = margin + (size_t)k * geo.n * geo.K;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < geo.n; i += gridDim.x * blockDim.x) {
+    const uint8_t* row = bins + (size_t)i * geo.Fs;
+    int id = 0;
+    int2 t = tk[0];
+    while (t.x >= 0) { id = (row[t.x] <= t.y) ? 2 * id + 1 : 2 * id + 2; t = tk[id]; }
+    mk[(size_t)i * geo.K + c] += lk[id];
   }
 }
 
-// ---- G8: metric partial sums over a fold's train / test rows -----------------
-// out[0..3] = (train sum, train count, test sum, test count); metric 0 rmse, 1 mae, 2 logloss, 3 error
-__global__ void metric_kernel(const float* __restrict__ margin, const float* __restrict__ y,
-                              const int* __restrict__ fold_of, int fold, int n, int metric, int objective, int K,
-                              double* __restrict__ out) {
-  // engine.cpp eval_metric: rmse/mae on sigmoid(margin) for reg:logistic / binary:logistic,
-  // logloss on sigmoid, error thresholds margin 0 for binary:logitraw, merror / mlogloss over K
+// ---- G8: metric partial sums over every fold's train / test rows -------------
+// out[(k * gridDim.x + block) * 4 + (train sum, train count, test sum, test count)];
+// metric 0 rmse, 1 mae, 2 logloss, 3 error, 5 merror, 6 mlogloss (engine.cpp eval_metric)
+__global__ void __launch_bounds__(256) metric_kernel(Geo geo, const float* __restrict__ margin,
+                                                     const float* __restrict__ y, const int* __restrict__ fold_of,
+                                                     int metric, int objective, double* __restrict__ out) {
   __shared__ double red[4][256];
+  const int k = blockIdx.y, K = geo.K;
+  const float* mk = margin + (size_t)k * geo.n * K;
   double s[4] = {0, 0, 0, 0};
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const float* m = margin + (size_t)i * K;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < geo.n; i += gridDim.x * blockDim.x) {
+    const float* m = mk + (size_t)i * K;
     const float sig = 1.f / (1.f + expf(-m[0]));
     float v;
     if (metric == 0 || metric == 1) {
@@ -425,35 +603,26 @@ __global__ void metric_kernel(const float* __restrict__ margin, const float* __r
       v = (pos != (y[i] > 0.5f)) ? 1.f : 0.f;
     } else {
       int arg = 0;
-      float mx = m[0];
-      for (int k = 1; k < K; ++k) if (m[k] > mx) { mx = m[k]; arg = k; }
+      float mxv = m[0];
+      for (int q = 1; q < K; ++q) if (m[q] > mxv) { mxv = m[q]; arg = q; }
       if (metric == 5) v = (arg != (int)y[i]) ? 1.f : 0.f;
       else {
         float z = 0.f;
-        for (int k = 0; k < K; ++k) z += expf(m[k] - mx);
-        v = -logf(fmaxf(1e-15f, expf(m[(int)y[i]] - mx) / z));
+        for (int q = 0; q < K; ++q) z += expf(m[q] - mxv);
+        v = -logf(fmaxf(1e-15f, expf(m[(int)y[i]] - mxv) / z));
       }
     }
-    const int k = (fold_of[i] == fold) ? 2 : 0;
-    s[k] += v; s[k + 1] += 1.0;
+    const int q = (fold_of[i] == k) ? 2 : 0;
+    s[q] += v; s[q + 1] += 1.0;
   }
-  for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = s[k];
+  for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = s[q];
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o)
-      for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+      for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x < 4) out[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];   // host sums in block order
-}
-
-inline double h_thr(double g, double a) { return g > a ? g - a : (g < -a ? g + a : 0.0); }
-inline double h_weight(const double* P, double G, double H) {
-  // P: eta, mcw, depth, gamma, mds, subsample, cbt, cbl, lambda, alpha, spw, base
-  if (H < P[1] || H <= 0.0) return 0.0;
-  double w = -h_thr(G, P[9]) / (H + P[8]);
-  if (P[4] != 0.0 && std::fabs(w) > P[4]) w = std::copysign(P[4], w);
-  return w;
+  if (threadIdx.x < 4) out[((size_t)k * gridDim.x + blockIdx.x) * 4 + threadIdx.x] = red[threadIdx.x][0];
 }
 
 uint64_t smix(uint64_t x) {
@@ -463,7 +632,7 @@ uint64_t smix(uint64_t x) {
   return x ^ (x >> 31);
 }
 
-#define HC(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) return -100 - (int)e_; } while (0)
+#define HC(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { rc = -100 - (int)e_; goto done; } } while (0)
 
 }  // namespace
 
@@ -481,129 +650,131 @@ extern "C" {
 // multi:softmax/softprob: one tree per class) and every metric but auc
 // (rmse, mae, logloss, error, merror, mlogloss; early stopping on the last).
 // bins_h may be null when gbdt_quantize_hip already left the dataset's bins
-// on the device under cache_key (returns -7 if they were evicted). bins: ROW-major [n][Fs] uint8 (Fs >= F,
-// Fs % 4 == 0), precomputed on the host. cache_key != 0 keeps the device copy
-// of the bins across calls for the same key (one dataset, many candidates).
+// on the device under cache_key (returns -7 if they were evicted). bins:
+// ROW-major [n][Fs] uint8 (Fs >= F, Fs % 4 == 0). cache_key != 0 keeps the
+// device copy of the bins across calls for the same key (one dataset, many
+// candidates).
 int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F, const float* y_h,
                 const int* fold_h, int nfold, const double* P, int objective, int num_class, const int* metrics,
                 int n_metrics, int num_boost_round, int early_stopping_rounds, unsigned long long seed,
                 long long cache_key, double* out_hist) {
-  if (objective < 0 || objective > 5 || n_metrics < 1 || Fs % 4 || Fs < F || n <= 0 || nfold <= 0) return -1;
+  if (objective < 0 || objective > 5 || n_metrics < 1 || Fs % 4 || Fs < F || n <= 0 || nfold <= 0 || F <= 0)
+    return -1;
   for (int mi = 0; mi < n_metrics; ++mi)
     if (metrics[mi] < 0 || metrics[mi] > 6 || metrics[mi] == 4) return -1;   // auc: CPU engine
   const bool multi = objective >= 4;
   const int K = multi ? std::max(2, num_class) : 1;
-  const int obj = objective == 0 ? 0 : (objective == 1 ? 1 : 2);
-  const int max_depth = std::max(0, std::min((int)P[2], 12));
+  const int obj = multi ? 3 : (objective == 0 ? 0 : (objective == 1 ? 1 : 2));
+  const int D = std::max(0, std::min((int)P[2], GB_MAXD));
   std::lock_guard<std::mutex> lock(gbdt_cache::mu);   // one GBDT call at a time per process (bins cache)
-  // ---- device buffers
-  const size_t nbytes = (size_t)n * Fs;
-  if (cache_key == 0 || cache_key != gbdt_cache::key || gbdt_cache::bytes != nbytes || gbdt_cache::bins == nullptr) {
-    if (bins_h == nullptr) return -7;      // device copy evicted: the caller quantises again
-    if (gbdt_cache::bins) (void)hipFree(gbdt_cache::bins);
-    gbdt_cache::bins = nullptr; gbdt_cache::key = 0; gbdt_cache::bytes = 0;
-    HC(hipMalloc(&gbdt_cache::bins, nbytes));
-    HC(hipMemcpy(gbdt_cache::bins, bins_h, nbytes, hipMemcpyHostToDevice));
-    gbdt_cache::key = cache_key; gbdt_cache::bytes = nbytes;
+  int rc = 0;
+  Geo geo;
+  geo.n = n; geo.F = F; geo.Fs = Fs; geo.nfold = nfold; geo.K = K; geo.max_depth = D;
+  geo.Lmax = 1 << D;
+  geo.Lh = 1 << std::max(0, D - 1);
+  const int rchunks = (n + GB_R - 1) / GB_R;
+  geo.maxch = rchunks + geo.Lh + 2;
+  geo.maxslot = 2 * rchunks + 2;
+  geo.lg_n = 0;
+  while ((1ll << geo.lg_n) < (long long)n + 1) ++geo.lg_n;
+  const int tsz = (2 << D) - 1;
+  const size_t per_node = (size_t)F * 2 * GB_BINS;      // int64 per histogram node
+  DevParams dp{P[1], P[8], P[9], P[4], P[0], P[3]};
+  const int blocks = std::min(2048, (n + 255) / 256);
+  const int pblocks = (n + 255) / 256;
+  const int mblocks = std::min(blocks, 256);
+  const int nfb = (F + HB_F - 1) / HB_F;
+  const int ylen = std::max(1, (int)(per_node / 4096));
+  // device buffers
+  float *d_y = nullptr, *d_margin = nullptr, *d_leaf = nullptr;
+  int *d_fold = nullptr, *d_nb = nullptr, *d_rows[2] = {nullptr, nullptr}, *d_order = nullptr, *d_counts = nullptr,
+      *d_nroot = nullptr;
+  float2* d_gh = nullptr;
+  i64 *d_hist[2] = {nullptr, nullptr}, *d_part = nullptr;
+  LNode* d_lvl[2] = {nullptr, nullptr};
+  Chunk* d_chunks = nullptr;
+  Red* d_reds = nullptr;
+  SplitOut* d_cand = nullptr;
+  NodeBest* d_best = nullptr;
+  int2 *d_tree = nullptr, *d_split = nullptr, *d_cur = nullptr;
+  unsigned int* d_mx = nullptr;
+  u64* d_keys = nullptr;
+  double* d_met = nullptr;
+  void* h_up = nullptr;           // pinned upload block: keys [K][nfold] u64, orders [K][nfold][D+1][F] int
+  double* h_met = nullptr;        // pinned metric read-back
+  const size_t keys_bytes = sizeof(u64) * K * nfold;
+  const size_t order_elems = (size_t)nfold * (D + 1) * F;
+  const size_t up_bytes = keys_bytes + sizeof(int) * K * order_elems;
+  const size_t met_elems = (size_t)n_metrics * nfold * mblocks * 4;
+  const uint8_t* d_bins = nullptr;
+  double base = P[11];
+  const bool lower_better = true;
+  double best_score = INFINITY;
+  int best_round = 0, rounds_done = 0;
+  static const bool timing = std::getenv("GENTUN_GBDT_TIMING") != nullptr;
+  static const int progress = std::getenv("GENTUN_GBDT_PROGRESS") ? std::atoi(std::getenv("GENTUN_GBDT_PROGRESS")) : 0;
+  const auto t_start = std::chrono::steady_clock::now();
+
+  {
+    const size_t nbytes = (size_t)n * Fs;
+    if (cache_key == 0 || cache_key != gbdt_cache::key || gbdt_cache::bytes != nbytes || gbdt_cache::bins == nullptr) {
+      if (bins_h == nullptr) return -7;      // device copy evicted: the caller quantises again
+      if (gbdt_cache::bins) (void)hipFree(gbdt_cache::bins);
+      gbdt_cache::bins = nullptr; gbdt_cache::key = 0; gbdt_cache::bytes = 0;
+      if (hipMalloc(&gbdt_cache::bins, nbytes) != hipSuccess) return -100;
+      if (hipMemcpy(gbdt_cache::bins, bins_h, nbytes, hipMemcpyHostToDevice) != hipSuccess) return -100;
+      gbdt_cache::key = cache_key; gbdt_cache::bytes = nbytes;
+    }
+    d_bins = gbdt_cache::bins;
   }
-  const uint8_t* d_bins = gbdt_cache::bins;
-  float *d_y, *d_margin, *d_leaf;
-  int *d_fold, *d_nb, *d_rows[3];
-  float2 *d_gh, *d_hist[2], *d_tot;
-  uint8_t* d_fok;
-  int4 *d_chunks, *d_tree, *d_pairs;
-  int2 *d_split, *d_cur;
-  SplitOut* d_cand;
-  NodeBest* d_best;
-  double* d_met;
-  const int max_level_nodes = 1 << max_depth;                         // nodes on the deepest level
-  const int max_hist_nodes = 1 << std::max(0, max_depth - 1);         // levels that are split searched
-  const size_t hist_node = (size_t)F * GB_BINS;
   HC(hipMalloc(&d_y, sizeof(float) * n));
   HC(hipMalloc(&d_fold, sizeof(int) * n));
-  for (int b = 0; b < 3; ++b) HC(hipMalloc(&d_rows[b], sizeof(int) * n));
-  HC(hipMalloc(&d_margin, sizeof(float) * (size_t)n * nfold * K));
-  HC(hipMalloc(&d_gh, sizeof(float2) * n));
-  for (int b = 0; b < 2; ++b) HC(hipMalloc(&d_hist[b], sizeof(float2) * (size_t)max_hist_nodes * hist_node));
-  HC(hipMalloc(&d_tot, sizeof(float2) * max_level_nodes));
-  HC(hipMalloc(&d_cand, sizeof(SplitOut) * (size_t)max_hist_nodes * F));
-  HC(hipMalloc(&d_best, sizeof(NodeBest) * max_hist_nodes));
   HC(hipMalloc(&d_nb, sizeof(int) * F));
-  HC(hipMalloc(&d_fok, F));
-  const int max_chunks = 4096 + 2 * max_level_nodes;
-  HC(hipMalloc(&d_chunks, sizeof(int4) * max_chunks));
-  HC(hipMalloc(&d_pairs, sizeof(int4) * max_level_nodes));
-  int4* d_reds;
-  HC(hipMalloc(&d_reds, sizeof(int4) * max_chunks));
-  HC(hipMalloc(&d_split, sizeof(int2) * max_level_nodes));
-  HC(hipMalloc(&d_cur, sizeof(int2) * max_level_nodes));
-  HC(hipMalloc(&d_tree, sizeof(int4) * 2 * max_level_nodes * 2));
-  HC(hipMalloc(&d_leaf, sizeof(float) * 2 * max_level_nodes * 2));
-  HC(hipMalloc(&d_met, sizeof(double) * 4 * 1024));
+  for (int b = 0; b < 2; ++b) HC(hipMalloc(&d_rows[b], sizeof(int) * (size_t)nfold * n));
+  HC(hipMalloc(&d_margin, sizeof(float) * (size_t)nfold * n * K));
+  HC(hipMalloc(&d_gh, sizeof(float2) * (size_t)nfold * n));
+  for (int b = 0; b < 2; ++b) HC(hipMalloc(&d_hist[b], sizeof(i64) * (size_t)nfold * geo.Lh * per_node));
+  HC(hipMalloc(&d_part, sizeof(i64) * (size_t)nfold * geo.maxslot * per_node));
+  for (int b = 0; b < 2; ++b) HC(hipMalloc(&d_lvl[b], sizeof(LNode) * (size_t)nfold * geo.Lmax));
+  HC(hipMalloc(&d_chunks, sizeof(Chunk) * (size_t)nfold * geo.maxch));
+  HC(hipMalloc(&d_reds, sizeof(Red) * (size_t)nfold * geo.maxch));
+  HC(hipMalloc(&d_counts, sizeof(int) * 2 * nfold));
+  HC(hipMalloc(&d_nroot, sizeof(int) * nfold));
+  HC(hipMalloc(&d_cand, sizeof(SplitOut) * (size_t)nfold * geo.Lh * F));
+  HC(hipMalloc(&d_best, sizeof(NodeBest) * (size_t)nfold * geo.Lh));
+  HC(hipMalloc(&d_tree, sizeof(int2) * (size_t)nfold * tsz));
+  HC(hipMalloc(&d_leaf, sizeof(float) * (size_t)nfold * tsz));
+  HC(hipMalloc(&d_split, sizeof(int2) * (size_t)nfold * geo.Lmax));
+  HC(hipMalloc(&d_cur, sizeof(int2) * (size_t)nfold * geo.Lmax));
+  HC(hipMalloc(&d_mx, sizeof(unsigned int) * 2 * nfold));
+  HC(hipMalloc(&d_keys, keys_bytes));
+  HC(hipMalloc(&d_order, sizeof(int) * K * order_elems));
+  HC(hipMalloc(&d_met, sizeof(double) * met_elems));
+  HC(hipHostMalloc(&h_up, up_bytes, hipHostMallocDefault));
+  HC(hipHostMalloc((void**)&h_met, sizeof(double) * met_elems, hipHostMallocDefault));
   HC(hipMemcpy(d_y, y_h, sizeof(float) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_fold, fold_h, sizeof(int) * n, hipMemcpyHostToDevice));
   HC(hipMemcpy(d_nb, nbins_h, sizeof(int) * F, hipMemcpyHostToDevice));
-  double base = P[11];
   if (objective == 1 || objective == 2) {   // engine.cpp: logit base margin for the logistic objectives only
     const double b = std::min(1 - 1e-7, std::max(1e-7, P[11]));
     base = std::log(b / (1 - b));
   }
   {
-    std::vector<float> m((size_t)n * nfold * K, (float)base);
+    std::vector<float> m((size_t)nfold * n * K, (float)base);
     HC(hipMemcpy(d_margin, m.data(), sizeof(float) * m.size(), hipMemcpyHostToDevice));
   }
-  DevParams dp{(float)P[1], (float)P[8], (float)P[9], (float)P[4]};
-  const int blocks = std::min(2048, (n + 255) / 256);
-  const int nfb = (F + HB_F - 1) / HB_F;
-  int* d_count;
-  HC(hipMalloc(&d_count, sizeof(int)));
-  unsigned int* d_mx;                      // max |g|, |h| of the current tree (fixed-point scale)
-  HC(hipMalloc(&d_mx, 2 * sizeof(unsigned int)));
-  int lg_n = 0;
-  while ((1ll << lg_n) < (long long)n + 1) ++lg_n;
-  unsigned long long* d_part = nullptr;    // exact partial histograms of multi-chunk nodes
-  int part_cap = 0;
-  std::vector<int4> reds;
-  std::vector<uint8_t> fok(F);
-  std::vector<NodeBest> best(max_hist_nodes);
-  std::vector<int4> chunks, pairs;
-  std::vector<int2> split, cur;
-  std::vector<float2> tot;
 
-  struct Node { int gnode, start, count, parent; float G, H; bool built; };
-  // chunk a set of (node, start, count) segments into row chunks of <= R rows
-  auto add_chunks = [&](std::vector<int4>& out, int node, int start, int count, int R) {
-    for (int o = 0; o < count; o += R) out.push_back(make_int4(node, start + o, std::min(R, count - o), 0));
-  };
-  const bool lower_better = true;
-  double best_score = INFINITY;
-  int best_round = 0, rounds_done = 0;
-  // GENTUN_GBDT_TIMING=1: host wall time per phase (each phase ends in a blocking copy)
-  static const bool timing = std::getenv("GENTUN_GBDT_TIMING") != nullptr;
-  double ph[6] = {0, 0, 0, 0, 0, 0};    // rows, hist, split, partition, predict+metric, trees
-  auto now = []() { return std::chrono::steady_clock::now(); };
-  auto since = [&](std::chrono::steady_clock::time_point t) {
-    return std::chrono::duration<double>(now() - t).count();
-  };
   for (int round = 0; round < num_boost_round; ++round) {
-    std::vector<double> trv((size_t)nfold * n_metrics), tev((size_t)nfold * n_metrics);
+    // ---- host: every tree's random draws (engine.cpp round_fold / build_tree streams)
+    u64* h_keys = reinterpret_cast<u64*>(h_up);
+    int* h_order = reinterpret_cast<int*>(reinterpret_cast<char*>(h_up) + keys_bytes);
+    std::memset(h_order, 0, sizeof(int) * K * order_elems);
     for (int k = 0; k < nfold; ++k) {
-      auto t0 = now();
-      // same splitmix stream and draw order as the CPU engine (engine.cpp round_fold / build_tree)
-      uint64_t rs = smix(seed ^ smix((uint64_t)k * 1000003ull + (uint64_t)round * 7919ull + 17));
-      auto next = [&]() { rs = smix(rs); return rs; };
-      auto uni = [&]() { return (next() >> 11) * (1.0 / 9007199254740992.0); };
-      float* margin = d_margin + (size_t)k * n * K;
-      for (int c = 0; c < K; ++c) {     // one tree per class (engine.cpp round_fold), margins updated in turn
-        const unsigned long long row_key = P[5] < 1.0 ? next() : 0ull;   // engine.cpp: one draw keys the rows
-        HC(hipMemsetAsync(d_count, 0, sizeof(int), 0));
-        hipLaunchKernelGGL(root_rows_kernel, dim3(blocks), dim3(256), 0, 0, d_fold, k, n, row_key, P[5], d_rows[0],
-                           d_count);
-        int nroot = 0;
-        HC(hipMemcpy(&nroot, d_count, sizeof(int), hipMemcpyDeviceToHost));
-        ph[0] += since(t0);
-        ph[5] += 1;
-        // colsample_bytree
+      const uint64_t fold_round = smix(seed ^ smix((uint64_t)k * 1000003ull + (uint64_t)round * 7919ull + 17));
+      for (int c = 0; c < K; ++c) {
+        uint64_t rs = c == 0 ? fold_round : smix(fold_round ^ smix((uint64_t)c * 0x51ED27ull + 3));
+        auto next = [&]() { rs = smix(rs); return rs; };
+        h_keys[(size_t)c * nfold + k] = P[5] < 1.0 ? next() : 0ull;
         std::vector<int> feats(F);
         for (int f = 0; f < F; ++f) feats[f] = f;
         if (P[6] < 1.0) {
@@ -612,174 +783,94 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
           feats.resize(kk);
           std::sort(feats.begin(), feats.end());
         }
-        if (multi)
-          hipLaunchKernelGGL(grad_multi_kernel, dim3(blocks), dim3(256), 0, 0, margin, d_y, d_gh, n, K, c);
-        else
-          hipLaunchKernelGGL(grad_kernel, dim3(blocks), dim3(256), 0, 0, margin, d_y, d_gh, n, obj, (float)P[10]);
-        HC(hipMemsetAsync(d_mx, 0, 2 * sizeof(unsigned int), 0));
-        hipLaunchKernelGGL(gh_max_kernel, dim3(std::min(blocks, 512)), dim3(256), 0, 0, d_gh, n, d_mx);
-        std::vector<int4> tree(1, make_int4(-1, 0, 0, 0));
-        std::vector<float> leaf(1, 0.f);
-        std::vector<Node> level(1, Node{0, 0, nroot, -1, 0.f, 0.f, true});
-        int rb = 0;                   // row-list buffer holding this level's segments
-        int hb = 0;                   // histogram buffer of this level
-        for (int depth = 0; depth <= max_depth && !level.empty(); ++depth) {
-          const int L = (int)level.size();
-          if (depth == max_depth && depth > 0) {   // deepest level: leaves only, totals from the parent splits
-            for (const Node& nd : level) leaf[nd.gnode] = (float)(h_weight(P, nd.G, nd.H) * P[0]);
-            break;
-          }
-          // ---- histograms: built children over their rows, siblings by subtraction
-          auto t1 = now();
-          float2* hcur = d_hist[hb];
-          chunks.clear(); pairs.clear(); reds.clear();
-          long long built_rows = 0;
-          for (const Node& nd : level) if (nd.built) built_rows += nd.count;
-          const int R = std::max(2048, (int)((built_rows + 63) / 64));
-          int nslots = 0;
-          for (int j = 0; j < L; ++j) {
-            const Node& nd = level[j];
-            if (!nd.built) {
-              pairs.push_back(make_int4(j, nd.parent, j ^ 1, 0));   // siblings are adjacent (2i, 2i+1)
-            } else if (nd.count <= R) {                             // one chunk: written in place
-              chunks.push_back(make_int4(j, nd.start, nd.count, -1));
-            } else {                                                // partial slots + reduction
-              const int first = nslots;
-              for (int o = 0; o < nd.count; o += R)
-                chunks.push_back(make_int4(j, nd.start + o, std::min(R, nd.count - o), nslots++));
-              reds.push_back(make_int4(j, first, nslots - first, 0));
-            }
-          }
-          if ((int)chunks.size() > max_chunks || (int)reds.size() > max_chunks) return -3;
-          if (nslots > part_cap) {
-            if (d_part) (void)hipFree(d_part);
-            part_cap = std::max(nslots, 2 * part_cap);
-            HC(hipMalloc(&d_part, sizeof(unsigned long long) * 2 * (size_t)part_cap * hist_node));
-          }
-          if (!chunks.empty()) {
-            HC(hipMemcpy(d_chunks, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice));
-            hipLaunchKernelGGL(hist_kernel, dim3((unsigned)chunks.size(), nfb), dim3(HB_T), 0, 0, d_bins, Fs, F,
-                               d_rows[rb], d_gh, d_chunks, hcur, d_part, d_mx, lg_n);
-          }
-          if (!reds.empty()) {
-            HC(hipMemcpy(d_reds, reds.data(), sizeof(int4) * reds.size(), hipMemcpyHostToDevice));
-            hipLaunchKernelGGL(reduce_kernel, dim3((unsigned)reds.size(), std::max(1, (int)(hist_node * 2 / 4096))),
-                               dim3(256), 0, 0, d_part, reinterpret_cast<float*>(hcur), d_reds, F, d_mx, lg_n);
-          }
-          if (!pairs.empty()) {
-            HC(hipMemcpy(d_pairs, pairs.data(), sizeof(int4) * pairs.size(), hipMemcpyHostToDevice));
-            hipLaunchKernelGGL(subtract_kernel, dim3((unsigned)pairs.size(), std::max(1, (int)(hist_node / 2048))),
-                               dim3(256), 0, 0, d_hist[hb ^ 1], hcur, d_pairs, F);
-          }
-          // ---- node totals: root from its histogram, children from the parent's split
-          if (depth == 0) {
-            hipLaunchKernelGGL(totals_kernel, dim3(1), dim3(64), 0, 0, hcur, d_tot, F);
-            float2 t0;
-            HC(hipMemcpy(&t0, d_tot, sizeof(float2), hipMemcpyDeviceToHost));
-            level[0].G = t0.x; level[0].H = t0.y;
-          } else {
-            tot.resize(L);
-            for (int j = 0; j < L; ++j) tot[j] = make_float2(level[j].G, level[j].H);
-            HC(hipMemcpy(d_tot, tot.data(), sizeof(float2) * L, hipMemcpyHostToDevice));
-          }
-          if (timing) { HC(hipDeviceSynchronize()); ph[1] += since(t1); t1 = now(); }
-          // ---- split search (colsample_bylevel draw as in the CPU engine)
-          std::fill(fok.begin(), fok.end(), 0);
+        const uint64_t level_key = P[7] < 1.0 ? next() : 0ull;
+        for (int d = 0; d <= D; ++d) {
           std::vector<int> lf = feats;
           if (P[7] < 1.0 && lf.size() > 1) {
             const int m = (int)lf.size();
             const int kk = std::max(1, (int)std::floor(P[7] * m + 1e-9));
-            for (int i = 0; i < m; ++i) std::swap(lf[i], lf[i + (int)(next() % (uint64_t)(m - i))]);
+            uint64_t ls = smix(level_key ^ smix((uint64_t)d + 1));
+            for (int i = 0; i < m; ++i) {
+              ls = smix(ls);
+              std::swap(lf[i], lf[i + (int)(ls % (uint64_t)(m - i))]);
+            }
             lf.resize(kk);
           }
-          for (int f : lf) fok[f] = 1;
-          HC(hipMemcpy(d_fok, fok.data(), F, hipMemcpyHostToDevice));
-          hipLaunchKernelGGL(split_kernel, dim3(F, L), dim3(64), 0, 0, hcur, d_nb, d_fok, d_tot, d_cand, F, dp);
-          hipLaunchKernelGGL(best_kernel, dim3(L), dim3(256), 0, 0, d_cand, d_best, F);
-          HC(hipMemcpy(best.data(), d_best, sizeof(NodeBest) * L, hipMemcpyDeviceToHost));
-          if (timing) { ph[2] += since(t1); t1 = now(); }
-          // ---- host: leaves, gamma pruning, next level layout
-          split.assign(L, make_int2(-1, 0));
-          cur.assign(L, make_int2(0, 0));
-          chunks.clear();
-          std::vector<Node> nextl;
-          std::vector<int> split_of;       // level node -> index of its left child in nextl (or -1)
-          split_of.assign(L, -1);
-          for (int j = 0; j < L; ++j) {
-            Node& nd = level[j];
-            leaf[nd.gnode] = (float)(h_weight(P, nd.G, nd.H) * P[0]);
-            const NodeBest& b = best[j];
-            if (depth >= max_depth || b.feature < 0 || b.bin < 0 || b.gain < P[3] || b.gain <= 1e-12f ||
-                nd.count <= 0)
-              continue;
-            const int li = (int)tree.size();
-            tree.push_back(make_int4(-1, 0, 0, 0));
-            tree.push_back(make_int4(-1, 0, 0, 0));
-            leaf.push_back(0.f);
-            leaf.push_back(0.f);
-            tree[nd.gnode] = make_int4(b.feature, b.bin, li, li + 1);
-            split[j] = make_int2(b.feature, b.bin);
-            cur[j] = make_int2(nd.start, nd.start + nd.count);
-            split_of[j] = (int)nextl.size();
-            nextl.push_back(Node{li, nd.start, 0, j, b.GL, b.HL, false});
-            nextl.push_back(Node{li + 1, 0, 0, j, nd.G - b.GL, nd.H - b.HL, false});
-            add_chunks(chunks, j, nd.start, nd.count, 4096);
-          }
-          if (nextl.empty()) break;
-          if ((int)chunks.size() > max_chunks) return -3;
-          // ---- partition the split nodes' rows into the other row buffer
-          const int ob = (rb == 1) ? 2 : 1;
-          HC(hipMemcpy(d_split, split.data(), sizeof(int2) * L, hipMemcpyHostToDevice));
-          HC(hipMemcpy(d_cur, cur.data(), sizeof(int2) * L, hipMemcpyHostToDevice));
-          HC(hipMemcpy(d_chunks, chunks.data(), sizeof(int4) * chunks.size(), hipMemcpyHostToDevice));
-          hipLaunchKernelGGL(partition_kernel, dim3((unsigned)chunks.size()), dim3(256), 0, 0, d_bins, Fs,
-                             d_rows[rb], d_rows[ob], d_chunks, d_split, d_cur);
-          HC(hipMemcpy(cur.data(), d_cur, sizeof(int2) * L, hipMemcpyDeviceToHost));
-          for (int j = 0; j < L; ++j) {
-            if (split_of[j] < 0) continue;
-            const Node& nd = level[j];
-            const int lc = cur[j].x - nd.start;
-            Node& l = nextl[split_of[j]];
-            Node& r = nextl[split_of[j] + 1];
-            l.count = lc;
-            r.start = nd.start + lc; r.count = nd.count - lc;
-            l.parent = r.parent = j;
-            (l.count <= r.count ? l : r).built = true;     // smaller child: histogram; sibling: subtraction
-          }
-          if (timing) ph[3] += since(t1);
-          level.swap(nextl);
-          rb = ob;
-          hb ^= 1;
+          int* o = h_order + (size_t)c * order_elems + ((size_t)k * (D + 1) + d) * F;
+          for (int i = 0; i < (int)lf.size(); ++i) o[lf[i]] = i + 1;
         }
-        auto t4 = now();
-        HC(hipMemcpy(d_tree, tree.data(), sizeof(int4) * tree.size(), hipMemcpyHostToDevice));
-        HC(hipMemcpy(d_leaf, leaf.data(), sizeof(float) * leaf.size(), hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(predict_kernel, dim3(blocks), dim3(256), 0, 0, d_bins, Fs, d_tree, d_leaf, margin, n, K, c);
       }
-      auto t4 = now();
-      const int mblocks = std::min(blocks, 1024);
-      std::vector<double> mpart((size_t)mblocks * 4);
-      for (int mi = 0; mi < n_metrics; ++mi) {
-        const int metric = metrics[mi];
-        hipLaunchKernelGGL(metric_kernel, dim3(mblocks), dim3(256), 0, 0, margin, d_y, d_fold, k, n, metric,
-                           objective, K, d_met);
-        HC(hipMemcpy(mpart.data(), d_met, sizeof(double) * mpart.size(), hipMemcpyDeviceToHost));
-        double met[4] = {0, 0, 0, 0};
-        for (int b = 0; b < mblocks; ++b)
-          for (int q = 0; q < 4; ++q) met[q] += mpart[(size_t)b * 4 + q];
-        double tr = met[0] / std::max(1.0, met[1]), te = met[2] / std::max(1.0, met[3]);
-        if (metric == 0) { tr = std::sqrt(tr); te = std::sqrt(te); }
-        trv[k * n_metrics + mi] = tr; tev[k * n_metrics + mi] = te;
-      }
-      ph[4] += since(t4);
     }
+    HC(hipMemcpyAsync(d_keys, h_keys, keys_bytes, hipMemcpyHostToDevice, 0));
+    HC(hipMemcpyAsync(d_order, h_order, sizeof(int) * K * order_elems, hipMemcpyHostToDevice, 0));
+    // ---- device: one tree per class for every fold, levels decided on the device
+    for (int c = 0; c < K; ++c) {
+      hipLaunchKernelGGL(grad_kernel, dim3(blocks, nfold), dim3(256), 0, 0, d_margin, d_y, d_gh, n, K, c, obj,
+                         (float)P[10]);
+      HC(hipMemsetAsync(d_mx, 0, sizeof(unsigned int) * 2 * nfold, 0));
+      hipLaunchKernelGGL(gh_max_kernel, dim3(std::min(blocks, 512), nfold), dim3(256), 0, 0, d_gh, n, d_mx);
+      HC(hipMemsetAsync(d_nroot, 0, sizeof(int) * nfold, 0));
+      hipLaunchKernelGGL(root_rows_kernel, dim3(blocks, nfold), dim3(256), 0, 0, d_fold, n, d_keys + (size_t)c * nfold,
+                         P[5], d_rows[0], d_nroot);
+      hipLaunchKernelGGL(level0_kernel, dim3(nfold), dim3(64), 0, 0, geo, d_nroot, d_lvl[0], d_chunks, d_reds,
+                         d_counts);
+      const int* order_c = d_order + (size_t)c * order_elems;
+      for (int d = 0; d <= D; ++d) {
+        const int L = 1 << d;
+        LNode* cur = d_lvl[d & 1];
+        LNode* nxt = d_lvl[(d + 1) & 1];
+        i64* hcur = d_hist[d & 1];
+        if (d < D || d == 0) {
+          hipLaunchKernelGGL(hist_kernel, dim3(geo.maxch, nfb, nfold), dim3(HB_T), 0, 0, geo, d_bins, d_rows[d & 1],
+                             d_gh, d_chunks, d_counts, hcur, d_part, d_mx);
+          hipLaunchKernelGGL(reduce_kernel, dim3(geo.maxch, ylen, nfold), dim3(256), 0, 0, geo, d_part, hcur, d_reds,
+                             d_counts);
+          if (d > 0)
+            hipLaunchKernelGGL(subtract_kernel, dim3(L, ylen, nfold), dim3(256), 0, 0, geo, cur, d_hist[(d - 1) & 1],
+                               hcur);
+          else
+            hipLaunchKernelGGL(root_totals_kernel, dim3(nfold), dim3(64), 0, 0, geo, hcur, cur);
+        }
+        if (d < D) {
+          hipLaunchKernelGGL(split_kernel, dim3(F, L, nfold), dim3(64), 0, 0, geo, d, hcur, d_nb, order_c, cur, d_mx,
+                             d_cand, dp);
+          hipLaunchKernelGGL(best_kernel, dim3(L, nfold), dim3(256), 0, 0, geo, d_cand, d_best);
+        }
+        hipLaunchKernelGGL(plan_split_kernel, dim3(nfold), dim3(256), 0, 0, geo, d, cur, d_best, d_mx, d_tree, d_leaf,
+                           d_split, d_cur, nxt, dp);
+        if (d < D) {
+          hipLaunchKernelGGL(partition_kernel, dim3(pblocks, nfold), dim3(256), 0, 0, geo, d, d_bins, d_nroot, cur,
+                             d_split, d_rows[d & 1], d_rows[(d + 1) & 1], d_cur);
+          hipLaunchKernelGGL(plan_next_kernel, dim3(nfold), dim3(256), 0, 0, geo, d, cur, d_split, d_cur, nxt,
+                             d_chunks, d_reds, d_counts);
+        }
+      }
+      hipLaunchKernelGGL(predict_kernel, dim3(blocks, nfold), dim3(256), 0, 0, geo, d_bins, d_tree, d_leaf, d_margin,
+                         c);
+    }
+    for (int mi = 0; mi < n_metrics; ++mi)
+      hipLaunchKernelGGL(metric_kernel, dim3(mblocks, nfold), dim3(256), 0, 0, geo, d_margin, d_y, d_fold,
+                         metrics[mi], objective, d_met + (size_t)mi * nfold * mblocks * 4);
+    HC(hipGetLastError());
+    // the round's one blocking copy: early stopping needs the test metric
+    HC(hipMemcpy(h_met, d_met, sizeof(double) * met_elems, hipMemcpyDeviceToHost));
     double tem_last = 0;
     for (int mi = 0; mi < n_metrics; ++mi) {
+      std::vector<double> trv(nfold), tev(nfold);
+      for (int k = 0; k < nfold; ++k) {
+        double met[4] = {0, 0, 0, 0};
+        const double* pm = h_met + ((size_t)mi * nfold + k) * mblocks * 4;
+        for (int b = 0; b < mblocks; ++b)
+          for (int q = 0; q < 4; ++q) met[q] += pm[(size_t)b * 4 + q];
+        double tr = met[0] / std::max(1.0, met[1]), te = met[2] / std::max(1.0, met[3]);
+        if (metrics[mi] == 0) { tr = std::sqrt(tr); te = std::sqrt(te); }
+        trv[k] = tr; tev[k] = te;
+      }
       double trm = 0, tem = 0, trs = 0, tes = 0;
-      for (int k = 0; k < nfold; ++k) { trm += trv[k * n_metrics + mi]; tem += tev[k * n_metrics + mi]; }
+      for (int k = 0; k < nfold; ++k) { trm += trv[k]; tem += tev[k]; }
       trm /= nfold; tem /= nfold;
       for (int k = 0; k < nfold; ++k) {
-        const double a = trv[k * n_metrics + mi] - trm, b = tev[k * n_metrics + mi] - tem;
+        const double a = trv[k] - trm, b = tev[k] - tem;
         trs += a * a; tes += b * b;
       }
       double* o = &out_hist[((size_t)round * n_metrics + mi) * 4];
@@ -787,22 +878,27 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
       tem_last = tem;                  // early stopping on the last metric (engine.cpp)
     }
     rounds_done = round + 1;
+    if (progress > 0 && rounds_done % progress == 0)
+      std::fprintf(stderr, "[gbdt_hip] round %d  test metric %.6g  %.2f s\n", rounds_done, tem_last,
+                   std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
     if (lower_better ? tem_last < best_score : tem_last > best_score) { best_score = tem_last; best_round = round; }
     if (early_stopping_rounds > 0 && round - best_round >= early_stopping_rounds) break;
   }
   if (timing)
-    std::fprintf(stderr, "[gbdt_hip] trees %.0f  rows %.3fs  hist %.3fs  split %.3fs  partition %.3fs  "
-                 "predict+metric %.3fs\n", ph[5], ph[0], ph[1], ph[2], ph[3], ph[4]);
-  (void)hipFree(d_count);
-  (void)hipFree(d_mx);
-  (void)hipFree(d_reds);
-  if (d_part) (void)hipFree(d_part);
-  for (void* p : {(void*)d_y, (void*)d_fold, (void*)d_rows[0], (void*)d_rows[1], (void*)d_rows[2],
-                  (void*)d_margin, (void*)d_gh, (void*)d_hist[0], (void*)d_hist[1], (void*)d_tot, (void*)d_cand,
-                  (void*)d_best, (void*)d_nb, (void*)d_fok, (void*)d_chunks, (void*)d_pairs, (void*)d_split,
-                  (void*)d_cur, (void*)d_tree, (void*)d_leaf, (void*)d_met})
-    (void)hipFree(p);
-  return early_stopping_rounds > 0 ? best_round + 1 : rounds_done;
+    std::fprintf(stderr, "[gbdt_hip] %d rounds x %d folds in %.3f s (fold-batched device levels, depth %d)\n",
+                 rounds_done, nfold,
+                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count(), D);
+  rc = early_stopping_rounds > 0 ? best_round + 1 : rounds_done;
+done:
+  for (void* p : {(void*)d_y, (void*)d_fold, (void*)d_nb, (void*)d_rows[0], (void*)d_rows[1], (void*)d_margin,
+                  (void*)d_gh, (void*)d_hist[0], (void*)d_hist[1], (void*)d_part, (void*)d_lvl[0], (void*)d_lvl[1],
+                  (void*)d_chunks, (void*)d_reds, (void*)d_counts, (void*)d_nroot, (void*)d_cand, (void*)d_best,
+                  (void*)d_tree, (void*)d_leaf, (void*)d_split, (void*)d_cur, (void*)d_mx, (void*)d_keys,
+                  (void*)d_order, (void*)d_met})
+    if (p) (void)hipFree(p);
+  if (h_up) (void)hipHostFree(h_up);
+  if (h_met) (void)hipHostFree(h_met);
+  return rc;
 }
 
 }  // extern "C"

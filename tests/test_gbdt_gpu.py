@@ -1,5 +1,8 @@
-"""HIP GBDT path (histogram / split / partition / predict kernels) against
-the CPU engine on the same folds."""
+"""HIP GBDT path (fold-batched, device-resident level loop: histogram /
+split / plan / partition / predict kernels) against the CPU engine on the
+same folds and sampling streams. Histograms are exact fixed-point sums and the
+split search runs in fp64, so the two engines agree to rounding level over
+whole runs (<= 1 %), not just the first rounds."""
 
 import numpy as np
 import pytest
@@ -23,10 +26,9 @@ def test_hip_matches_cpu_regression(params):
     gpu = gbdt.cv(params, x, y, num_boost_round=40, nfold=3, seed=0, device="cuda:0")
     a, b = np.array(cpu['test-rmse-mean']), np.array(gpu['test-rmse-mean'])
     assert len(a) == len(b)
-    # identical sampling streams; only float summation order differs (LDS / global
-    # atomics), which can flip near-tie splits and lets long runs drift apart
-    assert np.max(np.abs(a[:8] - b[:8]) / a[:8]) < 0.01, (a[:8], b[:8])
-    assert np.max(np.abs(a - b) / a) < 0.08, (a[-5:], b[-5:])
+    # identical sampling streams, exact histograms, fp64 gains: only the fp32
+    # margins differ from the CPU engine's fp64 ones
+    assert np.max(np.abs(a - b) / a) < 0.01, (a[-5:], b[-5:])
 
 
 def test_hip_binary_logistic_and_early_stopping():
@@ -35,7 +37,9 @@ def test_hip_binary_logistic_and_early_stopping():
     p = {'objective': 'binary:logistic', 'eval_metric': 'logloss', 'max_depth': 3}
     cpu = gbdt.cv(p, x, yb, num_boost_round=200, nfold=5, early_stopping_rounds=10)
     gpu = gbdt.cv(p, x, yb, num_boost_round=200, nfold=5, early_stopping_rounds=10, device="cuda:0")
-    assert abs(cpu['test-logloss-mean'][-1] - gpu['test-logloss-mean'][-1]) < 0.03
+    assert len(cpu['test-logloss-mean']) == len(gpu['test-logloss-mean'])
+    a, b = np.array(cpu['test-logloss-mean']), np.array(gpu['test-logloss-mean'])
+    assert np.max(np.abs(a - b) / a) < 0.01, (a[-3:], b[-3:])
     assert gpu['test-logloss-mean'][-1] == min(gpu['test-logloss-mean'])
 
 
@@ -49,9 +53,9 @@ def test_hip_deep_trees_odd_feature_counts(f, depth):
     gpu = gbdt.cv(p, x, y, num_boost_round=15, nfold=3, seed=1, device="cuda:0")
     a, b = np.array(cpu['test-rmse-mean']), np.array(gpu['test-rmse-mean'])
     assert len(a) == len(b)
-    assert np.max(np.abs(a - b) / a) < 0.03, (a, b)
+    assert np.max(np.abs(a - b) / a) < 0.01, (a, b)
     tr_a, tr_b = np.array(cpu['train-rmse-mean']), np.array(gpu['train-rmse-mean'])
-    assert np.max(np.abs(tr_a - tr_b) / tr_a) < 0.03, (tr_a, tr_b)
+    assert np.max(np.abs(tr_a - tr_b) / tr_a) < 0.01, (tr_a, tr_b)
 
 
 def test_hip_bins_cache_reused_and_bitwise_deterministic():
@@ -76,8 +80,10 @@ def test_hip_multiclass_matches_cpu(obj):
     cpu = gbdt.cv(p, x, y, num_boost_round=60, nfold=5, early_stopping_rounds=10, seed=0)
     gpu = gbdt.cv(p, x, y, num_boost_round=60, nfold=5, early_stopping_rounds=10, seed=0, device="cuda:0")
     assert set(gpu) == set(cpu)
-    assert abs(cpu['test-mlogloss-mean'][-1] - gpu['test-mlogloss-mean'][-1]) < 0.03
-    assert abs(cpu['test-merror-mean'][-1] - gpu['test-merror-mean'][-1]) < 0.03
+    assert len(cpu['test-mlogloss-mean']) == len(gpu['test-mlogloss-mean'])
+    a, b = np.array(cpu['test-mlogloss-mean']), np.array(gpu['test-mlogloss-mean'])
+    assert np.max(np.abs(a - b) / a) < 0.01, (a[-3:], b[-3:])
+    assert abs(cpu['test-merror-mean'][-1] - gpu['test-merror-mean'][-1]) < 0.01
     assert gpu['test-mlogloss-mean'][-1] == min(gpu['test-mlogloss-mean'])
 
 
@@ -115,3 +121,17 @@ def test_device_quantisation_bit_identical_to_cpu_engine():
     assert fs == 12 and not b_gpu[:, 9:].any()
     np.testing.assert_array_equal(nb, nb_cpu)
     np.testing.assert_array_equal(b_gpu[:, :9], b_cpu)
+
+
+def test_hip_subsample_colsample_multiclass_streams_match_cpu():
+    """Row subsampling and both column samplers with several trees per round:
+    every tree draws from its own stream (engine.cpp round_fold), so the GPU
+    engine, which derives the draws before the round, samples exactly the CPU
+    engine's rows and features."""
+    x, y = load_iris_xy()
+    p = {'objective': 'multi:softprob', 'num_class': 3, 'max_depth': 4, 'eta': 0.3, 'subsample': 0.7,
+         'colsample_bytree': 0.75, 'colsample_bylevel': 0.5, 'eval_metric': 'mlogloss'}
+    cpu = gbdt.cv(p, x, y, num_boost_round=30, nfold=3, seed=3)
+    gpu = gbdt.cv(p, x, y, num_boost_round=30, nfold=3, seed=3, device="cuda:0")
+    a, b = np.array(cpu['test-mlogloss-mean']), np.array(gpu['test-mlogloss-mean'])
+    assert np.max(np.abs(a - b) / a) < 0.01, (a[-3:], b[-3:])

@@ -44,10 +44,18 @@ if args.device != "cpu":
     from gentun_amd.models import gbdt_hip  # noqa: E402
     gbdt_hip.quantize_device(x)
     t_prep = time.perf_counter() - t0
+per = []
+for i, ind in enumerate(pop):
+    t1 = time.perf_counter()
+    f = ind.get_fitness()
+    per.append({"candidate": i, "s": round(time.perf_counter() - t1, 2), "rmse": round(float(f), 5),
+                "eta": round(float(ind.get_genes()["eta"]), 5), "max_depth": int(ind.get_genes()["max_depth"]),
+                "rounds": len((getattr(ind, "fold_metrics", None) or {}).get("history", [])) or None})
+    print("[bench_gbdt] " + json.dumps(per[-1]), file=sys.stderr, flush=True)
 best = pop.get_fittest()
 dt = time.perf_counter() - t0
 print(json.dumps({"metric": "candidates/hour (XGB GA, GBDT 5-fold CV)", "value": round(3600 * args.pop / dt, 2),
                   "rows": args.rows, "features": args.features, "pop": args.pop, "num_boost_round": args.rounds,
                   "early_stopping_rounds": args.esr, "device": args.device, "eval_s": round(dt, 2),
                   "data_s": round(t_data, 2), "quantize_s": round(t_prep, 2), "best_rmse": best.get_fitness(),
-                  "fitness": [round(float(ind.get_fitness()), 5) for ind in pop]}), flush=True)
+                  "fitness": [round(float(ind.get_fitness()), 5) for ind in pop], "per_candidate": per}), flush=True)
