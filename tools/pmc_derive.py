@@ -38,10 +38,15 @@ for name, c in K.items():
     hbm = (rd + wr) / (us * 1e-6) / 1e12 if us > 0 else 0
     hit = c.get("TCC_HIT_sum", 0) / max(1.0, c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0))
     wait = c.get("SQ_WAIT_INST_ANY", 0) / max(1.0, c.get("SQ_WAVE_CYCLES", 0))
-    rows.append((us, name, mfma, lds, rd / 1e6, wr / 1e6, hbm, hit, wait))
+    # v_mfma_f32_16x16x32_bf16: 16 busy cycles, 16384 FLOP -> 1024 FLOP per busy cycle
+    tfs = 1024.0 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (us * 1e-6) / 1e12 if us > 0 else 0
+    rows.append((us, name, mfma, tfs, lds, rd / 1e6, wr / 1e6, hbm, hit, wait))
 
-print("{:48s} {:>8s} {:>6s} {:>6s} {:>8s} {:>8s} {:>7s} {:>6s} {:>6s}".format(
-    "kernel (per-call mean)", "us", "MFMA%", "LDSbc", "rd MB", "wr MB", "TB/s", "L2hit", "wait"))
-for us, name, mfma, lds, rd, wr, hbm, hit, wait in sorted(rows, reverse=True):
-    print("{:48s} {:8.1f} {:6.1f} {:6.2f} {:8.1f} {:8.1f} {:7.2f} {:6.2f} {:6.2f}".format(
-        name, us, 100 * mfma, lds, rd, wr, hbm, hit, wait))
+print("# MFMA TF/s = bf16 matrix-core FLOP rate (1024 FLOP per busy cycle of 16x16x32); an fp32 (split)")
+print("# product costs 6 of them, so the fp32-equivalent rate of a split kernel is TF/s / 6. HBM TB/s from")
+print("# the L2 fabric requests (read side doubled: gfx950 tallies 128-B reads at 64 B -> an upper bound).")
+print("{:48s} {:>8s} {:>6s} {:>8s} {:>6s} {:>8s} {:>8s} {:>7s} {:>6s} {:>6s}".format(
+    "kernel (per-call mean)", "us", "MFMA%", "MFMA TF/s", "LDSbc", "rd MB", "wr MB", "TB/s", "L2hit", "wait"))
+for us, name, mfma, tfs, lds, rd, wr, hbm, hit, wait in sorted(rows, reverse=True):
+    print("{:48s} {:8.1f} {:6.1f} {:8.1f} {:6.2f} {:8.1f} {:8.1f} {:7.2f} {:6.2f} {:6.2f}".format(
+        name, us, 100 * mfma, tfs, lds, rd, wr, hbm, hit, wait))
