@@ -675,6 +675,14 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
     CONV_FAST_CASE_F32(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
     CONV_FAST_CASE_F32(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
     CONV_FAST_CASE_F32(5, 5, 3, 16, 8, 4, 7, 4)   // s2 input conv (20 -> 50)
+    {
+      // A/B (GENTUN_F32_S2): 1 = whole 16x16 image per workgroup, 4 waves (8 pixel groups per wave: half
+      // the weight traffic per MFMA); 2 = whole image, 8 waves
+      static const int s2 = std::getenv("GENTUN_F32_S2") ? std::atoi(std::getenv("GENTUN_F32_S2")) : 0;
+      if (s2 == 1) CONV_FAST_CASE_F32(3, 3, 7, 16, 16, 4, 7, 4)
+      if (s2 == 2) CONV_FAST_CASE_F32(3, 3, 7, 16, 16, 4, 7, 8)
+      if (s2 == 1) CONV_FAST_CASE_F32(5, 5, 3, 16, 16, 4, 7, 4)
+    }
     CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
     CONV_FAST_CASE_F32(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
     return -100;
