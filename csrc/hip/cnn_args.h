@@ -15,7 +15,8 @@
 struct GroupRec {
   int g;          // group index into the slot tensors / weights
   int in_mask;    // bit k: in[k] is summed
-  int out_mask;   // bits 0-7: outputs written, 8-15: accumulate, 16-23: apply out_mask[k] ReLU mask
+  int out_mask;   // bits 0-7: outputs written, 8-15: accumulate, 16-23: apply out_mask[k] ReLU mask,
+                  // 24: forward launch pools this group's output tile into pool_y / pool_mask (fused 2x2 max-pool)
   int pad;
 };
 
@@ -47,6 +48,8 @@ struct ConvArgs {
   long wps;                         // weight plane stride in elements (prec 1)
   int cbb;                          // generic kernel, set by its launcher: input chunks (8 channels) per channel
                                     // block (0: all at once). Wide fp32 layers stage the patch block by block.
+  void* pool_y;                     // fused pool (groups with GroupRec bit 24): [Q][B][H/2][W/2][Coutp]
+  uint8_t* pool_mask;               // argmax mask [Q*B][H/2][W/2][Coutp] (training forward) or null
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

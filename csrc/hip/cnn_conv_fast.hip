@@ -54,6 +54,44 @@ struct FastCfg {
 // registers, 4 waves / SIMD) for the same 256-pixel tile. PREC 1 (fp32
 // tensors, six-term split MFMA): three operand planes per fragment, LDS-bound
 // at 2-3 workgroups per CU -> 2 waves / SIMD.
+// Fused 2x2 max-pool of a forward tile (K4): TH x W output pixels in LDS
+// (ld(pixel, chunk, f) reads 8 channels) -> pooled chunks + the argmax mask
+// of pool_fwd_kernel (cnn_conv.hip: first strict maximum over (0,0), (0,1),
+// (1,0), (1,1); bit 2 = maximum > 0), from the values exactly as stored.
+template <int TH, int W, int NCO, int NTH, int PREC, typename LD>
+__device__ __forceinline__ void fused_pool(const ConvArgs& a, LD ld, int g, int b, int h0, int tid) {
+  typedef typename ActT<PREC>::T AT;
+  constexpr int WO = W / 2, NPP = (TH / 2) * WO * NCO;
+  static_assert(TH % 2 == 0 && W % 2 == 0, "pooled tiles need even rows / columns");
+  const int Ho = a.H >> 1;
+  const long n = (long)g * a.B + b;
+  for (int i = tid; i < NPP; i += NTH) {
+    const int cb = i % NCO, pp = i / NCO, pr = pp / WO, pc = pp - pr * WO;
+    const int p0 = 2 * pr * W + 2 * pc;
+    float m[8], t[8];
+    int arg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    ld(p0, cb, m);
+    const int offs[3] = {1, W, W + 1};
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      ld(p0 + offs[q], cb, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (t[j] > m[j]) { m[j] = t[j]; arg[j] = q + 1; }
+    }
+    const long o = ((n * Ho + (h0 >> 1) + pr) * WO + pc) * (NCO * 8) + cb * 8;
+    st_chunk(static_cast<AT*>(a.pool_y) + o, m);
+    if (a.pool_mask) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lo |= (uint32_t)(arg[j] | (m[j] > 0.f ? 4 : 0)) << (8 * j);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hi |= (uint32_t)(arg[4 + j] | (m[4 + j] > 0.f ? 4 : 0)) << (8 * j);
+      *reinterpret_cast<uint2*>(a.pool_mask + o) = make_uint2(lo, hi);
+    }
+  }
+}
+
 template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0>
 __global__ void __launch_bounds__(NWV * 64)
 __attribute__((amdgpu_waves_per_eu(PREC ? 2 : (NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))))
@@ -307,6 +345,11 @@ conv_fast_kernel(ConvArgs a) {
       for (int k = 0; k < GT_MAXSLOT; ++k)
         if ((gr.out_mask >> k) & 1) *reinterpret_cast<uint4*>(static_cast<uint16_t*>(a.out[k]) + obase + (long)i * 8) = val;
     }
+    if constexpr (TH % 2 == 0)
+      if (a.pool_y && ((gr.out_mask >> 24) & 1))
+        fused_pool<TH, W, NCO, NTH, 0>(
+            a, [&](int p, int cb, float* f) { unpack8(*reinterpret_cast<const uint4*>(ot + p * OROWB + cb * 8), f); },
+            g, b, h0, tid);
     return;
   }
   // fp32 tile in LDS, then one contiguous chunk per thread and slot: plain
@@ -362,6 +405,10 @@ conv_fast_kernel(ConvArgs a) {
       st_chunk(dst, sum);
     }
   }
+  if constexpr (TH % 2 == 0)
+    if (a.pool_y && ((gr.out_mask >> 24) & 1))
+      fused_pool<TH, W, NCO, NTH, PREC>(
+          a, [&](int p, int cb, float* f) { load8f(otile + p * OROW + cb * 8, f); }, g, b, h0, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -621,8 +668,13 @@ static void lds_limit(F* fn, size_t bytes) {
                                          (int)bytes);
 }
 
+// probe mode (gt_conv_fast_probe): report the tile rows of the instantiation
+// that would run instead of launching it (0: none that fuses the pool)
+static int g_probe = 0;
+
 #define CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_)                               \
   {                                                                                                     \
+    if (g_probe) return 1000 + TH_;                                                                     \
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
     const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, PREC_>::lds(a->epi_bf16 != 0);      \
     auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_>;                      \
@@ -653,6 +705,7 @@ static void lds_limit(F* fn, size_t bytes) {
 // the persistent pipelined kernel unless switched off
 #define CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                       \
   {                                                                                                     \
+    if (g_probe) return 0;                                                                              \
     const int ntiles = a->ngroups * a->B * (a->H / TH_);                                                \
     const int grid = std::min(ntiles, g_f32_grid > 0 ? g_f32_grid : 512);                               \
     const size_t lds = (size_t)(TH_ + KH_ - 1) * (W_ + KW_ - 1) * NCBI_ * 16 * GT_NPL_F32;              \
@@ -699,6 +752,16 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   CONV_FAST_CASE_NW(3, 3, 13, 8, 8, 7, 13, 7)   // s3 nodes / output conv, and their dgrad (100 -> 100)
   CONV_FAST_CASE2(5, 5, 13, 8, 8, 4, 7, 4)      // s3 input conv dgrad (100 -> 50)
   return -100;
+}
+
+// rows of the shape-specialised tile gt_conv_fast would launch for these
+// arguments when that kernel can fuse the 2x2 pool (even rows), else 0
+extern "C" int gt_conv_fast_probe(const ConvArgs* a) {
+  g_probe = 1;
+  const int rc = gt_conv_fast(a, nullptr);
+  g_probe = 0;
+  const int th = rc >= 1000 ? rc - 1000 : 0;
+  return th % 2 == 0 ? th : 0;
 }
 
 // ===========================================================================

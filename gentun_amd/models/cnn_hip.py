@@ -312,6 +312,34 @@ class HipPopJob(FoldJob):
         a.train, a.prec = train, self.prec
         return a
 
+    def _stage_fwd_ops(self, st, gather_train, fuse):
+        """Forward launches of one stage; ``fuse``: each group's pool source
+        conv also writes the pooled output and the argmax mask."""
+        src = self.sched.pool_source(st)
+        x1 = self.sched.pool_x1(st)
+        pool_of = {}
+        if fuse:
+            pool_of.setdefault(st.inp, set()).update(q for q in range(self.Q) if not src[q])
+            pool_of.setdefault(x1, set()).update(q for q in range(self.Q) if src[q])
+        ops = []
+        for L in st.layers:
+            first = L.slots == ["input"]
+            out = self.zpre[L.name] if self.bn else self.act[L.name]
+            pools = pool_of.get(L.name, set())
+            a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [out.data_ptr()], [],
+                                L.w_bf, L.b[0], 0 if self.bn else 1,
+                                [(q, im, 1 | ((1 << 24) if q in pools else 0)) for q, im in L.rows],
+                                gather=gather_train if first else None)
+            if L.xin is not None:
+                a.xsum = self.act[L.xin].data_ptr()
+            a.epi_bf16 = 1            # forward outputs never accumulate: bf16 output tile
+            if pools:
+                a.pool_y, a.pool_mask = self.act[st.pool].data_ptr(), st.pmask.data_ptr()
+            ops.append(("conv", a, L))
+            if self.bn:
+                ops.append(("bn", self._bn_args(L, 1), L))
+        return ops
+
     def _slot_ptr(self, name, grad=False):
         if name == "input":
             return self.data.x.data_ptr()
@@ -323,29 +351,34 @@ class HipPopJob(FoldJob):
         Q, B = self.Q, self.B
         gather_train = self.epoch_idx.data_ptr()
         self.fwd_ops = []
+        # K4: the 2x2 max-pool (and its argmax mask) fused into the epilogue of
+        # the conv each group pools (the stage's output conv, or its input conv
+        # without a DAG) when that launch runs a shape-specialised kernel; the
+        # separate pool kernel otherwise (and with BatchNorm, which normalises
+        # after the conv)
+        L_ = self.L
+        fast_on = L_.gt_conv_set_fast(1)
+        L_.gt_conv_set_fast(fast_on)
+        fuse_ok = (not self.bn) and fast_on and os.environ.get("GENTUN_POOL_FUSE", "1") != "0"
+        self.pool_fused = []
         for st in self.stages:
-            for L in st.layers:
-                first = L.slots == ["input"]
-                out = self.zpre[L.name] if self.bn else self.act[L.name]
-                a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [out.data_ptr()], [],
-                                    L.w_bf, L.b[0], 0 if self.bn else 1, [(q, im, 1) for q, im in L.rows],
-                                    gather=gather_train if first else None)
-                if L.xin is not None:
-                    a.xsum = self.act[L.xin].data_ptr()
-                a.epi_bf16 = 1            # forward outputs never accumulate: bf16 output tile
-                self.fwd_ops.append(("conv", a, L))
-                if self.bn:
-                    self.fwd_ops.append(("bn", self._bn_args(L, 1), L))
+            hh, ww, cc = self.shapes[st.inp]
             sel = torch.tensor(self.sched.pool_source(st), dtype=torch.int32, device=self.device)
             self._keep.append(sel)
-            x1 = self.act[self.sched.pool_x1(st)]
-            hh, ww, cc = self.shapes[st.inp]
             st.sel = sel
             # argmax mask of the training forward (1 byte per pooled channel): pool_bwd reads it
-            # instead of the 4 bf16 inputs of every cell
+            # instead of the 4 inputs of every cell
             st.pmask = torch.zeros((Q * B, hh // 2, ww // 2, cc), dtype=torch.uint8, device=self.device)
-            self.fwd_ops.append(("pool", (self.act[st.inp].data_ptr(), x1.data_ptr(), sel.data_ptr(),
-                                          self.act[st.pool].data_ptr(), Q * B, B, hh, ww, cc), st.pmask.data_ptr()))
+            ops = self._stage_fwd_ops(st, gather_train, fuse=fuse_ok)
+            fused = fuse_ok and all(L_.gt_conv_fast_probe(a) > 0 for kind, a, _ in ops
+                                    if kind == "conv" and a.pool_y)
+            if not fused:
+                ops = self._stage_fwd_ops(st, gather_train, fuse=False)
+                x1 = self.act[self.sched.pool_x1(st)]
+                ops.append(("pool", (self.act[st.inp].data_ptr(), x1.data_ptr(), sel.data_ptr(),
+                                     self.act[st.pool].data_ptr(), Q * B, B, hh, ww, cc), st.pmask.data_ptr()))
+            self.pool_fused.append(fused)
+            self.fwd_ops.extend(ops)
         prec = self.prec
         # ---- head
         df = K.DenseFwdArgs()
@@ -616,6 +649,7 @@ class HipPopJob(FoldJob):
                 b = K.ConvArgs.from_buffer_copy(a)
                 b.st = self.eval_state.data_ptr()
                 b.xsum = 0
+                b.pool_mask = 0                      # fused pool: output only
                 ops.append((kind, b, Lr))
             elif kind == "bn":
                 b = K.BnArgs.from_buffer_copy(a)

@@ -36,7 +36,7 @@ class ConvArgs(C.Structure):
                 ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
                 ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long),
-                ("cbb", I)]
+                ("cbb", I), ("pool_y", P), ("pool_mask", P)]
 
 
 class WgradArgs(C.Structure):
@@ -145,6 +145,8 @@ def lib():
         L.gt_wgrad_fast_splits.argtypes = [I, I, I, I, I, I, I]
         L.gt_wgrad_fast_splits.restype = I
         L.gt_wgrad_fast_band.restype = I
+        L.gt_conv_fast_probe.argtypes = [C.POINTER(ConvArgs)]
+        L.gt_conv_fast_probe.restype = I
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
         L.gt_conv_set_nwv.argtypes = [I]

@@ -125,3 +125,41 @@ def test_sequential_folds_population_invariance(dtype):
     conc = E.make_job("hip", plans[0], x, y, folds, fast, dev).launch().finish()
     assert conc["val_loss"][0] == alone[0]["val_loss"][0]          # fold 0 starts from scratch either way
     assert conc["val_loss"][1:] != alone[0]["val_loss"][1:]        # later folds start from carried biases
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fused_pool_matches_separate_pool_kernel(dtype, monkeypatch):
+    """K4: the 2x2 max-pool + argmax mask fused into the pool-source conv's
+    epilogue gives bit-identical training to the separate pool kernel."""
+    import numpy as np
+    import torch
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.cnn_hip import HipPopJob
+    from gentun_amd.models.genome import make_plan
+    from gentun_amd.utils.data import make_cifar_like, stratified_kfold
+    x, y = make_cifar_like(n=600, seed=2)
+    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
+    genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '000', 'S_2': '0000000000'},
+             {'S_1': '111', 'S_2': '0000000001'}]
+    members = [(make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10), folds, [0, 1]) for g in genes]
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype=dtype, reset="all", use_graph=False)
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("GENTUN_POOL_FUSE", fuse)
+        job = HipPopJob(None, x, y, None, cfg, torch.device("cuda", 0), members=members)
+        assert all(job.pool_fused) == (fuse == "1"), job.pool_fused
+        job.init_params()
+        job.reset_optimizer(1e-3)
+        job._new_epoch_order()
+        for _ in range(4):
+            job.train_step()
+        ev = job.evaluate()
+        torch.cuda.synchronize()
+        out[fuse] = (job.flat.detach().clone(), [st.pmask.clone() for st in job.stages],
+                     [t.detach().clone() for t in ev])
+    assert torch.equal(out["1"][0], out["0"][0])
+    for a, b in zip(out["1"][1], out["0"][1]):
+        assert torch.equal(a, b)
+    for a, b in zip(out["1"][2], out["0"][2]):
+        assert torch.equal(a, b)
