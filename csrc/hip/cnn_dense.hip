@@ -42,7 +42,7 @@ __global__ void step_begin_kernel(StepState* s) {
 // ---------------------------------------------------------------------------
 struct DenseFwdArgs {
   const void* x;           // [G][B][Fp] (pooled features, NHWC flatten), bf16 or fp32 (prec)
-  const uint16_t* wt;      // [planes][G][Up][Fp] bf16 (transposed copy of W1; prec 1: 3 exact planes)
+  const void* wt;          // transposed copy of W1 [G][Up][Fp]: bf16 (prec 0), fp32 (prec 1: split on the fly)
   const float* bias;       // [G][Up]
   void* out;               // [G][B][Up] bf16 or fp32
   const float* w2;         // [G][Up][C] fp32: dense2 weights (fused partial logits)
@@ -56,8 +56,22 @@ struct DenseFwdArgs {
   unsigned seed;
   int C;
   int prec;                // 0: bf16 tensors, bf16 MFMA; 1: fp32 tensors, split-fp32 MFMA (common.h)
-  long wps;                // plane stride of wt (elements)
+  long wps;                // unused (kept for the ABI)
 };
+
+// an MFMA A operand of 8 consecutive weights of the transposed W1 copy: bf16
+// as is, fp32 split into the three exact planes in registers (4 bytes per
+// weight from HBM instead of 3 stored bf16 planes = 6)
+template <int PREC>
+__device__ __forceinline__ void w1_frag(const void* base, long off, bool ok, uint4* f) {
+  if (PREC) {
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (ok) load8f(static_cast<const float*>(base) + off, v);
+    split8(v, f[0], f[1], f[2]);
+  } else {
+    f[0] = ok ? *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(base) + off) : make_uint4(0, 0, 0, 0);
+  }
+}
 
 // an MFMA B operand of 8 consecutive activations: bf16 as is, fp32 split into planes
 template <int PREC>
@@ -83,19 +97,17 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
   const int u_t = blockIdx.x * 16;
   const int b0 = blockIdx.y * 32;
   const int nchunks = a.Fp >> 3;
-  const uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
+  const long wg = (long)g * a.Up * a.Fp;
   const long xg = (long)g * a.B * a.Fp;
   f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   const int urow = u_t + l16;
   const int br0 = b0 + l16, br1 = b0 + 16 + l16;
-  const uint16_t* pa = wt + (long)urow * a.Fp;
+  const long pa = wg + (long)urow * a.Fp;
   const bool ua = urow < a.Up, b0ok = br0 < a.B, b1ok = br1 < a.B;
   for (int ks = wave * 4; ks < nchunks; ks += 16) {
     const int c = ks + kq;
     uint4 af[NPL], bf0[NPL], bf1[NPL];
-#pragma unroll
-    for (int q = 0; q < NPL; ++q)
-      af[q] = (c < nchunks && ua) ? *reinterpret_cast<const uint4*>(pa + q * a.wps + c * 8) : make_uint4(0, 0, 0, 0);
+    w1_frag<PREC>(a.wt, pa + c * 8, c < nchunks && ua, af);
     act_frag<PREC>(a.x, xg + (long)br0 * a.Fp + c * 8, c < nchunks && b0ok, bf0);
     act_frag<PREC>(a.x, xg + (long)br1 * a.Fp + c * 8, c < nchunks && b1ok, bf1);
     acc[0] = mfma_np<NPL>(af, bf0, acc[0]);
@@ -313,11 +325,11 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
 // ---------------------------------------------------------------------------
 struct DenseDgradArgs {
   const float* dH;     // [G][B][Up]
-  const uint16_t* wt;  // [planes][G][Up][Fp] bf16 transposed copy of W1 (the values dense_fwd multiplied by)
+  const void* wt;      // transposed copy of W1 [G][Up][Fp] (the values dense_fwd multiplied by): bf16 / fp32 (prec)
   void* dx;            // [G][B][Fp] bf16 or fp32 (prec)
   int G, B, Fp, Up;
   int prec;
-  long wps;            // plane stride of wt (elements)
+  long wps;            // unused (kept for the ABI)
 };
 
 // grid (Fp/64, ceil(B/32), G): D[row = f][col = b], K = units.
@@ -336,7 +348,7 @@ __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
   const int fb = blockIdx.x * 64;
   const int f_t = fb + wave * 16;
   const int b0 = blockIdx.y * 32;
-  const uint16_t* wt = a.wt + (long)g * a.Up * a.Fp;
+  const long wg = (long)g * a.Up * a.Fp;
   const float* dH = a.dH + (long)g * a.B * a.Up;
   const int lu = tid >> 3, lf = (tid & 7) * 8;       // staging: unit row lu, features lf .. lf+7
   const bool fok = fb + lf < a.Fp;                   // Fp % 8 == 0: all 8 or none
@@ -346,10 +358,7 @@ __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
   for (int ks = 0; ks < nchunks; ks += 4) {
     const int u = ks * 8 + lu;
     uint4 qv[NPL];
-#pragma unroll
-    for (int pl = 0; pl < NPL; ++pl)
-      qv[pl] = (fok && u < a.Up) ? *reinterpret_cast<const uint4*>(wt + pl * a.wps + (long)u * a.Fp + fb + lf)
-                                 : make_uint4(0, 0, 0, 0);
+    w1_frag<PREC>(a.wt, wg + (long)u * a.Fp + fb + lf, fok && u < a.Up, qv);
     const int c = ks + kq;
     float f0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (c < nchunks) {
@@ -406,13 +415,13 @@ struct DenseWgradAdamArgs {
   const void* x;       // [G][B][Fp] bf16 or fp32 (prec)
   const float* dH;     // [G][B][Up]
   float* p; float* m; float* v;   // [G][Fp][Up]
-  uint16_t* wt;        // [planes][G][Up][Fp] bf16 copy (transposed; prec 1: exact 3-plane split)
+  void* wt;            // transposed copy [G][Up][Fp] for dense_fwd / dense_dgrad: bf16 (prec 0) or fp32 (prec 1)
   const StepState* st;
   int G, B, Fp, Up;
   int Cp, Cr, Ur;      // feature = pixel * Cp + channel; channels >= Cr and units >= Ur are padding
                        // (zero forever: skipped, 13 % of the layer's optimizer traffic)
   int prec;
-  long wps;            // plane stride of wt (elements)
+  long wps;            // unused (kept for the ABI)
 };
 
 // grid (Fp/16, G), 256 threads. Thread: unit quad q (4 units), rows fr, fr+2, ..., fr+14.
@@ -422,8 +431,7 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
   constexpr int NPL = PREC ? GT_NPL_F32 : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* xs = reinterpret_cast<float*>(smem);                       // [B][16]
-  uint16_t* tt = reinterpret_cast<uint16_t*>(xs + a.B * 16);        // [NPL][Up][16] transposed bf16 planes
-  const int tplane = a.Up * 16;
+  AT* tt = reinterpret_cast<AT*>(xs + a.B * 16);                    // [Up][16] transposed copy (bf16 / fp32)
   const int g = blockIdx.y, f0 = blockIdx.x * 16, tid = threadIdx.x;
   const AT* x = static_cast<const AT*>(a.x) + (long)g * a.B * a.Fp;
   for (int i = tid; i < a.B * 16; i += 256) {
@@ -457,11 +465,9 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
     for (int r = 0; r < 8; ++r) {
       const int f = f0 + fr + 2 * r;
       if (f >= a.Fp) continue;
-      if (a.Cp > 0 && f % a.Cp >= a.Cr) {      // padded channel: weights stay 0, only the bf16 tile
+      if (a.Cp > 0 && f % a.Cp >= a.Cr) {      // padded channel: weights stay 0, only the copy tile
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int pl = 0; pl < NPL; ++pl) tt[pl * tplane + (u0 + i) * 16 + fr + 2 * r] = 0;
+        for (int i = 0; i < 4; ++i) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
         continue;
       }
       const long off = ((long)g * a.Fp + f) * a.Up + u0;
@@ -472,14 +478,8 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         P[i] = opt_update(a.st, P[i], acc[r][i], M[i], V[i], lr_t);
-        const uint16_t h0 = f2bf(P[i]);
-        tt[(u0 + i) * 16 + fr + 2 * r] = h0;
-        if (PREC) {                              // exact 3-plane split of the fp32 master
-          const float r1 = P[i] - bf2f(h0);
-          const uint16_t h1 = f2bf(r1);
-          tt[tplane + (u0 + i) * 16 + fr + 2 * r] = h1;
-          tt[2 * tplane + (u0 + i) * 16 + fr + 2 * r] = f2bf(r1 - bf2f(h1));
-        }
+        if constexpr (PREC != 0) tt[(u0 + i) * 16 + fr + 2 * r] = P[i];
+        else tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
       }
       *reinterpret_cast<float4*>(a.p + off) = pp;
       *reinterpret_cast<float4*>(a.m + off) = mm;
@@ -487,21 +487,18 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
     }
   }
   __syncthreads();
-  // transposed bf16 copy: wt[u][f0 .. f0+15] (32 contiguous bytes per unit)
+  // transposed copy: wt[u][f0 .. f0+15] (32 / 64 contiguous bytes per unit), 8 values per store
   const int nu = a.Ur > 0 ? ((a.Ur + 3) >> 2) << 2 : a.Up;
-#pragma unroll
-  for (int pl = 0; pl < NPL; ++pl) {
-    uint16_t* wt = a.wt + pl * a.wps + (long)g * a.Up * a.Fp;
-    const uint16_t* tp = tt + pl * tplane;
-    for (int i = tid; i < nu * 2; i += 256) {
-      const int u = i >> 1, half = i & 1;
-      if (f0 + half * 8 + 8 <= a.Fp) {
-        *reinterpret_cast<uint4*>(wt + (long)u * a.Fp + f0 + half * 8) =
-            *reinterpret_cast<const uint4*>(&tp[u * 16 + half * 8]);
-      } else {
-        for (int j = 0; j < 8; ++j)
-          if (f0 + half * 8 + j < a.Fp) wt[(long)u * a.Fp + f0 + half * 8 + j] = tp[u * 16 + half * 8 + j];
-      }
+  AT* wt = static_cast<AT*>(a.wt) + (long)g * a.Up * a.Fp;
+  for (int i = tid; i < nu * 2; i += 256) {
+    const int u = i >> 1, half = i & 1;
+    if (f0 + half * 8 + 8 <= a.Fp) {
+      float v[8];
+      ld_chunk(&tt[u * 16 + half * 8], v);
+      st_chunk(wt + (long)u * a.Fp + f0 + half * 8, v);
+    } else {
+      for (int j = 0; j < 8; ++j)
+        if (f0 + half * 8 + j < a.Fp) wt[(long)u * a.Fp + f0 + half * 8 + j] = tt[u * 16 + half * 8 + j];
     }
   }
 }
@@ -642,8 +639,7 @@ int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
 
 int gt_dense_wgrad_adam(const DenseWgradAdamArgs* a, hipStream_t stream) {
   if (a->Up % 4 || (a->prec != 0 && a->prec != 1)) return -1;
-  const size_t npl = a->prec ? GT_NPL_F32 : 1;
-  const size_t lds = sizeof(float) * (size_t)a->B * 16 + npl * 2 * (size_t)a->Up * 16;
+  const size_t lds = sizeof(float) * (size_t)a->B * 16 + (a->prec ? 4 : 2) * (size_t)a->Up * 16;
   if (lds > 160 * 1024) return -2;
   dim3 grid((a->Fp + 15) / 16, a->G);
   if (a->prec) {

@@ -212,7 +212,9 @@ class HipPopJob(FoldJob):
             L.wT_bf = torch.zeros((npl, Q, L.cinp, L.KH, L.KW, L.coutp), dtype=torch.bfloat16, device=dev)
             L.part_w = torch.zeros((L.S, Q, L.coutp, L.Kdim), dtype=torch.float32, device=dev)   # split-K partials
             L.part_b = torch.zeros((L.S, Q, L.coutp), dtype=torch.float32, device=dev)
-        self.w1t_bf = torch.zeros((npl, Q, self.Up, self.Fp), dtype=torch.bfloat16, device=dev)
+        # transposed copy of W1 for dense_fwd / dense_dgrad (written by the W1
+        # optimizer): bf16, or fp32 split into planes in registers by the kernels
+        self.w1t = torch.zeros((Q, self.Up, self.Fp), dtype=self.adt, device=dev)
         self.gW2 = torch.zeros((Q, self.Up, self.classes), dtype=torch.float32, device=dev)
         self.gb2 = torch.zeros((Q, self.classes), dtype=torch.float32, device=dev)
         self.gb1 = torch.zeros((Q, self.Up), dtype=torch.float32, device=dev)
@@ -382,13 +384,13 @@ class HipPopJob(FoldJob):
         prec = self.prec
         # ---- head
         df = K.DenseFwdArgs()
-        df.x, df.wt, df.bias, df.out = (self.act[self.last].data_ptr(), self.w1t_bf.data_ptr(),
+        df.x, df.wt, df.bias, df.out = (self.act[self.last].data_ptr(), self.w1t.data_ptr(),
                                         self.views["b1"][0].data_ptr(), self.hdrop.data_ptr())
         df.st, df.fold_ids, df.seeds = self.state.data_ptr(), self.fold_ids_t.data_ptr(), self.drop_seeds_t.data_ptr()
         df.G, df.B, df.Fp, df.Up = Q, B, self.Fp, self.Up
         df.drop_p, df.train, df.seed = self.cfg.dropout, 1, 0
         df.w2, df.plog, df.C = self.views["W2"][0].data_ptr(), self.plog.data_ptr(), self.classes
-        df.prec, df.wps = prec, self.w1t_bf[0].numel()
+        df.prec, df.wps = prec, self.w1t.numel()
         self.dense_fwd_args = df
         hd = K.HeadArgs()
         hd.h, hd.w2, hd.b2 = self.hdrop.data_ptr(), self.views["W2"][0].data_ptr(), self.views["b2"][0].data_ptr()
@@ -405,18 +407,18 @@ class HipPopJob(FoldJob):
         hd.prec = prec
         self.head_args = hd
         dd = K.DenseDgradArgs()
-        dd.dH, dd.wt, dd.dx = self.dH.data_ptr(), self.w1t_bf.data_ptr(), self.grad[self.last].data_ptr()
+        dd.dH, dd.wt, dd.dx = self.dH.data_ptr(), self.w1t.data_ptr(), self.grad[self.last].data_ptr()
         dd.G, dd.B, dd.Fp, dd.Up = Q, B, self.Fp, self.Up
-        dd.prec, dd.wps = prec, self.w1t_bf[0].numel()
+        dd.prec, dd.wps = prec, self.w1t.numel()
         self.dense_dgrad_args = dd
         dw = K.DenseWgradAdamArgs()
         p, m, v = self.views["W1"]
         dw.x, dw.dH, dw.p, dw.m, dw.v = self.act[self.last].data_ptr(), self.dH.data_ptr(), p.data_ptr(), \
             m.data_ptr(), v.data_ptr()
-        dw.wt, dw.st = self.w1t_bf.data_ptr(), self.state.data_ptr()
+        dw.wt, dw.st = self.w1t.data_ptr(), self.state.data_ptr()
         dw.G, dw.B, dw.Fp, dw.Up = Q, B, self.Fp, self.Up
         dw.Cp, dw.Cr, dw.Ur = self.final_cp, self.plan.kernels_per_layer[-1], self.plan.dense_units
-        dw.prec, dw.wps = prec, self.w1t_bf[0].numel()
+        dw.prec, dw.wps = prec, self.w1t.numel()
         self.dense_wgrad_args = dw
         # ---- backward (records: models/pop_schedule.py PopulationSchedule.backward)
         self.bwd_ops = []
@@ -533,7 +535,7 @@ class HipPopJob(FoldJob):
             w = L.w[0]
             L.w_bf.copy_(split_planes(w, self.npl))
             L.wT_bf.copy_(split_planes(w.flip(2, 3).permute(0, 4, 2, 3, 1), self.npl))
-        self.w1t_bf.copy_(split_planes(self.views["W1"][0].transpose(1, 2), self.npl))
+        self.w1t.copy_(self.views["W1"][0].transpose(1, 2))
 
     def reset_optimizer(self, lr):
         self.m.zero_()

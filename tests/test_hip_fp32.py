@@ -261,7 +261,7 @@ def test_dense_fwd_dgrad_fp32():
     b1 = torch.randn(G, Up) * 0.1
     ref = F.relu(torch.baddbmm(b1[:, None].double(), x.double(), w1.double()))
     r32 = F.relu(torch.baddbmm(b1[:, None], x, w1))
-    wt = _split(w1.transpose(1, 2).contiguous().to(DEV)).contiguous()
+    wt = w1.transpose(1, 2).contiguous().to(DEV)          # fp32 copy: the kernels split it in registers
     xd, b1d = x.to(DEV).contiguous(), b1.to(DEV).contiguous()
     out = torch.zeros(G, B, Up, device=DEV)
     st = torch.zeros(8, dtype=torch.int32, device=DEV)
@@ -313,7 +313,7 @@ def test_dense_wgrad_adam_fp32_planes():
     vv = 0.999 * v.double() + 0.001 * g * g
     lr_t = 1e-3 * math.sqrt(1 - 0.999 ** 5) / (1 - 0.9 ** 5)
     rp = p.double() - lr_t * mm / (vv.sqrt() + 1e-7)
-    wt = torch.zeros(3, G, Up, Fp, dtype=torch.bfloat16, device=DEV)
+    wt = torch.zeros(G, Up, Fp, dtype=torch.float32, device=DEV)
     a = Km.DenseWgradAdamArgs()
     a.x, a.dH, a.p, a.m, a.v, a.wt, a.st = x.data_ptr(), dH.data_ptr(), p.data_ptr(), m.data_ptr(), v.data_ptr(), \
         wt.data_ptr(), st.data_ptr()
@@ -323,7 +323,7 @@ def test_dense_wgrad_adam_fp32_planes():
     torch.cuda.synchronize()
     assert rel(m, mm) < TOL
     assert (p.double() - rp).abs().max().item() < 1e-6
-    assert torch.equal(wt, _split(p.transpose(1, 2).contiguous()))
+    assert torch.equal(wt, p.transpose(1, 2).contiguous())
 
 
 @pytest.mark.gpu
