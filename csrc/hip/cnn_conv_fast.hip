@@ -29,6 +29,10 @@
 
 #include "cnn_args.h"
 
+#ifndef GT_F32_NO_BPIPE
+#define GT_F32_NO_BPIPE 0      // 1: fp32 conv main loop without the patch-fragment pipeline (A/B builds)
+#endif
+
 // LDS bytes of one launch: the patch (NPL bf16 planes) or the output tile
 // (fp32, or bf16 for prec-0 forward launches -- measured 7-9 % faster: more
 // workgroups per CU), whichever is larger
@@ -290,22 +294,42 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
     for (int h = 0; h < PG; ++h) acc[t][h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  if (!(a.dbg & 1))
-#pragma unroll
-  for (int s = 0; s < NKS; ++s) {
+  auto load_b = [&](int s, uint4 (*dst)[NPL]) {
     const uint4* pb = patch + lbase + gbase + coff[s * 4 + kq];
-    uint4 bfr[PG][NPL];
 #pragma unroll
     for (int h = 0; h < PG; ++h) {
       const int p = h * 16;                        // relative to the wave's first group
 #pragma unroll
-      for (int q = 0; q < NPL; ++q) bfr[h][q] = pb[q * NP + ((p / W) * PW + (p % W)) * NCBI];
+      for (int q = 0; q < NPL; ++q) dst[h][q] = pb[q * NP + ((p / W) * PW + (p % W)) * NCBI];
     }
+  };
+  if (!(a.dbg & 1)) {
+    if constexpr (PREC != 0 && !GT_F32_NO_BPIPE) {
+      // fp32: the next k-step's patch fragments are read while this step's 6 x CT x PG
+      // MFMAs run (the unpipelined loop waited for its LDS reads before every k-step)
+      uint4 bfr[2][PG][NPL];
+      load_b(0, bfr[0]);
 #pragma unroll
-    for (int t = 0; t < CT; ++t)
+      for (int s = 0; s < NKS; ++s) {
+        if (s + 1 < NKS) load_b(s + 1, bfr[(s + 1) & 1]);
 #pragma unroll
-      for (int h = 0; h < PG; ++h) acc[t][h] = mfma_np<NPL>(areg[s % PF][t], bfr[h], acc[t][h]);
-    if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h) acc[t][h] = mfma_np<NPL>(areg[s % PF][t], bfr[s & 1][h], acc[t][h]);
+        if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        uint4 bfr[PG][NPL];
+        load_b(s, bfr);
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h) acc[t][h] = mfma_np<NPL>(areg[s % PF][t], bfr[h], acc[t][h]);
+        if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
+      }
+    }
   }
 
   // ---- epilogue: accumulators -> tile in LDS -> 16-byte row stores ---------
