@@ -1120,11 +1120,9 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
           const char* d0 = reinterpret_cast<const char*>(ds[cur][pl]) + dlane + ks * 32 * DROW + m * 32;
           afr[m][pl] = tr_pair(d0, d0 + 4 * DROW);
         }
-#pragma unroll
-      for (int t = 0; t < TPW; ++t) {
+      // the next column tile's im2col fragments are read while this tile's MFMAs run
+      auto load_bt = [&](int t, uint4* bfr) {
         const int n = wave + NW * t;
-        if (n >= NKT) continue;
-        uint4 bfr[NPL];
 #pragma unroll
         for (int pl = 0; pl < NPL; ++pl) {
           const char* x0 = reinterpret_cast<const char*>(xs[cur][pl]) + xrow_off + xoff[t];
@@ -1134,8 +1132,16 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
           bfr[0] = make_uint4(0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u);
           bfr[1] = bfr[2] = make_uint4(0, 0, 0, 0);
         }
+      };
+      uint4 bfr[2][NPL];
+      load_bt(0, bfr[0]);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m][t] = mfma_np<NPL>(afr[m], bfr, acc[m][t]);
+      for (int t = 0; t < TPW; ++t) {
+        const int n = wave + NW * t;
+        if (t + 1 < TPW) load_bt(t + 1, bfr[(t + 1) & 1]);
+        if (n >= NKT) continue;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m][t] = mfma_np<NPL>(afr[m], bfr[t & 1], acc[m][t]);
       }
     }
     if (more) {
