@@ -53,7 +53,8 @@ CLIP_EPS = 1e-7
 class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
                  dtype="fp32", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9,
-                 reset="kernels", batching="keras", batch_norm=False, bn_momentum=0.99, bn_eps=1e-3):
+                 reset="kernels", batching="keras", batch_norm=False, bn_momentum=0.99, bn_eps=1e-3,
+                 dp_group=None):
         if isinstance(epochs, int):
             epochs = (epochs,)
         if isinstance(learning_rate, (int, float)):
@@ -78,6 +79,11 @@ class TrainConfig(object):
         self.batch_norm = bool(batch_norm)
         self.bn_momentum = float(bn_momentum)
         self.bn_eps = float(bn_eps)
+        # optional intra-candidate data parallelism (torch
+        # executor): a torch.distributed process group whose ranks each take a
+        # contiguous slice of every batch; gradients are all-reduced (RCCL over
+        # xGMI on GPUs) before the identical optimizer step on every rank
+        self.dp_group = dp_group
         self.epochs = epochs
         self.learning_rate = learning_rate
         self.batch_size = int(batch_size)
@@ -600,7 +606,10 @@ class TorchFoldJob(FoldJob):
                     gen = torch.Generator(device=self.device)
                     gen.manual_seed(_rng.stable_hash(self.base_seed, "dropout", self.fold_ids[g]) & 0x7FFFFFFF)
                     self.drop_gen.append(gen)
-            keep = torch.stack([torch.rand(h.shape[1:], generator=gen, device=self.device) for gen in self.drop_gen])
+            full = (self.B,) + tuple(h.shape[2:])
+            keep = torch.stack([torch.rand(full, generator=gen, device=self.device) for gen in self.drop_gen])
+            if keep.shape[1] != h.shape[1]:           # data-parallel slice: the full batch's masks, this rank's rows
+                keep = keep[:, self._dp_rows[0]:self._dp_rows[1]]
             h = h * (keep >= self.cfg.dropout).to(h.dtype) / (1.0 - self.cfg.dropout)
         return torch.baddbmm(P["dense2.b"][:, None, :], h, P["dense2.w"])
 
@@ -611,12 +620,30 @@ class TorchFoldJob(FoldJob):
         C, H, W = xb.shape[1:]
         return xb.view(G, Bn, C, H, W).permute(1, 0, 2, 3, 4).reshape(Bn, G * C, H, W)
 
+    def _dp(self):
+        """(group, rank, world, first row, end row) of the data-parallel slice."""
+        grp = self.cfg.dp_group
+        if grp is None:
+            return None
+        if self.cfg.batch_norm:
+            raise ValueError("data parallelism with BatchNorm would need synchronised batch statistics")
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(grp), dist.get_rank(grp)
+        r0, r1 = rank * self.B // world, (rank + 1) * self.B // world
+        self._dp_rows = (r0, r1)
+        return grp, rank, world, r0, r1
+
     def train_step(self):
+        dp = self._dp()
         idx = self.epoch_idx.index_select(0, self.step_ctr).view(self.G, self.B)
         nval = self.epoch_valid.index_select(0, self.step_ctr).view(self.G, 1).float()
         self.step_ctr.add_(1)
+        rows = torch.arange(self.B, device=self.device)[None, :].float()
+        wt = (rows < nval).float() / nval.clamp_min(1.0)
+        if dp is not None:                           # this rank's rows of every group's batch
+            idx, wt = idx[:, dp[3]:dp[4]], wt[:, dp[3]:dp[4]]
         xb = self._gather(idx)
-        yb = self.data.onehot.index_select(0, idx.reshape(-1)).view(self.G, self.B, -1)
+        yb = self.data.onehot.index_select(0, idx.reshape(-1)).view(self.G, idx.shape[1], -1)
         self.flat.grad.zero_()
         if self.amp:
             with torch.autocast(device_type="cuda", dtype=torch.bfloat16):
@@ -625,11 +652,12 @@ class TorchFoldJob(FoldJob):
             logits = self._forward(xb, True, nval.view(-1))
         per, _, _ = loss_and_metrics(logits, yb, self.cfg.loss)
         # mean over the real rows of each group's batch (Keras short batch)
-        rows = torch.arange(self.B, device=self.device)[None, :].float()
-        wt = (rows < nval).float() / nval.clamp_min(1.0)
         (per * wt).sum().backward()
         with torch.no_grad():
             g = self.flat.grad
+            if dp is not None:                       # X5: sum of the slices' gradients = the full batch's
+                import torch.distributed as dist
+                dist.all_reduce(g, op=dist.ReduceOp.SUM, group=dp[0])
             self.t.add_(1.0)
             if self.cfg.optimizer == "sgd":       # Keras SGD: v = mu v - lr g ; p += v
                 self.m.mul_(self.cfg.momentum).sub_(self.lr * g)
