@@ -16,7 +16,8 @@ struct GroupRec {
   int g;          // group index into the slot tensors / weights
   int in_mask;    // bit k: in[k] is summed
   int out_mask;   // bits 0-7: outputs written, 8-15: accumulate, 16-23: apply out_mask[k] ReLU mask,
-                  // 24: forward launch pools this group's output tile into pool_y / pool_mask (fused 2x2 max-pool)
+                  // 24: forward launch pools this group's output tile into pool_y / pool_mask (fused 2x2 max-pool),
+                  // 25: data-gradient launch writing a pool's gradient un-pools it instead (fused pool backward)
   int pad;
 };
 
@@ -49,7 +50,11 @@ struct ConvArgs {
   int cbb;                          // generic kernel, set by its launcher: input chunks (8 channels) per channel
                                     // block (0: all at once). Wide fp32 layers stage the patch block by block.
   void* pool_y;                     // fused pool (groups with GroupRec bit 24): [Q][B][H/2][W/2][Coutp]
-  uint8_t* pool_mask;               // argmax mask [Q*B][H/2][W/2][Coutp] (training forward) or null
+                                    // fused un-pool (bit 25): gradient of the pool source, slot 0 [Q][B][2H][2W][Coutp]
+  uint8_t* pool_mask;               // argmax mask [Q*B][H/2][W/2][Coutp] (training forward) or null; un-pool: the
+                                    // pooled layer's mask [Q*B][H][W][Coutp] (bit 2 = ReLU mask)
+  void* unpool_x1;                  // un-pool: gradient of the pool source, slot 1 (groups with sel[g] = 1)
+  const int* unpool_sel;            // un-pool: [Q] pool source per group (pop_schedule.pool_source)
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

@@ -96,6 +96,29 @@ __device__ __forceinline__ void fused_pool(const ConvArgs& a, LD ld, int g, int 
   }
 }
 
+// Fused pool backward (K4): a data-gradient launch whose output is a pool's
+// gradient scatters it straight to the pool source's gradient (2H x 2W):
+// each chunk of 8 channels to the 4 cell pixels, the value at the forward's
+// argmax when the maximum was > 0 (pool_bwd_mask_kernel's rule), else 0.
+// The pooled gradient itself is never stored.
+template <typename AT>
+__device__ __forceinline__ void unpool_chunk(const ConvArgs& a, int g, long n, int h, int w, int cb, const float* v) {
+  const int Cp = a.Coutp, H2 = 2 * a.H, W2 = 2 * a.W;
+  const long o = ((n * a.H + h) * a.W + w) * Cp + cb * 8;
+  const uint2 mk = *reinterpret_cast<const uint2*>(a.pool_mask + o);
+  AT* dst = static_cast<AT*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.pool_y);
+#pragma unroll
+  for (int me = 0; me < 4; ++me) {
+    float out[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t b = ((j < 4 ? mk.x : mk.y) >> (8 * (j & 3))) & 0xffu;
+      out[j] = ((int)(b & 3u) == me && (b & 4u)) ? v[j] : 0.f;
+    }
+    st_chunk(dst + ((n * H2 + 2 * h + (me >> 1)) * W2 + 2 * w + (me & 1)) * Cp + cb * 8, out);
+  }
+}
+
 template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0>
 __global__ void __launch_bounds__(NWV * 64)
 __attribute__((amdgpu_waves_per_eu(PREC ? 2 : (NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))))
@@ -408,6 +431,10 @@ conv_fast_kernel(ConvArgs a) {
     const float4 hi = *reinterpret_cast<const float4*>(otile + p * OROW + cb * 8 + 4);
     const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
     const long off = obase + (long)i * 8;
+    if ((gr.out_mask >> 25) & 1) {          // the output is a pool's gradient: un-pool it (slot 0)
+      unpool_chunk<AT>(a, g, (long)g * a.B + b, h0 + p / W, p % W, cb, v);
+      continue;
+    }
     for (int k = 0; k < GT_MAXSLOT; ++k) {
       if (!((gr.out_mask >> k) & 1)) continue;
       AT* dst = static_cast<AT*>(a.out[k]) + off;
@@ -786,6 +813,15 @@ extern "C" int gt_conv_fast_probe(const ConvArgs* a) {
   g_probe = 0;
   const int th = rc >= 1000 ? rc - 1000 : 0;
   return th % 2 == 0 ? th : 0;
+}
+
+// 1 when gt_conv_fast would run these (data-gradient) arguments on a
+// shape-specialised kernel, which can un-pool its output (fused pool backward)
+extern "C" int gt_conv_fast_probe_any(const ConvArgs* a) {
+  g_probe = 1;
+  const int rc = gt_conv_fast(a, nullptr);
+  g_probe = 0;
+  return rc >= 1000 ? 1 : 0;
 }
 
 // ===========================================================================

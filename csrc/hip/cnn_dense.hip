@@ -330,6 +330,14 @@ struct DenseDgradArgs {
   int G, B, Fp, Up;
   int prec;
   long wps;            // unused (kept for the ABI)
+  // fused pool backward (K4): dx is the last pool's gradient; with a mask the
+  // kernel scatters it to the pool source's gradient [G][B][Hs][Ws][Cp]
+  // instead (slot 1 for groups with sel[g] = 1), pool_bwd_mask_kernel's rule
+  const uint8_t* unpool_mask;   // [G*B][Hs/2][Ws/2][Cp] argmax mask of the forward, or null
+  void* unpool_x0;
+  void* unpool_x1;
+  const int* unpool_sel;        // [G]
+  int Hs, Ws, Cp;
 };
 
 // grid (Fp/64, ceil(B/32), G): D[row = f][col = b], K = units.
@@ -404,6 +412,27 @@ __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
     const int row = b0 + h * 16 + l16;
     if (row >= a.B) continue;
     float v[4] = {acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+    if (a.unpool_mask) {
+      // features fo .. fo+3 = channels c0 .. c0+3 of pooled pixel (ho, wo)
+      const long n = (long)g * a.B + row;
+      const int pix = fo / a.Cp, c0 = fo - pix * a.Cp, wo_n = a.Ws >> 1;
+      const int ho = pix / wo_n, wo = pix - ho * wo_n;
+      const uint32_t mk = *reinterpret_cast<const uint32_t*>(a.unpool_mask + n * a.Fp + fo);
+      AT* src = static_cast<AT*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.unpool_x0);
+#pragma unroll
+      for (int me = 0; me < 4; ++me) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t bb = (mk >> (8 * j)) & 0xffu;
+          o[j] = ((int)(bb & 3u) == me && (bb & 4u)) ? v[j] : 0.f;
+        }
+        AT* d = src + ((n * a.Hs + 2 * ho + (me >> 1)) * a.Ws + 2 * wo + (me & 1)) * a.Cp + c0;
+        if (PREC) *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
+        else *reinterpret_cast<uint2*>(d) = pack4(o);
+      }
+      continue;
+    }
     AT* dst = static_cast<AT*>(a.dx) + ((long)g * a.B + row) * a.Fp + fo;
     if (PREC) *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
     else *reinterpret_cast<uint2*>(dst) = pack4(v);
@@ -629,6 +658,8 @@ int gt_head(const HeadArgs* a, hipStream_t stream) {
 
 int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
   if (a->Fp % 64 && a->Fp % 8) return -1;
+  if (a->unpool_mask && (a->Cp % 8 || a->Hs % 2 || a->Ws % 2 || (long)(a->Hs / 2) * (a->Ws / 2) * a->Cp != a->Fp))
+    return -1;
   if (a->Up % 8) return -1;
   if (a->prec != 0 && a->prec != 1) return -1;
   dim3 grid((a->Fp + 63) / 64, (a->B + 31) / 32, a->G);

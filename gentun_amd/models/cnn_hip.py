@@ -423,9 +423,25 @@ class HipPopJob(FoldJob):
         # ---- backward (records: models/pop_schedule.py PopulationSchedule.backward)
         self.bwd_ops = []
         bn_done = set()
+        # K4 backward: the gradient of a pool is un-pooled by its producer (the
+        # dense data gradient for the last stage, the next stage's input-conv
+        # data gradient otherwise) straight into the pool source's gradient
+        fuse_bwd = fast_on and os.environ.get("GENTUN_POOL_FUSE", "1") != "0"
+        pool_stage = {st.pool: st for st in self.stages}
+        self.unpool_fused = set()
+        if fuse_bwd:
+            st = self.stages[-1]
+            hh, ww, cc = self.shapes[st.inp]
+            dd.unpool_mask, dd.unpool_sel = st.pmask.data_ptr(), st.sel.data_ptr()
+            dd.unpool_x0 = self.grad[st.inp].data_ptr()
+            dd.unpool_x1 = self.grad[self.sched.pool_x1(st)].data_ptr()
+            dd.Hs, dd.Ws, dd.Cp = hh, ww, cc
+            self.unpool_fused.add(st.pool)
         for rec in self.sched.backward():
             if rec[0] == "pool_bwd":
                 st = rec[1]
+                if st.pool in self.unpool_fused:
+                    continue
                 hh, ww, cc = self.shapes[st.inp]
                 x1 = self.sched.pool_x1(st)
                 self.bwd_ops.append(("pool_bwd", (st.pmask.data_ptr(),
@@ -460,9 +476,27 @@ class HipPopJob(FoldJob):
             else:
                 # dgrad = conv with flipped, transposed weights; per group the
                 # fan-out flags (write / accumulate / ReLU mask per input slot)
-                a = self._conv_args(L, [self.grad[L.name].data_ptr()], [self._slot_ptr(n, grad=True) for n in L.slots],
-                                    [self._slot_ptr(n) for n in L.slots], L.wT_bf, None, 0,
-                                    [(q, 1, of) for q, of in rows], Cinp=L.coutp, Coutp=L.cinp)
+                def dgrad_args(unpool):
+                    a = self._conv_args(L, [self.grad[L.name].data_ptr()],
+                                        [self._slot_ptr(n, grad=True) for n in L.slots],
+                                        [self._slot_ptr(n) for n in L.slots], L.wT_bf, None, 0,
+                                        [(q, 1, of | ((1 << 25) if unpool else 0)) for q, of in rows],
+                                        Cinp=L.coutp, Coutp=L.cinp)
+                    if unpool:
+                        st = pool_stage[L.slots[0]]
+                        a.pool_y, a.pool_mask = self.grad[st.inp].data_ptr(), st.pmask.data_ptr()
+                        a.unpool_x1 = self.grad[self.sched.pool_x1(st)].data_ptr()
+                        a.unpool_sel = st.sel.data_ptr()
+                    return a
+                a = None
+                if fuse_bwd and len(L.slots) == 1 and L.slots[0] in pool_stage:
+                    a = dgrad_args(True)
+                    if self.L.gt_conv_fast_probe_any(a):
+                        self.unpool_fused.add(L.slots[0])
+                    else:
+                        a = None
+                if a is None:
+                    a = dgrad_args(False)
                 self.bwd_ops.append(("conv", a, L))
         aa = K.AdamArgs()
         aa.segs, aa.blocks, aa.st = self.adam_segs.data_ptr(), self.adam_blocks.data_ptr(), self.state.data_ptr()

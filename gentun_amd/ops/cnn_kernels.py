@@ -36,7 +36,7 @@ class ConvArgs(C.Structure):
                 ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
                 ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long),
-                ("cbb", I), ("pool_y", P), ("pool_mask", P)]
+                ("cbb", I), ("pool_y", P), ("pool_mask", P), ("unpool_x1", P), ("unpool_sel", P)]
 
 
 class WgradArgs(C.Structure):
@@ -60,7 +60,8 @@ class HeadArgs(C.Structure):
 
 class DenseDgradArgs(C.Structure):
     _fields_ = [("dH", P), ("wt", P), ("dx", P), ("G", I), ("B", I), ("Fp", I), ("Up", I), ("prec", I),
-                ("wps", C.c_long)]
+                ("wps", C.c_long), ("unpool_mask", P), ("unpool_x0", P), ("unpool_x1", P), ("unpool_sel", P),
+                ("Hs", I), ("Ws", I), ("Cp", I)]
 
 
 class DenseWgradAdamArgs(C.Structure):
@@ -147,6 +148,8 @@ def lib():
         L.gt_wgrad_fast_band.restype = I
         L.gt_conv_fast_probe.argtypes = [C.POINTER(ConvArgs)]
         L.gt_conv_fast_probe.restype = I
+        L.gt_conv_fast_probe_any.argtypes = [C.POINTER(ConvArgs)]
+        L.gt_conv_fast_probe_any.restype = I
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
         L.gt_conv_set_nwv.argtypes = [I]

@@ -131,7 +131,9 @@ def test_sequential_folds_population_invariance(dtype):
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_fused_pool_matches_separate_pool_kernel(dtype, monkeypatch):
     """K4: the 2x2 max-pool + argmax mask fused into the pool-source conv's
-    epilogue gives bit-identical training to the separate pool kernel."""
+    epilogue, and the pool backward fused into the data gradients that
+    produce the pool gradients (next stage's input conv, dense layer), give
+    bit-identical training to the separate pool kernels."""
     import numpy as np
     import torch
     from gentun_amd.models import cnn_engine as E
@@ -149,6 +151,8 @@ def test_fused_pool_matches_separate_pool_kernel(dtype, monkeypatch):
         monkeypatch.setenv("GENTUN_POOL_FUSE", fuse)
         job = HipPopJob(None, x, y, None, cfg, torch.device("cuda", 0), members=members)
         assert all(job.pool_fused) == (fuse == "1"), job.pool_fused
+        # backward: every stage's pool gradient un-pooled by its producer
+        assert (len(job.unpool_fused) == len(job.stages)) == (fuse == "1"), job.unpool_fused
         job.init_params()
         job.reset_optimizer(1e-3)
         job._new_epoch_order()
