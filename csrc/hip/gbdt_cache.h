@@ -12,4 +12,5 @@ extern uint8_t* bins;      // row-major [n][Fs] uint8
 extern long long key;      // 0 = empty
 extern size_t bytes;
 extern std::mutex mu;
+void invalidate_derived();   // drop copies derived from bins (gbdt_hist.hip's feature-major copy); call with mu held
 }  // namespace gbdt_cache

@@ -63,7 +63,7 @@
 #define HB_STRIDE 514    // int64 per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
 #define HB_T 512
 #define HB_U 4
-#define GB_R 4096        // rows per histogram chunk
+#define GB_R 16384       // rows per histogram chunk (larger: fewer partial slots to reduce)
 #define GB_MAXD 12       // deepest supported tree
 
 namespace {
@@ -157,7 +157,14 @@ __global__ void gh_max_kernel(const float2* __restrict__ gh, int n, unsigned int
     mh = max(mh, __float_as_uint(fabsf(v.y)));
   }
   for (int o = 32; o > 0; o >>= 1) { mg = max(mg, __shfl_xor(mg, o)); mh = max(mh, __shfl_xor(mh, o)); }
-  if ((threadIdx.x & 63) == 0) { atomicMax(&mx[2 * k], mg); atomicMax(&mx[2 * k + 1], mh); }
+  __shared__ unsigned int sm[2][4];             // one atomic per workgroup (not per wave: they serialise at L2)
+  if ((threadIdx.x & 63) == 0) { sm[0][threadIdx.x >> 6] = mg; sm[1][threadIdx.x >> 6] = mh; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) { mg = max(mg, sm[0][w]); mh = max(mh, sm[1][w]); }
+    atomicMax(&mx[2 * k], mg);
+    atomicMax(&mx[2 * k + 1], mh);
+  }
 }
 
 // fixed-point exponent: max * 2^se * n < 2^62
@@ -169,29 +176,70 @@ __device__ __forceinline__ int fx_exp(unsigned int maxbits, int lg_n) {
 
 // root rows of fold k: rows of the other folds, Bernoulli(subsample) by the
 // counter-based hash of the CPU engine (engine.cpp row_uniform) keyed by one
-// draw of the tree's stream; unordered compaction (ballot + one atomic per wave)
+// draw of the tree's stream. Unordered compaction with ONE cursor atomic per
+// workgroup and 4096 rows (a per-wave atomic on the fold's single counter
+// serialised at L2: 0.9 ms per fold at 1M rows)
+#define RR_PER 16
 __global__ void __launch_bounds__(256) root_rows_kernel(const int* __restrict__ fold_of, int n,
                                                         const u64* __restrict__ keys, double subsample,
                                                         int* __restrict__ rows, int* __restrict__ counts) {
-  const int k = blockIdx.y, lane = threadIdx.x & 63;
-  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  __shared__ int wtot[4];
+  __shared__ int base_s;
+  const int k = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const u64 key = keys[k];
   int* rk = rows + (size_t)k * n;
-  for (int base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-    const int i = base + threadIdx.x;
-    bool keep = i < n && fold_of[i] != k;
-    if (keep && subsample < 1.0) {
-      u64 x = (u64)i + 0x9E3779B97F4A7C15ull;
-      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
-      x = (key ^ x) + 0x9E3779B97F4A7C15ull;
-      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
-      keep = (double)(x >> 11) * (1.0 / 9007199254740992.0) < subsample;
+  for (long s0 = (long)blockIdx.x * 256 * RR_PER; s0 < n; s0 += (long)gridDim.x * 256 * RR_PER) {
+    uint32_t keepm = 0;
+#pragma unroll
+    for (int j = 0; j < RR_PER; ++j) {
+      const long i = s0 + (long)j * 256 + tid;
+      bool keep = i < n && fold_of[i] != k;
+      if (keep && subsample < 1.0) {
+        u64 x = (u64)i + 0x9E3779B97F4A7C15ull;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
+        x = (key ^ x) + 0x9E3779B97F4A7C15ull;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull; x = (x ^ (x >> 27)) * 0x94D049BB133111EBull; x ^= x >> 31;
+        keep = (double)(x >> 11) * (1.0 / 9007199254740992.0) < subsample;
+      }
+      if (keep) keepm |= 1u << j;
     }
-    const u64 m = __ballot(keep);
-    int b0 = 0;
-    if (lane == 0 && m) b0 = atomicAdd(&counts[k], __popcll(m));
-    b0 = __shfl(b0, 0);
-    if (keep) rk[b0 + __popcll(m & below)] = i;
+    const int cnt = __popc(keepm);
+    int incl = cnt;                                // inclusive scan over the wave
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) wtot[wv] = incl;
+    __syncthreads();
+    if (tid == 0) {
+      const int tot = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+      base_s = tot ? atomicAdd(&counts[k], tot) : 0;
+    }
+    __syncthreads();
+    int pos = base_s + incl - cnt;
+    for (int w = 0; w < wv; ++w) pos += wtot[w];
+#pragma unroll
+    for (int j = 0; j < RR_PER; ++j)
+      if ((keepm >> j) & 1u) rk[pos++] = (int)(s0 + (long)j * 256 + tid);
+    __syncthreads();                               // wtot / base_s reused by the next slice
+  }
+}
+
+// feature-major copy of the bins [Fs][n] for the partition's per-row
+// lookups (row-major bins: every lookup its own cache line)
+__global__ void __launch_bounds__(256) transpose_bins_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                             int n, int Fs) {
+  __shared__ uint8_t t[64][65];
+  const long r0 = (long)blockIdx.x * 64;
+  const int f0 = blockIdx.y * 64;
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int r = i >> 6, f = i & 63;
+    if (r0 + r < n && f0 + f < Fs) t[r][f] = in[(r0 + r) * Fs + f0 + f];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * 64; i += 256) {
+    const int f = i >> 6, r = i & 63;
+    if (r0 + r < n && f0 + f < Fs) out[(long)(f0 + f) * n + r0 + r] = t[r][f];
   }
 }
 
@@ -472,60 +520,121 @@ __global__ void __launch_bounds__(256) plan_split_kernel(Geo geo, int depth, con
 }
 
 // ---- G5: partition of the level's row positions (grid: position blocks x folds)
-__global__ void __launch_bounds__(256) partition_kernel(Geo geo, int depth, const uint8_t* __restrict__ bins,
+// A workgroup owns PT_PER x 256 consecutive positions. When they all lie in
+// one node (the common case: segments are long), the block reserves its left
+// and right ranges with ONE cursor atomic per side (per-wave atomics on the
+// root's single cursor serialised at L2: 1 ms per level at 4M rows); blocks
+// that straddle segment boundaries use per-wave ballots, per-lane atomics
+// where a wave straddles one.
+#define PT_PER 16
+__global__ void __launch_bounds__(256) partition_kernel(Geo geo, int depth, const uint8_t* __restrict__ binsT,
                                                         const int* __restrict__ nroot, const LNode* __restrict__ cur,
                                                         const int2* __restrict__ splitv,
                                                         const int* __restrict__ rows_in, int* __restrict__ rows_out,
                                                         int2* __restrict__ cursor) {
   __shared__ int ends[1 << GB_MAXD];
-  const int k = blockIdx.y, L = 1 << depth, tid = threadIdx.x, lane = tid & 63;
-  const int p0 = blockIdx.x * 256;
-  if (p0 >= nroot[k]) return;
+  __shared__ int wl[4], wr[4], jfl[2], base_l, base_r;
+  const int k = blockIdx.y, L = 1 << depth, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nr = nroot[k];
+  const int p0 = blockIdx.x * 256 * PT_PER;
+  if (p0 >= nr) return;
   for (int j = tid; j < L; j += 256) {
     const LNode nd = cur[(size_t)k * geo.Lmax + j];
     ends[j] = nd.start + nd.count;
   }
   __syncthreads();
-  const int p = p0 + tid;
-  bool valid = p < nroot[k];
-  int j = -1;
-  if (valid) {                               // first node whose segment ends after p
+  auto node_of = [&](int p) {                  // node whose segment holds position p, or -1
     int lo = 0, hi = L;
     while (lo < hi) { const int mid = (lo + hi) >> 1; if (ends[mid] > p) hi = mid; else lo = mid + 1; }
-    j = lo;
-    valid = j < L && cur[(size_t)k * geo.Lmax + j].start <= p;
+    return (lo < L && cur[(size_t)k * geo.Lmax + lo].start <= p) ? lo : -1;
+  };
+  if (tid == 0) {
+    jfl[0] = node_of(p0);
+    jfl[1] = node_of(min(p0 + 256 * PT_PER, nr) - 1);
   }
-  int2 sp = make_int2(-1, 0);
-  if (valid) sp = splitv[(size_t)k * geo.Lmax + j];
-  valid = valid && sp.x >= 0;
-  int r = 0;
-  bool left = false;
-  if (valid) {
-    r = rows_in[(size_t)k * geo.n + p];
-    left = bins[(size_t)r * geo.Fs + sp.x] <= (uint8_t)sp.y;
-  }
-  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const u64 vm = __ballot(valid);
-  if (!vm) return;
-  const int lead = __builtin_ctzll(vm);
-  const int j0 = __shfl(j, lead);
-  const bool uniform = __ballot(valid && j != j0) == 0ull;
+  __syncthreads();
+  const int* rin = rows_in + (size_t)k * geo.n;
   int* out = rows_out + (size_t)k * geo.n;
-  if (uniform) {
-    const u64 lm = __ballot(valid && left), rm = __ballot(valid && !left);
-    int l0 = 0, r0 = 0;
-    if (lane == lead) {
-      int2* cu = cursor + (size_t)k * geo.Lmax + j0;
-      l0 = atomicAdd(&cu->x, __popcll(lm));
-      r0 = atomicSub(&cu->y, __popcll(rm)) - __popcll(rm);
+  const u64 below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  if (jfl[0] == jfl[1]) {
+    if (jfl[0] < 0) return;
+    const int j0 = jfl[0];
+    const int2 sp = splitv[(size_t)k * geo.Lmax + j0];
+    if (sp.x < 0) return;                      // a leaf: its rows leave the tree
+    const uint8_t* col = binsT + (size_t)sp.x * geo.n;
+    int rr[PT_PER];
+    uint32_t lm = 0, vm = 0;
+#pragma unroll
+    for (int q = 0; q < PT_PER; ++q) {
+      const int p = p0 + q * 256 + tid;
+      rr[q] = 0;
+      if (p < nr) {
+        rr[q] = rin[p];
+        vm |= 1u << q;
+        if (col[rr[q]] <= (uint8_t)sp.y) lm |= 1u << q;
+      }
     }
-    l0 = __shfl(l0, lead);
-    r0 = __shfl(r0, lead);
-    if (valid) out[left ? l0 + __popcll(lm & below) : r0 + __popcll(rm & below)] = r;
-  } else if (valid) {                        // segment boundary inside the wave
-    int2* cu = cursor + (size_t)k * geo.Lmax + j;
-    const int pos = left ? atomicAdd(&cu->x, 1) : atomicSub(&cu->y, 1) - 1;
-    out[pos] = r;
+    const int cl = __popc(lm), cr = __popc(vm & ~lm);
+    int il = cl, ir = cr;                      // inclusive wave scans
+    for (int o = 1; o < 64; o <<= 1) {
+      const int tl = __shfl_up(il, o), tr = __shfl_up(ir, o);
+      if (lane >= o) { il += tl; ir += tr; }
+    }
+    if (lane == 63) { wl[wv] = il; wr[wv] = ir; }
+    __syncthreads();
+    if (tid == 0) {
+      const int tl = wl[0] + wl[1] + wl[2] + wl[3], tr = wr[0] + wr[1] + wr[2] + wr[3];
+      int2* cu = cursor + (size_t)k * geo.Lmax + j0;
+      base_l = tl ? atomicAdd(&cu->x, tl) : 0;
+      base_r = tr ? atomicSub(&cu->y, tr) - tr : 0;
+    }
+    __syncthreads();
+    int pl = base_l + il - cl, pr = base_r + ir - cr;
+    for (int w = 0; w < wv; ++w) { pl += wl[w]; pr += wr[w]; }
+#pragma unroll
+    for (int q = 0; q < PT_PER; ++q) {
+      if (!((vm >> q) & 1u)) continue;
+      if ((lm >> q) & 1u) out[pl++] = rr[q];
+      else out[pr++] = rr[q];
+    }
+    return;
+  }
+  // segment boundary inside the block
+  for (int q = 0; q < PT_PER; ++q) {
+    const int p = p0 + q * 256 + tid;
+    bool valid = p < nr;
+    int j = valid ? node_of(p) : -1;
+    valid = valid && j >= 0;
+    int2 sp = make_int2(-1, 0);
+    if (valid) sp = splitv[(size_t)k * geo.Lmax + j];
+    valid = valid && sp.x >= 0;
+    int r = 0;
+    bool left = false;
+    if (valid) {
+      r = rin[p];
+      left = binsT[(size_t)sp.x * geo.n + r] <= (uint8_t)sp.y;
+    }
+    const u64 vmw = __ballot(valid);
+    if (!vmw) continue;
+    const int lead = __builtin_ctzll(vmw);
+    const int jw = __shfl(j, lead);
+    const bool uniform = __ballot(valid && j != jw) == 0ull;
+    if (uniform) {
+      const u64 lmw = __ballot(valid && left), rmw = __ballot(valid && !left);
+      int l0 = 0, r0 = 0;
+      if (lane == lead) {
+        int2* cu = cursor + (size_t)k * geo.Lmax + jw;
+        l0 = atomicAdd(&cu->x, __popcll(lmw));
+        r0 = atomicSub(&cu->y, __popcll(rmw)) - __popcll(rmw);
+      }
+      l0 = __shfl(l0, lead);
+      r0 = __shfl(r0, lead);
+      if (valid) out[left ? l0 + __popcll(lmw & below) : r0 + __popcll(rmw & below)] = r;
+    } else if (valid) {
+      int2* cu = cursor + (size_t)k * geo.Lmax + j;
+      const int pos = left ? atomicAdd(&cu->x, 1) : atomicSub(&cu->y, 1) - 1;
+      out[pos] = r;
+    }
   }
 }
 
@@ -636,11 +745,18 @@ uint64_t smix(uint64_t x) {
 
 }  // namespace
 
+// feature-major copy of the cached bins (partition), rebuilt when the cache changes
+static uint8_t* g_binsT = nullptr;
+static const uint8_t* g_binsT_src = nullptr;
+static long long g_binsT_key = 0;
+static size_t g_binsT_bytes = 0;
+
 namespace gbdt_cache {
 uint8_t* bins = nullptr;
 long long key = 0;
 size_t bytes = 0;
 std::mutex mu;
+void invalidate_derived() { g_binsT_key = 0; }
 }  // namespace gbdt_cache
 
 extern "C" {
@@ -681,7 +797,7 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   const size_t per_node = (size_t)F * 2 * GB_BINS;      // int64 per histogram node
   DevParams dp{P[1], P[8], P[9], P[4], P[0], P[3]};
   const int blocks = std::min(2048, (n + 255) / 256);
-  const int pblocks = (n + 255) / 256;
+  const int pblocks = (n + 256 * PT_PER - 1) / (256 * PT_PER);
   const int mblocks = std::min(blocks, 256);
   const int nfb = (F + HB_F - 1) / HB_F;
   const int ylen = std::max(1, (int)(per_node / 4096));
@@ -726,6 +842,15 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
       gbdt_cache::key = cache_key; gbdt_cache::bytes = nbytes;
     }
     d_bins = gbdt_cache::bins;
+    if (g_binsT == nullptr || g_binsT_key == 0 || g_binsT_key != gbdt_cache::key || g_binsT_src != d_bins ||
+        g_binsT_bytes != nbytes) {
+      if (g_binsT) (void)hipFree(g_binsT);
+      g_binsT = nullptr;
+      if (hipMalloc(&g_binsT, nbytes) != hipSuccess) return -100;
+      hipLaunchKernelGGL(transpose_bins_kernel, dim3((n + 63) / 64, (Fs + 63) / 64), dim3(256), 0, 0, d_bins, g_binsT,
+                         n, Fs);
+      g_binsT_src = d_bins; g_binsT_key = gbdt_cache::key; g_binsT_bytes = nbytes;
+    }
   }
   HC(hipMalloc(&d_y, sizeof(float) * n));
   HC(hipMalloc(&d_fold, sizeof(int) * n));
@@ -808,9 +933,10 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
       hipLaunchKernelGGL(grad_kernel, dim3(blocks, nfold), dim3(256), 0, 0, d_margin, d_y, d_gh, n, K, c, obj,
                          (float)P[10]);
       HC(hipMemsetAsync(d_mx, 0, sizeof(unsigned int) * 2 * nfold, 0));
-      hipLaunchKernelGGL(gh_max_kernel, dim3(std::min(blocks, 512), nfold), dim3(256), 0, 0, d_gh, n, d_mx);
+      hipLaunchKernelGGL(gh_max_kernel, dim3(std::min(blocks, 256), nfold), dim3(256), 0, 0, d_gh, n, d_mx);
       HC(hipMemsetAsync(d_nroot, 0, sizeof(int) * nfold, 0));
-      hipLaunchKernelGGL(root_rows_kernel, dim3(blocks, nfold), dim3(256), 0, 0, d_fold, n, d_keys + (size_t)c * nfold,
+      hipLaunchKernelGGL(root_rows_kernel, dim3(std::max(1, std::min(1024, (n + 256 * RR_PER - 1) / (256 * RR_PER))), nfold),
+                         dim3(256), 0, 0, d_fold, n, d_keys + (size_t)c * nfold,
                          P[5], d_rows[0], d_nroot);
       hipLaunchKernelGGL(level0_kernel, dim3(nfold), dim3(64), 0, 0, geo, d_nroot, d_lvl[0], d_chunks, d_reds,
                          d_counts);
@@ -839,7 +965,7 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
         hipLaunchKernelGGL(plan_split_kernel, dim3(nfold), dim3(256), 0, 0, geo, d, cur, d_best, d_mx, d_tree, d_leaf,
                            d_split, d_cur, nxt, dp);
         if (d < D) {
-          hipLaunchKernelGGL(partition_kernel, dim3(pblocks, nfold), dim3(256), 0, 0, geo, d, d_bins, d_nroot, cur,
+          hipLaunchKernelGGL(partition_kernel, dim3(pblocks, nfold), dim3(256), 0, 0, geo, d, g_binsT, d_nroot, cur,
                              d_split, d_rows[d & 1], d_rows[(d + 1) & 1], d_cur);
           hipLaunchKernelGGL(plan_next_kernel, dim3(nfold), dim3(256), 0, 0, geo, d, cur, d_split, d_cur, nxt,
                              d_chunks, d_reds, d_counts);

@@ -152,6 +152,7 @@ int gbdt_quantize_hip(const float* X_h, int n, int F, int Fs, long long cache_ke
     gbdt_cache::bytes = nbytes;
   }
   gbdt_cache::key = 0;                                    // invalid until the bins are written
+  gbdt_cache::invalidate_derived();
   hipLaunchKernelGGL(qt_bins, dim3(2048), dim3(256), 0, 0, d_X, n, F, Fs, d_upper, d_nb, gbdt_cache::bins);
   QHC(hipGetLastError());
   QHC(hipMemcpy(nbins_out, d_nb, sizeof(int) * F, hipMemcpyDeviceToHost));
