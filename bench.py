@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--per-gpu", type=int, default=None,
-                    help="candidates per GPU per round (default: 3 fp32 / 6 bf16)")
+                    help="candidates per GPU per round (default: 5 fp32 / 8 bf16; larger rounds = larger population launches: 794 / 862 / 936 candidates/h at 3 / 4 / 6, profiles/bench_round_size_r2.txt)")
     ap.add_argument("--pop-per-gpu", type=int, default=32, help="GA population per GPU")
     ap.add_argument("--streams", type=int, default=1, help="concurrent population jobs per GPU")
     ap.add_argument("--pop-batch", type=int, default=16, help="candidates (x folds) per population job")
@@ -116,7 +116,7 @@ def run(args):
 
     epochs = tuple(int(e) for e in args.epochs.split(","))
     lrs = tuple(float(x) for x in args.lr.split(","))
-    per_gpu = args.per_gpu or (3 if args.dtype == "fp32" else 6)
+    per_gpu = args.per_gpu or (5 if args.dtype == "fp32" else 8)
     x, y = make_cifar_like(n=args.samples, seed=0)
     nodes, kernels = ((3, 4, 5), (20, 50, 100)) if args.space == "deep" else ((3, 5), (20, 50))
     if args.kernels:
@@ -154,10 +154,23 @@ def run(args):
         ga.breed()
         ga.generation += 1
 
+    best_seen = {}          # fittest individual evaluated so far (any generation, complete or not)
+
+    def track():
+        for ind in ga.population:
+            if not ind.get_fitness_status():
+                continue
+            cat = (getattr(ind, "fold_metrics", None) or {}).get("categorical_accuracy")
+            f = ind.get_fitness()
+            if cat and (not best_seen or f > best_seen["fitness"]):
+                best_seen.update(fitness=f, cat=float(sum(cat) / len(cat)), genes=dict(ind.get_genes()))
+
     def one_round():
         if not ga.population.pending():
             advance()
-        return ga.population.evaluate_in_parallel(limit=round_size)
+        n = ga.population.evaluate_in_parallel(limit=round_size)
+        track()
+        return n
 
     total_evals = 0
     timed_evals = 0
@@ -215,6 +228,9 @@ def run(args):
         "best_genes": last["best_genes"] if last else None,
         "best_val_cat_acc_by_gen": [round(c["best_cat_acc"], 4) if c["best_cat_acc"] is not None else None
                                     for c in completed],
+        # the fittest individual evaluated in the run (also when no generation completed)
+        "best_val_acc_evaluated": round(best_seen["cat"], 5) if best_seen else None,
+        "best_genes_evaluated": best_seen.get("genes"),
     }
     return out
 

@@ -119,6 +119,11 @@ class HipPopJob(FoldJob):
         self.side2 = torch.cuda.Stream(dev)
         self.overlap = True
         self.w1_stream = os.environ.get("GENTUN_W1_STREAM", "1") != "0"
+        # conv-layer optimizer updates per layer on a third stream (A/B switch, off:
+        # 907 vs 958 candidates/h with it on -- it competes with the dgrad chain,
+        # profiles/bench_round_size_r2.txt)
+        self.side3 = torch.cuda.Stream(dev)
+        self.adam_overlap = os.environ.get("GENTUN_ADAM_OVERLAP", "0") == "1"
         self._build_adam_table()
         self._build_args()
 
@@ -255,8 +260,11 @@ class HipPopJob(FoldJob):
                 for o in range(0, p.numel(), 256):
                     blocks.append((idx, o))
 
-        # conv layers: one segment per (layer, group that has the layer)
+        # conv layers: one segment per (layer, group that has the layer); the
+        # layer's blocks are contiguous (L.adam_range) so its update can run as
+        # soon as its wgrad and dgrad are done (train_step)
         for L in self.layers:
+            b0 = len(blocks)
             for q, _ in L.rows:
                 p, m, v = (t[q] for t in L.w)
                 add(p, m, v, L.part_w[0, q], L.S, L.part_w[0].numel(), bf=L.w_bf[0, q], bfT=L.wT_bf[0, q],
@@ -267,6 +275,8 @@ class HipPopJob(FoldJob):
                     for t, g in ((L.gamma, L.g_gamma), (L.beta, L.g_beta)):
                         p, m, v = (x[q] for x in t)
                         add(p, m, v, g[q], 1, g[q].numel())
+            L.adam_range = (b0, len(blocks))
+        self.adam_head_range = (len(blocks), None)
         for name, g in (("b1", self.gb1), ("W2", self.gW2), ("b2", self.gb2)):
             p, m, v = self.views[name]
             add(p, m, v, g, 1, g.numel())
@@ -275,6 +285,7 @@ class HipPopJob(FoldJob):
         self.adam_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self.adam_blocks = torch.tensor(np.asarray(blocks, np.int32).reshape(-1, 2), device=self.device)
         self.adam_nblocks = len(blocks)
+        self.adam_head_range = (self.adam_head_range[0], len(blocks))
 
     def _conv_args(self, L, in_ptrs, out_ptrs, mask_ptrs, w, bias, relu, rows, gather=None, Cinp=None, Coutp=None):
         a = K.ConvArgs()
@@ -502,6 +513,20 @@ class HipPopJob(FoldJob):
         aa.segs, aa.blocks, aa.st = self.adam_segs.data_ptr(), self.adam_blocks.data_ptr(), self.state.data_ptr()
         self.adam_args = aa
 
+        def adam_part(rng):
+            b = K.AdamArgs.from_buffer_copy(aa)
+            b.blocks = self.adam_blocks.data_ptr() + rng[0] * self.adam_blocks.stride(0) * 4
+            return b, rng[1] - rng[0]
+        for L in self.layers:
+            L.adam_part = adam_part(L.adam_range)
+        self.adam_head = adam_part(self.adam_head_range)
+        # index of the last backward op of every layer: its optimizer update
+        # may start once that op (and the layer's wgrad) has run
+        self.bwd_last = {}
+        for i, (kind, a, Lr) in enumerate(self.bwd_ops):
+            if Lr is not None:
+                self.bwd_last[Lr.name] = i
+
     # -------------------------------------------------------------- protocol
     def _build_init_table(self):
         """Segment table of the one-launch Philox Glorot initialiser (K11):
@@ -647,7 +672,11 @@ class HipPopJob(FoldJob):
         # (unchanged) inputs: it overlaps the layer's dgrad and everything after.
         fork(side2)
         K.check(L.gt_dense_wgrad_adam(self.dense_wgrad_args, side2.cuda_stream), "dense_wgrad_adam")
-        for kind, a, _ in self.bwd_ops:
+        # per-layer optimizer updates on a third stream (off the dgrad chain):
+        # layer L's update waits for its wgrad (side) and for its last
+        # main-stream op (the dgrad reading its flipped weights / BN backward)
+        side3 = self.side3 if (self.overlap and self.adam_overlap) else None
+        for i, (kind, a, Lr) in enumerate(self.bwd_ops):
             if kind == "wgrad":
                 fork(side)
                 K.check(L.gt_conv_wgrad(a, ss), "conv_wgrad")
@@ -657,12 +686,21 @@ class HipPopJob(FoldJob):
                 K.check(L.gt_bn_bwd(a, s), "bn_bwd")
             else:
                 K.check(L.gt_pool_bwd_mask(*a, s), "pool_bwd")
-        for stream in (side, side2):
-            if stream is not main:
+            if side3 is not None and Lr is not None and self.bwd_last.get(Lr.name) == i and Lr.adam_part[1] > 0:
+                for stream in (main, side):
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    side3.wait_event(ev)
+                K.check(L.gt_adam_segments(Lr.adam_part[0], Lr.adam_part[1], side3.cuda_stream), "adam")
+        for stream in (side, side2, side3):
+            if stream is not None and stream is not main:
                 ev = torch.cuda.Event()
                 ev.record(stream)
                 main.wait_event(ev)
-        K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
+        if side3 is not None:
+            K.check(L.gt_adam_segments(self.adam_head[0], self.adam_head[1], s), "adam")
+        else:
+            K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
 
     def evaluate(self):
         """Forward the validation folds in batches of B (no dropout)."""
