@@ -55,6 +55,7 @@ struct ConvArgs {
                                     // pooled layer's mask [Q*B][H][W][Coutp] (bit 2 = ReLU mask)
   void* unpool_x1;                  // un-pool: gradient of the pool source, slot 1 (groups with sel[g] = 1)
   const int* unpool_sel;            // un-pool: [Q] pool source per group (pop_schedule.pool_source)
+  int cout_real;                    // real output channels (<= Coutp; 0 = unknown): prec-1 packed last co tile
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,
@@ -84,6 +85,7 @@ struct WgradArgs {
   int G, B, H, W, Cinp, Coutp, KH, KW, S, pps;  // pps = pixels per split (multiple of 64)
   int ngroups;
   int prec;                  // 0: bf16 tensors; 1: fp32 tensors (split-fp32 MFMA)
+  int cout_real;             // real output channels (<= Coutp; 0 = unknown): prec-1 packed last co tile
 };
 
 // "> 0" on a stored activation: bf16 bits (sign clear, not +0) or fp32

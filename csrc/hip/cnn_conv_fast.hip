@@ -119,7 +119,15 @@ __device__ __forceinline__ void unpool_chunk(const ConvArgs& a, int g, long n, i
   }
 }
 
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0>
+// PK (prec 1, shapes where every wave owns all NT co tiles): the last
+// output-channel tile holds <= 4 real channels (20 = 16 + 4, 100 = 96 + 4),
+// so 12+ of its 16 MFMA rows would multiply zero weights. Its rows carry the
+// three weight planes of those channels instead (row 4c + p = plane p of
+// channel 16 (NT-1) + c, row 4c + 3 = 0): three MFMAs (one per patch plane,
+// one accumulator) give every row a_p (b0 + b1 + b2), and the epilogue sums
+// the plane rows of a channel -- all nine split terms in 3 MFMAs instead of
+// six terms in 6.
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0, int PK = 0>
 __global__ void __launch_bounds__(NWV * 64)
 __attribute__((amdgpu_waves_per_eu(PREC ? 2 : (NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))))
 conv_fast_kernel(ConvArgs a) {
@@ -140,6 +148,7 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int PFM = PREC ? 2 : 4;                 // weight prefetch depth (k-steps; 3 planes each in prec 1)
   constexpr int PF = NKS < PFM ? NKS : PFM;
   static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == NWV, "tile shape");
+  static_assert(!PK || (PREC == 1 && WC == 1), "packed last tile: fp32, every wave owns all co tiles");
   static_assert(W % 16 == 0 || 16 % W == 0, "pixel groups must tile image rows");
 
   using FC = FastCfg<KH, KW, NCBI, W, TH, NT, NCO, PREC>;
@@ -170,6 +179,12 @@ conv_fast_kernel(ConvArgs a) {
   bool wok[CT];
 #pragma unroll
   for (int t = 0; t < CT; ++t) {
+    if (PK && t == CT - 1) {                        // packed tile: row l16 = (channel l16/4, plane l16%4)
+      const int co = (wco + t) * 16 + (l16 >> 2), pl = l16 & 3;
+      wok[t] = pl < 3 && co < a.cout_real;
+      wrow[t] = a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8) + (wok[t] ? pl : 0) * a.wps;
+      continue;
+    }
     const int co = (wco + t) * 16 + l16;
     wok[t] = co < NCO * 8;
     wrow[t] = a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8);
@@ -180,9 +195,18 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
     for (int t = 0; t < CT; ++t)
 #pragma unroll
-      for (int p = 0; p < NPL; ++p)
+      for (int p = 0; p < ((PK && t == CT - 1) ? 1 : NPL); ++p)
         dst[t][p] = (wok[t] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[t] + p * a.wps + c * 8)
                                          : make_uint4(0, 0, 0, 0);
+  };
+  // one k-step of tile t: the six-term product, or the packed tile's three MFMAs
+  auto mma = [&](int t, const uint4* af, const uint4* bf, f32x4_t c) {
+    if (PK && t == CT - 1) {
+      c = mfma16(af[0], bf[2], c);
+      c = mfma16(af[0], bf[1], c);
+      return mfma16(af[0], bf[0], c);
+    }
+    return mfma_np<NPL>(af, bf, c);
   };
 
   // ---- patch: summed inputs (or gathered dataset image), zero halo --------
@@ -298,7 +322,7 @@ conv_fast_kernel(ConvArgs a) {
   for (int t = 0; t < CT; ++t)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int co = (wco + t) * 16 + kq * 4 + i;
+      const int co = (PK && t == CT - 1) ? (i == 0 ? (wco + t) * 16 + kq : NCO * 8) : (wco + t) * 16 + kq * 4 + i;
       bias_v[t][i] = (a.bias && co < NCO * 8) ? a.bias[(long)g * (NCO * 8) + co] : 0.f;
     }
   __syncthreads();
@@ -338,7 +362,7 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
         for (int t = 0; t < CT; ++t)
 #pragma unroll
-          for (int h = 0; h < PG; ++h) acc[t][h] = mfma_np<NPL>(areg[s % PF][t], bfr[s & 1][h], acc[t][h]);
+          for (int h = 0; h < PG; ++h) acc[t][h] = mma(t, areg[s % PF][t], bfr[s & 1][h], acc[t][h]);
         if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
       }
     } else {
@@ -349,7 +373,7 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
         for (int t = 0; t < CT; ++t)
 #pragma unroll
-          for (int h = 0; h < PG; ++h) acc[t][h] = mfma_np<NPL>(areg[s % PF][t], bfr[h], acc[t][h]);
+          for (int h = 0; h < PG; ++h) acc[t][h] = mma(t, areg[s % PF][t], bfr[h], acc[t][h]);
         if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
       }
     }
@@ -410,6 +434,17 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
     for (int h = 0; h < PG; ++h) {
       const int p = (pgw + h) * 16 + l16;
+      if (PK && t == CT - 1) {
+        // channel (wco + t) * 16 + kq = sum of its three plane rows; the tile's other columns are 0
+        float s0 = acc[t][h][0] + acc[t][h][1] + acc[t][h][2] + bias_v[t][0];
+        if (a.relu) s0 = fmaxf(s0, 0.f);
+        float* orow = otile + p * OROW + (wco + t) * 16;
+        orow[kq] = s0;
+        orow[4 + kq] = 0.f;
+        orow[8 + kq] = 0.f;
+        orow[12 + kq] = 0.f;
+        continue;
+      }
       float4 v;
       v.x = acc[t][h][0] + bias_v[t][0];
       v.y = acc[t][h][1] + bias_v[t][1];
@@ -723,16 +758,26 @@ static void lds_limit(F* fn, size_t bytes) {
 // that would run instead of launching it (0: none that fuses the pool)
 static int g_probe = 0;
 
-#define CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_)                               \
+#define CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_, PK_)                        \
   {                                                                                                     \
     if (g_probe) return 1000 + TH_;                                                                     \
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
     const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, PREC_>::lds(a->epi_bf16 != 0);      \
-    auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_>;                      \
+    auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_, PK_>;                 \
     lds_limit(fn, lds);                                                                                 \
     hipLaunchKernelGGL(fn, grid, dim3(NWV_ * 64), lds, stream, *a);                                     \
     return (int)hipGetLastError();                                                                      \
   }
+#define CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_)                               \
+  CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_, 0)
+
+// the packed last co tile applies: fp32, the real output channels leave <= 4 in the last 16-channel tile
+static int g_conv_pk = -1;     // A/B switch (GENTUN_CONV_PK=0 disables)
+static bool pk_ok(const ConvArgs* a, int nt) {
+  if (g_conv_pk < 0) g_conv_pk = std::getenv("GENTUN_CONV_PK") ? std::atoi(std::getenv("GENTUN_CONV_PK")) : 1;
+  const int last = a->cout_real - 16 * (nt - 1);
+  return g_conv_pk && a->prec == 1 && a->cout_real > 0 && last >= 1 && last <= 4;
+}
 
 #define CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)                                             \
   (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->W == W_ && a->Coutp == NCO_ * 8 &&       \
@@ -771,13 +816,20 @@ static int g_probe = 0;
     if (g_f32_persistent && (W_ % 16) == 0) CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)   \
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
   }
+// shapes whose every wave owns all NT co tiles: packed last tile when the real channels allow
+#define CONV_FAST_CASE_F32_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                  \
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
+    if (g_f32_persistent && (W_ % 16) == 0) CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)   \
+    if (pk_ok(a, NT_)) CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 1)             \
+    CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
+  }
 
 extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
   if (a->prec == 1) {
     // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
-    CONV_FAST_CASE_F32(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
-    CONV_FAST_CASE_F32(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
+    CONV_FAST_CASE_F32_PK(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
+    CONV_FAST_CASE_F32_PK(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
     CONV_FAST_CASE_F32(5, 5, 3, 16, 8, 4, 7, 4)   // s2 input conv (20 -> 50)
     {
       // A/B (GENTUN_F32_S2): 1 = whole 16x16 image per workgroup, 4 waves (8 pixel groups per wave: half
@@ -788,7 +840,7 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
       if (s2 == 1) CONV_FAST_CASE_F32(5, 5, 3, 16, 16, 4, 7, 4)
     }
     CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
-    CONV_FAST_CASE_F32(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
+    CONV_FAST_CASE_F32_PK(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
     return -100;
   }
   if (a->prec != 0) return -1;
@@ -1031,7 +1083,12 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
 // next band's global loads are issued before the current band's MFMAs and
 // written to LDS after them (async-STAGE split).
 // ---------------------------------------------------------------------------
-template <int KH, int KW, int NCBI, int NCBO, int W, int R, int NW, int NB>
+//
+// PK: the last output-channel tile has <= 4 real channels (conv_fast_kernel's
+// packed tile, on the M side): a per-band LDS block holds, per pixel, the
+// three dz planes of those channels at row 4c + p, and that tile costs three
+// MFMAs per column tile and K-step (one per input plane) instead of six.
+template <int KH, int KW, int NCBI, int NCBO, int W, int R, int NW, int NB, int PK = 0>
 __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
   constexpr int NPL = GT_NPL_F32;
   constexpr int NT_ = NW * 64;                     // threads
@@ -1049,6 +1106,10 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 
   __shared__ __attribute__((aligned(16))) uint4 xs[NB][NPL][XCH];
   __shared__ __attribute__((aligned(16))) uint4 ds[NB][NPL][DCH];
+  constexpr int PKC = 2 * (MT - 1);                // dz chunk holding the packed tile's channels
+  constexpr int PKR = PK ? R * W : 1;
+  __shared__ __attribute__((aligned(16))) uint4 dpk[NB][PKR][2];   // packed plane rows per pixel (PK)
+  static_assert(!PK || PKC < NCBO, "packed tile inside the staged dz chunks");
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int s = blockIdx.x;
@@ -1109,7 +1170,28 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < DT; ++j) {
       const int i = tid + NT_ * j;
-      if (i < DCH) split8(dr[j], ds[buf][0][i], ds[buf][1][i], ds[buf][2][i]);
+      if (i >= DCH) continue;
+      uint4 q0, q1, q2;
+      split8(dr[j], q0, q1, q2);
+      ds[buf][0][i] = q0;
+      ds[buf][1][i] = q1;
+      ds[buf][2][i] = q2;
+      if (PK && i % NCBO == PKC) {
+        // channels 16 (MT-1) + c, c < 4: plane p at element 4c + p (element 4c + 3 = 0)
+        const int creal = a.cout_real - 16 * (MT - 1);
+        uint32_t w[8];
+        const uint32_t h0[4] = {q0.x & 0xffffu, q0.x >> 16, q0.y & 0xffffu, q0.y >> 16};
+        const uint32_t h1[4] = {q1.x & 0xffffu, q1.x >> 16, q1.y & 0xffffu, q1.y >> 16};
+        const uint32_t h2[4] = {q2.x & 0xffffu, q2.x >> 16, q2.y & 0xffffu, q2.y >> 16};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          w[2 * c] = c < creal ? (h0[c] | (h1[c] << 16)) : 0u;
+          w[2 * c + 1] = c < creal ? h2[c] : 0u;
+        }
+        const int px = i / NCBO;
+        dpk[buf][px][0] = make_uint4(w[0], w[1], w[2], w[3]);
+        dpk[buf][px][1] = make_uint4(w[4], w[5], w[6], w[7]);
+      }
     }
   };
 
@@ -1150,12 +1232,18 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
       const int xrow_off = ((ks * 32) / W) * PW * XROW;        // compile-time after unrolling
       uint4 afr[MT][NPL];
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int m = 0; m < MT; ++m) {
+        if (PK && m == MT - 1) {
+          const char* d0 = reinterpret_cast<const char*>(dpk[cur]) + px0 * 32 + p * 8 + ks * 32 * 32;
+          afr[m][0] = tr_pair(d0, d0 + 4 * 32);
+          continue;
+        }
 #pragma unroll
         for (int pl = 0; pl < NPL; ++pl) {
           const char* d0 = reinterpret_cast<const char*>(ds[cur][pl]) + dlane + ks * 32 * DROW + m * 32;
           afr[m][pl] = tr_pair(d0, d0 + 4 * DROW);
         }
+      }
       // the next column tile's im2col fragments are read while this tile's MFMAs run
       auto load_bt = [&](int t, uint4* bfr) {
         const int n = wave + NW * t;
@@ -1177,7 +1265,15 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
         if (t + 1 < TPW) load_bt(t + 1, bfr[(t + 1) & 1]);
         if (n >= NKT) continue;
 #pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m][t] = mfma_np<NPL>(afr[m], bfr[t & 1], acc[m][t]);
+        for (int m = 0; m < MT; ++m) {
+          if (PK && m == MT - 1) {
+            acc[m][t] = mfma16(afr[m][0], bfr[t & 1][2], acc[m][t]);
+            acc[m][t] = mfma16(afr[m][0], bfr[t & 1][1], acc[m][t]);
+            acc[m][t] = mfma16(afr[m][0], bfr[t & 1][0], acc[m][t]);
+          } else {
+            acc[m][t] = mfma_np<NPL>(afr[m], bfr[t & 1], acc[m][t]);
+          }
+        }
       }
     }
     if (more) {
@@ -1198,12 +1294,15 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
     for (int m = 0; m < MT; ++m)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int co = m * 16 + kq * 4 + i;
+        // packed tile: row 4kq + p = plane p of channel 16 (MT-1) + kq; its sum is that channel's value
+        const bool pkm = PK && m == MT - 1;
+        const int co = pkm ? m * 16 + kq + 4 * i : m * 16 + kq * 4 + i;
+        const float v = pkm ? (i == 0 ? acc[m][t][0] + acc[m][t][1] + acc[m][t][2] : 0.f) : acc[m][t][i];
         if (co >= a.Coutp) continue;
         if (col < Kdim)
-          a.part_w[(((long)s * a.G + g) * a.Coutp + co) * Kdim + col] = acc[m][t][i];
+          a.part_w[(((long)s * a.G + g) * a.Coutp + co) * Kdim + col] = v;
         else if (col == Kdim && a.part_b)
-          a.part_b[((long)s * a.G + g) * a.Coutp + co] = acc[m][t][i];
+          a.part_b[((long)s * a.G + g) * a.Coutp + co] = v;
       }
   }
 }
@@ -1227,18 +1326,30 @@ extern "C" int gt_wgrad_set_nb(int nb) {
     return (int)hipGetLastError();                                                                       \
   }
 
+#define WGRAD_F32_LAUNCH(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_, PK_)                                   \
+  hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_, PK_>), grid,           \
+                     dim3(NW_ * 64), 0, stream, *a)
 #define WGRAD_FAST_CASE_F32(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_)                                     \
   if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->Coutp == NCBO_ * 8 && a->W == W_ &&     \
       a->H % R_ == 0 && a->pps % (R_ * W_) == 0) {                                                        \
     dim3 grid(a->S, a->ngroups);                                                                         \
-    if ((g_wgrad_nb ? g_wgrad_nb : NB_) == 1)                                                            \
-      hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1>), grid, dim3(NW_ * 64), 0, \
-                         stream, *a);                                                                    \
-    else                                                                                                 \
-      hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 2>), grid, dim3(NW_ * 64), 0, \
-                         stream, *a);                                                                    \
+    const bool pk = wgrad_pk_ok(a, (NCBO_ * 8 + 15) / 16);                                               \
+    if ((g_wgrad_nb ? g_wgrad_nb : NB_) == 1) {                                                          \
+      if (pk) WGRAD_F32_LAUNCH(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 1);                               \
+      else WGRAD_F32_LAUNCH(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 0);                                  \
+    } else {                                                                                             \
+      if (pk) WGRAD_F32_LAUNCH(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 2, 1);                               \
+      else WGRAD_F32_LAUNCH(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 2, 0);                                  \
+    }                                                                                                    \
     return (int)hipGetLastError();                                                                       \
   }
+
+// packed last co tile of the fp32 wgrad (A/B switch GENTUN_WGRAD_PK=0 disables)
+static bool wgrad_pk_ok(const WgradArgs* a, int mt) {
+  static const int on = std::getenv("GENTUN_WGRAD_PK") ? std::atoi(std::getenv("GENTUN_WGRAD_PK")) : 1;
+  const int last = a->cout_real - 16 * (mt - 1);
+  return on && a->cout_real > 0 && last >= 1 && last <= 4;
+}
 
 // band rows of the specialised wgrad per precision (the host sizes the split
 // in whole bands: pps multiple of R*W); 0 = generic kernel

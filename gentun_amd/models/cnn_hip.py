@@ -305,6 +305,7 @@ class HipPopJob(FoldJob):
         a.G, a.B, a.H, a.W = self.Q, self.B, L.H, L.W
         a.Cinp = L.cinp if Cinp is None else Cinp
         a.Coutp = L.coutp if Coutp is None else Coutp
+        a.cout_real = L.cout if Coutp is None else L.cin      # data gradient: the layer's input channels
         a.KH, a.KW, a.TH = L.KH, L.KW, L.TH
         a.prec = self.prec
         a.wps = w[0].numel()                 # weights are [planes][...]
@@ -483,6 +484,7 @@ class HipPopJob(FoldJob):
                 wa.G, wa.B, wa.H, wa.W = Q, B, L.H, L.W
                 wa.Cinp, wa.Coutp, wa.KH, wa.KW, wa.S, wa.pps = L.cinp, L.coutp, L.KH, L.KW, L.S, L.pps
                 wa.prec = prec
+                wa.cout_real = L.cout
                 self.bwd_ops.append(("wgrad", wa, L))
             else:
                 # dgrad = conv with flipped, transposed weights; per group the

@@ -36,13 +36,15 @@ class ConvArgs(C.Structure):
                 ("n_in", I), ("n_out", I), ("acc_flags", I), ("relu", I),
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
                 ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long),
-                ("cbb", I), ("pool_y", P), ("pool_mask", P), ("unpool_x1", P), ("unpool_sel", P)]
+                ("cbb", I), ("pool_y", P), ("pool_mask", P), ("unpool_x1", P), ("unpool_sel", P),
+                ("cout_real", I)]
 
 
 class WgradArgs(C.Structure):
     _fields_ = [("inp", P * MAXSLOT), ("gather", P), ("st", P), ("dz", P), ("part_w", P),
                 ("part_b", P), ("gtab", P), ("n_in", I), ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I),
-                ("Coutp", I), ("KH", I), ("KW", I), ("S", I), ("pps", I), ("ngroups", I), ("prec", I)]
+                ("Coutp", I), ("KH", I), ("KW", I), ("S", I), ("pps", I), ("ngroups", I), ("prec", I),
+                ("cout_real", I)]
 
 
 class DenseFwdArgs(C.Structure):

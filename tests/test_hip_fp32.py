@@ -80,10 +80,13 @@ CONV_SHAPES = [(32, 32, 3, 20, 5, 1), (32, 32, 20, 20, 3, 3), (16, 16, 20, 50, 5
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,cin,cout,k,nin", CONV_SHAPES)
-def test_conv_fwd_fp32(H, W, cin, cout, k, nin):
+@pytest.mark.parametrize("pk", [0, 1])
+def test_conv_fwd_fp32(H, W, cin, cout, k, nin, pk):
     """Forward conv (shape-specialised and generic kernels): fused N-ary Add
     in fp32, split MFMA, bias + ReLU; the input sum written for the wgrad
-    (``xsum``) is the exact fp32 sum."""
+    (``xsum``) is the exact fp32 sum. ``pk``: the real output channel count
+    is passed, so shapes with <= 4 real channels in the last 16-channel tile
+    run the packed-tile kernel (plane rows, 3 MFMAs per k-step)."""
     Km = K()
     torch.manual_seed(10)
     G, B = 2, 3
@@ -110,6 +113,7 @@ def test_conv_fwd_fp32(H, W, cin, cout, k, nin):
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
     a.TH = Km.conv_tile_rows(H, W)
     a.prec = 1
+    a.cout_real = cout if pk else 0
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv")
     torch.cuda.synchronize()
     worst = worst32 = 0.0
@@ -160,6 +164,7 @@ def test_conv_dgrad_fanout_fp32(k, H):
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, coutp, cinp, k, k
     a.TH = Km.conv_tile_rows(H, W)
     a.prec = 1
+    a.cout_real = cin                      # packed last tile where the shape allows (20 = 16 + 4)
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "dgrad")
     torch.cuda.synchronize()
     got0 = out0[..., :cin].permute(0, 1, 4, 2, 3)
@@ -176,9 +181,12 @@ def test_conv_dgrad_fanout_fp32(k, H):
                                                       (16, 16, 20, 50, 5, 1, False), (16, 16, 50, 50, 3, 2, False),
                                                       (8, 8, 64, 128, 3, 1, False), (14, 14, 50, 50, 3, 3, False),
                                                       (8, 8, 256, 256, 5, 1, False), (16, 16, 128, 128, 5, 2, False)])
-def test_conv_wgrad_fp32(H, W, cin, cout, k, nin, first):
+@pytest.mark.parametrize("pk", [0, 1])
+def test_conv_wgrad_fp32(H, W, cin, cout, k, nin, first, pk):
     """Weight + bias gradient (specialised register-staged kernel and the
-    generic one), deterministic split-K partials summed in fixed order."""
+    generic one), deterministic split-K partials summed in fixed order.
+    ``pk``: real output channels passed -> packed last co tile where <= 4 real
+    channels fall in it (20, 50); the padded rows' partials stay exactly 0."""
     Km = K()
     torch.manual_seed(12)
     G, B = 2, 4
@@ -217,8 +225,10 @@ def test_conv_wgrad_fp32(H, W, cin, cout, k, nin, first):
     a.dz, a.part_w, a.part_b = dz_p.data_ptr(), pw.data_ptr(), pb.data_ptr()
     a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.S, a.pps = G, B, H, W, cinp, coutp, k, k, S, pps
     a.prec = 1
+    a.cout_real = cout if pk else 0
     Km.check(Km.lib().gt_conv_wgrad(a, stream()), "wgrad")
     torch.cuda.synchronize()
+    assert torch.all(pw[:, :, cout:] == 0) and torch.all(pb[:, :, cout:] == 0)
     got = pw.sum(0).view(G, coutp, k, k, cinp)[:, :cout, :, :, :cin].permute(0, 1, 4, 2, 3)
     ew, e32 = rel(got, ref), rel(r32, ref)
     eb = rel(pb.sum(0)[:, :cout], refb)

@@ -94,6 +94,7 @@ for name, H, cin, cout, k, nin in shapes:
                 a.xsum = xsum.data_ptr() if nin > 1 else 0
                 a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
                 a.TH, a.prec, a.dbg = K.conv_tile_rows(H, W), prec, dbg
+                a.cout_real = cout
                 fn = lambda s: K.check(L.gt_conv_fwd(a, s), kind)      # noqa: E731
             elif kind == "conv_dgrad":
                 a = K.ConvArgs()
@@ -102,6 +103,7 @@ for name, H, cin, cout, k, nin in shapes:
                 a.w, a.bias, a.st, a.wps = wT.data_ptr(), 0, st.data_ptr(), wT[0].numel()
                 a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, coutp, cinp, k, k
                 a.TH, a.prec, a.dbg = K.conv_tile_rows(H, W), prec, dbg
+                a.cout_real = cin
                 fn = lambda s: K.check(L.gt_conv_fwd(a, s), kind)      # noqa: E731
             else:
                 npix = B * H * W
@@ -117,6 +119,7 @@ for name, H, cin, cout, k, nin in shapes:
                 a.dz, a.part_w, a.part_b = dy.data_ptr(), pw.data_ptr(), pb.data_ptr()
                 a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.S, a.pps = G, B, H, W, cinp, coutp, k, k, S, pps
                 a.prec = prec
+                a.cout_real = cout
                 fn = lambda s: K.check(L.gt_conv_wgrad(a, s), kind)    # noqa: E731
             us = timeit(fn)
             print(json.dumps({"f32p": os.environ.get("F32P", "1"), "grid": os.environ.get("F32P_GRID", "0"),
