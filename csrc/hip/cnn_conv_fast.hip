@@ -141,7 +141,8 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int NKS = (NCH + 3) / 4;                // k-steps (32 k each)
   constexpr int TP = TH * W;                        // tile pixels
   constexpr int NPG = TP / 16;                      // pixel groups
-  constexpr int CT = (NT >= 2 && NT % 2 == 0) ? 2 : 1;   // co tiles per wave (odd NT: one per wave)
+  // co tiles per wave (odd NT: one per wave; packed last tile: all NT, so every wave carries the same work)
+  constexpr int CT = PK ? NT : ((NT >= 2 && NT % 2 == 0) ? 2 : 1);
   constexpr int WC = NT / CT;                       // waves along co
   constexpr int WP = NWV / WC;                        // waves along pixels
   constexpr int PG = NPG / WP;                      // pixel groups per wave
@@ -839,6 +840,8 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
       if (s2 == 2) CONV_FAST_CASE_F32(3, 3, 7, 16, 16, 4, 7, 8)
       if (s2 == 1) CONV_FAST_CASE_F32(5, 5, 3, 16, 16, 4, 7, 4)
     }
+    // (a packed tile here needs every wave to own all 4 co tiles: 2x the weight traffic per MFMA,
+    // measured 20 % slower than the 2 + 2 split -- profiles/conv_f32_packed_tile_ab_r2.txt)
     CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
     CONV_FAST_CASE_F32_PK(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
     return -100;

@@ -131,14 +131,16 @@ def test_conv_fwd_fp32(H, W, cin, cout, k, nin, pk):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,H", [(3, 16), (5, 16), (3, 32), (3, 8)])
+@pytest.mark.parametrize("k,H", [(3, 16), (5, 16), (3, 32), (3, 8), (3, -16)])
 def test_conv_dgrad_fanout_fp32(k, H):
     """Data gradient = conv of dz with the flipped / transposed weight planes;
     DAG fan-out into two slots, one accumulating, one ReLU-masked."""
     Km = K()
     torch.manual_seed(11)
+    wide = H < 0                           # H = -16: 50 -> 50 at 16x16 (4 output tiles, packed last)
+    H = abs(H)
     G, B, W = 2, 2, H
-    cin, cout = (20, 50) if H == 16 else (20, 20) if H == 32 else (64, 128)
+    cin, cout = (50, 50) if wide else (20, 50) if H == 16 else (20, 20) if H == 32 else (64, 128)
     cinp, coutp = (cin + 7) // 8 * 8, (cout + 7) // 8 * 8
     w = torch.randn(G, cout, cin, k, k) / math.sqrt(cout * k * k)
     dz = torch.randn(G, B, cout, H, W)

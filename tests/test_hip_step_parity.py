@@ -12,6 +12,7 @@ executor started from the same weights on the same batches.
 
 Genes: fan-out, isolated nodes and multiple sinks."""
 
+
 import numpy as np
 import pytest
 import torch
@@ -153,13 +154,20 @@ def _one_step_parity(gi, loss, bn):
     # flips there moves that layer's gradient by O(1e-2). With BN the fp64
     # reference therefore takes the HIP forward's ReLU decisions (the
     # arithmetic is compared, not the tie-breaking).
-    masks = None
-    if bn:
-        masks = {L.name: (job.act[L.name][0][..., :L.cout] > 0).permute(0, 3, 1, 2).cpu() for L in job.layers}
+    # Without BN the same happens at genuine near-ties (the all-ones genome: one
+    # flipped decision moves s2_n1.w by 1.6e-2, while torch fp32 flips others
+    # there and on genome 2 at 2.3e-2): the strict check below is on the HIP
+    # forward's ReLU decisions; the free-running comparison only has to stay
+    # within what one flipped decision does.
+    hip_masks = {L.name: (job.act[L.name][0][..., :L.cout] > 0).permute(0, 3, 1, 2).cpu() for L in job.layers}
+    masks = hip_masks if bn else None
     ref = _reference_grads(plan, w0, xb, yb, loss, bn_eps=eps, masks=masks)
     r32 = _reference_grads(plan, w0, xb, yb, loss, torch.float32, bn_eps=eps, masks=masks)    # torch fp32, same inputs
+    if not bn:
+        ref_m = _reference_grads(plan, w0, xb, yb, loss, masks=hip_masks)
+        r32_m = _reference_grads(plan, w0, xb, yb, loss, torch.float32, masks=hip_masks)
 
-    def errs(g):
+    def errs(g, ref=ref):
         out = {}
         for k, r in ref.items():
             if isinstance(r, tuple):
@@ -178,8 +186,16 @@ def _one_step_parity(gi, loss, bn):
     print("[parity] genes {} loss {} bn {}: worst rel grad err HIP {:.2e} ({}); torch fp32 there {:.2e}, worst {:.2e}"
           .format(genes, loss, bn, worst[kmax], kmax, worst32[kmax], max(worst32.values())))
     assert set(k.split(".")[0] for k in worst) >= set(L.name for L in job.layers)
+    if not bn:
+        # free-running: fp32-level, or one flipped near-tie ReLU decision away
+        for k, e in worst.items():
+            assert e < max(2e-4, 4 * worst32[k], 3e-2), (k, e, worst32[k])
+        worst, worst32 = errs(got, ref_m), errs(r32_m, ref_m)
+        kmax = max(worst, key=worst.get)
+        print("[parity]   on the HIP ReLU decisions: worst rel grad err HIP {:.2e} ({}); torch fp32 there {:.2e}"
+              .format(worst[kmax], kmax, worst32[kmax]))
     # fp32-level: within 2e-4 of the fp64 gradient, or no further than torch's
-    # own fp32 CPU autograd (ReLU / max-pool decisions near ties flip in fp32)
+    # own fp32 CPU autograd (max-pool decisions near ties flip in fp32)
     for k, e in worst.items():
         assert e < max(2e-4, 4 * worst32[k]), (k, e, worst32[k])
     # the update itself: p1 = p0 + v = p0 - g

@@ -9,12 +9,12 @@ timeout -k 10 600 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-metho
 tail -2 gpurun_out/gpu_tests_pk.log
 : > gpurun_out/pk_conv.log
 for pk in 1 0; do
-  GENTUN_WGRAD_PK=$pk G=25 DBGS=0 F32P=0 timeout -k 10 300 python -u tools/bench_conv.py 10 2>&1 | grep '^{' | sed "s/^/pk=$pk /" >> gpurun_out/pk_conv.log || exit 1
+  GENTUN_CONV_PK=$pk G=25 DBGS=0 F32P=0 timeout -k 10 300 python -u tools/bench_conv.py 10 2>&1 | grep '^{' | sed "s/^/pk=$pk /" >> gpurun_out/pk_conv.log || exit 1
 done
 echo conv done
 [ -n "$NOBENCH" ] && exit 0
 : > gpurun_out/pk_bench.log
 for pk in 1 0; do
-  GENTUN_WGRAD_PK=$pk timeout -k 10 400 python -u bench.py --gpus 1 --per-gpu 5 --steps 4 --warmup 1 > gpurun_out/pk_bench_$pk.json 2> gpurun_out/pk_bench_$pk.err || { tail -20 gpurun_out/pk_bench_$pk.err; exit 1; }
+  GENTUN_CONV_PK=$pk timeout -k 10 400 python -u bench.py --gpus 1 --per-gpu 5 --steps 4 --warmup 1 > gpurun_out/pk_bench_$pk.json 2> gpurun_out/pk_bench_$pk.err || { tail -20 gpurun_out/pk_bench_$pk.err; exit 1; }
   echo "pk=$pk $(cut -c1-300 gpurun_out/pk_bench_$pk.json)" >> gpurun_out/pk_bench.log; echo "bench pk=$pk done"
 done
