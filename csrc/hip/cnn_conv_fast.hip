@@ -817,6 +817,9 @@ static bool pk_ok(const ConvArgs* a, int nt) {
     if (g_f32_persistent && (W_ % 16) == 0) CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)   \
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
   }
+// narrow images (W < 16: no persistent variant)
+#define CONV_FAST_CASE_F32_NARROW(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                              \
+  if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)
 // shapes whose every wave owns all NT co tiles: packed last tile when the real channels allow
 #define CONV_FAST_CASE_F32_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                  \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
@@ -844,6 +847,10 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
     // measured 20 % slower than the 2 + 2 split -- profiles/conv_f32_packed_tile_ab_r2.txt)
     CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
     CONV_FAST_CASE_F32_PK(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
+    // deep S=(3,4,5) space, kernels (20, 50, 100): stage 3 at 8x8, one image per workgroup
+    CONV_FAST_CASE_F32_NARROW(5, 5, 7, 8, 8, 7, 13, 7)   // s3 input conv (50 -> 100): one co tile per wave, 7 waves
+    CONV_FAST_CASE_F32_NARROW(3, 3, 13, 8, 8, 7, 13, 7)  // s3 nodes / output conv, and their dgrad (100 -> 100)
+    CONV_FAST_CASE_F32_NARROW(5, 5, 13, 8, 8, 4, 7, 4)   // s3 input conv dgrad (100 -> 50)
     return -100;
   }
   if (a->prec != 0) return -1;
@@ -1091,7 +1098,11 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_kernel(WgradArgs a) {
 // packed tile, on the M side): a per-band LDS block holds, per pixel, the
 // three dz planes of those channels at row 4c + p, and that tile costs three
 // MFMAs per column tile and K-step (one per input plane) instead of six.
-template <int KH, int KW, int NCBI, int NCBO, int W, int R, int NW, int NB, int PK = 0>
+// NZ > 1 (wide layers: 104 x 936 weights do not fit one workgroup's
+// registers): grid.z splits the k-column tiles into NZ slices, each workgroup
+// stages the same bands and owns its slice; the co tiles are then walked in
+// the outer loop (one dz fragment set live at a time).
+template <int KH, int KW, int NCBI, int NCBO, int W, int R, int NW, int NB, int PK = 0, int NZ = 1>
 __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
   constexpr int NPL = GT_NPL_F32;
   constexpr int NT_ = NW * 64;                     // threads
@@ -1099,13 +1110,14 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
   constexpr int NCH = KH * KW * NCBI;              // weight chunks (8 input channels each)
   constexpr int NKT = (NCH + 1 + 1) / 2;           // 16-column tiles incl. the bias chunk
   constexpr int MT = (NCBO * 8 + 15) / 16;         // output-channel tiles
-  constexpr int TPW = (NKT + NW - 1) / NW;         // k-column tiles per wave
+  constexpr int TPW = ((NKT + NZ - 1) / NZ + NW - 1) / NW;   // k-column tiles per wave (in its slice)
   constexpr int KS = R * W / 32;                   // K-steps per band
   constexpr int XCH = PR * PW * NCBI;              // staged input chunks per band (per plane)
   constexpr int DCH = R * W * NCBO;                // staged dz chunks per band (per plane)
   constexpr int XT = (XCH + NT_ - 1) / NT_, DT = (DCH + NT_ - 1) / NT_;
   constexpr int XROW = NCBI * 16, DROW = NCBO * 16;   // LDS bytes per pixel (one plane)
-  static_assert(R * W % 32 == 0 && (W == 16 || W == 32), "bands must be whole 32-pixel K-steps");
+  constexpr bool MOUT = NZ > 1;                    // co tiles in the outer loop
+  static_assert(R * W % 32 == 0 && (W == 8 || W == 16 || W == 32), "bands must be whole 32-pixel K-steps");
 
   __shared__ __attribute__((aligned(16))) uint4 xs[NB][NPL][XCH];
   __shared__ __attribute__((aligned(16))) uint4 ds[NB][NPL][DCH];
@@ -1116,6 +1128,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int s = blockIdx.x;
+  const int nz0 = NZ > 1 ? (int)blockIdx.z * NW * TPW : 0;       // first column tile of this slice
   const GroupRec gr = group_rec(a.gtab, blockIdx.y, a.n_in, 0, 0, nullptr);
   const int g = gr.g;
   const int nbi = a.H / R;                                     // bands per image
@@ -1207,7 +1220,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
   int xoff[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
-    const int n = wave + NW * t;
+    const int n = nz0 + wave + NW * t;
     int c = 2 * n + (p >> 1);
     if (c >= NCH) c = 0;                                       // bias / padding columns: any valid row
     const int kk = c / NCBI, cb = c % NCBI;
@@ -1233,23 +1246,22 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int xrow_off = ((ks * 32) / W) * PW * XROW;        // compile-time after unrolling
-      uint4 afr[MT][NPL];
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
+      // dz^T fragments of co tile m (three planes, or the packed plane rows)
+      auto load_at = [&](int m, uint4* af) {
         if (PK && m == MT - 1) {
           const char* d0 = reinterpret_cast<const char*>(dpk[cur]) + px0 * 32 + p * 8 + ks * 32 * 32;
-          afr[m][0] = tr_pair(d0, d0 + 4 * 32);
-          continue;
+          af[0] = tr_pair(d0, d0 + 4 * 32);
+          return;
         }
 #pragma unroll
         for (int pl = 0; pl < NPL; ++pl) {
           const char* d0 = reinterpret_cast<const char*>(ds[cur][pl]) + dlane + ks * 32 * DROW + m * 32;
-          afr[m][pl] = tr_pair(d0, d0 + 4 * DROW);
+          af[pl] = tr_pair(d0, d0 + 4 * DROW);
         }
-      }
-      // the next column tile's im2col fragments are read while this tile's MFMAs run
+      };
+      // the im2col fragments of column tile t
       auto load_bt = [&](int t, uint4* bfr) {
-        const int n = wave + NW * t;
+        const int n = nz0 + wave + NW * t;
 #pragma unroll
         for (int pl = 0; pl < NPL; ++pl) {
           const char* x0 = reinterpret_cast<const char*>(xs[cur][pl]) + xrow_off + xoff[t];
@@ -1260,22 +1272,42 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
           bfr[1] = bfr[2] = make_uint4(0, 0, 0, 0);
         }
       };
-      uint4 bfr[2][NPL];
-      load_bt(0, bfr[0]);
+      auto mma = [&](int m, const uint4* af, const uint4* bf, f32x4_t c) {
+        if (PK && m == MT - 1) {
+          c = mfma16(af[0], bf[2], c);
+          c = mfma16(af[0], bf[1], c);
+          return mfma16(af[0], bf[0], c);
+        }
+        return mfma_np<NPL>(af, bf, c);
+      };
+      if constexpr (MOUT) {
+        // all of this wave's column fragments live; co tiles streamed (next one read during the MFMAs)
+        uint4 bfr[TPW][NPL];
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        const int n = wave + NW * t;
-        if (t + 1 < TPW) load_bt(t + 1, bfr[(t + 1) & 1]);
-        if (n >= NKT) continue;
+        for (int t = 0; t < TPW; ++t) load_bt(t, bfr[t]);
+        uint4 af[2][NPL];
+        load_at(0, af[0]);
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
-          if (PK && m == MT - 1) {
-            acc[m][t] = mfma16(afr[m][0], bfr[t & 1][2], acc[m][t]);
-            acc[m][t] = mfma16(afr[m][0], bfr[t & 1][1], acc[m][t]);
-            acc[m][t] = mfma16(afr[m][0], bfr[t & 1][0], acc[m][t]);
-          } else {
-            acc[m][t] = mfma_np<NPL>(afr[m], bfr[t & 1], acc[m][t]);
-          }
+          if (m + 1 < MT) load_at(m + 1, af[(m + 1) & 1]);
+#pragma unroll
+          for (int t = 0; t < TPW; ++t)
+            if (nz0 + wave + NW * t < NKT) acc[m][t] = mma(m, af[m & 1], bfr[t], acc[m][t]);
+        }
+      } else {
+        uint4 afr[MT][NPL];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) load_at(m, afr[m]);
+        // the next column tile's im2col fragments are read while this tile's MFMAs run
+        uint4 bfr[2][NPL];
+        load_bt(0, bfr[0]);
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) {
+          const int n = wave + NW * t;
+          if (t + 1 < TPW) load_bt(t + 1, bfr[(t + 1) & 1]);
+          if (n >= NKT) continue;
+#pragma unroll
+          for (int m = 0; m < MT; ++m) acc[m][t] = mma(m, afr[m], bfr[t & 1], acc[m][t]);
         }
       }
     }
@@ -1290,7 +1322,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
   constexpr int Kdim = NCH * 8;
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
-    const int n = wave + NW * t;
+    const int n = nz0 + wave + NW * t;
     if (n >= NKT) continue;
     const int col = n * 16 + l16;
 #pragma unroll
@@ -1347,6 +1379,20 @@ extern "C" int gt_wgrad_set_nb(int nb) {
     return (int)hipGetLastError();                                                                       \
   }
 
+// wide layers: NZ column slices per (split, group), single band buffer
+#define WGRAD_FAST_CASE_F32Z(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NZ_)                                    \
+  if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->Coutp == NCBO_ * 8 && a->W == W_ &&     \
+      a->H % R_ == 0 && a->pps % (R_ * W_) == 0) {                                                        \
+    dim3 grid(a->S, a->ngroups, NZ_);                                                                    \
+    if (wgrad_pk_ok(a, (NCBO_ * 8 + 15) / 16))                                                           \
+      hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 1, NZ_>), grid,       \
+                         dim3(NW_ * 64), 0, stream, *a);                                                 \
+    else                                                                                                 \
+      hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 0, NZ_>), grid,       \
+                         dim3(NW_ * 64), 0, stream, *a);                                                 \
+    return (int)hipGetLastError();                                                                       \
+  }
+
 // packed last co tile of the fp32 wgrad (A/B switch GENTUN_WGRAD_PK=0 disables)
 static bool wgrad_pk_ok(const WgradArgs* a, int mt) {
   static const int on = std::getenv("GENTUN_WGRAD_PK") ? std::atoi(std::getenv("GENTUN_WGRAD_PK")) : 1;
@@ -1362,6 +1408,8 @@ static int wgrad_rows(int KH, int KW, int Cinp, int Coutp, int H, int W, int pre
     if (KH == 3 && KW == 3 && Cinp == 24 && Coutp == 24 && W == 32 && H % 4 == 0) return 4;
     if (KH == 5 && KW == 5 && Cinp == 24 && Coutp == 56 && W == 16 && H % 4 == 0) return 4;
     if (KH == 3 && KW == 3 && Cinp == 56 && Coutp == 56 && W == 16 && H % 4 == 0) return 4;
+    if (KH == 5 && KW == 5 && Cinp == 56 && Coutp == 104 && W == 8 && H % 4 == 0) return 4;    // deep s3
+    if (KH == 3 && KW == 3 && Cinp == 104 && Coutp == 104 && W == 8 && H % 4 == 0) return 4;
     return 0;
   }
   if (KH == 5 && KW == 5 && Cinp == 8 && Coutp == 24 && W == 32 && H % 8 == 0) return 8;
@@ -1390,7 +1438,8 @@ extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, 
   (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H;
   if (prec == 1) {
     const char* e = getenv("GENTUN_F32_SPLITS16");     // A/B: splits of the 16-wide stage
-    return W >= 32 ? 32 : (e ? atoi(e) : 8);
+    // 8-wide (deep stage 3): 4 splits x 4 column slices per group
+    return W >= 32 ? 32 : W <= 8 ? 4 : (e ? atoi(e) : 8);
   }
   return W >= 32 ? 16 : 3;
 }
@@ -1401,6 +1450,8 @@ extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
     WGRAD_FAST_CASE_F32(3, 3, 3, 3, 32, 4, 4, 1)      // s1 nodes / output conv (20 -> 20)
     WGRAD_FAST_CASE_F32(5, 5, 3, 7, 16, 4, 8, 2)      // s2 input conv (20 -> 50)
     WGRAD_FAST_CASE_F32(3, 3, 7, 7, 16, 4, 8, 2)      // s2 nodes / output conv (50 -> 50)
+    WGRAD_FAST_CASE_F32Z(5, 5, 7, 13, 8, 4, 8, 4)     // deep s3 input conv (50 -> 100)
+    WGRAD_FAST_CASE_F32Z(3, 3, 13, 13, 8, 4, 8, 4)    // deep s3 nodes / output conv (100 -> 100)
     return -100;
   }
   if (a->prec != 0) return -1;

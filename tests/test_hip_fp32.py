@@ -74,6 +74,8 @@ def report(name, ours, torch32):
 
 CONV_SHAPES = [(32, 32, 3, 20, 5, 1), (32, 32, 20, 20, 3, 3), (16, 16, 20, 50, 5, 1), (16, 16, 50, 50, 3, 2),
                (16, 16, 50, 20, 5, 1), (8, 8, 64, 128, 3, 1), (7, 7, 50, 50, 3, 4), (14, 14, 20, 50, 5, 2),
+               # stage 3 of the deep (20,50,100) space: shape-specialised 8x8 kernels
+               (8, 8, 50, 100, 5, 1), (8, 8, 100, 100, 3, 2), (8, 8, 100, 50, 5, 1),
                # wide layers of the deep (64,128,256) space: channel-blocked patch staging
                (8, 8, 256, 256, 5, 1), (8, 8, 256, 100, 5, 2), (16, 16, 128, 128, 5, 3), (32, 32, 64, 64, 5, 2)]
 
@@ -182,7 +184,8 @@ def test_conv_dgrad_fanout_fp32(k, H):
 @pytest.mark.parametrize("H,W,cin,cout,k,nin,first", [(32, 32, 3, 20, 5, 1, True), (32, 32, 20, 20, 3, 1, False),
                                                       (16, 16, 20, 50, 5, 1, False), (16, 16, 50, 50, 3, 2, False),
                                                       (8, 8, 64, 128, 3, 1, False), (14, 14, 50, 50, 3, 3, False),
-                                                      (8, 8, 256, 256, 5, 1, False), (16, 16, 128, 128, 5, 2, False)])
+                                                      (8, 8, 256, 256, 5, 1, False), (16, 16, 128, 128, 5, 2, False),
+                                                      (8, 8, 50, 100, 5, 1, False), (8, 8, 100, 100, 3, 2, False)])
 @pytest.mark.parametrize("pk", [0, 1])
 def test_conv_wgrad_fp32(H, W, cin, cout, k, nin, first, pk):
     """Weight + bias gradient (specialised register-staged kernel and the
