@@ -215,8 +215,9 @@ def run(args):
                    "epochs": list(epochs), "learning_rate": list(lrs), "samples": args.samples,
                    "loss": args.loss, "backend": args.backend or ("hip" if device.type == "cuda" else "torch"),
                    "fold_reset": args.fold_reset, "batch_norm": args.batch_norm, "batching": "keras (8000 = 250 x 32: no short batch)",
-                   "fp32_impl": "fp32 tensors, 3-way exact bf16 split x 6 MFMA terms per product"
-                   if args.dtype == "fp32" else None,
+                   "fp32_impl": ("fp32 tensors, 3-way exact bf16 split x 6 MFMA terms per product"
+                                 if device.type == "cuda" and (args.backend or "hip") == "hip"
+                                 else "stock PyTorch fp32 ops") if args.dtype == "fp32" else None,
                    "streams_per_gpu": args.streams, "pop_batch": args.pop_batch},
         "generations": len(completed),
         "evals": total_evals,
