@@ -88,6 +88,14 @@ def main():
                 f.write(line + "\n")
 
 
+def _teardown(comm):
+    """Every rank leaves the RCCL / gloo group explicitly (after the STOP
+    broadcast): no communicator is left for interpreter shutdown to tear down."""
+    if hasattr(comm, "destroy"):
+        comm.barrier()
+        comm.destroy()
+
+
 def run(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -134,6 +142,7 @@ def run(args):
     if comm.rank != 0:
         # evaluator rank: serves EVAL / SYNC (timing fence) / STOP from rank 0
         GentunWorker(GeneticCnnIndividual, x, y, comm=comm, evaluator=evaluator).work()
+        _teardown(comm)
         return None
 
     grng.seed(args.seed)
@@ -191,6 +200,7 @@ def run(args):
     if not ga.population.pending():
         advance()                                # close the generation the last round finished
     ga.population.shutdown()
+    _teardown(comm)
 
     cph = 3600.0 * timed_evals / elapsed
     last = completed[-1] if completed else None
