@@ -122,8 +122,8 @@ class HipPopJob(FoldJob):
         # conv-layer optimizer updates per layer on a third stream (A/B switch, off:
         # 907 vs 958 candidates/h with it on -- it competes with the dgrad chain,
         # profiles/bench_round_size_r2.txt)
-        self.side3 = torch.cuda.Stream(dev)
         self.adam_overlap = os.environ.get("GENTUN_ADAM_OVERLAP", "0") == "1"
+        self.side3 = torch.cuda.Stream(dev) if self.adam_overlap else None
         self._build_adam_table()
         self._build_args()
 

@@ -9,5 +9,5 @@ timeout -k 10 900 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-metho
 tail -3 gpurun_out/gpu_tests.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -2 gpurun_out/smoke.log | cut -c1-300
-timeout -k 10 600 python -u bench.py --gpus 1 --steps 5 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 3 --warmup 1 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
