@@ -42,6 +42,12 @@ struct BnArgs {
   float momentum, eps;
   int train;                // 1: batch statistics (training forward); 0: running statistics
   int prec;
+  // fused 2x2 max-pool (K1/K4 with BatchNorm: conv -> BN -> ReLU -> pool): groups whose GroupRec
+  // out_mask bit 24 is set pool this layer's output into pool_y [Q][B][H/2][W/2][Cp] and the argmax
+  // mask (pool_fwd_kernel's format; null in evaluation). Chunks hold whole row pairs (chunk_px % 2W == 0).
+  void* pool_y;
+  uint8_t* pool_mask;
+  int W;
 };
 
 #define BN_THREADS 256
@@ -165,6 +171,45 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(BnArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[c8 * 8 + e] + sh[c8 * 8 + e], 0.f);
     st_chunk(y + p * Cp + c8 * 8, v);
+  }
+  if (!a.pool_y || !((r.out_mask >> 24) & 1)) return;
+  // pooled cells of this chunk, from z (the values exactly as stored in y: bf16-rounded in prec 0);
+  // first strict maximum over (0,0), (0,1), (1,0), (1,1), bit 2 = maximum > 0
+  const int W = a.W, Wo = W >> 1;
+  AT* py = reinterpret_cast<AT*>(a.pool_y) + (long)g * a.B * (a.HW >> 2) * Cp;
+  uint8_t* pm = a.pool_mask ? a.pool_mask + (long)g * a.B * (a.HW >> 2) * Cp : nullptr;
+  const long rp0 = p0 / (2 * W);                   // first row pair of the chunk (flat over images)
+  const long ncell = (p1 - p0) >> 2;
+  for (long i = t; i < ncell * nc8; i += BN_THREADS) {
+    const long k = i / nc8;
+    const int c8 = (int)(i % nc8);
+    const long rp = rp0 + k / Wo;
+    const int pc = (int)(k % Wo);
+    const long ptl = rp * 2 * W + 2 * pc;          // top-left pixel
+    const long offs[4] = {0, 1, (long)W, (long)W + 1};
+    float m[8], v[8];
+    int arg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ld_chunk(z + (ptl + offs[q]) * Cp + c8 * 8, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float o = fmaxf(v[e] * sc[c8 * 8 + e] + sh[c8 * 8 + e], 0.f);
+        if constexpr (!PREC) o = bf2f(f2bf(o));
+        if (q == 0) m[e] = o;
+        else if (o > m[e]) { m[e] = o; arg[e] = q; }
+      }
+    }
+    const long o = (rp * Wo + pc) * Cp + c8 * 8;
+    st_chunk(py + o, m);
+    if (pm) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lo |= (uint32_t)(arg[j] | (m[j] > 0.f ? 4 : 0)) << (8 * j);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hi |= (uint32_t)(arg[4 + j] | (m[4 + j] > 0.f ? 4 : 0)) << (8 * j);
+      *reinterpret_cast<uint2*>(pm + o) = make_uint2(lo, hi);
+    }
   }
 }
 

@@ -311,13 +311,15 @@ class HipPopJob(FoldJob):
         a.wps = w[0].numel()                 # weights are [planes][...]
         return a
 
-    def _bn_args(self, L, train):
+    def _bn_args(self, L, train, pools=()):
+        """``pools``: groups whose pool source is this layer (fused BN -> ReLU -> 2x2 max-pool)."""
         a = K.BnArgs()
         a.z, a.y = self.zpre[L.name].data_ptr(), self.act[L.name].data_ptr()
         a.gamma, a.beta = L.gamma[0].data_ptr(), L.beta[0].data_ptr()
         a.stat, a.run, a.part = L.bn_stat.data_ptr(), L.bn_run.data_ptr(), L.bn_part.data_ptr()
         a.ggamma, a.gbeta = L.g_gamma.data_ptr(), L.g_beta.data_ptr()
-        a.gtab = self._gtab([(q, 0, 0) for q, _ in L.rows]).data_ptr()
+        a.gtab = self._gtab([(q, 0, (1 << 24) if q in pools else 0) for q, _ in L.rows]).data_ptr()
+        a.W = L.W
         a.valid = self.epoch_valid.data_ptr()
         a.st = self.state.data_ptr()
         a.ngroups, a.G, a.B, a.HW, a.Cp = len(L.rows), self.Q, self.B, L.H * L.W, L.coutp
@@ -328,7 +330,8 @@ class HipPopJob(FoldJob):
 
     def _stage_fwd_ops(self, st, gather_train, fuse):
         """Forward launches of one stage; ``fuse``: each group's pool source
-        conv also writes the pooled output and the argmax mask."""
+        conv (with BatchNorm: its BN-apply launch) also writes the pooled
+        output and the argmax mask."""
         src = self.sched.pool_source(st)
         x1 = self.sched.pool_x1(st)
         pool_of = {}
@@ -340,18 +343,22 @@ class HipPopJob(FoldJob):
             first = L.slots == ["input"]
             out = self.zpre[L.name] if self.bn else self.act[L.name]
             pools = pool_of.get(L.name, set())
+            cpools = set() if self.bn else pools
             a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [out.data_ptr()], [],
                                 L.w_bf, L.b[0], 0 if self.bn else 1,
-                                [(q, im, 1 | ((1 << 24) if q in pools else 0)) for q, im in L.rows],
+                                [(q, im, 1 | ((1 << 24) if q in cpools else 0)) for q, im in L.rows],
                                 gather=gather_train if first else None)
             if L.xin is not None:
                 a.xsum = self.act[L.xin].data_ptr()
             a.epi_bf16 = 1            # forward outputs never accumulate: bf16 output tile
-            if pools:
+            if cpools:
                 a.pool_y, a.pool_mask = self.act[st.pool].data_ptr(), st.pmask.data_ptr()
             ops.append(("conv", a, L))
             if self.bn:
-                ops.append(("bn", self._bn_args(L, 1), L))
+                b = self._bn_args(L, 1, pools)
+                if pools:
+                    b.pool_y, b.pool_mask = self.act[st.pool].data_ptr(), st.pmask.data_ptr()
+                ops.append(("bn", b, L))
         return ops
 
     def _slot_ptr(self, name, grad=False):
@@ -373,10 +380,12 @@ class HipPopJob(FoldJob):
         L_ = self.L
         fast_on = L_.gt_conv_set_fast(1)
         L_.gt_conv_set_fast(fast_on)
-        fuse_ok = (not self.bn) and fast_on and os.environ.get("GENTUN_POOL_FUSE", "1") != "0"
+        fuse_env = os.environ.get("GENTUN_POOL_FUSE", "1") != "0"
         self.pool_fused = []
         for st in self.stages:
             hh, ww, cc = self.shapes[st.inp]
+            # with BatchNorm the pool runs in the BN-apply launch (its chunks hold whole row pairs)
+            fuse_ok = fuse_env and (K.BN_CHUNK_PX % (2 * ww) == 0 and hh % 2 == 0 if self.bn else fast_on)
             sel = torch.tensor(self.sched.pool_source(st), dtype=torch.int32, device=self.device)
             self._keep.append(sel)
             st.sel = sel
@@ -384,8 +393,8 @@ class HipPopJob(FoldJob):
             # instead of the 4 inputs of every cell
             st.pmask = torch.zeros((Q * B, hh // 2, ww // 2, cc), dtype=torch.uint8, device=self.device)
             ops = self._stage_fwd_ops(st, gather_train, fuse=fuse_ok)
-            fused = fuse_ok and all(L_.gt_conv_fast_probe(a) > 0 for kind, a, _ in ops
-                                    if kind == "conv" and a.pool_y)
+            fused = fuse_ok and (self.bn or all(L_.gt_conv_fast_probe(a) > 0 for kind, a, _ in ops
+                                                if kind == "conv" and a.pool_y))
             if not fused:
                 ops = self._stage_fwd_ops(st, gather_train, fuse=False)
                 x1 = self.act[self.sched.pool_x1(st)]
@@ -730,6 +739,7 @@ class HipPopJob(FoldJob):
             elif kind == "bn":
                 b = K.BnArgs.from_buffer_copy(a)
                 b.train = 0                          # running statistics
+                b.pool_mask = 0                      # fused pool: output only
                 ops.append((kind, b, Lr))
             else:
                 ops.append((kind, a, None))          # no argmax mask in evaluation

@@ -94,7 +94,8 @@ class BnArgs(C.Structure):
     _fields_ = [("z", P), ("y", P), ("gamma", P), ("beta", P), ("stat", P), ("run", P), ("part", P),
                 ("ggamma", P), ("gbeta", P), ("gtab", P), ("valid", P), ("st", P),
                 ("ngroups", I), ("G", I), ("B", I), ("HW", I), ("Cp", I), ("nchunk", I), ("chunk_px", I),
-                ("momentum", C.c_float), ("eps", C.c_float), ("train", I), ("prec", I)]
+                ("momentum", C.c_float), ("eps", C.c_float), ("train", I), ("prec", I),
+                ("pool_y", P), ("pool_mask", P), ("W", I)]
 
 
 BN_CHUNK_PX = 512     # pixels per BatchNorm workgroup (fixed per shape: batch-invariant sums)

@@ -129,10 +129,12 @@ def test_sequential_folds_population_invariance(dtype):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_fused_pool_matches_separate_pool_kernel(dtype, monkeypatch):
+@pytest.mark.parametrize("bn", [False, True])
+def test_fused_pool_matches_separate_pool_kernel(dtype, bn, monkeypatch):
     """K4: the 2x2 max-pool + argmax mask fused into the pool-source conv's
-    epilogue, and the pool backward fused into the data gradients that
-    produce the pool gradients (next stage's input conv, dense layer), give
+    epilogue (with BatchNorm: into the BN-apply launch, conv -> BN -> ReLU ->
+    pool), and the pool backward fused into the data gradients that produce
+    the pool gradients (next stage's input conv, dense layer), give
     bit-identical training to the separate pool kernels."""
     import numpy as np
     import torch
@@ -145,7 +147,8 @@ def test_fused_pool_matches_separate_pool_kernel(dtype, monkeypatch):
     genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '000', 'S_2': '0000000000'},
              {'S_1': '111', 'S_2': '0000000001'}]
     members = [(make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10), folds, [0, 1]) for g in genes]
-    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype=dtype, reset="all", use_graph=False)
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype=dtype, reset="all", use_graph=False,
+                        batch_norm=bn)
     out = {}
     for fuse in ("1", "0"):
         monkeypatch.setenv("GENTUN_POOL_FUSE", fuse)
