@@ -1342,6 +1342,45 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
   }
 }
 
+// Split-K reduction of a wgrad launch's partials, launched right after it on
+// the weight-gradient stream: split 0 <- sum over splits in split order
+// (adam_segments' order, so the update is bit-identical); the optimizer at the
+// end of the step then reads one gradient instead of S partials. Grid
+// (chunks of 4 elements per thread, launch groups).
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgradArgs a) {
+  const GroupRec gr = group_rec(a.gtab, blockIdx.y, a.n_in, 0, 0, nullptr);
+  const int g = gr.g;
+  const long kd = (long)a.KH * a.KW * a.Cinp;
+  const long n = (long)a.Coutp * kd;
+  const long gs = (long)a.G * n;                   // split stride of part_w
+  float* pw = a.part_w + (long)g * n;
+  const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i4 < n) {                                    // n % 4 == 0 (Cinp % 8 == 0)
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < a.S; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(pw + (long)sp * gs + i4);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *reinterpret_cast<float4*>(pw + i4) = acc;
+  }
+  if (blockIdx.x == 0 && a.part_b) {
+    float* pb = a.part_b + (long)g * a.Coutp;
+    for (int i = threadIdx.x; i < a.Coutp; i += 256) {
+      float acc = 0.f;
+      for (int sp = 0; sp < a.S; ++sp) acc += pb[(long)sp * a.G * a.Coutp + i];
+      pb[i] = acc;
+    }
+  }
+}
+
+extern "C" int gt_wgrad_reduce(const WgradArgs* a, hipStream_t stream) {
+  const long n = (long)a->Coutp * a->KH * a->KW * a->Cinp;
+  if (n % 4 || a->S < 2) return -1;
+  dim3 grid((unsigned)((n / 4 + 255) / 256), a->ngroups);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, grid, dim3(256), 0, stream, *a);
+  return (int)hipGetLastError();
+}
+
 static int g_wgrad_nb = 0;   // 0: per-shape default, 1 / 2: force band buffers (A/B switch)
 
 extern "C" int gt_wgrad_set_nb(int nb) {

@@ -139,8 +139,11 @@ class HipPopJob(FoldJob):
             L.cinp, L.coutp = pad8(L.cin), pad8(L.cout)
             L.Kdim = L.KH * L.KW * L.cinp
             L.TH = K.conv_tile_rows(L.H, L.W)
-            L.pps, L.S = K.wgrad_split(self.B * L.H * L.W, L.Kdim, L.coutp,
-                                       band=K.wgrad_band(L.KH, L.KW, L.cinp, L.coutp, L.H, L.W, self.prec))
+            band = K.wgrad_band(L.KH, L.KW, L.cinp, L.coutp, L.H, L.W, self.prec)
+            L.pps, L.S = K.wgrad_split(self.B * L.H * L.W, L.Kdim, L.coutp, band=band)
+            # split-K partials summed by a reduce launch right after the layer's wgrad, on the
+            # weight-gradient stream (off the data-gradient chain); the optimizer then reads one gradient
+            L.wred = L.S > 1 and (L.coutp * L.Kdim) % 4 == 0 and os.environ.get("GENTUN_WGRAD_REDUCE", "1") != "0"
         self.last = self.sched.last
         hs, ws = h0 >> len(p0.kernels_per_layer), w0 >> len(p0.kernels_per_layer)
         if hs < 1 or ws < 1:
@@ -267,10 +270,11 @@ class HipPopJob(FoldJob):
             b0 = len(blocks)
             for q, _ in L.rows:
                 p, m, v = (t[q] for t in L.w)
-                add(p, m, v, L.part_w[0, q], L.S, L.part_w[0].numel(), bf=L.w_bf[0, q], bfT=L.wT_bf[0, q],
+                S = 1 if L.wred else L.S            # reduced into split 0 by gt_wgrad_reduce
+                add(p, m, v, L.part_w[0, q], S, L.part_w[0].numel(), bf=L.w_bf[0, q], bfT=L.wT_bf[0, q],
                     tdims=(1, L.coutp, L.KH, L.KW, L.cinp), pstrides=(L.w_bf[0].numel(), L.wT_bf[0].numel()))
                 p, m, v = (t[q] for t in L.b)
-                add(p, m, v, L.part_b[0, q], L.S, L.part_b[0].numel())
+                add(p, m, v, L.part_b[0, q], S, L.part_b[0].numel())
                 if self.bn:
                     for t, g in ((L.gamma, L.g_gamma), (L.beta, L.g_beta)):
                         p, m, v = (x[q] for x in t)
@@ -691,6 +695,8 @@ class HipPopJob(FoldJob):
             if kind == "wgrad":
                 fork(side)
                 K.check(L.gt_conv_wgrad(a, ss), "conv_wgrad")
+                if Lr.wred:
+                    K.check(L.gt_wgrad_reduce(a, ss), "wgrad_reduce")
             elif kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
             elif kind == "bn_bwd":

@@ -153,6 +153,8 @@ def lib():
         L.gt_conv_fast_probe.restype = I
         L.gt_conv_fast_probe_any.argtypes = [C.POINTER(ConvArgs)]
         L.gt_conv_fast_probe_any.restype = I
+        L.gt_wgrad_reduce.argtypes = [C.POINTER(WgradArgs), P]
+        L.gt_wgrad_reduce.restype = I
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
         L.gt_conv_set_nwv.argtypes = [I]
