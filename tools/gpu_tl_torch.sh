@@ -11,6 +11,7 @@ python3 tools/timeline.py "$f" > gpurun_out/timeline/summary_p5.txt
 s=$(find /tmp/tl -name "*kernel_stats.csv" | head -1)
 cp "$s" gpurun_out/timeline/kernel_stats_p5.csv
 head -30 gpurun_out/timeline/summary_p5.txt
+[ -z "$TORCHCMP" ] && exit 0
 timeout -k 10 900 python -u bench.py --gpus 1 --backend torch --per-gpu 2 --steps 1 --warmup 0 \
   > gpurun_out/bench_torch.json 2> gpurun_out/bench_torch.err || { tail -20 gpurun_out/bench_torch.err; exit 1; }
 cat gpurun_out/bench_torch.json
