@@ -5,27 +5,33 @@ Genetic-CNN CIFAR-10 1/2/4/8 GPU" -- the reference's paper-replica search
 
 What runs: the real Russian-roulette GA (RussianRouletteGA, pC 0.2 / pM 0.8;
 individuals qC 0.3 / qM 0.1) over Genetic-CNN S=(3,5) candidates (kernels
-(20,50), 5x5 stage convs, dense 500, dropout 0.5, 10 classes), population
-``32 x N`` (weak scaling: 32 individuals per GPU), every evaluation the full
-reference protocol: stratified 5-fold CV on 10,000 synthetic 32x32x3 samples,
-epochs (20,4,1) with lr (1e-3,1e-4,1e-5), Adam, batch 32, Keras
-softmax + binary_crossentropy loss, **fp32** (the reference's TF float32;
-HIP kernels compute every product as the exact 3-way bf16 split on the
-matrix cores, fp32-level error: tests/test_hip_fp32.py). Random-init
-weights, synthetic learnable data (no network).
+(20,50), 5x5 stage convs, dense 500, dropout 0.5, 10 classes) at BASELINE
+config 3's shape: population 32 IN TOTAL over the N evaluator ranks
+(``--population``; strong scaling; ``--pop-per-gpu`` gives the weak-scaling
+variant). Every evaluation is the reference's training protocol: 5-fold CV on
+10,000 synthetic 32x32x3 samples, epochs (20,4,1) with lr (1e-3,1e-4,1e-5),
+Adam, batch 32, Keras softmax + binary_crossentropy loss, **fp32** (the
+reference's TF float32; HIP kernels compute every product as the exact 3-way
+bf16 split on the matrix cores, fp32-level error: tests/test_hip_fp32.py).
+Random-init weights, synthetic data (no network).
 
-One bench *step* = one evaluation round of the GA: the next ``per_gpu x N``
-pending individuals of the current generation are dispatched over the N
-evaluator ranks (one per GPU; RCCL broadcast of the genome table,
+Fold semantics (``--fold-reset``): ``all`` (default, the fast mode) trains
+the 5 folds of a candidate CONCURRENTLY, each from fresh weights;
+``kernels`` is the reference's protocol -- folds in sequence, kernels
+re-drawn per fold, biases carried over (keras_models.py:120-125,132-142) --
+and is the library default. Both train the same number of steps.
+
+One bench *step* = one evaluation round of the GA: the pending individuals of
+the current generation are cut into near-equal rounds of at most
+``per_gpu x N`` (``DistributedPopulation.evaluate_round``), dispatched over the
+N evaluator ranks (one per GPU; RCCL broadcast of the genome table,
 all_gather of per-fold scores) and trained population-batched on each GPU.
-When a generation has no pending individuals left, rank 0 breeds the next
-one (selection / crossover / mutation on the host, milliseconds) and the
-following rounds evaluate it. Rounds keep the step time bounded (a whole
-generation of 14+ full 5-fold trainings per GPU would take minutes).
-``value`` = candidates fully evaluated in the K timed rounds / timed hours,
-over the whole job; ``best_val_acc_at_gen`` = categorical validation
-accuracy (5-fold mean) of the fittest individual of the last completed
-generation (fitness itself is the reference's binary accuracy).
+When a generation has no pending individuals left, rank 0 breeds the next one
+(selection / crossover / mutation on the host, milliseconds). ``value`` =
+candidates fully evaluated in the K timed rounds / timed hours, over the
+whole job; ``best_val_acc_at_gen`` = categorical validation accuracy (5-fold
+mean) of the fittest individual of the last completed generation (fitness
+itself is the reference's binary accuracy).
 
 Run: ``python bench.py --gpus 1 --steps 2 --warmup 1`` or, for N>1,
 ``torchrun --nproc-per-node N bench.py --gpus N ...``.
@@ -47,7 +53,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--per-gpu", type=int, default=None,
                     help="candidates per GPU per round (default: 5 fp32 / 8 bf16; larger rounds = larger population launches: 794 / 862 / 936 candidates/h at 3 / 4 / 6, profiles/bench_round_size_r2.txt)")
-    ap.add_argument("--pop-per-gpu", type=int, default=32, help="GA population per GPU")
+    ap.add_argument("--population", type=int, default=32,
+                    help="GA population in total (BASELINE cfg 3: 32 on 8 evaluators; strong scaling)")
+    ap.add_argument("--pop-per-gpu", type=int, default=None,
+                    help="GA population per GPU instead (weak scaling: population = pop_per_gpu x N)")
     ap.add_argument("--streams", type=int, default=1, help="concurrent population jobs per GPU")
     ap.add_argument("--pop-batch", type=int, default=16, help="candidates (x folds) per population job")
     ap.add_argument("--backend", default=None, help="hip (default on GPU) or torch")
@@ -146,7 +155,8 @@ def run(args):
         return None
 
     grng.seed(args.seed)
-    pop = DistributedPopulation(GeneticCnnIndividual, x, y, size=args.pop_per_gpu * N, crossover_rate=0.3,
+    population = args.pop_per_gpu * N if args.pop_per_gpu else args.population
+    pop = DistributedPopulation(GeneticCnnIndividual, x, y, size=population, crossover_rate=0.3,
                                 mutation_rate=0.1, additional_parameters=extra, comm=comm, evaluator=evaluator)
     ga = RussianRouletteGA(pop, crossover_probability=0.2, mutation_probability=0.8, seed=args.seed,
                            verbose=False)
@@ -177,12 +187,13 @@ def run(args):
     def one_round():
         if not ga.population.pending():
             advance()
-        n = ga.population.evaluate_in_parallel(limit=round_size)
+        n = ga.population.evaluate_round(per_gpu)
         track()
         return n
 
     total_evals = 0
     timed_evals = 0
+    round_sizes = []
     t_start = None
     for step in range(args.warmup + args.steps):
         if step == args.warmup:
@@ -192,6 +203,7 @@ def run(args):
         total_evals += n
         if step >= args.warmup:
             timed_evals += n
+            round_sizes.append(n)
         print("[bench] step {} gen {} evaluated {} ({}) dispatch={}".format(
             step, ga.generation, n, "timed" if step >= args.warmup else "warmup",
             ga.population.last_dispatch), file=sys.stderr, flush=True)
@@ -213,21 +225,24 @@ def run(args):
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * elapsed / max(1, args.steps), 2),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.pop_per_gpu else "strong",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (CIFAR-10-shaped {}k x 32x32x3 coloured stroke glyphs + clutter + noise; "
                 "random-init weights)".format(args.samples // 1000),
         "config": {"model": "Genetic-CNN {} dense 500".format(space), "global_batch": 32 * args.nfold,
-                   "seq_len": None, "parallelism": "population-dp{} (RCCL genome bcast / score all_gather)".format(N),
-                   "algorithm": "RussianRouletteGA pC0.2 pM0.8 qC0.3 qM0.1", "population": args.pop_per_gpu * N,
-                   "candidates_per_round": round_size, "per_gpu": per_gpu, "nfold": args.nfold,
+                   "seq_len": None,
+                   "parallelism": ("population-dp{} (RCCL genome bcast / score all_gather over xGMI)".format(N)
+                                   if N > 1 else "population-dp1 (single evaluator, no collectives)"),
+                   "algorithm": "RussianRouletteGA pC0.2 pM0.8 qC0.3 qM0.1", "population": population,
+                   "population_total": population, "max_candidates_per_round": round_size,
+                   "per_gpu": per_gpu, "rounds": round_sizes, "nfold": args.nfold,
                    "epochs": list(epochs), "learning_rate": list(lrs), "samples": args.samples,
                    "loss": args.loss, "backend": args.backend or ("hip" if device.type == "cuda" else "torch"),
                    "fold_reset": args.fold_reset, "batch_norm": args.batch_norm, "batching": "keras (8000 = 250 x 32: no short batch)",
                    "fp32_impl": ("fp32 tensors, 3-way exact bf16 split x 6 MFMA terms per product"
                                  if device.type == "cuda" and (args.backend or "hip") == "hip"
-                                 else "stock PyTorch fp32 ops") if args.dtype == "fp32" else None,
+                                 else "stock PyTorch fp32 ops (MIOpen / hipBLASLt)") if args.dtype == "fp32" else None,
                    "streams_per_gpu": args.streams, "pop_batch": args.pop_batch},
         "generations": len(completed),
         "evals": total_evals,

@@ -722,6 +722,427 @@ conv_f32p_kernel(ConvArgs a, int ntiles) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// fp32 (prec 1), "duo": one persistent workgroup of 8 waves per CU = two
+// TEAMS of 4 waves, each the 4-wave geometry of conv_fast_kernel with its own
+// 3-plane patch buffer in LDS (2 x 60 KB for the 16-wide 3x3 stage), walking
+// the workgroup's tiles alternately (team 0: tiles 0, 2, 4, ...; team 1:
+// 1, 3, 5, ...) in lock-step PHASES separated by one s_barrier:
+//
+//   phase k:  team (k & 1) runs the MFMA loop of tile k from its buffer,
+//             the other team stores tile k-1 (straight from its accumulators)
+//             and stages tile k+1 (global loads -> exact 3-way split -> LDS)
+//             into the buffer it just finished reading.
+//
+// Every SIMD holds one wave of each team, so the matrix pipe runs one team's
+// k loop while the other team's loads, splits, LDS writes and stores use the
+// vector / memory pipes: the tile kernel ran those phases back to back (its
+// time ~= MFMA time + memory time, profiles/conv_f32_phases_r2.txt); here a
+// tile costs ~max of the two. No team-internal synchronisation is needed:
+// the epilogue is register-direct (16-byte stores of 4 channels per lane; the
+// fused 2x2 max-pool and its argmax mask from lane shuffles and the paired
+// pixel-group register -- a wave's pixel groups cover whole row pairs), and a
+// buffer is only written by the team that reads it, one barrier apart.
+// Results are bit-identical to conv_fast_kernel (same k order, same MFMA
+// sequence, same epilogue arithmetic): tests/test_hip_duo.py.
+// ---------------------------------------------------------------------------
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int PK>
+struct DuoCfg {
+  static constexpr int NPL = GT_NPL_F32;
+  static constexpr int PH = TH + KH - 1, PW = W + KW - 1;
+  static constexpr int NP = PH * PW * NCBI;          // patch chunks per plane
+  static constexpr int NCH = KH * KW * NCBI;
+  static constexpr int NKS = (NCH + 3) / 4;
+  static constexpr int BUF = NPL * NP;               // chunks per team buffer
+  static constexpr size_t LDS = (size_t)2 * BUF * 16 + (size_t)NKS * 4 * 4;
+  // the register-direct epilogue fuses the 2x2 pool when a wave's pixel groups cover whole row pairs
+  static constexpr bool poolable() {
+    constexpr int CT = PK ? NT : ((NT >= 2 && NT % 2 == 0) ? 2 : 1);
+    constexpr int PG = (TH * W / 16) / (4 / (NT / CT));
+    return TH % 2 == 0 && PG % (2 * (W / 16)) == 0;
+  }
+};
+
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int PK>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
+conv_duo_f32_kernel(ConvArgs a, int ntiles) {
+  using DC = DuoCfg<KH, KW, NCBI, W, TH, NT, NCO, PK>;
+  constexpr int NPL = DC::NPL, PW = DC::PW, NP = DC::NP, NCH = DC::NCH, NKS = DC::NKS, BUF = DC::BUF;
+  constexpr int TNT = 256;                                 // threads per team
+  constexpr int NPT = (NP + TNT - 1) / TNT;                // patch chunks per thread
+  constexpr int TP = TH * W;
+  constexpr int NPG = TP / 16;
+  constexpr int CT = PK ? NT : ((NT >= 2 && NT % 2 == 0) ? 2 : 1);
+  constexpr int WC = NT / CT;
+  constexpr int WP = 4 / WC;
+  constexpr int PG = NPG / WP;
+  constexpr int PF = NKS < 2 ? NKS : 2;
+  constexpr int COP = NCO * 8;                             // padded output channels (tensor row)
+  static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == 4, "tile shape");
+  static_assert(!PK || WC == 1, "packed last tile: every wave owns all co tiles");
+  static_assert(W % 16 == 0, "pixel groups of one image row");
+  // pool pairing: rows r, r+1 of a wave's pixel groups are groups h, h + W/16
+  constexpr int RG = W / 16;                               // pixel groups per image row
+  constexpr bool POOLABLE = DC::poolable();
+  static_assert(POOLABLE == ((PG % (2 * RG)) == 0 && TH % 2 == 0), "pool pairing");
+
+  extern __shared__ __attribute__((aligned(16))) uint4 smem[];   // [2][BUF] patch buffers, then coff
+  int* coff = reinterpret_cast<int*>(smem + 2 * BUF);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  const int team = wave >> 2, twave = wave & 3, ttid = tid & (TNT - 1);
+  uint4* patch = smem + team * BUF;
+
+  for (int c = tid; c < NKS * 4; c += 512) {
+    const int kk = c / NCBI, cb = c % NCBI;
+    coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
+  }
+  // XCD-aware: the hardware deals consecutive workgroups to consecutive XCDs;
+  // virtual id v gives every XCD a contiguous range of tiles (a few groups'
+  // weights per L2), and each workgroup a contiguous run of tiles
+  const int nwg = gridDim.x;
+  int v = blockIdx.x;
+  if ((nwg & 7) == 0) v = (v & 7) * (nwg >> 3) + (v >> 3);
+  const int t_begin = (int)(((long)v * ntiles) / nwg), t_end = (int)(((long)(v + 1) * ntiles) / nwg);
+  const int nloc = t_end - t_begin;
+
+  const int nband = a.H / TH;
+  const int tpg = a.B * nband;                             // tiles per launch group
+  const long img = (long)a.H * W * NCBI * 8;
+  const long oimg = (long)a.H * W * COP;
+  struct Tile { GroupRec gr; int b, h0; };
+  auto tile_of = [&](int t) {
+    Tile x;
+    const int q = t / tpg, r = t - q * tpg;
+    x.gr = group_rec(a.gtab, q, a.n_in, a.n_out, a.acc_flags, a.out_mask);
+    x.b = r / nband;
+    x.h0 = (r - x.b * nband) * TH;
+    return x;
+  };
+
+  // ---- staging (memory phase of a team) ------------------------------------
+  int pdh[NPT], pdw[NPT], pcb[NPT];
+#pragma unroll
+  for (int j = 0; j < NPT; ++j) {
+    const int i = ttid + TNT * j;
+    const int pix = i / NCBI;
+    pcb[j] = i % NCBI;
+    pdh[j] = pix / PW - KH / 2;
+    pdw[j] = pix % PW - KW / 2;
+  }
+  float xr[NPT][8];
+  auto stage_issue = [&](const Tile& x) {                 // first input slot / gathered image -> xr
+    const float* src = a.gather
+        ? static_cast<const float*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + x.gr.g) * a.B + x.b] * img
+        : static_cast<const float*>(a.in[__builtin_ctz(x.gr.in_mask | 0x100) & 7]) + ((long)x.gr.g * a.B + x.b) * img;
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int hh = x.h0 + pdh[j], ww = pdw[j];
+      const bool ok = ttid + TNT * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
+      if (ok) load8f(src + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, xr[j]);
+    }
+  };
+  auto stage_finish = [&](const Tile& x, uint4* buf) {    // other DAG inputs, split, LDS, xsum
+    const int first = __builtin_ctz(x.gr.in_mask | 0x100) & 7;
+    const bool multi = !a.gather && __builtin_popcount(x.gr.in_mask) > 1;
+    const long gimg = ((long)x.gr.g * a.B + x.b) * img;
+    if (multi) {
+      for (int k = first + 1; k < GT_MAXSLOT; ++k) {
+        if (!((x.gr.in_mask >> k) & 1)) continue;
+        const float* sk = static_cast<const float*>(a.in[k]) + gimg;
+#pragma unroll
+        for (int j = 0; j < NPT; ++j) {
+          const int hh = x.h0 + pdh[j], ww = pdw[j];
+          if (ttid + TNT * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W) {
+            float t8[8];
+            load8f(sk + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, t8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xr[j][e] += t8[e];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const int i = ttid + TNT * j;
+      if (i >= NP) continue;
+      split8(xr[j], buf[i], buf[NP + i], buf[2 * NP + i]);
+      if (multi && a.xsum) {
+        const int hh = x.h0 + pdh[j], ww = pdw[j];
+        if (pdh[j] >= 0 && pdh[j] < TH && hh < a.H && ww >= 0 && ww < W)      // band interior
+          store8f(static_cast<float*>(a.xsum) + gimg + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, xr[j]);
+      }
+    }
+  };
+
+  // ---- MFMA phase -----------------------------------------------------------
+  const int wco = (twave % WC) * CT;
+  const int pgw = (twave / WC) * PG;
+  const int lbase = ((l16 / W) * PW + (l16 % W)) * NCBI;
+  const int gbase = (((pgw * 16) / W) * PW + (pgw * 16) % W) * NCBI;
+  f32x4_t acc[CT][PG];
+  auto compute = [&](const Tile& x, const uint4* buf) {
+    const int g = x.gr.g;
+    const uint16_t* wrow[CT];
+    bool wok[CT];
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      if (PK && t == CT - 1) {
+        const int co = (wco + t) * 16 + (l16 >> 2), pl = l16 & 3;
+        wok[t] = pl < 3 && co < a.cout_real;
+        wrow[t] = a.w + ((long)g * COP + (wok[t] ? co : 0)) * (NCH * 8) + (wok[t] ? pl : 0) * a.wps;
+        continue;
+      }
+      const int co = (wco + t) * 16 + l16;
+      wok[t] = co < COP;
+      wrow[t] = a.w + ((long)g * COP + (wok[t] ? co : 0)) * (NCH * 8);
+    }
+    uint4 areg[PF][CT][NPL];
+    auto load_a = [&](int s, uint4 (*dst)[NPL]) {
+      const int c = s * 4 + kq;
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int p = 0; p < ((PK && t == CT - 1) ? 1 : NPL); ++p)
+          dst[t][p] = (wok[t] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[t] + p * a.wps + c * 8)
+                                           : make_uint4(0, 0, 0, 0);
+    };
+    auto mma = [&](int t, const uint4* af, const uint4* bf, f32x4_t c) {
+      if (PK && t == CT - 1) {
+        c = mfma16(af[0], bf[2], c);
+        c = mfma16(af[0], bf[1], c);
+        return mfma16(af[0], bf[0], c);
+      }
+      return mfma_np<NPL>(af, bf, c);
+    };
+    auto load_b = [&](int s, uint4 (*dst)[NPL]) {
+      const uint4* pb = buf + lbase + gbase + coff[s * 4 + kq];
+#pragma unroll
+      for (int h = 0; h < PG; ++h) {
+        const int p = h * 16;
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) dst[h][q] = pb[q * NP + ((p / W) * PW + (p % W)) * NCBI];
+      }
+    };
+#pragma unroll
+    for (int s = 0; s < PF; ++s) load_a(s, areg[s]);
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int h = 0; h < PG; ++h) acc[t][h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    if (a.dbg & 1) return;
+    uint4 bfr[2][PG][NPL];
+    load_b(0, bfr[0]);
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      if (s + 1 < NKS) load_b(s + 1, bfr[(s + 1) & 1]);
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int h = 0; h < PG; ++h) acc[t][h] = mma(t, areg[s % PF][t], bfr[s & 1][h], acc[t][h]);
+      if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
+    }
+  };
+
+  // ---- epilogue straight from the accumulators -------------------------------
+  // lane: channels co0..co0+3 of pixel p = (pgw + h) * 16 + l16 of the tile
+  auto epilogue = [&](const Tile& x) {
+    if (a.dbg & 2) return;
+    const int g = x.gr.g;
+    const long n = (long)g * a.B + x.b;
+    const long obase = n * oimg + (long)x.h0 * W * COP;
+    const bool pool = a.pool_y && ((x.gr.out_mask >> 24) & 1);
+    const bool unpool = (x.gr.out_mask >> 25) & 1;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      const bool pkt = PK && t == CT - 1;
+      const int co0 = (wco + t) * 16 + kq * 4;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (a.bias) {
+        if (pkt) {
+          const int co = (wco + t) * 16 + kq;
+          bv[0] = co < COP ? a.bias[(long)g * COP + co] : 0.f;
+        } else if (co0 < COP) {
+          const float4 q = *reinterpret_cast<const float4*>(a.bias + (long)g * COP + co0);
+          bv[0] = q.x; bv[1] = q.y; bv[2] = q.z; bv[3] = q.w;
+        }
+      }
+      float val[PG][4];
+#pragma unroll
+      for (int h = 0; h < PG; ++h) {
+        if (pkt) {
+          // channel (wco+t)*16 + kq (its three plane rows summed) -> lane kq == 0 gathers channels +0..+3
+          float s0 = acc[t][h][0] + acc[t][h][1] + acc[t][h][2] + bv[0];
+          if (a.relu) s0 = fmaxf(s0, 0.f);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float o = __shfl(s0, l16 + 16 * i, 64);
+            val[h][i] = kq == 0 ? o : 0.f;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v = acc[t][h][i] + bv[i];
+            if (a.relu) v = fmaxf(v, 0.f);
+            val[h][i] = v;
+          }
+        }
+      }
+      if (co0 >= COP) continue;                            // whole float4 beyond the padded row
+#pragma unroll
+      for (int h = 0; h < PG; ++h) {
+        const int p = (pgw + h) * 16 + l16;
+        const long off = obase + (long)p * COP + co0;
+        if (unpool) {
+          // the output is a pool's gradient: scatter each value to the forward's argmax cell (if > 0)
+          const int hh = x.h0 + p / W, ww = p % W;
+          const uint32_t mk = *reinterpret_cast<const uint32_t*>(a.pool_mask + off);
+          float* dst = static_cast<float*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.pool_y);
+          const int H2 = 2 * a.H, W2 = 2 * W;
+#pragma unroll
+          for (int me = 0; me < 4; ++me) {
+            float o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint32_t bb = (mk >> (8 * i)) & 0xffu;
+              o[i] = ((int)(bb & 3u) == me && (bb & 4u)) ? val[h][i] : 0.f;
+            }
+            *reinterpret_cast<float4*>(dst + ((n * H2 + 2 * hh + (me >> 1)) * W2 + 2 * ww + (me & 1)) * COP + co0) =
+                make_float4(o[0], o[1], o[2], o[3]);
+          }
+          continue;
+        }
+        for (int k = 0; k < GT_MAXSLOT; ++k) {
+          if (!((x.gr.out_mask >> k) & 1)) continue;
+          float* dst = static_cast<float*>(a.out[k]) + off;
+          float4 o = make_float4(val[h][0], val[h][1], val[h][2], val[h][3]);
+          if ((x.gr.out_mask >> (8 + k)) & 1) {
+            const float4 q = *reinterpret_cast<const float4*>(dst);
+            o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+          }
+          if ((x.gr.out_mask >> (16 + k)) & 1) {
+            const float4 m = *reinterpret_cast<const float4*>(static_cast<const float*>(a.out_mask[k]) + off);
+            o.x = m.x > 0.f ? o.x : 0.f; o.y = m.y > 0.f ? o.y : 0.f;
+            o.z = m.z > 0.f ? o.z : 0.f; o.w = m.w > 0.f ? o.w : 0.f;
+          }
+          *reinterpret_cast<float4*>(dst) = o;
+        }
+      }
+      if constexpr (POOLABLE) {
+        if (pool) {
+          // 2x2 max-pool + argmax mask (pool_fwd_kernel's rule: first strict maximum over
+          // (0,0), (0,1), (1,0), (1,1); bit 2 = maximum > 0) of the values as stored
+          const int Ho = a.H >> 1, Wo = W >> 1;
+#pragma unroll
+          for (int h = 0; h < PG; ++h) {
+            if ((h / RG) % 2) continue;                     // top row of each row pair
+            float m[4];
+            uint32_t mk = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float v00 = val[h][i], v10 = val[h + RG][i];
+              const float v01 = __shfl(v00, lane + 1, 64), v11 = __shfl(v10, lane + 1, 64);
+              float mm = v00;
+              int arg = 0;
+              if (v01 > mm) { mm = v01; arg = 1; }
+              if (v10 > mm) { mm = v10; arg = 2; }
+              if (v11 > mm) { mm = v11; arg = 3; }
+              m[i] = mm;
+              mk |= (uint32_t)(arg | (mm > 0.f ? 4 : 0)) << (8 * i);
+            }
+            if (l16 & 1) continue;
+            const int p = (pgw + h) * 16 + l16;
+            const int pr = (x.h0 + p / W) >> 1, pc = (p % W) >> 1;
+            const long o = ((n * Ho + pr) * Wo + pc) * COP + co0;
+            *reinterpret_cast<float4*>(static_cast<float*>(a.pool_y) + o) = make_float4(m[0], m[1], m[2], m[3]);
+            if (a.pool_mask) *reinterpret_cast<uint32_t*>(a.pool_mask + o) = mk;
+          }
+        }
+      }
+    }
+  };
+
+  // ---- phase loop ---------------------------------------------------------------
+  // prologue: team 0 stages local tile 0
+  Tile tc, tn, tp;                                         // this wave's compute / next / previous tiles
+  if (nloc > 0 && team == 0) {
+    tc = tile_of(t_begin);
+    stage_issue(tc);
+    stage_finish(tc, patch);
+  }
+  __syncthreads();
+  for (int k = 0; k <= nloc; ++k) {
+    if ((k & 1) == team) {
+      if (k < nloc) {                                      // this team's MFMA phase: tile k
+        compute(tc, patch);
+        tp = tc;
+      }
+    } else {
+      // memory phase: store tile k-1 (this team computed it last phase), stage tile k+1
+      const bool nxt = k + 1 < nloc;
+      if (nxt) {
+        tn = tile_of(t_begin + k + 1);
+        stage_issue(tn);
+      }
+      if (k >= 1) epilogue(tp);
+      if (nxt) {
+        stage_finish(tn, patch);
+        tc = tn;
+      }
+    }
+    if (k < nloc) __syncthreads();
+  }
+}
+
+// duo kernel dispatch: 0 off, 1 auto (>= 2 tiles per workgroup on every CU), 2 force
+static int g_f32_duo = -1;
+static int g_duo_wgs = 256;        // persistent workgroups (one per CU)
+
+extern "C" int gt_conv_set_duo(int mode, int wgs) {
+  if (g_f32_duo < 0) g_f32_duo = 1;
+  const int old = g_f32_duo;
+  g_f32_duo = mode;
+  if (wgs > 0) g_duo_wgs = wgs;
+  return old;
+}
+
+static bool duo_ok(int ntiles) {
+  if (g_f32_duo < 0) g_f32_duo = std::getenv("GENTUN_F32_DUO") ? std::atoi(std::getenv("GENTUN_F32_DUO")) : 1;
+  if (g_f32_duo == 0) return false;
+  return g_f32_duo == 2 || ntiles >= 2 * g_duo_wgs;
+}
+
+// -100: not launched (the LDS of two 3-plane patches does not fit, or the
+// launch is too small for two tiles per workgroup); the discarded branch is
+// never instantiated
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int PK>
+static int launch_duo(const ConvArgs* a, hipStream_t stream, int probe) {
+  using DC = DuoCfg<KH, KW, NCBI, W, TH, NT, NCO, PK>;
+  if constexpr (DC::LDS <= 163840) {
+    const int ntiles = a->ngroups * a->B * (a->H / TH);
+    if (!duo_ok(ntiles)) return -100;
+    if (probe) return 1000 + (DC::poolable() ? TH : 1);
+    const int wgs = std::min(ntiles, g_duo_wgs);
+    auto* fn = conv_duo_f32_kernel<KH, KW, NCBI, W, TH, NT, NCO, PK>;
+    if (DC::LDS > 65536)
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)DC::LDS);
+    hipLaunchKernelGGL(fn, dim3(wgs), dim3(512), DC::LDS, stream, *a, ntiles);
+    return (int)hipGetLastError();
+  } else {
+    (void)a; (void)stream; (void)probe;
+    return -100;
+  }
+}
+
+#define CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, PK_)                                         \
+  {                                                                                                     \
+    const int rc_ = launch_duo<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, PK_>(a, stream, g_probe);           \
+    if (rc_ != -100) return rc_;                                                                        \
+  }
+
 // persistent pipelined fp32 conv: measured no faster than the tile kernel on
 // the S=(3,5) shapes (profiles/conv_f32_persistent_ab_r2.txt: the k loop, not
 // the staging, sets the time), so off by default; kept as the A/B switch
@@ -815,6 +1236,7 @@ static bool pk_ok(const ConvArgs* a, int nt) {
 #define CONV_FAST_CASE_F32(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                     \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
     if (g_f32_persistent && (W_ % 16) == 0) CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)   \
+    if (NWV_ == 4) CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 0)                              \
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
   }
 // narrow images (W < 16: no persistent variant)
@@ -824,7 +1246,11 @@ static bool pk_ok(const ConvArgs* a, int nt) {
 #define CONV_FAST_CASE_F32_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                  \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
     if (g_f32_persistent && (W_ % 16) == 0) CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)   \
-    if (pk_ok(a, NT_)) CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 1)             \
+    if (pk_ok(a, NT_)) {                                                                                \
+      CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 1)                                           \
+      CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 1)                              \
+    }                                                                                                   \
+    CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 0)                                             \
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
   }
 

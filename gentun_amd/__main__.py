@@ -75,8 +75,12 @@ def _run_search(args, species, x, y, extra, maximize):
     from .parallel.distributed import DistributedPopulation, GentunWorker
     from .utils import rng
     cfg = _config(args)
-    if args.watchdog:
+    from .parallel.fault import parse_watchdog
+    parse_watchdog(args.watchdog)             # malformed spec: one clear error at startup, on every rank
+    if args.watchdog and args.watchdog.strip():
         os.environ["GENTUN_WATCHDOG"] = args.watchdog
+    else:
+        os.environ.pop("GENTUN_WATCHDOG", None)
     if args.resume == "auto":
         latest = os.path.join(cfg.checkpoint_dir or "", "latest.json")
         args.resume = latest if cfg.checkpoint_dir and os.path.exists(latest) else None

@@ -38,6 +38,7 @@ Backends: ``hip`` (MI355X kernels, :mod:`gentun_amd.models.cnn_hip`) and
 """
 
 import math
+import os
 
 import numpy as np
 import torch
@@ -277,6 +278,17 @@ class FoldJob(object):
         raise NotImplementedError
 
     # -- driver --------------------------------------------------------------
+    def graph_steps(self):
+        """Train steps per graph replay: the largest divisor of the epoch's
+        step count up to ``GENTUN_GRAPH_STEPS`` (default 1). One replay of a
+        k-step graph is one host launch for k steps, so at small population
+        sizes the host no longer paces the GPU (every step reads its batch
+        through the device-side step counter, so k consecutive steps capture
+        as k copies of the same launches)."""
+        kmax = max(1, int(os.environ.get("GENTUN_GRAPH_STEPS", getattr(self.cfg, "graph_steps", 1) or 1)))
+        n = self.steps_per_epoch
+        return max(d for d in range(1, min(kmax, n) + 1) if n % d == 0)
+
     def _capture(self):
         snap = self.snapshot()
         # warm-up steps read the (still all-zero, i.e. valid) batch table; the
@@ -293,7 +305,8 @@ class FoldJob(object):
         with torch.cuda.stream(side):
             graph.capture_begin(capture_error_mode="thread_local")
             try:
-                self.train_step()
+                for _ in range(self._k_steps):
+                    self.train_step()
             finally:
                 graph.capture_end()
         torch.cuda.current_stream(self.device).wait_stream(side)
@@ -311,6 +324,7 @@ class FoldJob(object):
             self.init_params()
             if self.after_init is not None:
                 self.after_init(self)
+            self._k_steps = self.graph_steps() if use_graph else 1
             graph = self._capture() if use_graph else None
             if timed:
                 ev[1].record()
@@ -318,10 +332,11 @@ class FoldJob(object):
                 self.reset_optimizer(lr)
                 for _ in range(epochs):
                     self._new_epoch_order()
-                    for _ in range(self.steps_per_epoch):
-                        if graph is not None:
+                    if graph is not None:
+                        for _ in range(self.steps_per_epoch // self._k_steps):
                             graph.replay()
-                        else:
+                    else:
+                        for _ in range(self.steps_per_epoch):
                             self.train_step()
             if timed:
                 ev[2].record()

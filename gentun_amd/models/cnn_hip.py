@@ -719,40 +719,90 @@ class HipPopJob(FoldJob):
         else:
             K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
 
-    def evaluate(self):
-        """Forward the validation folds in batches of B (no dropout)."""
-        Q, B, dev = self.Q, self.B, self.device
-        maxv = self.val_mat.shape[1]
-        nch = -(-maxv // B)
-        idx = torch.zeros((Q, nch * B), dtype=torch.int64, device=dev)
-        mask = torch.zeros((Q, nch * B), dtype=torch.float32, device=dev)
-        idx[:, :maxv] = self.val_mat
-        mask[:, :maxv] = self.val_mask
-        table = idx.view(Q, nch, B).permute(1, 0, 2).contiguous()        # [nch][Q][B]
-        out = torch.zeros((nch, Q, B, 3), dtype=torch.float32, device=dev)
-        self._eval_keep = (table, out)
-        s = self._stream()
-        L = self.L
-        # eval copies of the forward argument structs: gather from the eval table, eval state
+    def eval_batch(self):
+        """Rows per evaluation launch (K13): ``cfg.eval_batch`` (1,000 by
+        default), capped at 256, at the validation fold size and by a 4 GB
+        budget for the forward-only activation slots of all Q groups; never
+        below the training batch. Larger eval launches fill the GPU with Q
+        groups x EB rows instead of Q x 32 (63 launches of 32 per 2,000-sample
+        fold become 8 of 256)."""
+        per_img = sum(t[0, 0].numel() * t.element_size() for t in self.act.values())
+        per_img += sum(t[0, 0].numel() * t.element_size() for t in self.zpre.values())
+        per_img += self.Up * 4 * 2
+        maxv = int(self.val_mat.shape[1])
+        eb = min(int(getattr(self.cfg, "eval_batch", 256) or 256), 256, round_up(maxv, 32))
+        eb = min(eb, max(1, int(256e6 // max(1, per_img))) // 32 * 32)     # <= 256 MB per group
+        return max(self.B, eb)
+
+    def _eval_ops(self, EB):
+        """Forward-only argument copies at batch EB on their own activation
+        buffers (pointers of the training buffers remapped), the dense / head
+        copies, and the buffers to keep alive."""
+        Q = self.Q
+        remap, keep = {}, []
+
+        def twin(t):
+            e = torch.empty((Q, EB) + tuple(t.shape[2:]), dtype=t.dtype, device=t.device)
+            remap[t.data_ptr()] = e.data_ptr()
+            keep.append(e)
+            return e
+        for t in list(self.act.values()) + list(self.zpre.values()):
+            twin(t)
+        hdrop, plog = twin(self.hdrop), torch.empty((Q, self.Up // 16, EB, self.classes), dtype=torch.float32,
+                                                    device=self.device)
+        keep.append(plog)
+
+        def rp(ptr):
+            return remap.get(ptr, ptr)
         ops = []
         for kind, a, Lr in self.fwd_ops:
             if kind == "conv":
                 b = K.ConvArgs.from_buffer_copy(a)
+                for i in range(K.MAXSLOT):
+                    b.inp[i], b.out[i] = rp(b.inp[i] or 0), rp(b.out[i] or 0)
                 b.st = self.eval_state.data_ptr()
                 b.xsum = 0
+                b.pool_y = rp(b.pool_y or 0)
                 b.pool_mask = 0                      # fused pool: output only
+                b.B = EB
                 ops.append((kind, b, Lr))
             elif kind == "bn":
                 b = K.BnArgs.from_buffer_copy(a)
+                b.z, b.y, b.pool_y = rp(b.z or 0), rp(b.y or 0), rp(b.pool_y or 0)
                 b.train = 0                          # running statistics
-                b.pool_mask = 0                      # fused pool: output only
+                b.pool_mask = 0
+                b.B = EB
+                b.nchunk = -(-(EB * b.HW) // b.chunk_px)
                 ops.append((kind, b, Lr))
             else:
-                ops.append((kind, a, None))          # no argmax mask in evaluation
+                xin, x1, sel, py, _qb, _b, hh, ww, cc = a
+                ops.append((kind, (rp(xin), rp(x1), sel, rp(py), Q * EB, EB, hh, ww, cc), None))
         df = K.DenseFwdArgs.from_buffer_copy(self.dense_fwd_args)
-        df.train = 0
+        df.x, df.out, df.plog = rp(df.x), hdrop.data_ptr(), plog.data_ptr()
+        df.B, df.train = EB, 0
         hd = K.HeadArgs.from_buffer_copy(self.head_args)
-        hd.eval, hd.st = 1, self.eval_state.data_ptr()
+        hd.h, hd.plog = hdrop.data_ptr(), plog.data_ptr()
+        hd.B, hd.eval, hd.st = EB, 1, self.eval_state.data_ptr()
+        return ops, df, hd, keep
+
+    def evaluate(self):
+        """Forward the validation folds in batches of ``eval_batch()`` rows
+        (no dropout, running BatchNorm statistics); per-sample loss and
+        accuracies summed over the real rows."""
+        Q, dev = self.Q, self.device
+        EB = self.eval_batch()
+        maxv = self.val_mat.shape[1]
+        nch = -(-maxv // EB)
+        idx = torch.zeros((Q, nch * EB), dtype=torch.int64, device=dev)
+        mask = torch.zeros((Q, nch * EB), dtype=torch.float32, device=dev)
+        idx[:, :maxv] = self.val_mat
+        mask[:, :maxv] = self.val_mask
+        table = idx.view(Q, nch, EB).permute(1, 0, 2).contiguous()        # [nch][Q][EB]
+        out = torch.zeros((nch, Q, EB, 3), dtype=torch.float32, device=dev)
+        ops, df, hd, keep = self._eval_ops(EB)
+        self._eval_keep = (table, out, keep)
+        s = self._stream()
+        L = self.L
         for c in range(nch):
             gptr = table[c].data_ptr()
             for kind, b, _ in ops:
@@ -762,8 +812,8 @@ class HipPopJob(FoldJob):
             K.check(L.gt_dense_fwd(df, s), "dense_fwd(eval)")
             hd.gather, hd.eval_out = gptr, out[c].data_ptr()
             K.check(L.gt_head(hd, s), "head(eval)")
-        res = out.permute(1, 0, 2, 3).reshape(Q, nch * B, 3) * mask[:, :, None]
-        sums = res.sum(1)
+        res = out.permute(1, 0, 2, 3).reshape(Q, nch * EB, 3) * mask[:, :, None]
+        sums = res.double().sum(1).float()      # fp64 accumulation: independent of the chunking
         return sums[:, 0], sums[:, 1], sums[:, 2]
 
 

@@ -74,10 +74,15 @@ _DTYPES = [np.float64, np.float32, np.int64, np.int32, np.uint8]
 
 def _attempt_store(timeout):
     """Under torchrun's static rendezvous the agent's TCPStore outlives a
-    restart (``--max-restarts``): without a per-attempt key prefix a restarted
-    rank can read a dead peer's gloo / RCCL bootstrap address left over from
-    the previous attempt and fail to connect. Returns the agent store under
-    ``gentun/attempt_<TORCHELASTIC_RESTART_COUNT>`` (None outside torchrun)."""
+    restart (``--max-restarts``); this returns that store under the key
+    prefix ``gentun/attempt_<TORCHELASTIC_RESTART_COUNT>`` (None outside
+    torchrun), so a restarted group never meets keys of the attempt before.
+
+    torch 2.10's env rendezvous opens a fresh agent-store client per attempt
+    as well, but measured here that is not enough for our restart path: with
+    this function disabled (round 3), tests/test_dead_rank.py's killed / hung
+    rank restarts hang until the test timeout instead of resuming, so the
+    prefix stays."""
     import torch.distributed as dist
     if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") != "True" or "TORCHELASTIC_RESTART_COUNT" not in os.environ:
         return None

@@ -40,7 +40,7 @@ from ..populations import Population, GridPopulation
 from .comm import LocalComm, from_env
 from . import fault as _fault
 from .evaluators import LocalBatchEvaluator
-from .scheduler import lpt_assign, make_units
+from .scheduler import balanced_round, lpt_assign, make_units
 
 CMD_STOP, CMD_EVAL, CMD_SYNC = 0, 1, 2
 ST_NONE, ST_OK, ST_ERR = 0.0, 1.0, 2.0
@@ -317,12 +317,53 @@ class DistributedPopulation(Population):
     def evaluate_in_parallel(self, limit=None):
         """Dispatch pending individuals to every rank and collect fitness.
         ``limit``: evaluate at most that many (in population order) -- one
-        evaluation *round*; the rest stay pending."""
+        evaluation *round*; the rest stay pending.
+
+        Failed units (status codes in the gather) are re-queued ONCE as a
+        second dispatched round on the ranks that did not fail (SURVEY.md
+        §5.3): every rank takes part, so no evaluator sits in a collective
+        while rank 0 retrains candidates on its own (their watchdogs stay
+        inside one dispatch's budget). A candidate that fails again gets the
+        worst fitness. With one rank the retry is a local re-evaluation."""
         todo = self.pending()
         if limit is not None:
             todo = todo[:max(0, int(limit))]
         if not todo:
             return 0
+        t0 = time.perf_counter()
+        merged, info = self._dispatch(todo)
+        failed = [slot for slot in range(len(todo)) if merged[slot][0] != ST_OK]
+        if failed and self.comm.world_size > 1:
+            again, _ = self._dispatch([todo[slot] for slot in failed], exclude=info["failed_ranks"])
+            for slot, res in zip(failed, again):
+                merged[slot] = res
+        for slot, ind in enumerate(todo):
+            status, fitness, scores, aux = merged[slot]
+            if status != ST_OK:
+                if self.comm.world_size == 1:
+                    try:
+                        ind.set_fitness(None)
+                        ind.evaluate_fitness()
+                        continue
+                    except Exception as exc:   # noqa: BLE001
+                        warnings.warn("re-evaluation of slot {} failed: {}".format(slot, exc))
+                else:
+                    warnings.warn("slot {} failed on its rank and on the retry round".format(slot))
+                ind.set_fitness(float("-inf") if self.maximize else float("inf"))
+            else:
+                ind.set_fitness(fitness)
+                ind.fold_scores = scores
+                if aux is not None:
+                    ind.fold_metrics = dict(getattr(ind, "fold_metrics", None) or {}, categorical_accuracy=aux)
+        self.last_dispatch = {"units": info["units"], "candidates": len(todo), "retried": len(failed),
+                              "wall_s": time.perf_counter() - t0, "schedule": info["schedule"],
+                              "per_rank_units": info["per_rank_units"]}
+        return len(todo)
+
+    def _dispatch(self, todo, exclude=()):
+        """One dispatch of ``todo`` over the ranks (not in ``exclude``):
+        broadcast, local evaluation, all_gather. Returns the merged
+        ``(status, fitness, fold_scores, aux)`` per candidate and a summary."""
         self.generation_counter += 1
         comm = self.comm
         nfold = int(getattr(todo[0], "nfold", 1) or 1)
@@ -336,8 +377,9 @@ class DistributedPopulation(Population):
         # population-batched evaluators take (candidate, fold) units: equal
         # group counts per rank at any generation size
         per_fold = splittable and getattr(self.local_evaluator, "pop_batch", 1) > 1
-        units, ucost = make_units(costs, nfold, comm.world_size, splittable, per_fold=per_fold)
-        dynamic = self.schedule == "dynamic" and comm.world_size > 1
+        allowed = [r for r in range(comm.world_size) if r not in set(exclude)] or list(range(comm.world_size))
+        units, ucost = make_units(costs, nfold, len(allowed), splittable, per_fold=per_fold)
+        dynamic = self.schedule == "dynamic" and comm.world_size > 1 and len(allowed) == comm.world_size
         if dynamic:
             # table order = claim order: most expensive first (on-line LPT)
             order = sorted(range(len(units)), key=lambda i: (-ucost[i], i))
@@ -345,7 +387,7 @@ class DistributedPopulation(Population):
             ucost = [ucost[i] for i in order]
             owner = [-1] * len(units)
         else:
-            owner = lpt_assign(ucost, comm.world_size)
+            owner = [allowed[o] for o in lpt_assign(ucost, len(allowed))]
         table = np.zeros((len(units), 3 + codec.width), np.float64)
         for k, (slot, fids) in enumerate(units):
             table[k, 0] = slot
@@ -357,12 +399,16 @@ class DistributedPopulation(Population):
             wd.arm("generation {} (rank 0)".format(self.generation_counter))
         extra = _jsonable(todo[0].get_additional_parameters())
         genome = {k: (list(v) if isinstance(v, tuple) else v) for k, v in todo[0].get_genome().items()}
-        blob = np.frombuffer(json.dumps({"species": self.species.__name__, "extra": extra,
-                                         "genome": genome}).encode(), np.uint8)
-        t0 = time.perf_counter()
-        comm.broadcast_array(np.array([CMD_EVAL, self.generation_counter, len(todo), nfold], np.int64))
-        comm.broadcast_array(blob)
+        blob = json.dumps({"species": self.species.__name__, "extra": extra, "genome": genome}).encode()
+        # X1: the config blob travels once (and again only if it changes); the
+        # evaluator ranks keep the last one
+        send_blob = blob != getattr(comm, "_gentun_last_blob", None)
+        comm.broadcast_array(np.array([CMD_EVAL, self.generation_counter, len(todo), nfold, int(send_blob)], np.int64))
+        if send_blob:
+            comm.broadcast_array(np.frombuffer(blob, np.uint8))
+            comm._gentun_last_blob = blob
         comm.broadcast_array(table)
+
         def make_unit(k):
             slot, fids = units[k]
             return _Unit(slot, todo[slot] if len(fids) == nfold else _clone(todo[slot]), fids)
@@ -380,39 +426,35 @@ class DistributedPopulation(Population):
         if wd is not None:
             wd.disarm()
         merged = _merge(gathered, units, len(todo), nfold)
-        retried = 0
-        for slot, ind in enumerate(todo):
-            status, fitness, scores, aux = merged[slot]
-            if status != ST_OK:
-                retried += 1
-                try:
-                    ind.set_fitness(None)
-                    ind.evaluate_fitness()
-                except Exception as exc:   # noqa: BLE001
-                    warnings.warn("re-evaluation of slot {} failed: {}".format(slot, exc))
-                    ind.set_fitness(float("-inf") if self.maximize else float("inf"))
-            else:
-                ind.set_fitness(fitness)
-                ind.fold_scores = scores
-                if aux is not None:
-                    ind.fold_metrics = dict(getattr(ind, "fold_metrics", None) or {}, categorical_accuracy=aux)
-        self.last_dispatch = {"units": len(units), "candidates": len(todo), "retried": retried,
-                              "wall_s": time.perf_counter() - t0,
-                              "schedule": "dynamic" if dynamic else "lpt",
-                              "per_rank_units": [int(np.sum(g[:, 0] != ST_NONE)) for g in gathered]}
-        return len(todo)
+        # ranks to leave out of a retry: owners of units that came back empty, ranks that reported errors
+        failed_ranks = set()
+        for k in range(len(units)):
+            got = [r for r, g in enumerate(gathered) if g[k, 0] != ST_NONE]
+            if not got and owner[k] >= 0:
+                failed_ranks.add(owner[k])
+            failed_ranks.update(r for r in got if gathered[r][k, 0] == ST_ERR)
+        info = {"units": len(units), "schedule": "dynamic" if dynamic else "lpt", "failed_ranks": failed_ranks,
+                "per_rank_units": [int(np.sum(g[:, 0] != ST_NONE)) for g in gathered]}
+        return merged, info
+
+    def evaluate_round(self, per_rank):
+        """One balanced evaluation round: at most ``per_rank`` candidates per
+        rank, the pending set cut into near-equal rounds
+        (:func:`~gentun_amd.parallel.scheduler.balanced_round`)."""
+        return self.evaluate_in_parallel(
+            limit=balanced_round(len(self.pending()), int(per_rank) * self.comm.world_size))
 
     def sync_ranks(self):
         """Device-synchronise every rank and barrier (bench timing fence)."""
         if self.comm.world_size > 1:
-            self.comm.broadcast_array(np.array([CMD_SYNC, self.generation_counter, 0, 0], np.int64))
+            self.comm.broadcast_array(np.array([CMD_SYNC, self.generation_counter, 0, 0, 0], np.int64))
         _device_sync(self.local_evaluator)
         self.comm.barrier()
 
     def shutdown(self):
         """Release the evaluator ranks (they return from ``work()``)."""
         if self.comm.world_size > 1:
-            self.comm.broadcast_array(np.array([CMD_STOP, self.generation_counter, 0, 0], np.int64))
+            self.comm.broadcast_array(np.array([CMD_STOP, self.generation_counter, 0, 0, 0], np.int64))
 
 
 def _clone(ind):
@@ -491,6 +533,7 @@ class GentunWorker(object):
         self.comm = comm if comm is not None else _comm_from_args(host, port)
         self.evaluator = evaluator if evaluator is not None else LocalBatchEvaluator()
         self.served = 0
+        self._meta = None           # last config blob (X1) broadcast by rank 0
 
     def serve_one(self):
         """Handle one broadcast; returns False on STOP."""
@@ -499,7 +542,7 @@ class GentunWorker(object):
         if wd is not None:
             wd.arm("evaluator rank {} waiting / evaluating".format(comm.rank))
         hdr = comm.broadcast_array(None)
-        cmd, generation, _ncand, nfold = (int(v) for v in hdr)
+        cmd, generation, _ncand, nfold, has_blob = (int(v) for v in hdr)
         if cmd == CMD_STOP:
             if wd is not None:
                 wd.disarm()
@@ -510,8 +553,13 @@ class GentunWorker(object):
             if wd is not None:
                 wd.disarm()
             return True
-        blob = comm.broadcast_array(None)
-        meta = json.loads(bytes(blob.astype(np.uint8)).decode())
+        if has_blob:
+            blob = comm.broadcast_array(None)
+            self._meta = json.loads(bytes(blob.astype(np.uint8)).decode())
+        meta = self._meta
+        if meta is None:
+            raise RuntimeError("evaluator rank {}: generation {} arrived before the config blob".format(
+                comm.rank, generation))
         table = comm.broadcast_array(None)
         extra = {k: _tuplify(v) for k, v in meta["extra"].items()}
         # genome spec comes with the broadcast: building a throw-away individual

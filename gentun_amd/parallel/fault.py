@@ -134,14 +134,28 @@ def watchdog():
     """The process-wide watchdog, created on first use from
     ``GENTUN_WATCHDOG`` = ``first_s[:factor[:min_s]]`` ("0" disables)."""
     global _WATCHDOG
-    spec = os.environ.get("GENTUN_WATCHDOG")
-    if spec is None or spec == "0":
+    kw = parse_watchdog(os.environ.get("GENTUN_WATCHDOG"))
+    if kw is None:
         return None
     if _WATCHDOG is None:
-        parts = [float(v) for v in spec.split(":")]
-        kw = dict(zip(("first_s", "factor", "min_s"), parts))
         _WATCHDOG = Watchdog(**kw)
     return _WATCHDOG
+
+
+def parse_watchdog(spec):
+    """``first_s[:factor[:min_s]]`` -> Watchdog kwargs; None when unset,
+    empty / blank (e.g. ``GENTUN_WATCHDOG= torchrun ...``) or "0". A malformed
+    spec raises ValueError naming the variable (the CLI validates it once at
+    startup, so every rank fails at once with that message)."""
+    if spec is None or not spec.strip() or spec.strip() == "0":
+        return None
+    try:
+        parts = [float(v) for v in spec.strip().split(":")]
+    except ValueError:
+        raise ValueError("GENTUN_WATCHDOG={!r}: expected first_s[:factor[:min_s]] (numbers) or 0".format(spec))
+    if not 1 <= len(parts) <= 3 or any(p <= 0 for p in parts):
+        raise ValueError("GENTUN_WATCHDOG={!r}: expected 1-3 positive numbers first_s[:factor[:min_s]]".format(spec))
+    return dict(zip(("first_s", "factor", "min_s"), parts))
 
 
 def supervise(cmd, max_restarts=3, env=None, restart_codes=None):

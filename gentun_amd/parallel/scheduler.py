@@ -60,6 +60,19 @@ def make_units(costs, nfold, world_size, split_folds=True, per_fold=False):
     return units, ucost
 
 
+def balanced_round(n_pending, cap):
+    """Size of the next evaluation round when at most ``cap`` candidates fit a
+    round: the pending set is cut into ``ceil(n / cap)`` near-equal rounds
+    (11 pending at cap 5 -> 4, 4, 3 instead of 5, 5, 1; a 1-candidate round
+    costs ~40 % of a 5-candidate one on a GPU, so it halves the throughput of
+    its time slice)."""
+    if n_pending <= 0:
+        return 0
+    cap = max(1, int(cap))
+    rounds = -(-n_pending // cap)
+    return -(-n_pending // rounds)
+
+
 def makespan(costs, owner, world_size):
     loads = [0.0] * world_size
     for c, r in zip(costs, owner):

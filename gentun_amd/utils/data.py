@@ -92,6 +92,140 @@ def make_glyph_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, no
     return x.astype(dtype), y
 
 
+def _stroke(rng, size, width, lo=0.15, hi=0.85):
+    """One anti-aliased line segment in [0, 1] on a ``size`` x ``size`` canvas."""
+    yy, xx = np.meshgrid(np.arange(size, dtype=np.float32), np.arange(size, dtype=np.float32), indexing="ij")
+    a, b = rng.uniform(lo * size, hi * size, size=(2, 2)).astype(np.float32)
+    d = b - a
+    t = np.clip(((yy - a[0]) * d[0] + (xx - a[1]) * d[1]) / max(float(d @ d), 1e-6), 0.0, 1.0)
+    dist = np.hypot(yy - (a[0] + t * d[0]), xx - (a[1] + t * d[1]))
+    return np.clip(1.0 - (dist - width) / 1.2, 0.0, 1.0)
+
+
+def make_parts_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, parts=8, per_class=3,
+                              distractors=2, distract=(0.5, 1.0), same_color=False, noise=0.8, shift=4,
+                              dtype=np.float32):
+    """Compositional synthetic images: a pool of ``parts`` stroke primitives,
+    every class the union of ``per_class`` of them (distinct combinations, so
+    classes share strokes), a sample its class glyph translated by up to
+    ``shift`` pixels plus ``distractors`` random single primitives of the
+    pool at intensity ``distract`` (in their own colours), over a random
+    background gradient, with Gaussian noise.
+
+    Telling classes apart means recognising a CONJUNCTION of strokes among
+    extra strokes from the same vocabulary: a sample with its class strokes
+    plus a distractor also contains most of another class's strokes. Unlike
+    :func:`make_glyph_classification` (one unique glyph per class; every
+    architecture of the S=(3,5) space reaches ~0.99), accuracy here depends on
+    the network: the bench data of BASELINE cfg 2-4 (``make_cifar_like``)."""
+    rng = np.random.default_rng(seed)
+    h, w, c = shape
+    size = max(h, w) + 2 * shift
+    prims = np.stack([_stroke(rng, size, 0.8 + 0.6 * rng.uniform()) for _ in range(parts)])
+    combos, seen = [], set()
+    while len(combos) < classes:
+        k = tuple(sorted(rng.choice(parts, size=per_class, replace=False).tolist()))
+        if k not in seen:
+            seen.add(k)
+            combos.append(k)
+    glyphs = np.stack([prims[list(k)].max(0) for k in combos])
+    labels = np.arange(n) % classes
+    rng.shuffle(labels)
+    dy = rng.integers(0, 2 * shift + 1, size=n)
+    dx = rng.integers(0, 2 * shift + 1, size=n)
+    color = rng.uniform(0.45, 1.0, size=(n, c)).astype(np.float32)
+    bg0 = rng.uniform(0.0, 0.25, size=(n, c)).astype(np.float32)
+    bgslope = rng.uniform(-0.15, 0.15, size=(n, 2, c)).astype(np.float32)
+    ramp_y = np.linspace(-0.5, 0.5, h, dtype=np.float32)[:, None, None]
+    ramp_x = np.linspace(-0.5, 0.5, w, dtype=np.float32)[None, :, None]
+    dpart = rng.integers(0, parts, size=(n, distractors))
+    dalpha = rng.uniform(distract[0], distract[1], size=(n, distractors)).astype(np.float32)
+    dcolor = rng.uniform(0.3, 1.0, size=(n, distractors, c)).astype(np.float32)
+    if same_color:                   # distractor strokes in the class glyph's colour: only shape tells them apart
+        dcolor[:] = color[:, None, :]
+    ddy = rng.integers(0, 2 * shift + 1, size=(n, distractors))
+    ddx = rng.integers(0, 2 * shift + 1, size=(n, distractors))
+    x = np.empty((n, h, w, c), np.float32)
+    for i in range(n):
+        g = glyphs[labels[i], dy[i]:dy[i] + h, dx[i]:dx[i] + w][:, :, None]
+        img = (bg0[i] + ramp_y * bgslope[i, 0] + ramp_x * bgslope[i, 1]) * (1.0 - g) + color[i] * g
+        for j in range(distractors):
+            o = prims[dpart[i, j], ddy[i, j]:ddy[i, j] + h, ddx[i, j]:ddx[i, j] + w][:, :, None] * dalpha[i, j]
+            img = img * (1.0 - o) + dcolor[i, j] * o
+        x[i] = img
+    x += noise * 0.25 * rng.standard_normal(size=x.shape).astype(np.float32)
+    np.clip(x, 0.0, 1.0, out=x)
+    y = np.zeros((n, classes), np.float32)
+    y[np.arange(n), labels] = 1.0
+    return x.astype(dtype), y
+
+
+def make_relation_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, ptypes=5, psize=9, dist=(9, 13),
+                                 distractors=2, noise=1.0, dtype=np.float32):
+    """Relational synthetic images: ``ptypes`` small stroke parts
+    (``psize`` x ``psize``); a class is an ordered PAIR of part types at a
+    relative DIRECTION (right / below / left / above of each other, ``dist``
+    pixels apart, +-1 jitter), classes chosen so that they share part types
+    and directions. A sample places its pair anywhere in the image, adds
+    ``distractors`` random parts elsewhere, all in one random colour, over a
+    random background gradient, with Gaussian noise.
+
+    The label is a relation between two parts ~11 pixels apart anywhere in the
+    image: a network must see both parts in one receptive field, so deeper /
+    wider DAG stages should beat shallow ones, and the distractors keep the
+    part inventory alone from answering."""
+    rng = np.random.default_rng(seed)
+    h, w, c = shape
+    parts = []
+    for _ in range(ptypes):
+        img = np.zeros((psize, psize), np.float32)
+        for _ in range(2):
+            img = np.maximum(img, _stroke(rng, psize, 0.5 + 0.4 * rng.uniform(), lo=0.05, hi=0.95))
+        parts.append(img)
+    parts = np.stack(parts)
+    dirs = [(0, 1), (1, 0), (0, -1), (-1, 0)]
+    combos, seen = [], set()
+    while len(combos) < classes:
+        a, b = rng.choice(ptypes, size=2, replace=True)
+        d = int(rng.integers(0, 4))
+        key = (int(a), int(b), d)
+        mirror = (int(b), int(a), (d + 2) % 4)            # the same picture as another class
+        if key not in seen and mirror not in seen:
+            seen.add(key)
+            combos.append(key)
+    labels = np.arange(n) % classes
+    rng.shuffle(labels)
+    color = rng.uniform(0.45, 1.0, size=(n, c)).astype(np.float32)
+    bg0 = rng.uniform(0.0, 0.25, size=(n, c)).astype(np.float32)
+    bgslope = rng.uniform(-0.15, 0.15, size=(n, 2, c)).astype(np.float32)
+    ramp_y = np.linspace(-0.5, 0.5, h, dtype=np.float32)[:, None, None]
+    ramp_x = np.linspace(-0.5, 0.5, w, dtype=np.float32)[None, :, None]
+    x = np.empty((n, h, w, c), np.float32)
+    for i in range(n):
+        a, b, d = combos[labels[i]]
+        r = int(rng.integers(dist[0], dist[1] + 1))
+        dy, dx = dirs[d][0] * r + int(rng.integers(-1, 2)), dirs[d][1] * r + int(rng.integers(-1, 2))
+        # anchor of part a so that both parts are inside the image
+        y0lo, y0hi = max(0, -dy), min(h - psize, h - psize - dy)
+        x0lo, x0hi = max(0, -dx), min(w - psize, w - psize - dx)
+        y0, x0 = int(rng.integers(y0lo, y0hi + 1)), int(rng.integers(x0lo, x0hi + 1))
+        g = np.zeros((h, w), np.float32)
+        g[y0:y0 + psize, x0:x0 + psize] = np.maximum(g[y0:y0 + psize, x0:x0 + psize], parts[a])
+        g[y0 + dy:y0 + dy + psize, x0 + dx:x0 + dx + psize] = np.maximum(
+            g[y0 + dy:y0 + dy + psize, x0 + dx:x0 + dx + psize], parts[b])
+        for _ in range(distractors):
+            k = int(rng.integers(0, ptypes))
+            yy, xx = int(rng.integers(0, h - psize + 1)), int(rng.integers(0, w - psize + 1))
+            g[yy:yy + psize, xx:xx + psize] = np.maximum(g[yy:yy + psize, xx:xx + psize], parts[k])
+        gg = g[:, :, None]
+        x[i] = (bg0[i] + ramp_y * bgslope[i, 0] + ramp_x * bgslope[i, 1]) * (1.0 - gg) + color[i] * gg
+    x += noise * 0.25 * rng.standard_normal(size=x.shape).astype(np.float32)
+    np.clip(x, 0.0, 1.0, out=x)
+    y = np.zeros((n, classes), np.float32)
+    y[np.arange(n), labels] = 1.0
+    return x.astype(dtype), y
+
+
 def make_image_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, noise=0.35, shift=3,
                               dtype=np.float32):
     """Synthetic image classification set: x in [0,1] NHWC, y one-hot.

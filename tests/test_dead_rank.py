@@ -67,6 +67,29 @@ def test_killed_or_hung_rank_run_completes_from_checkpoint(tmp_path, clean_run, 
     assert os.path.exists(os.path.join(str(tmp_path), "gen_00004.json"))
 
 
+def test_failed_share_is_retried_on_the_survivors(tmp_path, clean_run):
+    """Every unit of rank 1 raises in one dispatch: the failed units are
+    re-dispatched as a second round on the surviving rank (not retrained by
+    rank 0 while the evaluators wait in a collective), so a TIGHT watchdog
+    (factor 1.5 over the slowest dispatch) never fires, and the trajectory is
+    the clean run's (serial rank-0 retries outlived the evaluators'
+    deadlines)."""
+    r, out = _search(tmp_path, fault="1:2:raise", restarts=0, watchdog="60:1.5:2")
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "injected fault on rank 1 generation 2" in r.stderr
+    assert "[watchdog]" not in r.stderr
+    assert _trajectory(out) == _trajectory(clean_run)
+
+
+def test_blank_watchdog_spec_is_disabled_and_bad_spec_is_rejected():
+    from gentun_amd.parallel.fault import parse_watchdog
+    assert parse_watchdog(None) is None and parse_watchdog("") is None and parse_watchdog("  ") is None
+    assert parse_watchdog("0") is None
+    assert parse_watchdog("30:2:5") == {"first_s": 30.0, "factor": 2.0, "min_s": 5.0}
+    with pytest.raises(ValueError, match="GENTUN_WATCHDOG"):
+        parse_watchdog("soon")
+
+
 def test_without_restarts_a_dead_rank_fails_fast(tmp_path):
     """No supervisor: the run ends with an error well before the 30-minute
     collective timeout (gloo connection error / watchdog), not a hang."""

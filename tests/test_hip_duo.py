@@ -1,0 +1,165 @@
+"""The persistent two-team fp32 conv kernel (``conv_duo_f32_kernel``,
+csrc/hip/cnn_conv_fast.hip) against the one-tile kernel it replaces at
+population launch sizes: every output -- forward with bias / ReLU / N-ary
+input sum / ``xsum`` / fused 2x2 pool + argmax mask, data gradient with the
+DAG fan-out (accumulate, ReLU mask, several output slots) and the fused
+un-pool -- must be BIT-identical (same k order, same MFMA sequence, same
+epilogue arithmetic), for every shape-specialised fp32 layer of the S=(3,5)
+space incl. the packed last co tile, and for workgroups that walk an odd or
+even number of tiles (both teams finish)."""
+
+import pytest
+import torch
+
+DEV = torch.device("cuda", 0) if torch.cuda.is_available() else None
+
+# (H, W, cin, cout, k): the fp32 shape-specialised layers (gt_conv_fast)
+SHAPES = [(32, 32, 3, 20, 5), (32, 32, 20, 20, 3), (16, 16, 20, 50, 5), (16, 16, 50, 50, 3), (16, 16, 50, 20, 5)]
+
+
+def K():
+    from gentun_amd.ops import cnn_kernels
+    cnn_kernels.lib()
+    return cnn_kernels
+
+
+def pad8(c):
+    return (c + 7) // 8 * 8
+
+
+def _run(Km, a, mode, wgs):
+    import ctypes
+    L = Km.lib()
+    L.gt_conv_set_duo.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.gt_conv_set_duo.restype = ctypes.c_int
+    old = L.gt_conv_set_duo(mode, wgs)
+    try:
+        Km.check(L.gt_conv_fwd(a, torch.cuda.current_stream().cuda_stream), "conv")
+        torch.cuda.synchronize()
+    finally:
+        L.gt_conv_set_duo(old, 256)
+
+
+def _split(w):
+    from gentun_amd.models.cnn_hip import split_planes
+    return split_planes(w, 3).contiguous()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,cin,cout,k", SHAPES)
+@pytest.mark.parametrize("nin", [1, 3])
+@pytest.mark.parametrize("wgs", [5, 8])
+def test_duo_forward_bit_identical(H, W, cin, cout, k, nin, wgs):
+    Km = K()
+    torch.manual_seed(H + cin + k + nin)
+    G, B = 3, 8
+    cinp, coutp = pad8(cin), pad8(cout)
+    xs = []
+    for _ in range(nin):
+        x = torch.zeros(G, B, H, W, cinp, device=DEV)
+        x[..., :cin] = torch.randn(G, B, H, W, cin, device=DEV)
+        xs.append(x)
+    w = torch.zeros(G, coutp, k, k, cinp, device=DEV)
+    w[:, :cout, :, :, :cin] = torch.randn(G, cout, k, k, cin, device=DEV) * 0.1
+    wpl = _split(w)
+    bias = torch.zeros(G, coutp, device=DEV)
+    bias[:, :cout] = torch.randn(G, cout, device=DEV) * 0.1
+    # group 0 sums every input and pools, group 1 reads input 0 only, group 2 sums and pools
+    full = (1 << nin) - 1
+    rows = torch.tensor([[0, full, 1 | (1 << 24), 0], [1, 1, 1, 0], [2, full, 1 | (1 << 24), 0]],
+                        dtype=torch.int32, device=DEV)
+    outs = {}
+    for mode in (0, 2):
+        out = torch.full((G, B, H, W, coutp), 7.0, device=DEV)
+        xsum = torch.full((G, B, H, W, cinp), 3.0, device=DEV)
+        py = torch.full((G, B, H // 2, W // 2, coutp), 5.0, device=DEV)
+        pm = torch.full((G * B, H // 2, W // 2, coutp), 9, dtype=torch.uint8, device=DEV)
+        a = Km.ConvArgs()
+        for i, t in enumerate(xs):
+            a.inp[i] = t.data_ptr()
+        a.out[0] = out.data_ptr()
+        a.gtab, a.ngroups, a.relu, a.epi_bf16 = rows.data_ptr(), G, 1, 1
+        a.w, a.bias, a.wps = wpl.data_ptr(), bias.data_ptr(), wpl[0].numel()
+        a.xsum = xsum.data_ptr() if nin > 1 else 0
+        a.pool_y, a.pool_mask = py.data_ptr(), pm.data_ptr()
+        a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
+        a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
+        _run(Km, a, mode, wgs)
+        outs[mode] = (out, xsum, py, pm)
+    for name, t0, t2 in zip(("out", "xsum", "pool_y", "pool_mask"), outs[0], outs[2]):
+        assert torch.equal(t0, t2), name
+    # the reference kernel really pooled groups 0 and 2 (sanity of the comparison itself)
+    assert not torch.equal(outs[0][2][0], torch.full_like(outs[0][2][0], 5.0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,cin,cout,k", SHAPES)
+@pytest.mark.parametrize("wgs", [5, 8])
+def test_duo_data_gradient_bit_identical(H, W, cin, cout, k, wgs):
+    """Data-gradient launches (conv with flipped weights, no bias / ReLU):
+    per group write / accumulate / ReLU-mask into up to two output slots."""
+    Km = K()
+    torch.manual_seed(100 + H + cin)
+    G, B = 3, 8
+    cinp, coutp = pad8(cin), pad8(cout)
+    dz = torch.zeros(G, B, H, W, cinp, device=DEV)
+    dz[..., :cin] = torch.randn(G, B, H, W, cin, device=DEV)
+    w = torch.zeros(G, coutp, k, k, cinp, device=DEV)
+    w[:, :cout, :, :, :cin] = torch.randn(G, cout, k, k, cin, device=DEV) * 0.1
+    wpl = _split(w)
+    masks = [torch.randn(G, B, H, W, coutp, device=DEV) for _ in range(2)]
+    init = [torch.randn(G, B, H, W, coutp, device=DEV) for _ in range(2)]
+    # bits 0-7 write, 8-15 accumulate, 16-23 ReLU mask
+    rows = torch.tensor([[0, 1, 1 | (1 << 8) | (1 << 16), 0], [1, 1, 3 | (1 << 9) | (1 << 17), 0],
+                         [2, 1, 2 | (1 << 16 + 1), 0]], dtype=torch.int32, device=DEV)
+    outs = {}
+    for mode in (0, 2):
+        o = [t.clone() for t in init]
+        a = Km.ConvArgs()
+        a.inp[0] = dz.data_ptr()
+        a.out[0], a.out[1] = o[0].data_ptr(), o[1].data_ptr()
+        a.out_mask[0], a.out_mask[1] = masks[0].data_ptr(), masks[1].data_ptr()
+        a.gtab, a.ngroups, a.relu, a.epi_bf16 = rows.data_ptr(), G, 0, 0
+        a.w, a.bias, a.wps = wpl.data_ptr(), 0, wpl[0].numel()
+        a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
+        a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
+        _run(Km, a, mode, wgs)
+        outs[mode] = o
+    for i in range(2):
+        assert torch.equal(outs[0][i], outs[2][i]), i
+    assert not torch.equal(outs[0][0], init[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,cin,cout,k", [(16, 16, 50, 20, 5), (16, 16, 50, 50, 3)])
+def test_duo_unpool_bit_identical(H, W, cin, cout, k):
+    """A data gradient whose output is a pool's gradient scatters it to the
+    forward's argmax cells of the pool source (slot chosen per group)."""
+    Km = K()
+    torch.manual_seed(7)
+    G, B = 3, 8
+    cinp, coutp = pad8(cin), pad8(cout)
+    dz = torch.zeros(G, B, H, W, cinp, device=DEV)
+    dz[..., :cin] = torch.randn(G, B, H, W, cin, device=DEV)
+    w = torch.zeros(G, coutp, k, k, cinp, device=DEV)
+    w[:, :cout, :, :, :cin] = torch.randn(G, cout, k, k, cin, device=DEV) * 0.1
+    wpl = _split(w)
+    pm = torch.randint(0, 8, (G * B, H, W, coutp), dtype=torch.uint8, device=DEV)
+    sel = torch.tensor([0, 1, 0], dtype=torch.int32, device=DEV)
+    rows = torch.tensor([[g, 1, 1 | (1 << 25), 0] for g in range(G)], dtype=torch.int32, device=DEV)
+    outs = {}
+    for mode in (0, 2):
+        x0 = torch.full((G, B, 2 * H, 2 * W, coutp), 4.0, device=DEV)
+        x1 = torch.full((G, B, 2 * H, 2 * W, coutp), 6.0, device=DEV)
+        dummy = torch.zeros(G, B, H, W, coutp, device=DEV)
+        a = Km.ConvArgs()
+        a.inp[0], a.out[0] = dz.data_ptr(), dummy.data_ptr()
+        a.gtab, a.ngroups, a.relu, a.epi_bf16 = rows.data_ptr(), G, 0, 0
+        a.w, a.bias, a.wps = wpl.data_ptr(), 0, wpl[0].numel()
+        a.pool_y, a.pool_mask, a.unpool_x1, a.unpool_sel = x0.data_ptr(), pm.data_ptr(), x1.data_ptr(), sel.data_ptr()
+        a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
+        a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
+        _run(Km, a, mode, 6)
+        outs[mode] = (x0, x1, dummy)
+    for i in range(3):
+        assert torch.equal(outs[0][i], outs[2][i]), i

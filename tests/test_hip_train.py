@@ -170,3 +170,22 @@ def test_fused_pool_matches_separate_pool_kernel(dtype, bn, monkeypatch):
         assert torch.equal(a, b)
     for a, b in zip(out["1"][2], out["0"][2]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("bn", [False, True])
+def test_eval_batch_does_not_change_metrics(bn):
+    """K13: the validation forward runs ``eval_batch()`` rows per launch on
+    forward-only buffers; per-sample outputs do not depend on the batch, and
+    the fold sums accumulate in fp64, so metrics are identical at 32 and 256
+    rows per launch (with BatchNorm: running statistics)."""
+    from gentun_amd.models import cnn_engine as E
+    x, y, folds, plan = _setup(n=900)
+    dev = torch.device("cuda", 0)
+    res = []
+    for eb in (32, 256):
+        cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="fp32", loss="ce",
+                            reset="all", eval_batch=eb, batch_norm=bn)
+        job = E.make_job("hip", plan, x, y, folds, cfg, dev)
+        assert (job.eval_batch() == 32) if eb == 32 else (job.eval_batch() >= 128)   # 300-sample folds
+        res.append(job.launch().finish())
+    assert res[0] == res[1]
