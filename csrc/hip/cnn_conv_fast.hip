@@ -832,6 +832,7 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
   }
   float xr[NPT][8];
   auto stage_issue = [&](const Tile& x) {                 // first input slot / gathered image -> xr
+    if (a.dbg & 4) return;
     const float* src = a.gather
         ? static_cast<const float*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + x.gr.g) * a.B + x.b] * img
         : static_cast<const float*>(a.in[__builtin_ctz(x.gr.in_mask | 0x100) & 7]) + ((long)x.gr.g * a.B + x.b) * img;
@@ -839,12 +840,11 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
     for (int j = 0; j < NPT; ++j) {
       const int hh = x.h0 + pdh[j], ww = pdw[j];
       const bool ok = ttid + TNT * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
-      if (ok) load8f(src + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, xr[j]);
+      load8f_or0(src + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, ok, xr[j]);
     }
   };
   auto stage_finish = [&](const Tile& x, uint4* buf) {    // other DAG inputs, split, LDS, xsum
+    if (a.dbg & 4) return;
     const int first = __builtin_ctz(x.gr.in_mask | 0x100) & 7;
     const bool multi = !a.gather && __builtin_popcount(x.gr.in_mask) > 1;
     const long gimg = ((long)x.gr.g * a.B + x.b) * img;
@@ -852,16 +852,17 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
       for (int k = first + 1; k < GT_MAXSLOT; ++k) {
         if (!((x.gr.in_mask >> k) & 1)) continue;
         const float* sk = static_cast<const float*>(a.in[k]) + gimg;
+        float t8[NPT][8];
 #pragma unroll
         for (int j = 0; j < NPT; ++j) {
           const int hh = x.h0 + pdh[j], ww = pdw[j];
-          if (ttid + TNT * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W) {
-            float t8[8];
-            load8f(sk + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, t8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) xr[j][e] += t8[e];
-          }
+          const bool ok = ttid + TNT * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
+          load8f_or0(sk + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, ok, t8[j]);
         }
+#pragma unroll
+        for (int j = 0; j < NPT; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xr[j][e] += t8[j][e];
       }
     }
 #pragma unroll
@@ -948,6 +949,8 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
 
   // ---- epilogue straight from the accumulators -------------------------------
   // lane: channels co0..co0+3 of pixel p = (pgw + h) * 16 + l16 of the tile
+  // every global load of a slot's read-modify-write is issued before the
+  // first use (one round trip per slot and operand, not one per pixel group)
   auto epilogue = [&](const Tile& x) {
     if (a.dbg & 2) return;
     const int g = x.gr.g;
@@ -955,10 +958,13 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
     const long obase = n * oimg + (long)x.h0 * W * COP;
     const bool pool = a.pool_y && ((x.gr.out_mask >> 24) & 1);
     const bool unpool = (x.gr.out_mask >> 25) & 1;
+    float val[CT][PG][4];
+    bool cok[CT];
 #pragma unroll
     for (int t = 0; t < CT; ++t) {
       const bool pkt = PK && t == CT - 1;
       const int co0 = (wco + t) * 16 + kq * 4;
+      cok[t] = co0 < COP;                                  // whole float4 inside the padded row
       float bv[4] = {0.f, 0.f, 0.f, 0.f};
       if (a.bias) {
         if (pkt) {
@@ -969,7 +975,6 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
           bv[0] = q.x; bv[1] = q.y; bv[2] = q.z; bv[3] = q.w;
         }
       }
-      float val[PG][4];
 #pragma unroll
       for (int h = 0; h < PG; ++h) {
         if (pkt) {
@@ -979,62 +984,106 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float o = __shfl(s0, l16 + 16 * i, 64);
-            val[h][i] = kq == 0 ? o : 0.f;
+            val[t][h][i] = kq == 0 ? o : 0.f;
           }
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             float v = acc[t][h][i] + bv[i];
             if (a.relu) v = fmaxf(v, 0.f);
-            val[h][i] = v;
+            val[t][h][i] = v;
           }
         }
       }
-      if (co0 >= COP) continue;                            // whole float4 beyond the padded row
+    }
+    auto off_of = [&](int t, int h) {
+      return obase + (long)((pgw + h) * 16 + l16) * COP + (wco + t) * 16 + kq * 4;
+    };
+    if (unpool) {
+      // the output is a pool's gradient: scatter each value to the forward's argmax cell (if > 0)
+      uint32_t mk[CT][PG];
 #pragma unroll
-      for (int h = 0; h < PG; ++h) {
-        const int p = (pgw + h) * 16 + l16;
-        const long off = obase + (long)p * COP + co0;
-        if (unpool) {
-          // the output is a pool's gradient: scatter each value to the forward's argmax cell (if > 0)
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int h = 0; h < PG; ++h)
+          mk[t][h] = *reinterpret_cast<const uint32_t*>(a.pool_mask + (cok[t] ? off_of(t, h) : 0));
+      float* dst = static_cast<float*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.pool_y);
+      const int H2 = 2 * a.H, W2 = 2 * W;
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        if (!cok[t]) continue;
+#pragma unroll
+        for (int h = 0; h < PG; ++h) {
+          const int p = (pgw + h) * 16 + l16;
           const int hh = x.h0 + p / W, ww = p % W;
-          const uint32_t mk = *reinterpret_cast<const uint32_t*>(a.pool_mask + off);
-          float* dst = static_cast<float*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.pool_y);
-          const int H2 = 2 * a.H, W2 = 2 * W;
 #pragma unroll
           for (int me = 0; me < 4; ++me) {
             float o[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const uint32_t bb = (mk >> (8 * i)) & 0xffu;
-              o[i] = ((int)(bb & 3u) == me && (bb & 4u)) ? val[h][i] : 0.f;
+              const uint32_t bb = (mk[t][h] >> (8 * i)) & 0xffu;
+              o[i] = ((int)(bb & 3u) == me && (bb & 4u)) ? val[t][h][i] : 0.f;
             }
-            *reinterpret_cast<float4*>(dst + ((n * H2 + 2 * hh + (me >> 1)) * W2 + 2 * ww + (me & 1)) * COP + co0) =
-                make_float4(o[0], o[1], o[2], o[3]);
+            *reinterpret_cast<float4*>(dst + ((n * H2 + 2 * hh + (me >> 1)) * W2 + 2 * ww + (me & 1)) * COP +
+                                       (wco + t) * 16 + kq * 4) = make_float4(o[0], o[1], o[2], o[3]);
           }
-          continue;
-        }
-        for (int k = 0; k < GT_MAXSLOT; ++k) {
-          if (!((x.gr.out_mask >> k) & 1)) continue;
-          float* dst = static_cast<float*>(a.out[k]) + off;
-          float4 o = make_float4(val[h][0], val[h][1], val[h][2], val[h][3]);
-          if ((x.gr.out_mask >> (8 + k)) & 1) {
-            const float4 q = *reinterpret_cast<const float4*>(dst);
-            o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
-          }
-          if ((x.gr.out_mask >> (16 + k)) & 1) {
-            const float4 m = *reinterpret_cast<const float4*>(static_cast<const float*>(a.out_mask[k]) + off);
-            o.x = m.x > 0.f ? o.x : 0.f; o.y = m.y > 0.f ? o.y : 0.f;
-            o.z = m.z > 0.f ? o.z : 0.f; o.w = m.w > 0.f ? o.w : 0.f;
-          }
-          *reinterpret_cast<float4*>(dst) = o;
         }
       }
-      if constexpr (POOLABLE) {
-        if (pool) {
-          // 2x2 max-pool + argmax mask (pool_fwd_kernel's rule: first strict maximum over
-          // (0,0), (0,1), (1,0), (1,1); bit 2 = maximum > 0) of the values as stored
-          const int Ho = a.H >> 1, Wo = W >> 1;
+    } else {
+      for (int k = 0; k < GT_MAXSLOT; ++k) {
+        if (!((x.gr.out_mask >> k) & 1)) continue;
+        float* dst = static_cast<float*>(a.out[k]);
+        float o[CT][PG][4];
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[t][h][i] = val[t][h][i];
+        if ((x.gr.out_mask >> (8 + k)) & 1) {              // accumulate into the slot
+          float4 q[CT][PG];
+#pragma unroll
+          for (int t = 0; t < CT; ++t)
+#pragma unroll
+            for (int h = 0; h < PG; ++h) q[t][h] = *reinterpret_cast<const float4*>(dst + (cok[t] ? off_of(t, h) : 0));
+#pragma unroll
+          for (int t = 0; t < CT; ++t)
+#pragma unroll
+            for (int h = 0; h < PG; ++h) {
+              o[t][h][0] += q[t][h].x; o[t][h][1] += q[t][h].y; o[t][h][2] += q[t][h].z; o[t][h][3] += q[t][h].w;
+            }
+        }
+        if ((x.gr.out_mask >> (16 + k)) & 1) {             // ReLU mask of the slot's activation
+          const float* mp = static_cast<const float*>(a.out_mask[k]);
+          float4 q[CT][PG];
+#pragma unroll
+          for (int t = 0; t < CT; ++t)
+#pragma unroll
+            for (int h = 0; h < PG; ++h) q[t][h] = *reinterpret_cast<const float4*>(mp + (cok[t] ? off_of(t, h) : 0));
+#pragma unroll
+          for (int t = 0; t < CT; ++t)
+#pragma unroll
+            for (int h = 0; h < PG; ++h) {
+              o[t][h][0] = q[t][h].x > 0.f ? o[t][h][0] : 0.f; o[t][h][1] = q[t][h].y > 0.f ? o[t][h][1] : 0.f;
+              o[t][h][2] = q[t][h].z > 0.f ? o[t][h][2] : 0.f; o[t][h][3] = q[t][h].w > 0.f ? o[t][h][3] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
+          if (!cok[t]) continue;
+#pragma unroll
+          for (int h = 0; h < PG; ++h)
+            *reinterpret_cast<float4*>(dst + off_of(t, h)) = make_float4(o[t][h][0], o[t][h][1], o[t][h][2], o[t][h][3]);
+        }
+      }
+    }
+    if constexpr (POOLABLE) {
+      if (pool) {
+        // 2x2 max-pool + argmax mask (pool_fwd_kernel's rule: first strict maximum over
+        // (0,0), (0,1), (1,0), (1,1); bit 2 = maximum > 0) of the values as stored
+        const int Ho = a.H >> 1, Wo = W >> 1;
+#pragma unroll
+        for (int t = 0; t < CT; ++t) {
 #pragma unroll
           for (int h = 0; h < PG; ++h) {
             if ((h / RG) % 2) continue;                     // top row of each row pair
@@ -1042,7 +1091,7 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
             uint32_t mk = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float v00 = val[h][i], v10 = val[h + RG][i];
+              const float v00 = val[t][h][i], v10 = val[t][h + RG][i];
               const float v01 = __shfl(v00, lane + 1, 64), v11 = __shfl(v10, lane + 1, 64);
               float mm = v00;
               int arg = 0;
@@ -1052,10 +1101,10 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
               m[i] = mm;
               mk |= (uint32_t)(arg | (mm > 0.f ? 4 : 0)) << (8 * i);
             }
-            if (l16 & 1) continue;
+            if ((l16 & 1) || !cok[t]) continue;
             const int p = (pgw + h) * 16 + l16;
             const int pr = (x.h0 + p / W) >> 1, pc = (p % W) >> 1;
-            const long o = ((n * Ho + pr) * Wo + pc) * COP + co0;
+            const long o = ((n * Ho + pr) * Wo + pc) * COP + (wco + t) * 16 + kq * 4;
             *reinterpret_cast<float4*>(static_cast<float*>(a.pool_y) + o) = make_float4(m[0], m[1], m[2], m[3]);
             if (a.pool_mask) *reinterpret_cast<uint32_t*>(a.pool_mask + o) = mk;
           }
@@ -1101,7 +1150,7 @@ static int g_f32_duo = -1;
 static int g_duo_wgs = 256;        // persistent workgroups (one per CU)
 
 extern "C" int gt_conv_set_duo(int mode, int wgs) {
-  if (g_f32_duo < 0) g_f32_duo = 1;
+  if (g_f32_duo < 0) g_f32_duo = 0;
   const int old = g_f32_duo;
   g_f32_duo = mode;
   if (wgs > 0) g_duo_wgs = wgs;
@@ -1109,7 +1158,9 @@ extern "C" int gt_conv_set_duo(int mode, int wgs) {
 }
 
 static bool duo_ok(int ntiles) {
-  if (g_f32_duo < 0) g_f32_duo = std::getenv("GENTUN_F32_DUO") ? std::atoi(std::getenv("GENTUN_F32_DUO")) : 1;
+  // off by default: measured slower than the tile kernel (profiles/conv_f32_duo_ab_r3.txt -- the memory
+  // phases do overlap, but one MFMA wave per SIMD runs the k loop at ~80 % of the tile kernel's two)
+  if (g_f32_duo < 0) g_f32_duo = std::getenv("GENTUN_F32_DUO") ? std::atoi(std::getenv("GENTUN_F32_DUO")) : 0;
   if (g_f32_duo == 0) return false;
   return g_f32_duo == 2 || ntiles >= 2 * g_duo_wgs;
 }

@@ -57,6 +57,7 @@ struct DenseFwdArgs {
   int C;
   int prec;                // 0: bf16 tensors, bf16 MFMA; 1: fp32 tensors, split-fp32 MFMA (common.h)
   long wps;                // unused (kept for the ABI)
+  int row_off;             // data parallelism (X5): this rank's first row of the full batch (dropout keys)
 };
 
 // an MFMA A operand of 8 consecutive weights of the transposed W1 copy: bf16
@@ -141,7 +142,8 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
         float z = acc[h][i] + a.bias[(long)g * a.Up + u0 + i];
         z = fmaxf(z, 0.f);
         if (a.train && a.drop_p > 0.f) {
-          const uint32_t r = hash4(seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)row, (uint32_t)(u0 + i));
+          const uint32_t r = hash4(seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)(row + a.row_off),
+                                   (uint32_t)(u0 + i));
           z = (r >= thr) ? z * keep_scale : 0.f;
         }
         v[i] = PREC ? z : bf2f(f2bf(z));      // the head sees exactly the stored activation
@@ -192,6 +194,7 @@ struct HeadArgs {
   int eval;
   int prec;
   const int* valid;        // [steps][G] real rows of each training batch (Keras short batch) or null = B
+  const int* valid_norm;   // X5: [steps][G] real rows of the FULL batch (loss mean over all ranks' rows) or null
 };
 
 #define HEAD_MAXB 64
@@ -252,7 +255,8 @@ __global__ void __launch_bounds__(64) head_fwd_kernel(HeadArgs a) {
   float* dz = a.dz + ((long)g * a.B + b) * C;
   // mean over the batch's real rows; padding rows of a short batch: zero weight
   const int nv = a.valid ? a.valid[(long)step * a.G + g] : a.B;
-  const float inv_b = (b < nv && nv > 0) ? 1.0f / nv : 0.f;
+  const int nn = a.valid_norm ? a.valid_norm[(long)step * a.G + g] : nv;
+  const float inv_b = (b < nv && nn > 0) ? 1.0f / nn : 0.f;
   if (a.loss_ce) {
     for (int c = 0; c < C; ++c) dz[c] = (p[c] - ((c == y) ? 1.f : 0.f)) * inv_b;
   } else {
@@ -451,6 +455,9 @@ struct DenseWgradAdamArgs {
                        // (zero forever: skipped, 13 % of the layer's optimizer traffic)
   int prec;
   long wps;            // unused (kept for the ABI)
+  float* gbuf;         // X5 data parallelism: [G][Fp][Up] gradient buffer
+  int mode;            // 0: fused gradient + update; 1: gradient -> gbuf only (all-reduced next);
+                       // 2: update (and transposed copy) from gbuf
 };
 
 // grid (Fp/16, G), 256 threads. Thread: unit quad q (4 units), rows fr, fr+2, ..., fr+14.
@@ -482,13 +489,33 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
     float acc[8][4];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r][0] = acc[r][1] = acc[r][2] = acc[r][3] = 0.f;
-    for (int b = 0; b < a.B; ++b) {
+    if (a.mode == 2) {                                  // all-reduced gradient from gbuf
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int f = f0 + fr + 2 * r;
+        if (f < a.Fp) {
+          const float4 q4 = *reinterpret_cast<const float4*>(a.gbuf + ((long)g * a.Fp + f) * a.Up + u0);
+          acc[r][0] = q4.x; acc[r][1] = q4.y; acc[r][2] = q4.z; acc[r][3] = q4.w;
+        }
+      }
+    }
+    for (int b = 0; a.mode != 2 && b < a.B; ++b) {
       const float4 d = *reinterpret_cast<const float4*>(dH + (long)b * a.Up + u0);
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         const float xv = xs[b * 16 + fr + 2 * r];
         acc[r][0] += xv * d.x; acc[r][1] += xv * d.y; acc[r][2] += xv * d.z; acc[r][3] += xv * d.w;
       }
+    }
+    if (a.mode == 1) {                                  // gradient only (this rank's rows)
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int f = f0 + fr + 2 * r;
+        if (f < a.Fp)
+          *reinterpret_cast<float4*>(a.gbuf + ((long)g * a.Fp + f) * a.Up + u0) =
+              make_float4(acc[r][0], acc[r][1], acc[r][2], acc[r][3]);
+      }
+      continue;
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -515,6 +542,7 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
       *reinterpret_cast<float4*>(a.v + off) = vv;
     }
   }
+  if (a.mode == 1) return;                            // (uniform) no update, no copy
   __syncthreads();
   // transposed copy: wt[u][f0 .. f0+15] (32 / 64 contiguous bytes per unit), 8 values per store
   const int nu = a.Ur > 0 ? ((a.Ur + 3) >> 2) << 2 : a.Up;
@@ -649,7 +677,7 @@ int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
 }
 
 int gt_head(const HeadArgs* a, hipStream_t stream) {
-  if (a->B > HEAD_MAXB || a->C > HEAD_MAXC) return -1;
+  if ((!a->eval && a->B > HEAD_MAXB) || a->C > HEAD_MAXC) return -1;    // the batch limit is head_bwd's LDS
   if (a->Up % 16) return -2;
   hipLaunchKernelGGL(head_fwd_kernel, dim3(a->G * a->B), dim3(64), 0, stream, *a);
   if (!a->eval) hipLaunchKernelGGL(head_bwd_kernel, dim3((a->Up + 63) / 64, a->G), dim3(256), 0, stream, *a);

@@ -137,6 +137,16 @@ __device__ __forceinline__ void load8f(const float* p, float* f) {
   f[4] = q1.x; f[5] = q1.y; f[6] = q1.z; f[7] = q1.w;
 }
 
+// 32 zero bytes in global memory: the source of out-of-image patch chunks
+__device__ __attribute__((aligned(32), weak)) float gt_zero8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+
+// load8f of p, or 8 zeros when !ok -- without a branch: the address is
+// selected, the two loads always issue (a load under a per-chunk branch makes
+// hipcc wait vmcnt(0) at each branch, serialising a thread's whole staging)
+__device__ __forceinline__ void load8f_or0(const float* p, bool ok, float* f) {
+  load8f(ok ? p : gt_zero8, f);
+}
+
 __device__ __forceinline__ void store8f(float* p, const float* f) {
   reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
   reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);

@@ -82,6 +82,7 @@ class HipPopJob(FoldJob):
         super(HipPopJob, self).__init__(plan, x, y, folds, cfg, device, **kw)
         if self.device.type != "cuda":
             raise RuntimeError("the HIP backend needs a GPU device")
+        self._setup_dp()
         self.L = K.lib()
         self.prec = K.PREC[cfg.dtype]
         self.npl = K.NPL[cfg.dtype]
@@ -127,6 +128,68 @@ class HipPopJob(FoldJob):
         self._build_adam_table()
         self._build_args()
 
+    # ------------------------------------------------------------ X5
+    def _setup_dp(self):
+        """Intra-candidate data parallelism on the HIP
+        executor: ``cfg.dp_group`` ranks each train rows ``[r0, r1)`` of every
+        group's batch -- the kernels see a batch of ``r1 - r0`` -- with the
+        loss normalised by the FULL batch's real rows, dropout keyed by the
+        full-batch row, and every gradient (conv weight gradients after their
+        split-K reduce, dW1 written by the dense weight-gradient kernel in
+        gradient-only mode, dW2 / db2 / db1) summed over the ranks by one
+        all-reduce of a flat buffer before the identical optimizer step on
+        every rank (RCCL over xGMI with the nccl backend; gloo through host
+        memory). The step runs eagerly (no graph: the collective is host-side
+        for gloo)."""
+        grp = getattr(self.cfg, "dp_group", None)
+        self.dp = None
+        if grp is None:
+            return
+        if self.bn:
+            raise ValueError("data parallelism with BatchNorm would need synchronised batch statistics")
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(grp), dist.get_rank(grp)
+        B = self.B
+        r0, r1 = rank * B // world, (rank + 1) * B // world
+        if r1 <= r0:
+            raise ValueError("data parallelism: batch {} over {} ranks leaves a rank without rows".format(B, world))
+        self.dp = (grp, rank, world, r0, r1)
+        self.capture_ok = False
+        self.B_full = B
+        self.epoch_idx_full = self.epoch_idx
+        self.epoch_idx = torch.zeros((self.steps_per_epoch, self.G, r1 - r0), dtype=torch.int64, device=self.device)
+        self.epoch_valid_full = self.epoch_valid
+        self.epoch_valid = (self.epoch_valid_full - r0).clamp(0, r1 - r0).to(torch.int32).contiguous()
+        self.B = r1 - r0
+
+    def _new_epoch_order(self):
+        if getattr(self, "dp", None) is None:
+            return super(HipPopJob, self)._new_epoch_order()
+        r0, r1 = self.dp[3], self.dp[4]
+        local, self.epoch_idx, self.B = self.epoch_idx, self.epoch_idx_full, self.B_full
+        try:
+            super(HipPopJob, self)._new_epoch_order()        # the full batch order (same on every rank)
+        finally:
+            self.epoch_idx, self.B = local, r1 - r0
+        self.epoch_idx.copy_(self.epoch_idx_full[:, :, r0:r1])
+
+    def _dp_allreduce(self):
+        """Sum every gradient over the data-parallel ranks (one flat buffer)."""
+        import torch.distributed as dist
+        grads = self._dp_grads
+        flat = torch.cat([t.reshape(-1) for t in grads])
+        if dist.get_backend(self.dp[0]) == "nccl":
+            dist.all_reduce(flat, group=self.dp[0])
+        else:                                           # gloo: through host memory
+            host = flat.cpu()
+            dist.all_reduce(host, group=self.dp[0])
+            flat.copy_(host)
+        o = 0
+        for t in grads:
+            n = t.numel()
+            t.copy_(flat[o:o + n].view_as(t))
+            o += n
+
     # ------------------------------------------------------------ topology
     def _build_topology(self):
         """Superset layers / per-group launch records (models/pop_schedule.py)
@@ -143,7 +206,8 @@ class HipPopJob(FoldJob):
             L.pps, L.S = K.wgrad_split(self.B * L.H * L.W, L.Kdim, L.coutp, band=band)
             # split-K partials summed by a reduce launch right after the layer's wgrad, on the
             # weight-gradient stream (off the data-gradient chain); the optimizer then reads one gradient
-            L.wred = L.S > 1 and (L.coutp * L.Kdim) % 4 == 0 and os.environ.get("GENTUN_WGRAD_REDUCE", "1") != "0"
+            L.wred = L.S > 1 and (L.coutp * L.Kdim) % 4 == 0 and (
+                os.environ.get("GENTUN_WGRAD_REDUCE", "1") != "0" or self.dp is not None)
         self.last = self.sched.last
         hs, ws = h0 >> len(p0.kernels_per_layer), w0 >> len(p0.kernels_per_layer)
         if hs < 1 or ws < 1:
@@ -445,6 +509,16 @@ class HipPopJob(FoldJob):
         dw.Cp, dw.Cr, dw.Ur = self.final_cp, self.plan.kernels_per_layer[-1], self.plan.dense_units
         dw.prec, dw.wps = prec, self.w1t.numel()
         self.dense_wgrad_args = dw
+        if self.dp is not None:
+            # X5: dW1 to a buffer (mode 1), all-reduced, then the update from it (mode 2)
+            self.gW1 = torch.zeros((Q, self.Fp, self.Up), dtype=torch.float32, device=self.device)
+            dw.gbuf, dw.mode = self.gW1.data_ptr(), 1
+            self.dense_apply_args = K.DenseWgradAdamArgs.from_buffer_copy(dw)
+            self.dense_apply_args.mode = 2
+            df.row_off = self.dp[3]
+            hd.valid_norm = self.epoch_valid_full.data_ptr()
+            self._dp_grads = [t for L in self.layers for t in (L.part_w[0], L.part_b[0])] + \
+                [self.gW1, self.gW2, self.gb2, self.gb1]
         # ---- backward (records: models/pop_schedule.py PopulationSchedule.backward)
         self.bwd_ops = []
         bn_done = set()
@@ -714,6 +788,9 @@ class HipPopJob(FoldJob):
                 ev = torch.cuda.Event()
                 ev.record(stream)
                 main.wait_event(ev)
+        if self.dp is not None:
+            self._dp_allreduce()
+            K.check(L.gt_dense_wgrad_adam(self.dense_apply_args, s), "dense_wgrad_adam(apply)")
         if side3 is not None:
             K.check(L.gt_adam_segments(self.adam_head[0], self.adam_head[1], s), "adam")
         else:

@@ -50,14 +50,14 @@ class WgradArgs(C.Structure):
 class DenseFwdArgs(C.Structure):
     _fields_ = [("x", P), ("wt", P), ("bias", P), ("out", P), ("w2", P), ("plog", P), ("st", P), ("fold_ids", P),
                 ("seeds", P), ("G", I), ("B", I), ("Fp", I), ("Up", I), ("drop_p", C.c_float), ("train", I),
-                ("seed", C.c_uint), ("C", I), ("prec", I), ("wps", C.c_long)]
+                ("seed", C.c_uint), ("C", I), ("prec", I), ("wps", C.c_long), ("row_off", I)]
 
 
 class HeadArgs(C.Structure):
     _fields_ = [("h", P), ("w2", P), ("b2", P), ("labels", P), ("gather", P), ("st", P), ("dH", P),
                 ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P), ("dz", P), ("plog", P),
                 ("G", I), ("B", I), ("Up", I), ("C", I), ("loss_ce", I), ("drop_scale", C.c_float), ("eval", I),
-                ("prec", I), ("valid", P)]
+                ("prec", I), ("valid", P), ("valid_norm", P)]
 
 
 class DenseDgradArgs(C.Structure):
@@ -69,7 +69,7 @@ class DenseDgradArgs(C.Structure):
 class DenseWgradAdamArgs(C.Structure):
     _fields_ = [("x", P), ("dH", P), ("p", P), ("m", P), ("v", P), ("wt", P), ("st", P),
                 ("G", I), ("B", I), ("Fp", I), ("Up", I), ("Cp", I), ("Cr", I), ("Ur", I), ("prec", I),
-                ("wps", C.c_long)]
+                ("wps", C.c_long), ("gbuf", P), ("mode", I)]
 
 
 class AdamSeg(C.Structure):

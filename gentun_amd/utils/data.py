@@ -226,6 +226,66 @@ def make_relation_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0,
     return x.astype(dtype), y
 
 
+def make_compound_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, psize=11, msize=5, dist=(9, 12),
+                                 distractors=1, noise=1.0, dtype=np.float32):
+    """Two-level synthetic images: ``classes // 2`` glyph types (random
+    2-stroke parts, ``psize`` pixels) times a SIDE -- a small marker
+    (``msize``) sits left or right of the glyph, ``dist`` pixels apart
+    (+-2 vertical jitter). Class = (glyph type, side). Placement is random, one
+    distractor stroke is added elsewhere, colours / background / noise as in
+    :func:`make_glyph_classification`.
+
+    The glyph half of the label is easy (every architecture learns it: no
+    collapse to chance, unlike a purely relational task); the side half needs
+    the glyph and the marker in one receptive field ~12 pixels wide, which is
+    what deeper DAG stages buy. So candidates spread between ~0.5 (glyph only)
+    and ~1.0 (glyph and side) by architecture."""
+    rng = np.random.default_rng(seed)
+    h, w, c = shape
+    ntype = classes // 2
+    glyphs = []
+    for _ in range(ntype):
+        img = np.zeros((psize, psize), np.float32)
+        for _ in range(2):
+            img = np.maximum(img, _stroke(rng, psize, 0.6 + 0.4 * rng.uniform(), lo=0.05, hi=0.95))
+        glyphs.append(img)
+    yy, xx = np.meshgrid(np.arange(msize, dtype=np.float32), np.arange(msize, dtype=np.float32), indexing="ij")
+    r = (msize - 1) / 2.0
+    marker = np.clip(1.0 - (np.hypot(yy - r, xx - r) - 0.35 * msize) / 1.0, 0.0, 1.0)      # a filled dot
+    labels = np.arange(n) % (2 * ntype)
+    rng.shuffle(labels)
+    color = rng.uniform(0.45, 1.0, size=(n, c)).astype(np.float32)
+    bg0 = rng.uniform(0.0, 0.25, size=(n, c)).astype(np.float32)
+    bgslope = rng.uniform(-0.15, 0.15, size=(n, 2, c)).astype(np.float32)
+    ramp_y = np.linspace(-0.5, 0.5, h, dtype=np.float32)[:, None, None]
+    ramp_x = np.linspace(-0.5, 0.5, w, dtype=np.float32)[None, :, None]
+    mo = (psize - msize) // 2
+    x = np.empty((n, h, w, c), np.float32)
+    for i in range(n):
+        t, side = labels[i] // 2, labels[i] % 2
+        d = int(rng.integers(dist[0], dist[1] + 1)) * (1 if side else -1)
+        jy = int(rng.integers(-2, 3))
+        # glyph box at (y0, x0); marker box at (y0 + mo + jy, x0 + mo + d), both inside the image
+        xlo, xhi = max(0, -(mo + d)), min(w - psize, w - msize - mo - d)
+        ylo, yhi = max(0, -(mo + jy)), min(h - psize, h - msize - mo - jy)
+        y0, x0 = int(rng.integers(ylo, yhi + 1)), int(rng.integers(xlo, xhi + 1))
+        g = np.zeros((h, w), np.float32)
+        g[y0:y0 + psize, x0:x0 + psize] = glyphs[t]
+        my, mx = y0 + mo + jy, x0 + mo + d
+        g[my:my + msize, mx:mx + msize] = np.maximum(g[my:my + msize, mx:mx + msize], marker)
+        for _ in range(distractors):
+            s = _stroke(rng, 9, 0.6, lo=0.1, hi=0.9)
+            yy0, xx0 = int(rng.integers(0, h - 8)), int(rng.integers(0, w - 8))
+            g[yy0:yy0 + 9, xx0:xx0 + 9] = np.maximum(g[yy0:yy0 + 9, xx0:xx0 + 9], 0.8 * s)
+        gg = g[:, :, None]
+        x[i] = (bg0[i] + ramp_y * bgslope[i, 0] + ramp_x * bgslope[i, 1]) * (1.0 - gg) + color[i] * gg
+    x += noise * 0.25 * rng.standard_normal(size=x.shape).astype(np.float32)
+    np.clip(x, 0.0, 1.0, out=x)
+    y = np.zeros((n, 2 * ntype), np.float32)
+    y[np.arange(n), labels] = 1.0
+    return x.astype(dtype), y
+
+
 def make_image_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, noise=0.35, shift=3,
                               dtype=np.float32):
     """Synthetic image classification set: x in [0,1] NHWC, y one-hot.

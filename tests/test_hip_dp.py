@@ -1,0 +1,68 @@
+"""X5 on the HIP executor (optional): two ranks (gloo, both on
+GPU 0 -- the multi-GPU path is RCCL with the same code) each train rows
+[r0, r1) of every batch of a population job with the HIP kernels, the
+gradients (conv weight gradients after their split-K reduce, dW1 from the
+dense weight-gradient kernel in gradient-only mode, dW2 / db2 / db1) are
+summed by one all-reduce, and the identical optimizer step follows. The
+trajectory equals the single-process run of the same job (fp32 up to the
+gradient summation order; dropout keyed by the full-batch row, Keras short
+last batch normalised by the full batch)."""
+
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _job(dp_group=None):
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.genome import make_plan
+    from gentun_amd.utils.data import make_image_classification, stratified_kfold
+    x, y = make_image_classification(n=520, shape=(32, 32, 3), classes=10, seed=3, noise=0.35, shift=3)
+    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)     # 260 training rows: a short last batch
+    plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10)
+             for g in ({'S_1': '101', 'S_2': '0101110011'}, {'S_1': '000', 'S_2': '1000000001'})]
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="fp32", loss="bce_compat",
+                        reset="all", dp_group=dp_group)
+    return E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg, torch.device("cuda", 0))
+
+
+def _train(job):
+    job.launch()
+    res = job.finish()
+    torch.cuda.synchronize()
+    return job.flat.detach().cpu().clone(), res
+
+
+def _worker(rank, port, out):
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=2)
+    try:
+        flat, res = _train(_job(dp_group=dist.group.WORLD))
+        torch.save({"flat": flat, "cat": [r["categorical_accuracy"] for r in res]},
+                   os.path.join(out, "rank{}.pt".format(rank)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_hip_data_parallel_matches_single_process():
+    single, sres = _train(_job())
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(port, d), nprocs=2, join=True)
+        r0 = torch.load(os.path.join(d, "rank0.pt"), weights_only=True)
+        r1 = torch.load(os.path.join(d, "rank1.pt"), weights_only=True)
+    assert torch.equal(r0["flat"], r1["flat"])              # identical optimizer steps on every rank
+    scale = single.abs().max()
+    assert (r0["flat"] - single).abs().max() <= 1e-4 * scale, (r0["flat"] - single).abs().max()
+    for a, b in zip(r0["cat"], [r["categorical_accuracy"] for r in sres]):
+        assert np.allclose(a, b, atol=0.02)

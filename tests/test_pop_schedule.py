@@ -76,6 +76,7 @@ def _run_schedule(sched, x, P, R):
     """Forward then backward through the launch records; returns
     {(layer, group): (dW, db)}."""
     Q = sched.Q
+    B = x.shape[0]                     # the batch rows this (data-parallel) rank holds
     act, xin = {"input": x}, {}
     # ---- forward: one launch per superset layer, per group its input set
     for st in sched.stages:
