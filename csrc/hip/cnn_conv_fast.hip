@@ -1883,6 +1883,23 @@ extern "C" int gt_wgrad_set_nb(int nb) {
 #define WGRAD_FAST_CASE_F32(KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_)                                     \
   if (a->KH == KH_ && a->KW == KW_ && a->Cinp == NCBI_ * 8 && a->Coutp == NCBO_ * 8 && a->W == W_ &&     \
       a->H % R_ == 0 && a->pps % (R_ * W_) == 0) {                                                        \
+    const int nz_ = wgrad_nz(a);                                                                         \
+    if (nz_ > 1) {                                                                                       \
+      dim3 gz(a->S, a->ngroups, nz_);                                                                    \
+      const bool pkz = wgrad_pk_ok(a, (NCBO_ * 8 + 15) / 16);                                            \
+      if (nz_ == 2) {                                                                                    \
+        if (pkz) hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 1, 2>), gz, \
+                                    dim3(NW_ * 64), 0, stream, *a);                                      \
+        else hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 0, 2>), gz,     \
+                                dim3(NW_ * 64), 0, stream, *a);                                          \
+      } else {                                                                                           \
+        if (pkz) hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 1, 4>), gz, \
+                                    dim3(NW_ * 64), 0, stream, *a);                                      \
+        else hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 0, 4>), gz,     \
+                                dim3(NW_ * 64), 0, stream, *a);                                          \
+      }                                                                                                  \
+      return (int)hipGetLastError();                                                                     \
+    }                                                                                                    \
     dim3 grid(a->S, a->ngroups);                                                                         \
     const bool pk = wgrad_pk_ok(a, (NCBO_ * 8 + 15) / 16);                                               \
     if ((g_wgrad_nb ? g_wgrad_nb : NB_) == 1) {                                                          \
@@ -1908,6 +1925,29 @@ extern "C" int gt_wgrad_set_nb(int nb) {
                          dim3(NW_ * 64), 0, stream, *a);                                                 \
     return (int)hipGetLastError();                                                                       \
   }
+
+// Small launches (few groups x splits: a population job of 1-5 groups, the
+// reference's sequential folds or a rank's share on 8 GPUs): the k-column
+// tiles are sliced over NZ workgroups that stage the same bands, so the
+// grid fills more CUs and each workgroup's serial band loop carries 1/NZ of
+// the MFMAs. Every weight's sum runs in the same band / k-step order in any
+// slice: results are bit-identical for any NZ (tests/test_hip_kernels.py).
+// GENTUN_WGRAD_NZ: 0 auto (default), 1 / 2 / 4 forced.
+static int g_wgrad_nz = -1;
+
+extern "C" int gt_wgrad_set_nz(int nz) {
+  const int old = g_wgrad_nz;
+  g_wgrad_nz = nz;
+  return old;
+}
+
+static int wgrad_nz(const WgradArgs* a) {
+  if (g_wgrad_nz < 0) g_wgrad_nz = std::getenv("GENTUN_WGRAD_NZ") ? std::atoi(std::getenv("GENTUN_WGRAD_NZ")) : 0;
+  const int force = g_wgrad_nz;
+  if (force == 1 || force == 2 || force == 4) return force;
+  const int blocks = a->S * a->ngroups;
+  return blocks < 64 ? 4 : blocks < 160 ? 2 : 1;
+}
 
 // packed last co tile of the fp32 wgrad (A/B switch GENTUN_WGRAD_PK=0 disables)
 static bool wgrad_pk_ok(const WgradArgs* a, int mt) {

@@ -82,12 +82,12 @@ class HipPopJob(FoldJob):
         super(HipPopJob, self).__init__(plan, x, y, folds, cfg, device, **kw)
         if self.device.type != "cuda":
             raise RuntimeError("the HIP backend needs a GPU device")
-        self._setup_dp()
         self.L = K.lib()
         self.prec = K.PREC[cfg.dtype]
         self.npl = K.NPL[cfg.dtype]
         self.adt = torch.float32 if self.prec else torch.bfloat16      # activation / gradient storage
         self.bn = bool(getattr(cfg, "batch_norm", False))
+        self._setup_dp()
         p0 = self.plan
         Q, B, dev = self.G, self.B, self.device
         self.Q = Q
@@ -118,7 +118,8 @@ class HipPopJob(FoldJob):
         # the dense W1 optimizer (the largest single launch) on a stream of its
         # own, so it does not sit in front of the first conv wgrads
         self.side2 = torch.cuda.Stream(dev)
-        self.overlap = True
+        # GENTUN_OVERLAP=0: one stream (A/B of the fork / join edges at small launches)
+        self.overlap = os.environ.get("GENTUN_OVERLAP", "1") != "0"
         self.w1_stream = os.environ.get("GENTUN_W1_STREAM", "1") != "0"
         # conv-layer optimizer updates per layer on a third stream (A/B switch, off:
         # 907 vs 958 candidates/h with it on -- it competes with the dgrad chain,

@@ -286,6 +286,71 @@ def make_compound_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0,
     return x.astype(dtype), y
 
 
+def make_variant_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, noise=1.0, shift=5, clutter=0.8,
+                                tick=6, tick_width=0.7, label_noise=0.0, dtype=np.float32):
+    """Coarse + fine classes: ``classes // 2`` base glyphs (the 4-stroke
+    glyphs of :func:`make_glyph_classification`, whose strong, image-wide
+    signal every architecture picks up early -- no extra collapse to chance),
+    each in two VARIANTS that carry a short ``tick``-pixel stroke at one of two
+    glyph-relative places (variant A vs B). A sample is translated, coloured,
+    cluttered by another base glyph (without tick) and noised as in the glyph
+    set. The base glyph answers half of the label; the variant needs the small
+    tick localised relative to its glyph under clutter and noise -- the part
+    that should separate architectures (BASELINE cfg 2-4 bench data,
+    ``make_cifar_like``)."""
+    rng = np.random.default_rng(seed)
+    h, w, c = shape
+    size = max(h, w) + 2 * shift
+    nb = classes // 2
+    base = np.stack([_glyph(rng, size, 4, 0.9 + 0.5 * rng.uniform()) for _ in range(nb)])
+    variants = []
+    for k in range(nb):
+        for _ in range(2):
+            t = np.zeros((size, size), np.float32)
+            cy, cx = rng.uniform(0.3 * size, 0.7 * size, size=2)
+            ang = rng.uniform(0, np.pi)
+            a = np.array([cy - 0.5 * tick * np.sin(ang), cx - 0.5 * tick * np.cos(ang)], np.float32)
+            b = np.array([cy + 0.5 * tick * np.sin(ang), cx + 0.5 * tick * np.cos(ang)], np.float32)
+            yy, xx = np.meshgrid(np.arange(size, dtype=np.float32), np.arange(size, dtype=np.float32), indexing="ij")
+            d = b - a
+            tt = np.clip(((yy - a[0]) * d[0] + (xx - a[1]) * d[1]) / max(float(d @ d), 1e-6), 0.0, 1.0)
+            dist = np.hypot(yy - (a[0] + tt * d[0]), xx - (a[1] + tt * d[1]))
+            t = np.clip(1.0 - (dist - tick_width) / 1.2, 0.0, 1.0)
+            variants.append(np.maximum(base[k], t))
+    glyphs = np.stack(variants)                          # class k*2 + v
+    labels = np.arange(n) % (2 * nb)
+    rng.shuffle(labels)
+    dy = rng.integers(0, 2 * shift + 1, size=n)
+    dx = rng.integers(0, 2 * shift + 1, size=n)
+    ody = rng.integers(0, 2 * shift + 1, size=n)
+    odx = rng.integers(0, 2 * shift + 1, size=n)
+    other = (labels // 2 + rng.integers(1, nb, size=n)) % nb
+    alpha = rng.uniform(0.0, clutter, size=n).astype(np.float32)
+    color = rng.uniform(0.45, 1.0, size=(n, c)).astype(np.float32)
+    ocolor = rng.uniform(0.2, 1.0, size=(n, c)).astype(np.float32)
+    bg0 = rng.uniform(0.0, 0.25, size=(n, c)).astype(np.float32)
+    bgslope = rng.uniform(-0.15, 0.15, size=(n, 2, c)).astype(np.float32)
+    ramp_y = np.linspace(-0.5, 0.5, h, dtype=np.float32)[:, None, None]
+    ramp_x = np.linspace(-0.5, 0.5, w, dtype=np.float32)[None, :, None]
+    x = np.empty((n, h, w, c), np.float32)
+    for i in range(n):
+        g = glyphs[labels[i], dy[i]:dy[i] + h, dx[i]:dx[i] + w][:, :, None]
+        o = base[other[i], ody[i]:ody[i] + h, odx[i]:odx[i] + w][:, :, None]
+        bg = bg0[i] + ramp_y * bgslope[i, 0] + ramp_x * bgslope[i, 1]
+        img = bg * (1.0 - g) + color[i] * g
+        x[i] = img * (1.0 - alpha[i] * o) + alpha[i] * ocolor[i] * o
+    x += noise * 0.25 * rng.standard_normal(size=x.shape).astype(np.float32)
+    np.clip(x, 0.0, 1.0, out=x)
+    if label_noise > 0:
+        # a fraction of the labels names the OTHER variant of the same base glyph: the best achievable
+        # accuracy is 1 - label_noise, and a network that memorises the flips validates lower
+        flip = rng.uniform(size=n) < label_noise
+        labels = np.where(flip, labels ^ 1, labels)
+    y = np.zeros((n, 2 * nb), np.float32)
+    y[np.arange(n), labels] = 1.0
+    return x.astype(dtype), y
+
+
 def make_image_classification(n=10000, shape=(32, 32, 3), classes=10, seed=0, noise=0.35, shift=3,
                               dtype=np.float32):
     """Synthetic image classification set: x in [0,1] NHWC, y one-hot.

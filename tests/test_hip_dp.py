@@ -6,7 +6,7 @@ dense weight-gradient kernel in gradient-only mode, dW2 / db2 / db1) are
 summed by one all-reduce, and the identical optimizer step follows. The
 trajectory equals the single-process run of the same job (fp32 up to the
 gradient summation order; dropout keyed by the full-batch row, Keras short
-last batch normalised by the full batch)."""
+last batch normalised by the full batch; SGD-momentum -- see _job)."""
 
 import os
 import socket
@@ -28,8 +28,10 @@ def _job(dp_group=None):
     folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)     # 260 training rows: a short last batch
     plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10)
              for g in ({'S_1': '101', 'S_2': '0101110011'}, {'S_1': '000', 'S_2': '1000000001'})]
-    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="fp32", loss="bce_compat",
-                        reset="all", dp_group=dp_group)
+    # SGD: Adam turns the summation-order noise of near-zero gradients into +-lr steps (sign flips), which
+    # would hide a real mismatch; with SGD-momentum the two trajectories must agree to fp32 rounding
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-2,), batch_size=32, dtype="fp32", loss="bce_compat",
+                        reset="all", optimizer="sgd", momentum=0.9, dp_group=dp_group)
     return E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg, torch.device("cuda", 0))
 
 

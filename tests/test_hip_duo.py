@@ -163,3 +163,54 @@ def test_duo_unpool_bit_identical(H, W, cin, cout, k):
         outs[mode] = (x0, x1, dummy)
     for i in range(3):
         assert torch.equal(outs[0][i], outs[2][i]), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,cin,cout,k", SHAPES[:4])
+@pytest.mark.parametrize("nin", [1, 2])
+def test_wgrad_column_slices_bit_identical(H, W, cin, cout, k, nin):
+    """Small launches slice the fp32 wgrad's k-column tiles over NZ = 2 / 4
+    workgroups per (split, group): every weight gradient (and the bias
+    column) is bit-identical to the one-workgroup kernel, for single and
+    summed (DAG) inputs and the packed last co tile."""
+    import ctypes
+    Km = K()
+    L = Km.lib()
+    L.gt_wgrad_set_nz.argtypes = [ctypes.c_int]
+    L.gt_wgrad_set_nz.restype = ctypes.c_int
+    torch.manual_seed(3 + k + nin)
+    G, B = 2, 8
+    cinp, coutp = pad8(cin), pad8(cout)
+    xs = []
+    for _ in range(nin):
+        x = torch.zeros(G, B, H, W, cinp, device=DEV)
+        x[..., :cin] = torch.randn(G, B, H, W, cin, device=DEV)
+        xs.append(x)
+    dz = torch.zeros(G, B, H, W, coutp, device=DEV)
+    dz[..., :cout] = torch.randn(G, B, H, W, cout, device=DEV)
+    kd = k * k * cinp
+    pps, S = Km.wgrad_split(B * H * W, kd, coutp, G, band=Km.wgrad_band(k, k, cinp, coutp, H, W, 1))
+    rows = torch.tensor([[g, (1 << nin) - 1, 0, 0] for g in range(G)], dtype=torch.int32, device=DEV)
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    res = {}
+    for nz in (1, 2, 4):
+        pw = torch.full((S, G, coutp, kd), 9.0, device=DEV)
+        pb = torch.full((S, G, coutp), 9.0, device=DEV)
+        a = Km.WgradArgs()
+        for i, t in enumerate(xs):
+            a.inp[i] = t.data_ptr()
+        a.gtab, a.ngroups, a.gather, a.st = rows.data_ptr(), G, 0, st.data_ptr()
+        a.dz, a.part_w, a.part_b = dz.data_ptr(), pw.data_ptr(), pb.data_ptr()
+        a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW, a.S, a.pps = G, B, H, W, cinp, coutp, k, k, S, pps
+        a.prec, a.cout_real = 1, cout
+        old = L.gt_wgrad_set_nz(nz)
+        try:
+            Km.check(L.gt_conv_wgrad(a, torch.cuda.current_stream().cuda_stream), "wgrad")
+            torch.cuda.synchronize()
+        finally:
+            L.gt_wgrad_set_nz(old)
+        res[nz] = (pw, pb)
+    for nz in (2, 4):
+        assert torch.equal(res[1][0], res[nz][0]), nz
+        assert torch.equal(res[1][1], res[nz][1]), nz
+    assert not torch.equal(res[1][0], torch.full_like(res[1][0], 9.0))

@@ -2,7 +2,7 @@
 # round 3: eval-batch tests, streams-at-small-P probe, compound dataset spread
 export GENTUN_NO_AUTOBUILD=1
 mkdir -p gpurun_out; rm -f gpurun_out/streams.log gpurun_out/probe_spread3.log
-timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_hip_train.py > gpurun_out/hip_train_tests.log 2>&1 || { tail -30 gpurun_out/hip_train_tests.log; exit 1; }
+timeout -k 10 500 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_hip_dp.py > gpurun_out/hip_train_tests.log 2>&1 || { tail -30 gpurun_out/hip_train_tests.log; exit 1; }
 tail -2 gpurun_out/hip_train_tests.log
 for cfg in "5 5 1" "5 3 2" "2 2 1" "2 1 2" "10 5 2" "10 10 1"; do
   set -- $cfg

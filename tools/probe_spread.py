@@ -28,7 +28,9 @@ epochs = tuple(int(v) for v in (sys.argv[4] if len(sys.argv) > 4 else "20,4,1").
 lrs = tuple(float(v) for v in (sys.argv[5] if len(sys.argv) > 5 else "1e-3,1e-4,1e-5").split(","))
 dev = torch.device("cuda", 0)
 t0 = time.perf_counter()
-if gen == "compound":
+if gen == "variant":
+    x, y = D.make_variant_classification(n=10000, shape=(32, 32, 3), seed=0, **kw)
+elif gen == "compound":
     x, y = D.make_compound_classification(n=10000, shape=(32, 32, 3), seed=0, **kw)
 elif gen == "relation":
     x, y = D.make_relation_classification(n=10000, shape=(32, 32, 3), seed=0, **kw)

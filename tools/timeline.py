@@ -28,9 +28,11 @@ for a, b in zip(starts[5:], starts[6:]):           # skip the first steps (graph
             cur_e = max(cur_e, e)
     busy += cur_e - cur_s
     per = defaultdict(int)
+    cnt = defaultdict(int)
     for s, e, n, _ in seg:
         per[n.split("(")[0][:60]] += e - s
-    steps.append((t1 - t0, busy, sum(e - s for s, e, _, _ in seg), per))
+        cnt[n.split("(")[0][:60]] += 1
+    steps.append((t1 - t0, busy, sum(e - s for s, e, _, _ in seg), per, cnt, len(seg)))
 if not steps:
     print("no steps found")
     sys.exit(0)
@@ -40,9 +42,14 @@ busy = sum(s[1] for s in steps) / n
 ksum = sum(s[2] for s in steps) / n
 print("steps analysed: {}  wall/step {:.1f} us  busy (union) {:.1f} us ({:.0f}%)  sum of kernel times {:.1f} us "
       "(overlap factor {:.2f})".format(n, wall / 1e3, busy / 1e3, 100 * busy / wall, ksum / 1e3, ksum / busy))
-tot = defaultdict(int)
+print("launches per step: {:.1f}; gap (wall - busy) per launch: {:.2f} us".format(
+    sum(s[5] for s in steps) / n, (wall - busy) / 1e3 / max(1.0, sum(s[5] for s in steps) / n)))
+tot, tcnt = defaultdict(int), defaultdict(int)
 for s in steps:
     for k, v in s[3].items():
         tot[k] += v
+    for k, v in s[4].items():
+        tcnt[k] += v
 for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
-    print("{:62s} {:8.1f} us/step {:5.1f}% of wall".format(k, v / n / 1e3, 100 * v / n / wall))
+    print("{:62s} {:8.1f} us/step {:5.1f}% of wall  {:5.1f} calls/step {:7.1f} us/call".format(
+        k, v / n / 1e3, 100 * v / n / wall, tcnt[k] / n, v / max(1, tcnt[k]) / 1e3))
