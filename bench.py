@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--epochs", default="20,4,1")
     ap.add_argument("--lr", default="1e-3,1e-4,1e-5")
     ap.add_argument("--samples", type=int, default=10000)
+    ap.add_argument("--data", choices=("hard", "glyph"), default="hard",
+                    help="hard: base glyphs x tick variants, 30 %% variant-label noise (utils/data.make_cifar_hard: "
+                         "learned folds 0.61-0.66 by architecture); glyph: round-2 data (every learned fold ~0.99)")
     ap.add_argument("--nfold", type=int, default=5)
     ap.add_argument("--dtype", default="fp32", choices=("fp32", "bf16"))
     ap.add_argument("--loss", default="bce_compat", choices=("bce_compat", "ce"))
@@ -122,7 +125,7 @@ def run(args):
     from gentun_amd.parallel import DistComm, LocalComm
     from gentun_amd.parallel.distributed import DistributedPopulation, GentunWorker
     from gentun_amd.utils import rng as grng
-    from gentun_amd.utils.data import make_cifar_like
+    from gentun_amd.utils.data import make_cifar_hard, make_cifar_like
 
     if world > 1:
         # RCCL (backend "nccl") over xGMI between GPUs; GENTUN_DIST_BACKEND=gloo for rehearsals
@@ -134,7 +137,7 @@ def run(args):
     epochs = tuple(int(e) for e in args.epochs.split(","))
     lrs = tuple(float(x) for x in args.lr.split(","))
     per_gpu = args.per_gpu or (5 if args.dtype == "fp32" else 8)
-    x, y = make_cifar_like(n=args.samples, seed=0)
+    x, y = (make_cifar_hard if args.data == "hard" else make_cifar_like)(n=args.samples, seed=0)
     nodes, kernels = ((3, 4, 5), (20, 50, 100)) if args.space == "deep" else ((3, 5), (20, 50))
     if args.kernels:
         kernels = tuple(int(k) for k in args.kernels.split(","))
@@ -228,8 +231,10 @@ def run(args):
         "scaling": "weak" if args.pop_per_gpu else "strong",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (CIFAR-10-shaped {}k x 32x32x3 coloured stroke glyphs + clutter + noise; "
-                "random-init weights)".format(args.samples // 1000),
+        "data": ("synthetic (CIFAR-10-shaped {}k x 32x32x3: 5 stroke glyphs x 2 tick variants + clutter + noise, "
+                 "30% variant-label noise; random-init weights)" if args.data == "hard" else
+                 "synthetic (CIFAR-10-shaped {}k x 32x32x3 coloured stroke glyphs + clutter + noise; "
+                 "random-init weights)").format(args.samples // 1000),
         "config": {"model": "Genetic-CNN {} dense 500".format(space), "global_batch": 32 * args.nfold,
                    "seq_len": None,
                    "parallelism": ("population-dp{} (RCCL genome bcast / score all_gather over xGMI)".format(N)

@@ -119,10 +119,14 @@ def _run_search(args, species, x, y, extra, maximize):
 
 def cmd_cnn(args):
     from . import GeneticCnnIndividual
-    from .utils.data import make_glyph_classification
+    from .utils.data import make_glyph_classification, make_variant_classification
     shape = _ints(args.input_shape)
-    x, y = make_glyph_classification(n=args.samples, shape=shape, classes=args.classes, seed=args.data_seed,
-                                     noise=args.noise)
+    if args.data == "hard":
+        x, y = make_variant_classification(n=args.samples, shape=shape, classes=args.classes, seed=args.data_seed,
+                                           noise=0.7 if args.noise is None else args.noise, label_noise=0.3)
+    else:
+        x, y = make_glyph_classification(n=args.samples, shape=shape, classes=args.classes, seed=args.data_seed,
+                                         noise=1.0 if args.noise is None else args.noise)
     nodes = _ints(args.nodes)
     kernels = _ints(args.kernels)
     ks = tuple((k, k) for k in _ints(args.kernel_sizes))
@@ -182,7 +186,10 @@ def main(argv=None):
     c.add_argument("--input-shape", default="32,32,3")
     c.add_argument("--classes", type=int, default=10)
     c.add_argument("--samples", type=int, default=10000)
-    c.add_argument("--noise", type=float, default=1.0)
+    c.add_argument("--noise", type=float, default=None, help="image noise (default 1.0 glyph / 0.7 hard)")
+    c.add_argument("--data", choices=("glyph", "hard"), default="glyph",
+                   help="glyph: stroke glyphs (every learned fold ~0.99); hard: glyph x tick variants with 30 %% "
+                        "variant-label noise (accuracy depends on the architecture; the bench data)")
     c.add_argument("--data-seed", type=int, default=0)
     c.add_argument("--dense", type=int, default=500)
     c.add_argument("--dropout", type=float, default=0.5)

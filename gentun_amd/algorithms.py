@@ -75,6 +75,10 @@ class GeneticAlgorithm(object):
             "wall_s": wall,
             "candidates_per_hour": (3600.0 * pending / wall) if wall > 0 and pending else None,
         }
+        cat = (getattr(fittest, "fold_metrics", None) or {}).get("categorical_accuracy")
+        if cat:
+            # Genetic-CNN: the fitness is the reference's binary accuracy; record categorical too
+            rec["best_cat_acc"] = float(sum(cat) / len(cat))
         self.history.append(rec)
         if self.best_individual is None or self._better(fittest.get_fitness(), self.best_individual.get_fitness()):
             self.best_individual = fittest

@@ -396,6 +396,18 @@ def make_cifar_like(n=10000, seed=0, noise=1.0, shift=5, clutter=0.8):
                                      clutter=clutter)
 
 
+def make_cifar_hard(n=10000, seed=0):
+    """Discriminative bench dataset (round 3): :func:`make_variant_classification`
+    with 30 % of the variant labels flipped and noise 0.7 -- five base glyphs x
+    two tick variants. Measured on 12 random S=(3,5) candidates under the full
+    reference protocol (profiles/dataset_spread_r3.txt): a learned fold scores
+    0.61-0.66 (the flips cap it at 0.70; how much of them a network memorises
+    depends on its architecture), 4 of 60 folds collapsed to chance -- unlike
+    :func:`make_cifar_like`, where every learned fold saturates at 0.98-0.99 and
+    only fold collapse separates candidates."""
+    return make_variant_classification(n=n, shape=(32, 32, 3), classes=10, seed=seed, noise=0.7, label_noise=0.3)
+
+
 def make_mnist_like(n=10000, seed=0, noise=1.0, shift=4, clutter=0.8):
     """28x28x1 glyphs (reference driver config, tests/test_mnist.py:17-34,
     whose MNIST download is dead)."""
