@@ -127,7 +127,13 @@ __device__ __forceinline__ void unpool_chunk(const ConvArgs& a, int g, long n, i
 // one accumulator) give every row a_p (b0 + b1 + b2), and the epilogue sums
 // the plane rows of a channel -- all nine split terms in 3 MFMAs instead of
 // six terms in 6.
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0, int PK = 0>
+// forward declaration: the register-direct fp32 epilogue (defined with the duo kernel below)
+template <int CT, int PG, int PK, int W, int NCO, bool POOLABLE>
+__device__ __forceinline__ void f32_epi_regs(const ConvArgs& a, const GroupRec& gr, int b, int h0,
+                                             const f32x4_t (&acc)[CT][PG], int wco, int pgw, int lane);
+
+// RE (fp32 only): 1 = register-direct epilogue (f32_epi_regs), 0 = through the LDS output tile
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0, int PK = 0, int RE = 0>
 __global__ void __launch_bounds__(NWV * 64)
 __attribute__((amdgpu_waves_per_eu(PREC ? 2 : (NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))))
 conv_fast_kernel(ConvArgs a) {
@@ -380,6 +386,12 @@ conv_fast_kernel(ConvArgs a) {
     }
   }
 
+  if constexpr (RE != 0 && PREC != 0 && W % 16 == 0) {
+    // register-direct: no LDS round trip, no barrier (and the pool from lane shuffles)
+    constexpr bool PL = TH % 2 == 0 && PG % (2 * (W / 16)) == 0;
+    f32_epi_regs<CT, PG, PK, W, NCO, PL>(a, gr, b, h0, acc, wco, pgw, lane);
+    return;
+  }
   // ---- epilogue: accumulators -> tile in LDS -> 16-byte row stores ---------
   // (a lane holds 4 channels of one pixel per tile: 8-byte scattered stores
   // are store-issue bound; through LDS every store is a contiguous chunk of
@@ -763,6 +775,181 @@ struct DuoCfg {
   }
 };
 
+// Register-direct fp32 epilogue of one output tile (shared by the duo and the
+// tile kernel): lane = 4 channels of pixel (pgw + h) * 16 + l16; bias / ReLU;
+// plain store, or the data gradient's DAG fan-out (accumulate, ReLU mask, up to
+// 8 slots) with every global load of a slot's read-modify-write issued before
+// its first use; the fused un-pool; the fused 2x2 max-pool + argmax mask from
+// lane shuffles and the paired pixel-group register (a wave's pixel groups
+// cover whole row pairs). Bit-identical to the LDS-tile epilogue.
+template <int CT, int PG, int PK, int W, int NCO, bool POOLABLE>
+__device__ __forceinline__ void f32_epi_regs(const ConvArgs& a, const GroupRec& gr, int b, int h0,
+                                             const f32x4_t (&acc)[CT][PG], int wco, int pgw, int lane) {
+  constexpr int COP = NCO * 8, RG = W / 16;
+  const int kq = lane >> 4, l16 = lane & 15;
+  const long oimg = (long)a.H * W * COP;
+
+  if (a.dbg & 2) return;
+  const int g = gr.g;
+  const long n = (long)g * a.B + b;
+  const long obase = n * oimg + (long)h0 * W * COP;
+  const bool pool = a.pool_y && ((gr.out_mask >> 24) & 1);
+  const bool unpool = (gr.out_mask >> 25) & 1;
+  float val[CT][PG][4];
+  bool cok[CT];
+#pragma unroll
+  for (int t = 0; t < CT; ++t) {
+    const bool pkt = PK && t == CT - 1;
+    const int co0 = (wco + t) * 16 + kq * 4;
+    cok[t] = co0 < COP;                                  // whole float4 inside the padded row
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (a.bias) {
+      if (pkt) {
+        const int co = (wco + t) * 16 + kq;
+        bv[0] = co < COP ? a.bias[(long)g * COP + co] : 0.f;
+      } else if (co0 < COP) {
+        const float4 q = *reinterpret_cast<const float4*>(a.bias + (long)g * COP + co0);
+        bv[0] = q.x; bv[1] = q.y; bv[2] = q.z; bv[3] = q.w;
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < PG; ++h) {
+      if (pkt) {
+        // channel (wco+t)*16 + kq (its three plane rows summed) -> lane kq == 0 gathers channels +0..+3
+        float s0 = acc[t][h][0] + acc[t][h][1] + acc[t][h][2] + bv[0];
+        if (a.relu) s0 = fmaxf(s0, 0.f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float o = __shfl(s0, l16 + 16 * i, 64);
+          val[t][h][i] = kq == 0 ? o : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = acc[t][h][i] + bv[i];
+          if (a.relu) v = fmaxf(v, 0.f);
+          val[t][h][i] = v;
+        }
+      }
+    }
+  }
+  auto off_of = [&](int t, int h) {
+    return obase + (long)((pgw + h) * 16 + l16) * COP + (wco + t) * 16 + kq * 4;
+  };
+  if (unpool) {
+    // the output is a pool's gradient: scatter each value to the forward's argmax cell (if > 0)
+    uint32_t mk[CT][PG];
+#pragma unroll
+    for (int t = 0; t < CT; ++t)
+#pragma unroll
+      for (int h = 0; h < PG; ++h)
+        mk[t][h] = *reinterpret_cast<const uint32_t*>(a.pool_mask + (cok[t] ? off_of(t, h) : 0));
+    float* dst = static_cast<float*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.pool_y);
+    const int H2 = 2 * a.H, W2 = 2 * W;
+#pragma unroll
+    for (int t = 0; t < CT; ++t) {
+      if (!cok[t]) continue;
+#pragma unroll
+      for (int h = 0; h < PG; ++h) {
+        const int p = (pgw + h) * 16 + l16;
+        const int hh = h0 + p / W, ww = p % W;
+#pragma unroll
+        for (int me = 0; me < 4; ++me) {
+          float o[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t bb = (mk[t][h] >> (8 * i)) & 0xffu;
+            o[i] = ((int)(bb & 3u) == me && (bb & 4u)) ? val[t][h][i] : 0.f;
+          }
+          *reinterpret_cast<float4*>(dst + ((n * H2 + 2 * hh + (me >> 1)) * W2 + 2 * ww + (me & 1)) * COP +
+                                     (wco + t) * 16 + kq * 4) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
+  } else {
+    for (int k = 0; k < GT_MAXSLOT; ++k) {
+      if (!((gr.out_mask >> k) & 1)) continue;
+      float* dst = static_cast<float*>(a.out[k]);
+      float o[CT][PG][4];
+#pragma unroll
+      for (int t = 0; t < CT; ++t)
+#pragma unroll
+        for (int h = 0; h < PG; ++h)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[t][h][i] = val[t][h][i];
+      if ((gr.out_mask >> (8 + k)) & 1) {              // accumulate into the slot
+        float4 q[CT][PG];
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h) q[t][h] = *reinterpret_cast<const float4*>(dst + (cok[t] ? off_of(t, h) : 0));
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h) {
+            o[t][h][0] += q[t][h].x; o[t][h][1] += q[t][h].y; o[t][h][2] += q[t][h].z; o[t][h][3] += q[t][h].w;
+          }
+      }
+      if ((gr.out_mask >> (16 + k)) & 1) {             // ReLU mask of the slot's activation
+        const float* mp = static_cast<const float*>(a.out_mask[k]);
+        float4 q[CT][PG];
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h) q[t][h] = *reinterpret_cast<const float4*>(mp + (cok[t] ? off_of(t, h) : 0));
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h) {
+            o[t][h][0] = q[t][h].x > 0.f ? o[t][h][0] : 0.f; o[t][h][1] = q[t][h].y > 0.f ? o[t][h][1] : 0.f;
+            o[t][h][2] = q[t][h].z > 0.f ? o[t][h][2] : 0.f; o[t][h][3] = q[t][h].w > 0.f ? o[t][h][3] : 0.f;
+          }
+      }
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+        if (!cok[t]) continue;
+#pragma unroll
+        for (int h = 0; h < PG; ++h)
+          *reinterpret_cast<float4*>(dst + off_of(t, h)) = make_float4(o[t][h][0], o[t][h][1], o[t][h][2], o[t][h][3]);
+      }
+    }
+  }
+  if constexpr (POOLABLE) {
+    if (pool) {
+      // 2x2 max-pool + argmax mask (pool_fwd_kernel's rule: first strict maximum over
+      // (0,0), (0,1), (1,0), (1,1); bit 2 = maximum > 0) of the values as stored
+      const int Ho = a.H >> 1, Wo = W >> 1;
+#pragma unroll
+      for (int t = 0; t < CT; ++t) {
+#pragma unroll
+        for (int h = 0; h < PG; ++h) {
+          if ((h / RG) % 2) continue;                     // top row of each row pair
+          float m[4];
+          uint32_t mk = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float v00 = val[t][h][i], v10 = val[t][h + RG][i];
+            const float v01 = __shfl(v00, lane + 1, 64), v11 = __shfl(v10, lane + 1, 64);
+            float mm = v00;
+            int arg = 0;
+            if (v01 > mm) { mm = v01; arg = 1; }
+            if (v10 > mm) { mm = v10; arg = 2; }
+            if (v11 > mm) { mm = v11; arg = 3; }
+            m[i] = mm;
+            mk |= (uint32_t)(arg | (mm > 0.f ? 4 : 0)) << (8 * i);
+          }
+          if ((l16 & 1) || !cok[t]) continue;
+          const int p = (pgw + h) * 16 + l16;
+          const int pr = (h0 + p / W) >> 1, pc = (p % W) >> 1;
+          const long o = ((n * Ho + pr) * Wo + pc) * COP + (wco + t) * 16 + kq * 4;
+          *reinterpret_cast<float4*>(static_cast<float*>(a.pool_y) + o) = make_float4(m[0], m[1], m[2], m[3]);
+          if (a.pool_mask) *reinterpret_cast<uint32_t*>(a.pool_mask + o) = mk;
+        }
+      }
+    }
+  }
+}
+
 template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int PK>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 conv_duo_f32_kernel(ConvArgs a, int ntiles) {
@@ -949,168 +1136,8 @@ conv_duo_f32_kernel(ConvArgs a, int ntiles) {
 
   // ---- epilogue straight from the accumulators -------------------------------
   // lane: channels co0..co0+3 of pixel p = (pgw + h) * 16 + l16 of the tile
-  // every global load of a slot's read-modify-write is issued before the
-  // first use (one round trip per slot and operand, not one per pixel group)
   auto epilogue = [&](const Tile& x) {
-    if (a.dbg & 2) return;
-    const int g = x.gr.g;
-    const long n = (long)g * a.B + x.b;
-    const long obase = n * oimg + (long)x.h0 * W * COP;
-    const bool pool = a.pool_y && ((x.gr.out_mask >> 24) & 1);
-    const bool unpool = (x.gr.out_mask >> 25) & 1;
-    float val[CT][PG][4];
-    bool cok[CT];
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      const bool pkt = PK && t == CT - 1;
-      const int co0 = (wco + t) * 16 + kq * 4;
-      cok[t] = co0 < COP;                                  // whole float4 inside the padded row
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.bias) {
-        if (pkt) {
-          const int co = (wco + t) * 16 + kq;
-          bv[0] = co < COP ? a.bias[(long)g * COP + co] : 0.f;
-        } else if (co0 < COP) {
-          const float4 q = *reinterpret_cast<const float4*>(a.bias + (long)g * COP + co0);
-          bv[0] = q.x; bv[1] = q.y; bv[2] = q.z; bv[3] = q.w;
-        }
-      }
-#pragma unroll
-      for (int h = 0; h < PG; ++h) {
-        if (pkt) {
-          // channel (wco+t)*16 + kq (its three plane rows summed) -> lane kq == 0 gathers channels +0..+3
-          float s0 = acc[t][h][0] + acc[t][h][1] + acc[t][h][2] + bv[0];
-          if (a.relu) s0 = fmaxf(s0, 0.f);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float o = __shfl(s0, l16 + 16 * i, 64);
-            val[t][h][i] = kq == 0 ? o : 0.f;
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float v = acc[t][h][i] + bv[i];
-            if (a.relu) v = fmaxf(v, 0.f);
-            val[t][h][i] = v;
-          }
-        }
-      }
-    }
-    auto off_of = [&](int t, int h) {
-      return obase + (long)((pgw + h) * 16 + l16) * COP + (wco + t) * 16 + kq * 4;
-    };
-    if (unpool) {
-      // the output is a pool's gradient: scatter each value to the forward's argmax cell (if > 0)
-      uint32_t mk[CT][PG];
-#pragma unroll
-      for (int t = 0; t < CT; ++t)
-#pragma unroll
-        for (int h = 0; h < PG; ++h)
-          mk[t][h] = *reinterpret_cast<const uint32_t*>(a.pool_mask + (cok[t] ? off_of(t, h) : 0));
-      float* dst = static_cast<float*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.pool_y);
-      const int H2 = 2 * a.H, W2 = 2 * W;
-#pragma unroll
-      for (int t = 0; t < CT; ++t) {
-        if (!cok[t]) continue;
-#pragma unroll
-        for (int h = 0; h < PG; ++h) {
-          const int p = (pgw + h) * 16 + l16;
-          const int hh = x.h0 + p / W, ww = p % W;
-#pragma unroll
-          for (int me = 0; me < 4; ++me) {
-            float o[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const uint32_t bb = (mk[t][h] >> (8 * i)) & 0xffu;
-              o[i] = ((int)(bb & 3u) == me && (bb & 4u)) ? val[t][h][i] : 0.f;
-            }
-            *reinterpret_cast<float4*>(dst + ((n * H2 + 2 * hh + (me >> 1)) * W2 + 2 * ww + (me & 1)) * COP +
-                                       (wco + t) * 16 + kq * 4) = make_float4(o[0], o[1], o[2], o[3]);
-          }
-        }
-      }
-    } else {
-      for (int k = 0; k < GT_MAXSLOT; ++k) {
-        if (!((x.gr.out_mask >> k) & 1)) continue;
-        float* dst = static_cast<float*>(a.out[k]);
-        float o[CT][PG][4];
-#pragma unroll
-        for (int t = 0; t < CT; ++t)
-#pragma unroll
-          for (int h = 0; h < PG; ++h)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) o[t][h][i] = val[t][h][i];
-        if ((x.gr.out_mask >> (8 + k)) & 1) {              // accumulate into the slot
-          float4 q[CT][PG];
-#pragma unroll
-          for (int t = 0; t < CT; ++t)
-#pragma unroll
-            for (int h = 0; h < PG; ++h) q[t][h] = *reinterpret_cast<const float4*>(dst + (cok[t] ? off_of(t, h) : 0));
-#pragma unroll
-          for (int t = 0; t < CT; ++t)
-#pragma unroll
-            for (int h = 0; h < PG; ++h) {
-              o[t][h][0] += q[t][h].x; o[t][h][1] += q[t][h].y; o[t][h][2] += q[t][h].z; o[t][h][3] += q[t][h].w;
-            }
-        }
-        if ((x.gr.out_mask >> (16 + k)) & 1) {             // ReLU mask of the slot's activation
-          const float* mp = static_cast<const float*>(a.out_mask[k]);
-          float4 q[CT][PG];
-#pragma unroll
-          for (int t = 0; t < CT; ++t)
-#pragma unroll
-            for (int h = 0; h < PG; ++h) q[t][h] = *reinterpret_cast<const float4*>(mp + (cok[t] ? off_of(t, h) : 0));
-#pragma unroll
-          for (int t = 0; t < CT; ++t)
-#pragma unroll
-            for (int h = 0; h < PG; ++h) {
-              o[t][h][0] = q[t][h].x > 0.f ? o[t][h][0] : 0.f; o[t][h][1] = q[t][h].y > 0.f ? o[t][h][1] : 0.f;
-              o[t][h][2] = q[t][h].z > 0.f ? o[t][h][2] : 0.f; o[t][h][3] = q[t][h].w > 0.f ? o[t][h][3] : 0.f;
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < CT; ++t) {
-          if (!cok[t]) continue;
-#pragma unroll
-          for (int h = 0; h < PG; ++h)
-            *reinterpret_cast<float4*>(dst + off_of(t, h)) = make_float4(o[t][h][0], o[t][h][1], o[t][h][2], o[t][h][3]);
-        }
-      }
-    }
-    if constexpr (POOLABLE) {
-      if (pool) {
-        // 2x2 max-pool + argmax mask (pool_fwd_kernel's rule: first strict maximum over
-        // (0,0), (0,1), (1,0), (1,1); bit 2 = maximum > 0) of the values as stored
-        const int Ho = a.H >> 1, Wo = W >> 1;
-#pragma unroll
-        for (int t = 0; t < CT; ++t) {
-#pragma unroll
-          for (int h = 0; h < PG; ++h) {
-            if ((h / RG) % 2) continue;                     // top row of each row pair
-            float m[4];
-            uint32_t mk = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float v00 = val[t][h][i], v10 = val[t][h + RG][i];
-              const float v01 = __shfl(v00, lane + 1, 64), v11 = __shfl(v10, lane + 1, 64);
-              float mm = v00;
-              int arg = 0;
-              if (v01 > mm) { mm = v01; arg = 1; }
-              if (v10 > mm) { mm = v10; arg = 2; }
-              if (v11 > mm) { mm = v11; arg = 3; }
-              m[i] = mm;
-              mk |= (uint32_t)(arg | (mm > 0.f ? 4 : 0)) << (8 * i);
-            }
-            if ((l16 & 1) || !cok[t]) continue;
-            const int p = (pgw + h) * 16 + l16;
-            const int pr = (x.h0 + p / W) >> 1, pc = (p % W) >> 1;
-            const long o = ((n * Ho + pr) * Wo + pc) * COP + (wco + t) * 16 + kq * 4;
-            *reinterpret_cast<float4*>(static_cast<float*>(a.pool_y) + o) = make_float4(m[0], m[1], m[2], m[3]);
-            if (a.pool_mask) *reinterpret_cast<uint32_t*>(a.pool_mask + o) = mk;
-          }
-        }
-      }
-    }
+    f32_epi_regs<CT, PG, PK, W, NCO, POOLABLE>(a, x.gr, x.b, x.h0, acc, wco, pgw, lane);
   };
 
   // ---- phase loop ---------------------------------------------------------------
@@ -1237,12 +1264,27 @@ static int g_probe = 0;
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
     const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, PREC_>::lds(a->epi_bf16 != 0);      \
     auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_, PK_>;                 \
+    if (PREC_ == 1 && (W_ % 16) == 0 && regepi_on())                                                    \
+      fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_, PK_, 1>;                  \
     lds_limit(fn, lds);                                                                                 \
     hipLaunchKernelGGL(fn, grid, dim3(NWV_ * 64), lds, stream, *a);                                     \
     return (int)hipGetLastError();                                                                      \
   }
 #define CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_)                               \
   CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_, 0)
+
+// fp32 register-direct epilogue in the tile kernel (A/B: GENTUN_F32_REGEPI=0 / 1, gt_conv_set_regepi)
+static int g_regepi = -1;
+static bool regepi_on() {
+  if (g_regepi < 0) g_regepi = std::getenv("GENTUN_F32_REGEPI") ? std::atoi(std::getenv("GENTUN_F32_REGEPI")) : 0;
+  return g_regepi != 0;
+}
+extern "C" int gt_conv_set_regepi(int on) {
+  regepi_on();
+  const int old = g_regepi;
+  g_regepi = on;
+  return old;
+}
 
 // the packed last co tile applies: fp32, the real output channels leave <= 4 in the last 16-channel tile
 static int g_conv_pk = -1;     // A/B switch (GENTUN_CONV_PK=0 disables)

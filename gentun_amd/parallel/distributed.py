@@ -337,6 +337,7 @@ class DistributedPopulation(Population):
             again, _ = self._dispatch([todo[slot] for slot in failed], exclude=info["failed_ranks"])
             for slot, res in zip(failed, again):
                 merged[slot] = res
+        nworst = 0
         for slot, ind in enumerate(todo):
             status, fitness, scores, aux = merged[slot]
             if status != ST_OK:
@@ -350,11 +351,16 @@ class DistributedPopulation(Population):
                 else:
                     warnings.warn("slot {} failed on its rank and on the retry round".format(slot))
                 ind.set_fitness(float("-inf") if self.maximize else float("inf"))
+                nworst += 1
             else:
                 ind.set_fitness(fitness)
                 ind.fold_scores = scores
                 if aux is not None:
                     ind.fold_metrics = dict(getattr(ind, "fold_metrics", None) or {}, categorical_accuracy=aux)
+        if len(todo) > 1 and nworst == len(todo):
+            # nothing evaluated anywhere (a lost device, a broken build): a search on worst-fitness
+            # placeholders is meaningless -- stop loudly instead of breeding from them
+            raise RuntimeError("every evaluation of dispatch {} failed (and its retry)".format(self.generation_counter))
         self.last_dispatch = {"units": info["units"], "candidates": len(todo), "retried": len(failed),
                               "wall_s": time.perf_counter() - t0, "schedule": info["schedule"],
                               "per_rank_units": info["per_rank_units"]}

@@ -28,16 +28,22 @@ def pad8(c):
 
 
 def _run(Km, a, mode, wgs):
+    """mode 0: tile kernel (LDS-tile epilogue); 2: duo kernel forced; 3: tile kernel with the
+    register-direct epilogue (gt_conv_set_regepi)."""
     import ctypes
     L = Km.lib()
     L.gt_conv_set_duo.argtypes = [ctypes.c_int, ctypes.c_int]
     L.gt_conv_set_duo.restype = ctypes.c_int
-    old = L.gt_conv_set_duo(mode, wgs)
+    L.gt_conv_set_regepi.argtypes = [ctypes.c_int]
+    L.gt_conv_set_regepi.restype = ctypes.c_int
+    old = L.gt_conv_set_duo(2 if mode == 2 else 0, wgs)
+    old_re = L.gt_conv_set_regepi(1 if mode == 3 else 0)
     try:
         Km.check(L.gt_conv_fwd(a, torch.cuda.current_stream().cuda_stream), "conv")
         torch.cuda.synchronize()
     finally:
         L.gt_conv_set_duo(old, 256)
+        L.gt_conv_set_regepi(old_re)
 
 
 def _split(w):
@@ -69,7 +75,7 @@ def test_duo_forward_bit_identical(H, W, cin, cout, k, nin, wgs):
     rows = torch.tensor([[0, full, 1 | (1 << 24), 0], [1, 1, 1, 0], [2, full, 1 | (1 << 24), 0]],
                         dtype=torch.int32, device=DEV)
     outs = {}
-    for mode in (0, 2):
+    for mode in (0, 2, 3):
         out = torch.full((G, B, H, W, coutp), 7.0, device=DEV)
         xsum = torch.full((G, B, H, W, cinp), 3.0, device=DEV)
         py = torch.full((G, B, H // 2, W // 2, coutp), 5.0, device=DEV)
@@ -86,8 +92,9 @@ def test_duo_forward_bit_identical(H, W, cin, cout, k, nin, wgs):
         a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
         _run(Km, a, mode, wgs)
         outs[mode] = (out, xsum, py, pm)
-    for name, t0, t2 in zip(("out", "xsum", "pool_y", "pool_mask"), outs[0], outs[2]):
-        assert torch.equal(t0, t2), name
+    for m in (2, 3):
+        for name, t0, t2 in zip(("out", "xsum", "pool_y", "pool_mask"), outs[0], outs[m]):
+            assert torch.equal(t0, t2), (m, name)
     # the reference kernel really pooled groups 0 and 2 (sanity of the comparison itself)
     assert not torch.equal(outs[0][2][0], torch.full_like(outs[0][2][0], 5.0))
 
@@ -113,7 +120,7 @@ def test_duo_data_gradient_bit_identical(H, W, cin, cout, k, wgs):
     rows = torch.tensor([[0, 1, 1 | (1 << 8) | (1 << 16), 0], [1, 1, 3 | (1 << 9) | (1 << 17), 0],
                          [2, 1, 2 | (1 << 16 + 1), 0]], dtype=torch.int32, device=DEV)
     outs = {}
-    for mode in (0, 2):
+    for mode in (0, 2, 3):
         o = [t.clone() for t in init]
         a = Km.ConvArgs()
         a.inp[0] = dz.data_ptr()
@@ -125,8 +132,9 @@ def test_duo_data_gradient_bit_identical(H, W, cin, cout, k, wgs):
         a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
         _run(Km, a, mode, wgs)
         outs[mode] = o
-    for i in range(2):
-        assert torch.equal(outs[0][i], outs[2][i]), i
+    for m in (2, 3):
+        for i in range(2):
+            assert torch.equal(outs[0][i], outs[m][i]), (m, i)
     assert not torch.equal(outs[0][0], init[0])
 
 
@@ -148,7 +156,7 @@ def test_duo_unpool_bit_identical(H, W, cin, cout, k):
     sel = torch.tensor([0, 1, 0], dtype=torch.int32, device=DEV)
     rows = torch.tensor([[g, 1, 1 | (1 << 25), 0] for g in range(G)], dtype=torch.int32, device=DEV)
     outs = {}
-    for mode in (0, 2):
+    for mode in (0, 2, 3):
         x0 = torch.full((G, B, 2 * H, 2 * W, coutp), 4.0, device=DEV)
         x1 = torch.full((G, B, 2 * H, 2 * W, coutp), 6.0, device=DEV)
         dummy = torch.zeros(G, B, H, W, coutp, device=DEV)
@@ -161,8 +169,9 @@ def test_duo_unpool_bit_identical(H, W, cin, cout, k):
         a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
         _run(Km, a, mode, 6)
         outs[mode] = (x0, x1, dummy)
-    for i in range(3):
-        assert torch.equal(outs[0][i], outs[2][i]), i
+    for m in (2, 3):
+        for i in range(3):
+            assert torch.equal(outs[0][i], outs[m][i]), (m, i)
 
 
 @pytest.mark.gpu
