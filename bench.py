@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--per-gpu", type=int, default=None,
-                    help="candidates per GPU per round (default: 5 fp32 / 8 bf16; larger rounds = larger population launches: 794 / 862 / 936 candidates/h at 3 / 4 / 6, profiles/bench_round_size_r2.txt)")
+                    help="candidates per GPU per round (default: 5 fp32 / 8 bf16, 16 with --fold-reset kernels; larger rounds = larger population launches: 794 / 862 / 936 candidates/h at 3 / 4 / 6, profiles/bench_round_size_r2.txt)")
     ap.add_argument("--population", type=int, default=32,
                     help="GA population in total (BASELINE cfg 3: 32 on 8 evaluators; strong scaling)")
     ap.add_argument("--pop-per-gpu", type=int, default=None,
@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--streams", type=int, default=1, help="concurrent population jobs per GPU")
     ap.add_argument("--pop-batch", type=int, default=16, help="candidates (x folds) per population job")
     ap.add_argument("--backend", default=None, help="hip (default on GPU) or torch")
+    ap.add_argument("--torch-unbatched", action="store_true",
+                    help="--backend torch: one candidate per job (default: population-batched TorchPopJob, "
+                         "the same batching as the HIP path)")
     ap.add_argument("--epochs", default="20,4,1")
     ap.add_argument("--lr", default="1e-3,1e-4,1e-5")
     ap.add_argument("--samples", type=int, default=10000)
@@ -136,7 +139,9 @@ def run(args):
 
     epochs = tuple(int(e) for e in args.epochs.split(","))
     lrs = tuple(float(x) for x in args.lr.split(","))
-    per_gpu = args.per_gpu or (5 if args.dtype == "fp32" else 8)
+    # sequential folds (kernels) batch candidates only by fold position: a round takes the whole
+    # pending generation (up to 16 per GPU) so every fold launch carries ~14-16 groups
+    per_gpu = args.per_gpu or (16 if args.fold_reset == "kernels" else 5 if args.dtype == "fp32" else 8)
     x, y = (make_cifar_hard if args.data == "hard" else make_cifar_like)(n=args.samples, seed=0)
     nodes, kernels = ((3, 4, 5), (20, 50, 100)) if args.space == "deep" else ((3, 5), (20, 50))
     if args.kernels:
@@ -147,7 +152,8 @@ def run(args):
                  nfold=args.nfold, epochs=epochs, learning_rate=lrs, batch_size=32, dtype=args.dtype,
                  loss=args.loss, seed=args.seed, backend=args.backend, reset=args.fold_reset, batching="keras",
                  batch_norm=args.batch_norm)
-    evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch)
+    evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch,
+                                    torch_pop=not args.torch_unbatched)
     N = comm.world_size
     round_size = per_gpu * N
 
@@ -248,6 +254,7 @@ def run(args):
                    "fp32_impl": ("fp32 tensors, 3-way exact bf16 split x 6 MFMA terms per product"
                                  if device.type == "cuda" and (args.backend or "hip") == "hip"
                                  else "stock PyTorch fp32 ops (MIOpen / hipBLASLt)") if args.dtype == "fp32" else None,
+                   "torch_population_batched": (not args.torch_unbatched) if args.backend == "torch" else None,
                    "streams_per_gpu": args.streams, "pop_batch": args.pop_batch},
         "generations": len(completed),
         "evals": total_evals,

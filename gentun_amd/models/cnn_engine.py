@@ -463,11 +463,10 @@ class TorchFoldJob(FoldJob):
 
     def __init__(self, *a, **kw):
         super(TorchFoldJob, self).__init__(*a, **kw)
-        if len(self.members) != 1:
-            raise ValueError("the torch executor trains one architecture per job")
+        self._check_members()
         plan, G = self.plan, self.G
         shapes = []
-        for st in plan.convs():
+        for st in self._conv_specs():
             shapes.append((st.name + ".w", (G, st.cout, st.cin, st.k[0], st.k[1]), "glorot",
                            (st.cin * st.k[0] * st.k[1], st.cout * st.k[0] * st.k[1])))
             shapes.append((st.name + ".b", (G, st.cout), "zero", None))
@@ -493,8 +492,15 @@ class TorchFoldJob(FoldJob):
         self.amp = (self.cfg.dtype == "bf16") and self.device.type == "cuda"
         self.drop_gen = None
         # BatchNorm running statistics per conv: [2 (mean, var)][G][C]
-        self.bn_run = {st.name: torch.zeros((2, G, st.cout), device=self.device) for st in plan.convs()} \
+        self.bn_run = {st.name: torch.zeros((2, G, st.cout), device=self.device) for st in self._conv_specs()} \
             if self.cfg.batch_norm else {}
+
+    def _check_members(self):
+        if len(self.members) != 1:
+            raise ValueError("the torch executor trains one architecture per job (TorchPopJob: several)")
+
+    def _conv_specs(self):
+        return self.plan.convs()
 
     def init_params(self):
         with torch.no_grad():
@@ -609,6 +615,11 @@ class TorchFoldJob(FoldJob):
         last = acts[plan.steps[-1].name]
         Bn = last.shape[0]
         feat = last.reshape(Bn, G, -1).permute(1, 0, 2)                     # [G, B, F]
+        return self._head(feat, train, P)
+
+    def _head(self, feat, train, P):
+        """feat [G, B, F] -> logits [G, B, classes] (dense, ReLU, dropout, dense)."""
+        G = self.G
         h = torch.baddbmm(P["dense1.b"][:, None, :], feat, P["dense1.w"])
         h = F.relu(h)
         if train and self.cfg.dropout > 0:
@@ -619,7 +630,8 @@ class TorchFoldJob(FoldJob):
                 self.drop_gen = []
                 for g in range(G):
                     gen = torch.Generator(device=self.device)
-                    gen.manual_seed(_rng.stable_hash(self.base_seed, "dropout", self.fold_ids[g]) & 0x7FFFFFFF)
+                    gen.manual_seed(_rng.stable_hash(self.member_seeds[self.gmember[g]], "dropout", self.fold_ids[g])
+                                    & 0x7FFFFFFF)
                     self.drop_gen.append(gen)
             full = (self.B,) + tuple(h.shape[2:])
             keep = torch.stack([torch.rand(full, generator=gen, device=self.device) for gen in self.drop_gen])
@@ -708,6 +720,116 @@ class TorchFoldJob(FoldJob):
         return loss, binc, catc
 
 
+class TorchPopJob(TorchFoldJob):
+    """Population-batched stock-PyTorch executor (comparator (a) with the
+    HIP path's batching): several architectures of one search
+    space train in ONE set of grouped convolutions. Every group (member,
+    fold) runs the *superset* network of the space -- every node of every
+    stage -- and per-group 0/1 masks select its DAG
+    (genome.decode_stage): node i reads ``E_i x_in + sum_j A_ij n_j``, the
+    output conv reads ``sum_j O_j n_j``, and a stage without a DAG passes
+    its input conv through (``D``). Masked terms add exact zeros to the
+    ReLU outputs, so an active node computes what the one-architecture
+    oracle computes; inactive nodes get zero gradients and Adam leaves
+    them at their initial values. Weights are initialised per (member
+    seed, fold id, tensor name) like TorchFoldJob. Cost: the superset's
+    convolutions for every group (isolated nodes and DAG-less stages are
+    computed and discarded)."""
+
+    def _check_members(self):
+        p0 = self.members[0][0]
+        key = (p0.nodes, p0.input_shape, p0.kernels_per_layer, p0.kernel_sizes, p0.dense_units, p0.classes)
+        for p, _, _ in self.members:
+            if (p.nodes, p.input_shape, p.kernels_per_layer, p.kernel_sizes, p.dense_units, p.classes) != key:
+                raise ValueError("a population job needs one search space (nodes, shapes, kernels, head)")
+        self._build_masks()
+
+    def _conv_specs(self):
+        p0 = self.plan
+        specs, c = [], p0.input_shape[2]
+        for s, cout in enumerate(p0.kernels_per_layer):
+            specs.append(ConvSpec("s{}_in".format(s + 1), None, c, cout, tuple(p0.kernel_sizes[s]), s))
+            if s in self._dag_stages:
+                for i in range(p0.nodes[s]):
+                    specs.append(ConvSpec("s{}_n{}".format(s + 1, i), None, cout, cout, (3, 3), s))
+                specs.append(ConvSpec("s{}_out".format(s + 1), None, cout, cout, (3, 3), s))
+            c = cout
+        return specs
+
+    def _build_masks(self):
+        from .genome import decode_stage
+        p0, G = self.plan, self.G
+        self._dag_stages, self._masks = set(), {}
+        for s, K in enumerate(p0.nodes):
+            A = np.zeros((G, K, K), np.float32)
+            E = np.zeros((G, K), np.float32)
+            O = np.zeros((G, K), np.float32)
+            D = np.zeros((G,), np.float32)
+            for g in range(G):
+                bits = self.members[self.gmember[g]][0].genes["S_{}".format(s + 1)]
+                if not any(b == "1" for b in bits):
+                    continue
+                preds, _succs, active, outputs = decode_stage(bits, K)
+                D[g] = 1.0
+                for i in range(K):
+                    if not active[i]:
+                        continue
+                    if preds[i]:
+                        A[g, i, preds[i]] = 1.0
+                    else:
+                        E[g, i] = 1.0
+                O[g, outputs] = 1.0
+            if D.any():
+                self._dag_stages.add(s)
+            t = lambda v: torch.from_numpy(v).to(self.device)      # noqa: E731
+            self._masks[s] = {"A": t(A), "E": t(E), "O": t(O), "D": t(D), "A_np": A, "E_np": E}
+
+    def _forward(self, xb, train, nval=None):
+        G, p0, P = self.G, self.plan, self._views()
+
+        def conv(name, inp, k):
+            nonlocal nval
+            w = P[name + ".w"]
+            z = F.conv2d(inp, w.reshape(G * w.shape[1], w.shape[2], k[0], k[1]), P[name + ".b"].reshape(-1),
+                         padding=(k[0] // 2, k[1] // 2), groups=G)
+            if self.cfg.batch_norm:
+                if nval is None:
+                    nval = torch.full((G,), xb.shape[0], device=xb.device)
+                z = self._bn(z, name, P, train, nval)
+            return F.relu(z)
+
+        def scale(t, m):
+            Bn, GC, H, W = t.shape
+            return (t.view(Bn, G, GC // G, H, W) * m.view(1, G, 1, 1, 1)).view(Bn, GC, H, W)
+
+        cur = xb
+        for s, K in enumerate(p0.nodes):
+            x_in = conv("s{}_in".format(s + 1), cur, p0.kernel_sizes[s])
+            if s in self._dag_stages:
+                m = self._masks[s]
+                acts = []
+                for i in range(K):
+                    inp = scale(x_in, m["E"][:, i]) if m["E_np"][:, i].any() else None
+                    for j in range(i):
+                        if not m["A_np"][:, i, j].any():
+                            continue
+                        term = scale(acts[j], m["A"][:, i, j])
+                        inp = term if inp is None else inp + term
+                    if inp is None:                     # isolated in every group: zero input
+                        inp = torch.zeros_like(x_in)
+                    acts.append(conv("s{}_n{}".format(s + 1, i), inp, (3, 3)))
+                out_in = None
+                for j in range(K):
+                    term = scale(acts[j], m["O"][:, j])
+                    out_in = term if out_in is None else out_in + term
+                out = conv("s{}_out".format(s + 1), out_in, (3, 3))
+                x_in = scale(out, m["D"]) + scale(x_in, 1.0 - m["D"])
+            cur = F.max_pool2d(x_in, 2, 2)
+        Bn = cur.shape[0]
+        feat = cur.reshape(Bn, G, -1).permute(1, 0, 2)
+        return self._head(feat, train, P)
+
+
 def _one_job(backend, plan, x, y, folds, cfg, device, fold_ids, stream):
     if backend == "torch":
         return TorchFoldJob(plan, x, y, folds, cfg, device, fold_ids=fold_ids, stream=stream)
@@ -733,19 +855,23 @@ def make_population_job(backend, members, x, y, cfg, device, stream=None):
     of ``(plan, folds, fold_ids)``; ``finish()`` returns one result dict per
     member. The HIP executor batches them into shared launches (with
     ``reset="kernels"`` one launch set per fold position, folds in sequence);
-    the torch oracle has no such mode and is rejected."""
-    if backend != "hip":
-        raise ValueError("population batching needs the hip backend")
-    from .cnn_hip import HipPopJob
+    the torch executor batches them too (:class:`TorchPopJob`: superset
+    network + per-group DAG masks, comparator (a))."""
+    if backend == "hip":
+        from .cnn_hip import HipPopJob as Job
+    elif backend == "torch":
+        Job = TorchPopJob
+    else:
+        raise ValueError("unknown backend {!r}".format(backend))
     nf = {len(f) for _, f, _ in members}
     if cfg.reset == "all" or nf == {1}:
-        return HipPopJob(None, x, y, None, cfg, device, stream=stream, members=members)
+        return Job(None, x, y, None, cfg, device, stream=stream, members=members)
     if len(nf) != 1:
         raise ValueError("sequential-fold population jobs need the same number of folds per member")
 
     def make(k):
-        return HipPopJob(None, x, y, None, cfg, device, stream=stream,
-                         members=[(p, [f[k]], [ids[k]]) for p, f, ids in members])
+        return Job(None, x, y, None, cfg, device, stream=stream,
+                   members=[(p, [f[k]], [ids[k]]) for p, f, ids in members])
     return SequentialFoldJob(make, nf.pop(), multi=True)
 
 

@@ -9,6 +9,7 @@ and lets the GPU run them concurrently; the host never blocks until the
 results are read back.
 """
 
+import os
 import time
 
 import torch
@@ -65,13 +66,19 @@ class LocalBatchEvaluator(SequentialEvaluator):
     HIP backend are trained as *population jobs*: up to ``pop_batch``
     candidates x all their folds share every kernel launch
     (:class:`~gentun_amd.models.cnn_hip.HipPopJob`); up to ``streams`` such
-    jobs run concurrently on separate HIP streams. Other backends run one
-    fold-batched job per candidate per stream; other species fall back to
-    sequential evaluation.
+    jobs run concurrently on separate HIP streams. The torch executor does the
+    same with ``torch_pop`` (:class:`~gentun_amd.models.cnn_engine.TorchPopJob`),
+    else it runs one fold-batched job per candidate per stream; other species
+    fall back to sequential evaluation.
     """
 
-    def __init__(self, device=None, streams=2, cache=False, event_log=None, pop_batch=16):
+    def __init__(self, device=None, streams=2, cache=False, event_log=None, pop_batch=16, torch_pop=None):
         super(LocalBatchEvaluator, self).__init__(cache=cache, event_log=event_log)
+        # population-batch the torch executor too (TorchPopJob, comparator (a)); default
+        # GENTUN_TORCH_POP=1, else the torch oracle trains one candidate per job
+        if torch_pop is None:
+            torch_pop = os.environ.get("GENTUN_TORCH_POP", "0") == "1"
+        self.torch_pop = bool(torch_pop)
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \
                 else torch.device("cpu")
@@ -179,8 +186,10 @@ def run_cnn_units(units, evaluator, done):
         if len(window) >= len(streams):
             retire(window.pop(0))
         pending.sort(key=lambda e: -e[3])
-        hip = all(e[1].backend == "hip" for e in pending) and pop_batch > 1
-        if hip:
+        backends = {e[1].backend for e in pending}
+        torch_pop = getattr(evaluator, "torch_pop", False)
+        batched = pop_batch > 1 and (backends == {"hip"} or (torch_pop and backends == {"torch"}))
+        if batched:
             free = len(streams) - len(window)
             nchunks = min(free, max(1, -(-groups_of(pending) // max_groups))) if exhausted else 1
             take, ng = [], 0
@@ -202,7 +211,7 @@ def run_cnn_units(units, evaluator, done):
                     members.append(model.member(fold_ids))
                     items.append((ind, model, tag))
                 m0 = ch[0][1]
-                job = E.make_population_job("hip", members, m0.x_train, m0.y_train, m0.cfg, m0.device,
+                job = E.make_population_job(m0.backend, members, m0.x_train, m0.y_train, m0.cfg, m0.device,
                                             stream=stream)
                 t0 = time.perf_counter()
                 job.launch()
