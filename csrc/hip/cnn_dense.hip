@@ -21,6 +21,7 @@
 // eval_head    : per-sample loss / binary-accuracy / categorical-accuracy.
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -86,6 +87,73 @@ __device__ __forceinline__ void act_frag(const void* base, long off, bool ok, ui
   }
 }
 
+// bias + ReLU + dropout of one 16-unit x 32-row tile (D[row = unit][col =
+// batch row], two 16-row MFMA tiles), the activation store and the tile's
+// partial logits (plog tile index `utile`)
+template <int PREC>
+__device__ __forceinline__ void dense_fwd_epilogue(const DenseFwdArgs& a, int g, int u_t, int b0,
+                                                   const f32x4_t (&acc)[2], int lane, int utile) {
+  typedef typename ActT<PREC>::T AT;
+  const int kq = lane >> 4, l16 = lane & 15;
+  // D[row = unit][col = batch row]
+  const int u0 = u_t + kq * 4;
+  const bool uok = u0 < a.Up;
+  const float keep_scale = 1.0f / (1.0f - a.drop_p);
+  const uint32_t thr = (uint32_t)(a.drop_p * 4294967296.0);
+  const int gstep = a.st ? a.st->global_step : 0;
+  const uint32_t fid = a.fold_ids ? (uint32_t)a.fold_ids[g] : (uint32_t)g;
+  const uint32_t seed = a.seeds ? a.seeds[g] : a.seed;
+  const int C = a.C;
+  const float* w2 = a.w2 + ((long)g * a.Up + u0) * C;
+  // this lane's dense2 rows, all loads in flight at once (a load per class under
+  // a `c < C` branch waited for each one in turn)
+  float w2v[4][HEAD_MAXC_FWD];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < HEAD_MAXC_FWD; ++c)
+      w2v[i][c] = (a.plog != nullptr && uok) ? w2[i * C + min(c, C - 1)] : 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = b0 + h * 16 + l16;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (uok && row < a.B) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float z = acc[h][i] + a.bias[(long)g * a.Up + u0 + i];
+        z = fmaxf(z, 0.f);
+        if (a.train && a.drop_p > 0.f) {
+          const uint32_t r = hash4(seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)(row + a.row_off),
+                                   (uint32_t)(u0 + i));
+          z = (r >= thr) ? z * keep_scale : 0.f;
+        }
+        v[i] = PREC ? z : bf2f(f2bf(z));      // the head sees exactly the stored activation
+      }
+      AT* dst = static_cast<AT*>(a.out) + ((long)g * a.B + row) * a.Up + u0;
+      if (PREC) *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+      else *reinterpret_cast<uint2*>(dst) = pack4(v);
+    }
+    if (a.plog == nullptr) continue;
+    // partial logits of this 16-unit tile: 4 units per lane, reduced over the 4 lane groups
+    float pl[HEAD_MAXC_FWD];
+#pragma unroll
+    for (int c = 0; c < HEAD_MAXC_FWD; ++c) {
+      float t = 0.f;
+      if (c < C && uok) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t += v[i] * w2v[i][c];
+      }
+      t += __shfl_xor(t, 16);
+      t += __shfl_xor(t, 32);
+      pl[c] = t;
+    }
+    if (kq == 0 && row < a.B) {
+      float* dst = a.plog + (((long)g * (a.Up / 16) + utile) * a.B + row) * C;
+      for (int c = 0; c < C; ++c) dst[c] = pl[c];
+    }
+  }
+}
+
 // grid (Up/16, ceil(B/32), G): one 16-unit x 32-row tile per workgroup, the
 // K (feature) loop split over the 4 waves and reduced through LDS.
 template <int PREC>
@@ -122,54 +190,129 @@ __global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
   if (wave > 0) return;
 #pragma unroll
   for (int w = 0; w < 3; ++w) { acc[0] += red[w][0][lane]; acc[1] += red[w][1][lane]; }
-  // D[row = unit][col = batch row]
-  const int u0 = u_t + kq * 4;
-  const bool uok = u0 < a.Up;
-  const float keep_scale = 1.0f / (1.0f - a.drop_p);
-  const uint32_t thr = (uint32_t)(a.drop_p * 4294967296.0);
-  const int gstep = a.st ? a.st->global_step : 0;
-  const uint32_t fid = a.fold_ids ? (uint32_t)a.fold_ids[g] : (uint32_t)g;
-  const uint32_t seed = a.seeds ? a.seeds[g] : a.seed;
-  const int C = a.C;
-  const float* w2 = a.w2 + ((long)g * a.Up + u0) * C;
+  dense_fwd_epilogue<PREC>(a, g, u_t, b0, acc, lane, blockIdx.x);
+}
+
+// Streaming forward (the default): one workgroup = UT 16-unit tiles x 32 rows,
+// the same per-wave k-step assignment as dense_fwd_kernel (wave w: k-steps
+// w, w+4, ...; 4 chunks of 8 features each) and the same fixed-order
+// reduction over the 4 waves, so the result is bit-identical -- but every wave
+// carries UT unit tiles (the activation fragments are loaded and split once
+// per UT tiles: UT x less x traffic), the raw W1 / x values of the next k-step
+// are loaded while the current one multiplies (two register sets, loads with
+// selected addresses instead of branches), and the workgroups of one group
+// are placed on one XCD (its x stays in that L2).
+template <typename T>
+__device__ __forceinline__ void ld8_raw(const T* p, bool ok, float* f) {
+  if constexpr (sizeof(T) == 4) {
+    load8f(ok ? reinterpret_cast<const float*>(p) : gt_zero8, f);
+  } else {
+    const uint4 v = *reinterpret_cast<const uint4*>(ok ? reinterpret_cast<const void*>(p)
+                                                       : reinterpret_cast<const void*>(gt_zero8));
+    unpack8(v, f);
+  }
+}
+
+template <int PREC>
+__device__ __forceinline__ void planes8(const float* f, uint4* q) {
+  if (PREC) split8(f, q[0], q[1], q[2]);
+  else q[0] = pack8(f);
+}
+
+// linear workgroup id -> (x, z) with the workgroups of one z on as few XCDs as
+// possible (hardware deals consecutive ids round-robin over the 8 XCDs)
+__device__ __forceinline__ void xcd_tile(int& bx, int& bz) {
+  const int nbx = gridDim.x, total = nbx * gridDim.z;
+  int lin = blockIdx.z * nbx + blockIdx.x;
+  if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
+  bz = lin / nbx;
+  bx = lin - bz * nbx;
+}
+
+template <int PREC, int UT>
+__global__ void __launch_bounds__(256) dense_fwd_stream_kernel(DenseFwdArgs a) {
+  typedef typename ActT<PREC>::T AT;
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
+  __shared__ f32x4_t red[4][UT][2][64];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  int bx, g;
+  xcd_tile(bx, g);
+  const int u_t = bx * 16 * UT;
+  const int b0 = blockIdx.y * 32;
+  const int nchunks = a.Fp >> 3;
+  const int nks = (nchunks + 3) >> 2;                        // k-steps (4 chunks each)
+  const AT* wt = static_cast<const AT*>(a.wt) + (long)g * a.Up * a.Fp;
+  const AT* xg = static_cast<const AT*>(a.x) + (long)g * a.B * a.Fp;
+  const int br0 = b0 + l16, br1 = b0 + 16 + l16;
+  const AT* xr0 = xg + (long)min(br0, a.B - 1) * a.Fp;
+  const AT* xr1 = xg + (long)min(br1, a.B - 1) * a.Fp;
+  const AT* wr[UT];
+  bool uok[UT];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = b0 + h * 16 + l16;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (uok && row < a.B) {
+  for (int t = 0; t < UT; ++t) {
+    const int u = u_t + t * 16 + l16;
+    uok[t] = u < a.Up;
+    wr[t] = wt + (long)(uok[t] ? u : 0) * a.Fp;
+  }
+  f32x4_t acc[UT][2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float z = acc[h][i] + a.bias[(long)g * a.Up + u0 + i];
-        z = fmaxf(z, 0.f);
-        if (a.train && a.drop_p > 0.f) {
-          const uint32_t r = hash4(seed ^ (fid * 0x632be5abU), (uint32_t)gstep, (uint32_t)(row + a.row_off),
-                                   (uint32_t)(u0 + i));
-          z = (r >= thr) ? z * keep_scale : 0.f;
-        }
-        v[i] = PREC ? z : bf2f(f2bf(z));      // the head sees exactly the stored activation
-      }
-      AT* dst = static_cast<AT*>(a.out) + ((long)g * a.B + row) * a.Up + u0;
-      if (PREC) *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-      else *reinterpret_cast<uint2*>(dst) = pack4(v);
+  for (int t = 0; t < UT; ++t) acc[t][0] = acc[t][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float rw[2][UT][8], rx[2][2][8];
+  auto load = [&](int j, int buf) {                          // k-step j = wave + 4 i
+    const int c = 4 * j + kq;
+    const bool cok = c < nchunks;
+#pragma unroll
+    for (int t = 0; t < UT; ++t) ld8_raw(wr[t] + c * 8, cok && uok[t], rw[buf][t]);
+    ld8_raw(xr0 + c * 8, cok && br0 < a.B, rx[buf][0]);
+    ld8_raw(xr1 + c * 8, cok && br1 < a.B, rx[buf][1]);
+  };
+  auto step = [&](int buf) {
+    uint4 b0f[NPL], b1f[NPL];
+    planes8<PREC>(rx[buf][0], b0f);
+    planes8<PREC>(rx[buf][1], b1f);
+#pragma unroll
+    for (int t = 0; t < UT; ++t) {
+      uint4 af[NPL];
+      planes8<PREC>(rw[buf][t], af);
+      acc[t][0] = mfma_np<NPL>(af, b0f, acc[t][0]);
+      acc[t][1] = mfma_np<NPL>(af, b1f, acc[t][1]);
     }
-    if (a.plog == nullptr) continue;
-    // partial logits of this 16-unit tile: 4 units per lane, reduced over the 4 lane groups
-    float pl[HEAD_MAXC_FWD];
+  };
+  // no branch around a load (hipcc would wait vmcnt(0) at each): k-steps past
+  // the end load the zero chunk and add exact zeros
+  // (sched barriers: keep each refill where it is -- the scheduler otherwise
+  // sinks it next to its use and the wait becomes vmcnt(0))
+  int j = wave;
+  load(j, 0);
+  load(j + 4, 1);
+  for (; j < nks; j += 8) {
+    step(0);
+    __builtin_amdgcn_sched_barrier(0);
+    load(j + 8, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    step(1);
+    __builtin_amdgcn_sched_barrier(0);
+    load(j + 12, 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
-    for (int c = 0; c < HEAD_MAXC_FWD; ++c) {
-      float t = 0.f;
-      if (c < C && uok) {
+  for (int t = 0; t < UT; ++t) {
+    red[wave][t][0][lane] = acc[t][0];
+    red[wave][t][1][lane] = acc[t][1];
+  }
+  __syncthreads();
+  // one unit tile per wave; partials summed in wave order (dense_fwd_kernel's)
+  for (int t = wave; t < UT; t += 4) {
+    f32x4_t r2[2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) t += v[i] * w2[i * C + c];
-      }
-      t += __shfl_xor(t, 16);
-      t += __shfl_xor(t, 32);
-      pl[c] = t;
+    for (int h = 0; h < 2; ++h) {
+      f32x4_t v = red[0][t][h][lane];
+      v += red[1][t][h][lane];
+      v += red[2][t][h][lane];
+      v += red[3][t][h][lane];
+      r2[h] = v;
     }
-    if (kq == 0 && row < a.B) {
-      float* dst = a.plog + (((long)g * (a.Up / 16) + blockIdx.x) * a.B + row) * C;
-      for (int c = 0; c < C; ++c) dst[c] = pl[c];
-    }
+    dense_fwd_epilogue<PREC>(a, g, u_t + t * 16, b0, r2, lane, u_t / 16 + t);
   }
 }
 
@@ -342,7 +485,49 @@ struct DenseDgradArgs {
   void* unpool_x1;
   const int* unpool_sel;        // [G]
   int Hs, Ws, Cp;
+  const float* w1;              // fp32 master W1 [G][Fp][Up]: streaming kernel (null: the copy + LDS transpose)
 };
+
+// dx (or, with an unpool mask, the fused pool backward) of one 16-feature x
+// 32-row tile: D[row = feature][col = batch row]
+template <int PREC>
+__device__ __forceinline__ void dense_dgrad_epilogue(const DenseDgradArgs& a, int g, int f_t, int b0,
+                                                     const f32x4_t (&acc)[2], int lane) {
+  typedef typename ActT<PREC>::T AT;
+  const int kq = lane >> 4, l16 = lane & 15;
+  const int fo = f_t + kq * 4;
+  if (fo >= a.Fp) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = b0 + h * 16 + l16;
+    if (row >= a.B) continue;
+    float v[4] = {acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
+    if (a.unpool_mask) {
+      // features fo .. fo+3 = channels c0 .. c0+3 of pooled pixel (ho, wo)
+      const long n = (long)g * a.B + row;
+      const int pix = fo / a.Cp, c0 = fo - pix * a.Cp, wo_n = a.Ws >> 1;
+      const int ho = pix / wo_n, wo = pix - ho * wo_n;
+      const uint32_t mk = *reinterpret_cast<const uint32_t*>(a.unpool_mask + n * a.Fp + fo);
+      AT* src = static_cast<AT*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.unpool_x0);
+#pragma unroll
+      for (int me = 0; me < 4; ++me) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t bb = (mk >> (8 * j)) & 0xffu;
+          o[j] = ((int)(bb & 3u) == me && (bb & 4u)) ? v[j] : 0.f;
+        }
+        AT* d = src + ((n * a.Hs + 2 * ho + (me >> 1)) * a.Ws + 2 * wo + (me & 1)) * a.Cp + c0;
+        if (PREC) *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
+        else *reinterpret_cast<uint2*>(d) = pack4(o);
+      }
+      continue;
+    }
+    AT* dst = static_cast<AT*>(a.dx) + ((long)g * a.B + row) * a.Fp + fo;
+    if (PREC) *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+    else *reinterpret_cast<uint2*>(dst) = pack4(v);
+  }
+}
 
 // grid (Fp/64, ceil(B/32), G): D[row = f][col = b], K = units.
 // W1 is read from the bf16 transposed copy (half the bytes of the fp32 master
@@ -409,38 +594,70 @@ __global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
     acc[0] = mfma_np<NPL>(af, b0f, acc[0]);
     acc[1] = mfma_np<NPL>(af, b1f, acc[1]);
   }
-  const int fo = f_t + kq * 4;
-  if (fo >= a.Fp) return;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = b0 + h * 16 + l16;
-    if (row >= a.B) continue;
-    float v[4] = {acc[h][0], acc[h][1], acc[h][2], acc[h][3]};
-    if (a.unpool_mask) {
-      // features fo .. fo+3 = channels c0 .. c0+3 of pooled pixel (ho, wo)
-      const long n = (long)g * a.B + row;
-      const int pix = fo / a.Cp, c0 = fo - pix * a.Cp, wo_n = a.Ws >> 1;
-      const int ho = pix / wo_n, wo = pix - ho * wo_n;
-      const uint32_t mk = *reinterpret_cast<const uint32_t*>(a.unpool_mask + n * a.Fp + fo);
-      AT* src = static_cast<AT*>((a.unpool_sel && a.unpool_sel[g]) ? a.unpool_x1 : a.unpool_x0);
-#pragma unroll
-      for (int me = 0; me < 4; ++me) {
-        float o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t bb = (mk >> (8 * j)) & 0xffu;
-          o[j] = ((int)(bb & 3u) == me && (bb & 4u)) ? v[j] : 0.f;
-        }
-        AT* d = src + ((n * a.Hs + 2 * ho + (me >> 1)) * a.Ws + 2 * wo + (me & 1)) * a.Cp + c0;
-        if (PREC) *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
-        else *reinterpret_cast<uint2*>(d) = pack4(o);
-      }
-      continue;
+  dense_dgrad_epilogue<PREC>(a, g, f_t, b0, acc, lane);
+}
+
+// Streaming data gradient (the default when the fp32 master is given):
+// dX[b][f] = sum_u dH[b][u] W1[f][u] with A = the fp32 master W1 [G][Fp][Up]
+// itself -- 8 consecutive units of a feature row are one contiguous 32-byte
+// load, so there is no LDS transpose and no barrier in the k loop. The master
+// equals the copy dense_fwd multiplied by (the W1 update runs after this
+// kernel; prec 0 rounds it to bf16 exactly as the copy was rounded), and the
+// k-steps run in dense_dgrad_kernel's order: bit-identical. The next k-step's
+// raw values are loaded during the current one's MFMAs; XCD-grouped
+// workgroups (a group's dH stays in one L2).
+template <int PREC>
+__global__ void __launch_bounds__(256) dense_dgrad_stream_kernel(DenseDgradArgs a) {
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  int bx, g;
+  xcd_tile(bx, g);
+  const int f_t = bx * 64 + wave * 16;
+  const int b0 = blockIdx.y * 32;
+  const int fa = f_t + l16;
+  const bool fok = fa < a.Fp;
+  const float* wrow = a.w1 + ((long)g * a.Fp + (fok ? fa : 0)) * a.Up;
+  const float* dH = a.dH + (long)g * a.B * a.Up;
+  const int br0 = b0 + l16, br1 = b0 + 16 + l16;
+  const float* h0 = dH + (long)min(br0, a.B - 1) * a.Up;
+  const float* h1 = dH + (long)min(br1, a.B - 1) * a.Up;
+  const int nchunks = a.Up >> 3;
+  const int nks = (nchunks + 3) >> 2;
+  f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float rw[2][8], rh[2][2][8];
+  auto load = [&](int j, int buf) {
+    const int c = 4 * j + kq;
+    const bool cok = c < nchunks;
+    ld8_raw(wrow + c * 8, cok && fok, rw[buf]);
+    ld8_raw(h0 + c * 8, cok && br0 < a.B, rh[buf][0]);
+    ld8_raw(h1 + c * 8, cok && br1 < a.B, rh[buf][1]);
+  };
+  auto step = [&](int buf) {
+    uint4 af[NPL], b0f[NPL], b1f[NPL];
+    planes8<PREC>(rw[buf], af);
+    if constexpr (PREC != 0) {
+      split8(rh[buf][0], b0f[0], b0f[1], b0f[2]);
+      split8(rh[buf][1], b1f[0], b1f[1], b1f[2]);
+    } else {
+      b0f[0] = pack8(rh[buf][0]);
+      b1f[0] = pack8(rh[buf][1]);
     }
-    AT* dst = static_cast<AT*>(a.dx) + ((long)g * a.B + row) * a.Fp + fo;
-    if (PREC) *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-    else *reinterpret_cast<uint2*>(dst) = pack4(v);
+    acc[0] = mfma_np<NPL>(af, b0f, acc[0]);
+    acc[1] = mfma_np<NPL>(af, b1f, acc[1]);
+  };
+  load(0, 0);                              // (unconditional loads: see dense_fwd_stream_kernel)
+  load(1, 1);
+  for (int j = 0; j < nks; j += 2) {
+    step(0);
+    __builtin_amdgcn_sched_barrier(0);
+    load(j + 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    step(1);
+    __builtin_amdgcn_sched_barrier(0);
+    load(j + 3, 1);
+    __builtin_amdgcn_sched_barrier(0);
   }
+  dense_dgrad_epilogue<PREC>(a, g, f_t, b0, acc, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -661,7 +878,23 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// streaming dense fwd / dgrad (default) vs the round-2 kernels: A/B switch
+// GENTUN_DENSE_STREAM=0 / gt_dense_set_stream (bit-identical either way)
+static int g_dense_stream = -1;
+static bool dense_stream_on() {
+  if (g_dense_stream < 0)
+    g_dense_stream = std::getenv("GENTUN_DENSE_STREAM") ? std::atoi(std::getenv("GENTUN_DENSE_STREAM")) : 1;
+  return g_dense_stream != 0;
+}
+
 extern "C" {
+
+int gt_dense_set_stream(int on) {
+  dense_stream_on();
+  const int old = g_dense_stream;
+  g_dense_stream = on;
+  return old;
+}
 
 int gt_step_begin(StepState* s, hipStream_t stream) {
   hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, stream, s);
@@ -670,6 +903,21 @@ int gt_step_begin(StepState* s, hipStream_t stream) {
 
 int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
   if (a->Fp % 8 || a->Up % 64 || a->C > HEAD_MAXC_FWD || (a->prec != 0 && a->prec != 1)) return -1;
+  if (dense_stream_on()) {
+    // unit tiles per workgroup (A/B: GENTUN_DENSE_UT = 1 / 2 / 4)
+    static const int ut = std::getenv("GENTUN_DENSE_UT") ? std::atoi(std::getenv("GENTUN_DENSE_UT")) : 2;
+    dim3 grid(a->Up / (16 * ut), (a->B + 31) / 32, a->G);
+#define DENSE_FWD_UT(UT_)                                                                                 \
+  if (ut == UT_) {                                                                                        \
+    if (a->prec) hipLaunchKernelGGL((dense_fwd_stream_kernel<1, UT_>), grid, dim3(256), 0, stream, *a);   \
+    else hipLaunchKernelGGL((dense_fwd_stream_kernel<0, UT_>), grid, dim3(256), 0, stream, *a);           \
+    return (int)hipGetLastError();                                                                        \
+  }
+    DENSE_FWD_UT(1)
+    DENSE_FWD_UT(4)
+    DENSE_FWD_UT(2)
+#undef DENSE_FWD_UT
+  }
   dim3 grid(a->Up / 16, (a->B + 31) / 32, a->G);
   if (a->prec) hipLaunchKernelGGL(dense_fwd_kernel<1>, grid, dim3(256), 0, stream, *a);
   else hipLaunchKernelGGL(dense_fwd_kernel<0>, grid, dim3(256), 0, stream, *a);
@@ -691,6 +939,11 @@ int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
   if (a->Up % 8) return -1;
   if (a->prec != 0 && a->prec != 1) return -1;
   dim3 grid((a->Fp + 63) / 64, (a->B + 31) / 32, a->G);
+  if (a->w1 && dense_stream_on()) {
+    if (a->prec) hipLaunchKernelGGL(dense_dgrad_stream_kernel<1>, grid, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL(dense_dgrad_stream_kernel<0>, grid, dim3(256), 0, stream, *a);
+    return (int)hipGetLastError();
+  }
   if (a->prec) hipLaunchKernelGGL(dense_dgrad_kernel<1>, grid, dim3(256), 0, stream, *a);
   else hipLaunchKernelGGL(dense_dgrad_kernel<0>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();

@@ -500,6 +500,7 @@ class HipPopJob(FoldJob):
         dd.dH, dd.wt, dd.dx = self.dH.data_ptr(), self.w1t.data_ptr(), self.grad[self.last].data_ptr()
         dd.G, dd.B, dd.Fp, dd.Up = Q, B, self.Fp, self.Up
         dd.prec, dd.wps = prec, self.w1t.numel()
+        dd.w1 = self.views["W1"][0].data_ptr()      # the fp32 master (updated after dgrad): streaming kernel
         self.dense_dgrad_args = dd
         dw = K.DenseWgradAdamArgs()
         p, m, v = self.views["W1"]
@@ -746,7 +747,7 @@ class HipPopJob(FoldJob):
         self._run_fwd(s, self.fwd_ops)
         K.check(L.gt_dense_fwd(self.dense_fwd_args, s), "dense_fwd")
         K.check(L.gt_head(self.head_args, s), "head")
-        K.check(L.gt_dense_dgrad(self.dense_dgrad_args, s), "dense_dgrad")   # reads the bf16 W1 copy before its update
+        K.check(L.gt_dense_dgrad(self.dense_dgrad_args, s), "dense_dgrad")   # reads W1 before its update
         side = self.side if self.overlap else main
         side2 = (self.side2 if self.w1_stream else side) if self.overlap else main
         ss = side.cuda_stream

@@ -63,7 +63,7 @@ class HeadArgs(C.Structure):
 class DenseDgradArgs(C.Structure):
     _fields_ = [("dH", P), ("wt", P), ("dx", P), ("G", I), ("B", I), ("Fp", I), ("Up", I), ("prec", I),
                 ("wps", C.c_long), ("unpool_mask", P), ("unpool_x0", P), ("unpool_x1", P), ("unpool_sel", P),
-                ("Hs", I), ("Ws", I), ("Cp", I)]
+                ("Hs", I), ("Ws", I), ("Cp", I), ("w1", P)]
 
 
 class DenseWgradAdamArgs(C.Structure):

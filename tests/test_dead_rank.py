@@ -36,15 +36,17 @@ def _search(tmp, fault=None, restarts=0, watchdog="60:3:4"):
     r = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=900, cwd=ROOT)
     out = None
     for line in r.stdout.splitlines():
-        if line.startswith('{"'):
+        # (another rank's unflushed text can share the line under load: parse from the brace)
+        if '{"' in line:
             try:
-                out = json.loads(line)
+                out = json.loads(line[line.index('{"'):])
             except ValueError:
                 pass
     return r, out
 
 
 def _trajectory(out):
+    assert out is not None, "no result JSON on stdout"
     return [(h["generation"], h["best_fitness"]) for h in out["history"]]
 
 

@@ -1,0 +1,73 @@
+"""Streaming dense forward / data-gradient kernels (cnn_dense.hip:
+dense_fwd_stream_kernel, dense_dgrad_stream_kernel -- the defaults) against
+the round-2 kernels they replace (gt_dense_set_stream(0)): same k-step order
+and reduction order, so the outputs must be BIT-identical, in both
+precisions, with the fused partial logits, dropout and a padded batch."""
+
+import ctypes
+
+import pytest
+import torch
+
+from gentun_amd.ops import cnn_kernels as Km
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _lib():
+    L = Km.lib()
+    L.gt_dense_set_stream.argtypes = [ctypes.c_int]
+    L.gt_dense_set_stream.restype = ctypes.c_int
+    return L
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+@pytest.mark.parametrize("prec", [1, 0])
+@pytest.mark.parametrize("G,B,Fp,Up", [(5, 32, 3584, 512), (3, 20, 392, 128)])
+def test_dense_stream_bit_identical(prec, G, B, Fp, Up):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L = _lib()
+    torch.manual_seed(0)
+    adt = torch.float32 if prec else torch.bfloat16
+    C = 10
+    w1 = torch.randn(G, Fp, Up, device=DEV) * 0.05                 # fp32 master [G][Fp][Up]
+    wt = w1.transpose(1, 2).contiguous().to(adt)                   # the copy dense_fwd reads [G][Up][Fp]
+    x = torch.randn(G, B, Fp, device=DEV).to(adt)
+    b1 = torch.randn(G, Up, device=DEV) * 0.1
+    w2 = torch.randn(G, Up, C, device=DEV) * 0.05
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    fids = torch.arange(G, dtype=torch.int32, device=DEV)
+    dH = torch.randn(G, B, Up, device=DEV)
+    outs = []
+    for mode in (0, 1):
+        old = L.gt_dense_set_stream(mode)
+        try:
+            out = torch.zeros(G, B, Up, dtype=adt, device=DEV)
+            plog = torch.zeros(G, Up // 16, B, C, device=DEV)
+            a = Km.DenseFwdArgs()
+            a.x, a.wt, a.bias, a.out, a.st, a.fold_ids = x.data_ptr(), wt.data_ptr(), b1.data_ptr(), \
+                out.data_ptr(), st.data_ptr(), fids.data_ptr()
+            a.G, a.B, a.Fp, a.Up, a.drop_p, a.train, a.seed = G, B, Fp, Up, 0.5, 1, 7
+            a.w2, a.plog, a.C, a.prec = w2.data_ptr(), plog.data_ptr(), C, prec
+            Km.check(L.gt_dense_fwd(a, _stream()), "dense_fwd")
+            dx = torch.zeros(G, B, Fp, dtype=adt, device=DEV)
+            d = Km.DenseDgradArgs()
+            d.dH, d.wt, d.dx, d.G, d.B, d.Fp, d.Up, d.prec = dH.data_ptr(), wt.data_ptr(), dx.data_ptr(), \
+                G, B, Fp, Up, prec
+            d.w1 = w1.data_ptr() if mode else 0
+            Km.check(L.gt_dense_dgrad(d, _stream()), "dense_dgrad")
+            torch.cuda.synchronize()
+            outs.append((out.clone(), plog.clone(), dx.clone()))
+        finally:
+            L.gt_dense_set_stream(old)
+    for name, r0, r1 in zip(("h", "plog", "dx"), outs[0], outs[1]):
+        assert torch.equal(r0, r1), "{} differs: max {}".format(name, (r0.float() - r1.float()).abs().max().item())
+    # and against the math (fp32: split-MFMA level; bf16: bf16 level)
+    ref = torch.bmm(dH.double(), w1.double().transpose(1, 2))
+    err = (outs[1][2].double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < (1e-5 if prec else 2e-2)
