@@ -443,12 +443,14 @@ class DistributedPopulation(Population):
                 "per_rank_units": [int(np.sum(g[:, 0] != ST_NONE)) for g in gathered]}
         return merged, info
 
-    def evaluate_round(self, per_rank):
-        """One balanced evaluation round: at most ``per_rank`` candidates per
-        rank, the pending set cut into near-equal rounds
+    def evaluate_round(self, per_rank, slack=1):
+        """One balanced evaluation round: about ``per_rank`` candidates per
+        rank (up to ``slack`` more when that saves a round), the pending set
+        cut into near-equal rounds
         (:func:`~gentun_amd.parallel.scheduler.balanced_round`)."""
         return self.evaluate_in_parallel(
-            limit=balanced_round(len(self.pending()), int(per_rank) * self.comm.world_size))
+            limit=balanced_round(len(self.pending()), int(per_rank) * self.comm.world_size,
+                                 slack=int(slack) * self.comm.world_size))
 
     def sync_ranks(self):
         """Device-synchronise every rank and barrier (bench timing fence)."""

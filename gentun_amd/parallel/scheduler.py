@@ -60,16 +60,21 @@ def make_units(costs, nfold, world_size, split_folds=True, per_fold=False):
     return units, ucost
 
 
-def balanced_round(n_pending, cap):
+def balanced_round(n_pending, cap, slack=0):
     """Size of the next evaluation round when at most ``cap`` candidates fit a
     round: the pending set is cut into ``ceil(n / cap)`` near-equal rounds
     (11 pending at cap 5 -> 4, 4, 3 instead of 5, 5, 1; a 1-candidate round
     costs ~40 % of a 5-candidate one on a GPU, so it halves the throughput of
-    its time slice)."""
+    its time slice). ``slack``: rounds may exceed ``cap`` by up to that many
+    candidates when that saves a round (11 at cap 5, slack 1 -> 6, 5: larger
+    population launches, and no round below cap - 1)."""
     if n_pending <= 0:
         return 0
     cap = max(1, int(cap))
     rounds = -(-n_pending // cap)
+    fewer = n_pending // cap
+    if slack > 0 and fewer >= 1 and -(-n_pending // fewer) <= cap + int(slack):
+        rounds = fewer
     return -(-n_pending // rounds)
 
 

@@ -102,3 +102,25 @@ def test_sequential_fold_candidates_are_never_split():
     assert all(len(ind.fold_scores) == 3 for ind in pop)
     pop.shutdown()
     t.join(timeout=60)
+
+
+def test_balanced_round_slack_saves_a_round():
+    """cap 5 per round: without slack 11 pending -> 4, 4, 3; with one extra
+    candidate allowed per round -> 6, 5 (larger launches, no round below
+    cap - 1 whenever the pending set allows it)."""
+    from gentun_amd.parallel.scheduler import balanced_round
+
+    def rounds(n, slack):
+        out = []
+        while n:
+            r = balanced_round(n, 5, slack)
+            out.append(r)
+            n -= r
+        return out
+    assert rounds(11, 0) == [4, 4, 3]
+    assert rounds(11, 1) == [6, 5]
+    assert rounds(14, 1) == [5, 5, 4]
+    assert rounds(32, 1) == [6, 6, 5, 5, 5, 5]
+    for n in range(4, 40):
+        rs = rounds(n, 1)
+        assert sum(rs) == n and max(rs) <= 6 and (min(rs) >= 4 or n == 7)      # 7 = 4 + 3
