@@ -203,8 +203,8 @@ conv_fast_kernel(ConvArgs a) {
     for (int t = 0; t < CT; ++t)
 #pragma unroll
       for (int p = 0; p < ((PK && t == CT - 1) ? 1 : NPL); ++p)
-        dst[t][p] = (wok[t] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[t] + p * a.wps + c * 8)
-                                         : make_uint4(0, 0, 0, 0);
+        dst[t][p] = *reinterpret_cast<const uint4*>((wok[t] && c < NCH) ? (const void*)(wrow[t] + p * a.wps + c * 8)
+                                                                          : (const void*)gt_zero8);
   };
   // one k-step of tile t: the six-term product, or the packed tile's three MFMAs
   auto mma = [&](int t, const uint4* af, const uint4* bf, f32x4_t c) {
@@ -242,7 +242,7 @@ conv_fast_kernel(ConvArgs a) {
     uint4 v[NPT];
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
-      v[j] = pok[j] ? *reinterpret_cast<const uint4*>(src0 + poff[j]) : make_uint4(0, 0, 0, 0);
+      v[j] = *reinterpret_cast<const uint4*>(pok[j] ? (const void*)(src0 + poff[j]) : (const void*)gt_zero8);
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
       if (tid + NTH * j < NP) patch[tid + NTH * j] = v[j];
@@ -258,10 +258,14 @@ conv_fast_kernel(ConvArgs a) {
       for (int j = 0; j < JB; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc8[j][e] = 0.f;
+      // every chunk load is unconditional (halo / padding chunks read the zero
+      // chunk): a load under a per-chunk branch made hipcc wait for it at the
+      // branch, serialising the staging into one global round trip per chunk
+      const AT* zc = reinterpret_cast<const AT*>(gt_zero8);
       if (n_src == 1) {
 #pragma unroll
         for (int j = 0; j < JB; ++j)
-          if (j0 + j < NPT && pok[j0 + j]) ld_chunk(src0 + poff[j0 + j], acc8[j]);
+          if (j0 + j < NPT) ld_chunk(pok[j0 + j] ? src0 + poff[j0 + j] : zc, acc8[j]);
       } else {
 #pragma unroll
         for (int k = 0; k < GT_MAXSLOT; ++k) {
@@ -272,7 +276,7 @@ conv_fast_kernel(ConvArgs a) {
           for (int j = 0; j < JB; ++j) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) t8[j][e] = 0.f;
-            if (j0 + j < NPT && pok[j0 + j]) ld_chunk(sk + poff[j0 + j], t8[j]);
+            if (j0 + j < NPT) ld_chunk(pok[j0 + j] ? sk + poff[j0 + j] : zc, t8[j]);
           }
 #pragma unroll
           for (int j = 0; j < JB; ++j)
@@ -1675,16 +1679,16 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
       const int hh = h0 - KH / 2 + pix / PW, ww = pix % PW - KW / 2;
       const bool ok = i < XCH && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
       const long off = ((long)hh * W + ww) * (NCBI * 8) + cb * 8;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
-      if (!ok) continue;
+      // unconditional loads (zero chunk for the halo): see conv_fast_kernel's staging
       if (n_src == 1) {
-        load8f(src0 + off, xr[j]);
+        load8f_or0(src0 + off, ok, xr[j]);
       } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
         for (int k = 0; k < GT_MAXSLOT; ++k) {
           if (!((gr.in_mask >> k) & 1)) continue;
           float t8[8];
-          load8f(static_cast<const float*>(a.in[k]) + boff + off, t8);
+          load8f_or0(static_cast<const float*>(a.in[k]) + boff + off, ok, t8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) xr[j][e] += t8[e];
         }
@@ -1695,7 +1699,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < DT; ++j) {
       const int i = tid + NT_ * j;
-      if (i < DCH) load8f(dsrc + (long)i * 8, dr[j]);
+      load8f_or0(dsrc + (long)i * 8, i < DCH, dr[j]);
     }
   };
   auto store = [&](int buf) {
@@ -1877,8 +1881,18 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(WgradArgs a) {
   float* pw = a.part_w + (long)g * n;
   const long i4 = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i4 < n) {                                    // n % 4 == 0 (Cinp % 8 == 0)
+    // 8 partials in flight per batch (a dependent load-add chain waited for
+    // each one: ~20 us per call); summed in split order
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp = 0; sp < a.S; ++sp) {
+    int sp = 0;
+    for (; sp + 8 <= a.S; sp += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const float4*>(pw + (long)(sp + k) * gs + i4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { acc.x += v[k].x; acc.y += v[k].y; acc.z += v[k].z; acc.w += v[k].w; }
+    }
+    for (; sp < a.S; ++sp) {
       const float4 v = *reinterpret_cast<const float4*>(pw + (long)sp * gs + i4);
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }

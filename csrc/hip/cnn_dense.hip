@@ -284,7 +284,9 @@ __global__ void __launch_bounds__(256) dense_fwd_stream_kernel(DenseFwdArgs a) {
   // sinks it next to its use and the wait becomes vmcnt(0))
   int j = wave;
   load(j, 0);
+  __builtin_amdgcn_sched_barrier(0);      // the same load order as the loop body (exact vmcnt at its top)
   load(j + 4, 1);
+  __builtin_amdgcn_sched_barrier(0);
   for (; j < nks; j += 8) {
     step(0);
     __builtin_amdgcn_sched_barrier(0);
@@ -645,8 +647,10 @@ __global__ void __launch_bounds__(256) dense_dgrad_stream_kernel(DenseDgradArgs 
     acc[0] = mfma_np<NPL>(af, b0f, acc[0]);
     acc[1] = mfma_np<NPL>(af, b1f, acc[1]);
   };
-  load(0, 0);                              // (unconditional loads: see dense_fwd_stream_kernel)
+  load(0, 0);                              // (unconditional loads, ordered: see dense_fwd_stream_kernel)
+  __builtin_amdgcn_sched_barrier(0);
   load(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
   for (int j = 0; j < nks; j += 2) {
     step(0);
     __builtin_amdgcn_sched_barrier(0);
@@ -904,8 +908,8 @@ int gt_step_begin(StepState* s, hipStream_t stream) {
 int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
   if (a->Fp % 8 || a->Up % 64 || a->C > HEAD_MAXC_FWD || (a->prec != 0 && a->prec != 1)) return -1;
   if (dense_stream_on()) {
-    // unit tiles per workgroup (A/B: GENTUN_DENSE_UT = 1 / 2 / 4)
-    static const int ut = std::getenv("GENTUN_DENSE_UT") ? std::atoi(std::getenv("GENTUN_DENSE_UT")) : 2;
+    // unit tiles per workgroup (A/B: GENTUN_DENSE_UT = 1 / 2 / 4; 4: 53 vs 67 us at 25 groups, W1 in MALL)
+    static const int ut = std::getenv("GENTUN_DENSE_UT") ? std::atoi(std::getenv("GENTUN_DENSE_UT")) : 4;
     dim3 grid(a->Up / (16 * ut), (a->B + 31) / 32, a->G);
 #define DENSE_FWD_UT(UT_)                                                                                 \
   if (ut == UT_) {                                                                                        \
@@ -914,8 +918,8 @@ int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
     return (int)hipGetLastError();                                                                        \
   }
     DENSE_FWD_UT(1)
-    DENSE_FWD_UT(4)
     DENSE_FWD_UT(2)
+    DENSE_FWD_UT(4)
 #undef DENSE_FWD_UT
   }
   dim3 grid(a->Up / 16, (a->B + 31) / 32, a->G);
