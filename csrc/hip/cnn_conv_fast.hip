@@ -29,6 +29,14 @@
 
 #include "cnn_args.h"
 
+// 1: staging loads without per-chunk branches (halo / padding chunks read a
+// zero chunk; the loads of a batch all issue before the first wait). Measured
+// same-box 2-3 % SLOWER per population step than the per-chunk branches, so
+// 0 is the default (profiles/conv_stage_select_ab_r3.txt)
+#ifndef GT_STAGE_SELECT
+#define GT_STAGE_SELECT 0
+#endif
+
 #ifndef GT_F32_NO_BPIPE
 #define GT_F32_NO_BPIPE 0      // 1: fp32 conv main loop without the patch-fragment pipeline (A/B builds)
 #endif
@@ -265,7 +273,11 @@ conv_fast_kernel(ConvArgs a) {
       if (n_src == 1) {
 #pragma unroll
         for (int j = 0; j < JB; ++j)
+#if GT_STAGE_SELECT
           if (j0 + j < NPT) ld_chunk(pok[j0 + j] ? src0 + poff[j0 + j] : zc, acc8[j]);
+#else
+          if (j0 + j < NPT && pok[j0 + j]) ld_chunk(src0 + poff[j0 + j], acc8[j]);
+#endif
       } else {
 #pragma unroll
         for (int k = 0; k < GT_MAXSLOT; ++k) {
@@ -276,7 +288,11 @@ conv_fast_kernel(ConvArgs a) {
           for (int j = 0; j < JB; ++j) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) t8[j][e] = 0.f;
+#if GT_STAGE_SELECT
             if (j0 + j < NPT) ld_chunk(pok[j0 + j] ? sk + poff[j0 + j] : zc, t8[j]);
+#else
+            if (j0 + j < NPT && pok[j0 + j]) ld_chunk(sk + poff[j0 + j], t8[j]);
+#endif
           }
 #pragma unroll
           for (int j = 0; j < JB; ++j)
@@ -1681,7 +1697,13 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
       const long off = ((long)hh * W + ww) * (NCBI * 8) + cb * 8;
       // unconditional loads (zero chunk for the halo): see conv_fast_kernel's staging
       if (n_src == 1) {
+#if GT_STAGE_SELECT
         load8f_or0(src0 + off, ok, xr[j]);
+#else
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
+        if (ok) load8f(src0 + off, xr[j]);
+#endif
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
@@ -1699,7 +1721,11 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < DT; ++j) {
       const int i = tid + NT_ * j;
+#if GT_STAGE_SELECT
       load8f_or0(dsrc + (long)i * 8, i < DCH, dr[j]);
+#else
+      if (i < DCH) load8f(dsrc + (long)i * 8, dr[j]);
+#endif
     }
   };
   auto store = [&](int buf) {
@@ -1946,9 +1972,10 @@ extern "C" int gt_wgrad_set_nb(int nb) {
       dim3 gz(a->S, a->ngroups, nz_);                                                                    \
       const bool pkz = wgrad_pk_ok(a, (NCBO_ * 8 + 15) / 16);                                            \
       if (nz_ == 2) {                                                                                    \
-        if (pkz) hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 1, 2>), gz, \
+        /* the shape's band buffers (2 for the 16-wide stage: its 2 x S x G workgroups fit one per CU) */  \
+        if (pkz) hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_, 1, 2>), gz, \
                                     dim3(NW_ * 64), 0, stream, *a);                                      \
-        else hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 0, 2>), gz,     \
+        else hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_, 0, 2>), gz,     \
                                 dim3(NW_ * 64), 0, stream, *a);                                          \
       } else {                                                                                           \
         if (pkz) hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 1, 4>), gz, \

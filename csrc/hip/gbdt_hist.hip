@@ -63,7 +63,8 @@
 #define HB_STRIDE 514    // int64 per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
 #define HB_T 512
 #define HB_U 4
-#define GB_R 16384       // rows per histogram chunk (larger: fewer partial slots to reduce)
+#define GB_R 65536       // rows per histogram chunk: 4x fewer partial slots to reduce than 16K (reduce 231 -> 144 us
+                         // per call at 1M x 256, depth 10; same tree time: profiles/gbdt_chunk_ab_r3.txt)
 #define GB_MAXD 12       // deepest supported tree
 
 namespace {
@@ -116,6 +117,7 @@ struct Geo {
   int maxch;     // chunk records per fold
   int maxslot;   // partial histogram slots per fold
   int lg_n;
+  int rch;       // rows per histogram chunk (GB_R unless GENTUN_GBDT_CHUNK overrides)
 };
 
 // ---- G2: gradients of every fold (all rows; only indexed rows are read) ----
@@ -244,13 +246,14 @@ __global__ void __launch_bounds__(256) transpose_bins_kernel(const uint8_t* __re
 }
 
 // chunk records of one built node (thread-serial; plan kernels)
-__device__ void emit_node(Chunk* ch, Red* rd, int& nch, int& nrd, int& nslot, int node, int start, int count) {
-  if (count <= GB_R) {
+__device__ void emit_node(Chunk* ch, Red* rd, int& nch, int& nrd, int& nslot, int node, int start, int count,
+                          int rch) {
+  if (count <= rch) {
     ch[nch++] = Chunk{node, start, count, -1};
     return;
   }
   const int first = nslot;
-  for (int o = 0; o < count; o += GB_R) ch[nch++] = Chunk{node, start + o, min(GB_R, count - o), nslot++};
+  for (int o = 0; o < count; o += rch) ch[nch++] = Chunk{node, start + o, min(rch, count - o), nslot++};
   rd[nrd++] = Red{node, first, nslot - first, 0};
 }
 
@@ -263,7 +266,7 @@ __global__ void level0_kernel(Geo geo, const int* __restrict__ nroot, LNode* __r
   r.start = 0; r.count = nroot[k]; r.G = 0; r.H = 0; r.exists = 1; r.built = 1; r.parent = -1; r.pad = 0;
   cur[(size_t)k * geo.Lmax] = r;
   int nch = 0, nrd = 0, nslot = 0;
-  emit_node(chunks + (size_t)k * geo.maxch, reds + (size_t)k * geo.maxch, nch, nrd, nslot, 0, 0, r.count);
+  emit_node(chunks + (size_t)k * geo.maxch, reds + (size_t)k * geo.maxch, nch, nrd, nslot, 0, 0, r.count, geo.rch);
   counts[2 * k] = nch;
   counts[2 * k + 1] = nrd;
 }
@@ -675,7 +678,7 @@ __global__ void __launch_bounds__(256) plan_next_kernel(Geo geo, int depth, cons
     Red* rd = reds + (size_t)k * geo.maxch;
     for (int j = 0; j < 2 * L; ++j) {
       const LNode c = nxt[(size_t)k * geo.Lmax + j];
-      if (c.exists && c.built) emit_node(ch, rd, nch, nrd, nslot, j, c.start, c.count);
+      if (c.exists && c.built) emit_node(ch, rd, nch, nrd, nslot, j, c.start, c.count, geo.rch);
     }
   }
   counts[2 * k] = nch;
@@ -799,7 +802,10 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   geo.n = n; geo.F = F; geo.Fs = Fs; geo.nfold = nfold; geo.K = K; geo.max_depth = D;
   geo.Lmax = 1 << D;
   geo.Lh = 1 << std::max(0, D - 1);
-  const int rchunks = (n + GB_R - 1) / GB_R;
+  // rows per histogram chunk: fewer, longer chunks = fewer partial slots for the reduce to sum
+  static const int rch_env = std::getenv("GENTUN_GBDT_CHUNK") ? std::atoi(std::getenv("GENTUN_GBDT_CHUNK")) : 0;
+  geo.rch = rch_env >= 1024 ? rch_env : GB_R;
+  const int rchunks = (n + geo.rch - 1) / geo.rch;
   geo.maxch = rchunks + geo.Lh + 2;
   geo.maxslot = 2 * rchunks + 2;
   geo.lg_n = 0;

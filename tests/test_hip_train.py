@@ -71,15 +71,18 @@ def test_hip_fold_subset_equals_batched():
     assert one["val_loss"][0] == full["val_loss"][1]
 
 
-def test_population_batch_invariance():
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_population_batch_invariance(dtype):
     """A candidate's per-fold result is bit-identical whether it trains alone
     or batched with other architectures in one population job (shared
-    launches, per-group tables; SURVEY.md §7.3 hard part 4)."""
+    launches, per-group tables; SURVEY.md §7.3 hard part 4) -- in both
+    precisions (fp32: the launch-size-dependent wgrad column slices and
+    band buffers must not change any sum)."""
     from gentun_amd.models import cnn_engine as E
     from gentun_amd.models.genome import make_plan
     x, y, folds, _ = _setup(n=600)
     dev = torch.device("cuda", 0)
-    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="bf16", loss="ce", reset="all")
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype=dtype, loss="ce", reset="all")
     genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '000', 'S_2': '0000000000'},
              {'S_1': '111', 'S_2': '1111111111'}, {'S_1': '010', 'S_2': '1000000001'}]
     plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
