@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "cnn_args.h"
 
@@ -378,7 +379,28 @@ conv_fast_kernel(ConvArgs a) {
     }
   };
   if (!(a.dbg & 1)) {
-    if constexpr (PREC != 0 && !GT_F32_NO_BPIPE) {
+    if constexpr (PREC != 0 && !GT_F32_NO_BPIPE && NKS > 64) {
+      // long reductions (wide layers: 72-100 k-steps): a runtime loop over k-step PAIRS, so the
+      // register sets stay compile-time indexed (a fully unrolled loop this long is not unrolled
+      // by hipcc and its dynamically indexed operand arrays went to scratch); the prefetches are
+      // unconditional (clamped k-step: the tail re-reads the last one)
+      static_assert(PF == 2, "k-step pairs need a 2-deep weight prefetch");
+      uint4 bfr[2][PG][NPL];
+      load_b(0, bfr[0]);
+      auto kstep = [&](int s, auto par) {
+        constexpr int P = decltype(par)::value;
+        load_b(min(s + 1, NKS - 1), bfr[P ^ 1]);
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h) acc[t][h] = mma(t, areg[P][t], bfr[P][h], acc[t][h]);
+        load_a(min(s + PF, NKS - 1), areg[P]);
+      };
+      for (int s = 0; s < NKS; s += 2) {
+        kstep(s, std::integral_constant<int, 0>());
+        if (s + 1 < NKS) kstep(s + 1, std::integral_constant<int, 1>());
+      }
+    } else if constexpr (PREC != 0 && !GT_F32_NO_BPIPE) {
       // fp32: the next k-step's patch fragments are read while this step's 6 x CT x PG
       // MFMAs run (the unpipelined loop waited for its LDS reads before every k-step)
       uint4 bfr[2][PG][NPL];
@@ -1354,7 +1376,7 @@ static bool pk_ok(const ConvArgs* a, int nt) {
     if (NWV_ == 4) CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 0)                              \
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
   }
-// narrow images (W < 16: no persistent variant)
+// narrow images (W < 16: no persistent variant), and the wide deep-space shapes (tile kernel only)
 #define CONV_FAST_CASE_F32_NARROW(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                              \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)
 // shapes whose every wave owns all NT co tiles: packed last tile when the real channels allow
@@ -1392,6 +1414,16 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
     CONV_FAST_CASE_F32_NARROW(5, 5, 7, 8, 8, 7, 13, 7)   // s3 input conv (50 -> 100): one co tile per wave, 7 waves
     CONV_FAST_CASE_F32_NARROW(3, 3, 13, 8, 8, 7, 13, 7)  // s3 nodes / output conv, and their dgrad (100 -> 100)
     CONV_FAST_CASE_F32_NARROW(5, 5, 13, 8, 8, 4, 7, 4)   // s3 input conv dgrad (100 -> 50)
+    // wide deep space S=(3,4,5), kernels (64, 128, 256): the whole Cin patch in LDS (up to 154 KB: one
+    // workgroup of 8 waves per CU for stages 2-3), 2 co tiles x 4 pixel groups per wave
+    CONV_FAST_CASE_F32_NARROW(5, 5, 1, 32, 8, 4, 8, 4)     // s1 input conv (3 -> 64)
+    CONV_FAST_CASE_F32_NARROW(3, 3, 8, 32, 4, 4, 8, 4)     // s1 nodes / output conv, and their dgrad (64 -> 64)
+    CONV_FAST_CASE_F32_NARROW(5, 5, 8, 16, 8, 8, 16, 8)    // s2 input conv (64 -> 128)
+    CONV_FAST_CASE_F32_NARROW(3, 3, 16, 16, 8, 8, 16, 8)   // s2 nodes / output conv, and their dgrad (128 -> 128)
+    CONV_FAST_CASE_F32_NARROW(5, 5, 16, 16, 4, 4, 8, 4)    // s2 input conv dgrad (128 -> 64)
+    CONV_FAST_CASE_F32_NARROW(5, 5, 16, 8, 8, 16, 32, 8)   // s3 input conv (128 -> 256)
+    CONV_FAST_CASE_F32_NARROW(3, 3, 32, 8, 8, 16, 32, 8)   // s3 nodes / output conv, and their dgrad (256 -> 256)
+    CONV_FAST_CASE_F32_NARROW(5, 5, 32, 8, 4, 8, 16, 4)    // s3 input conv dgrad (256 -> 128)
     return -100;
   }
   if (a->prec != 0) return -1;

@@ -77,7 +77,10 @@ CONV_SHAPES = [(32, 32, 3, 20, 5, 1), (32, 32, 20, 20, 3, 3), (16, 16, 20, 50, 5
                # stage 3 of the deep (20,50,100) space: shape-specialised 8x8 kernels
                (8, 8, 50, 100, 5, 1), (8, 8, 100, 100, 3, 2), (8, 8, 100, 50, 5, 1),
                # wide layers of the deep (64,128,256) space: channel-blocked patch staging
-               (8, 8, 256, 256, 5, 1), (8, 8, 256, 100, 5, 2), (16, 16, 128, 128, 5, 3), (32, 32, 64, 64, 5, 2)]
+               (8, 8, 256, 256, 5, 1), (8, 8, 256, 100, 5, 2), (16, 16, 128, 128, 5, 3), (32, 32, 64, 64, 5, 2),
+               # ... and their shape-specialised tile kernels (round 3): every conv / dgrad shape of the space
+               (32, 32, 3, 64, 5, 1), (32, 32, 64, 64, 3, 2), (16, 16, 64, 128, 5, 1), (16, 16, 128, 128, 3, 2),
+               (16, 16, 128, 64, 5, 1), (8, 8, 128, 256, 5, 1), (8, 8, 256, 256, 3, 3), (8, 8, 256, 128, 5, 1)]
 
 
 @pytest.mark.gpu
