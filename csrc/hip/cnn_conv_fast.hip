@@ -2083,6 +2083,13 @@ static int wgrad_rows(int KH, int KW, int Cinp, int Coutp, int H, int W, int pre
     if (KH == 3 && KW == 3 && Cinp == 56 && Coutp == 56 && W == 16 && H % 4 == 0) return 4;
     if (KH == 5 && KW == 5 && Cinp == 56 && Coutp == 104 && W == 8 && H % 4 == 0) return 4;    // deep s3
     if (KH == 3 && KW == 3 && Cinp == 104 && Coutp == 104 && W == 8 && H % 4 == 0) return 4;
+    // wide deep space
+    if (KH == 5 && KW == 5 && Cinp == 8 && Coutp == 64 && W == 32 && H % 4 == 0) return 4;
+    if (KH == 3 && KW == 3 && Cinp == 64 && Coutp == 64 && W == 32 && H % 2 == 0) return 2;
+    if (KH == 5 && KW == 5 && Cinp == 64 && Coutp == 128 && W == 16 && H % 2 == 0) return 2;
+    if (KH == 3 && KW == 3 && Cinp == 128 && Coutp == 128 && W == 16 && H % 2 == 0) return 2;
+    if (KH == 5 && KW == 5 && Cinp == 128 && Coutp == 256 && W == 8 && H % 4 == 0) return 4;
+    if (KH == 3 && KW == 3 && Cinp == 256 && Coutp == 256 && W == 8 && H % 4 == 0) return 4;
     return 0;
   }
   if (KH == 5 && KW == 5 && Cinp == 8 && Coutp == 24 && W == 32 && H % 8 == 0) return 8;
@@ -2125,6 +2132,13 @@ extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
     WGRAD_FAST_CASE_F32(3, 3, 7, 7, 16, 4, 8, 2)      // s2 nodes / output conv (50 -> 50)
     WGRAD_FAST_CASE_F32Z(5, 5, 7, 13, 8, 4, 8, 4)     // deep s3 input conv (50 -> 100)
     WGRAD_FAST_CASE_F32Z(3, 3, 13, 13, 8, 4, 8, 4)    // deep s3 nodes / output conv (100 -> 100)
+    // wide deep space (64, 128, 256): column slices so each workgroup's dW slice fits its registers
+    WGRAD_FAST_CASE_F32(5, 5, 1, 8, 32, 4, 4, 1)      // s1 input conv (3 -> 64)
+    WGRAD_FAST_CASE_F32(3, 3, 8, 8, 32, 2, 8, 1)      // s1 nodes / output conv (64 -> 64)
+    WGRAD_FAST_CASE_F32Z(5, 5, 8, 16, 16, 2, 8, 7)    // s2 input conv (64 -> 128)
+    WGRAD_FAST_CASE_F32Z(3, 3, 16, 16, 16, 2, 8, 4)   // s2 nodes / output conv (128 -> 128)
+    WGRAD_FAST_CASE_F32Z(5, 5, 16, 32, 8, 4, 8, 13)   // s3 input conv (128 -> 256)
+    WGRAD_FAST_CASE_F32Z(3, 3, 32, 32, 8, 4, 8, 10)   // s3 nodes / output conv (256 -> 256)
     return -100;
   }
   if (a->prec != 0) return -1;

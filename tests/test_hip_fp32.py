@@ -188,7 +188,11 @@ def test_conv_dgrad_fanout_fp32(k, H):
                                                       (16, 16, 20, 50, 5, 1, False), (16, 16, 50, 50, 3, 2, False),
                                                       (8, 8, 64, 128, 3, 1, False), (14, 14, 50, 50, 3, 3, False),
                                                       (8, 8, 256, 256, 5, 1, False), (16, 16, 128, 128, 5, 2, False),
-                                                      (8, 8, 50, 100, 5, 1, False), (8, 8, 100, 100, 3, 2, False)])
+                                                      (8, 8, 50, 100, 5, 1, False), (8, 8, 100, 100, 3, 2, False),
+                                                      # wide deep space, shape-specialised (round 3)
+                                                      (32, 32, 3, 64, 5, 1, True), (32, 32, 64, 64, 3, 2, False),
+                                                      (16, 16, 64, 128, 5, 1, False), (16, 16, 128, 128, 3, 1, False),
+                                                      (8, 8, 128, 256, 5, 1, False), (8, 8, 256, 256, 3, 2, False)])
 @pytest.mark.parametrize("pk", [0, 1])
 def test_conv_wgrad_fp32(H, W, cin, cout, k, nin, first, pk):
     """Weight + bias gradient (specialised register-staged kernel and the
