@@ -24,3 +24,9 @@ trap 'kill $hb' EXIT
 timeout -k 10 720 python3 -u bench.py --gpus 1 --space deep --kernels 64,128,256 --batch-norm --per-gpu 2 --steps 2 --warmup 1 \
   --json-out gpurun_out/wide/bench.json > gpurun_out/wide/bench.out 2> gpurun_out/wide/bench.err || { tail -5 gpurun_out/wide/bench.err; exit 1; }
 cat gpurun_out/wide/bench.json
+# deep (20,50,100) + BN bench line at HEAD (round 2: 385.2)
+timeout -k 10 400 python3 -u bench.py --gpus 1 --space deep --batch-norm --per-gpu 3 --steps 3 --warmup 1 \
+  --json-out gpurun_out/wide/bench_deep.json > gpurun_out/wide/bench_deep.out 2> gpurun_out/wide/bench_deep.err || { tail -5 gpurun_out/wide/bench_deep.err; exit 1; }
+cat gpurun_out/wide/bench_deep.json
+# the 20-generation search: resume from profiles/ga20_ckpt (generations 19-20)
+TAG=_part2 BUDGET=600 bash tools/gpu_ga20.sh
