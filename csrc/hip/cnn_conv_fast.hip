@@ -142,7 +142,9 @@ __device__ __forceinline__ void f32_epi_regs(const ConvArgs& a, const GroupRec& 
                                              const f32x4_t (&acc)[CT][PG], int wco, int pgw, int lane);
 
 // RE (fp32 only): 1 = register-direct epilogue (f32_epi_regs), 0 = through the LDS output tile
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0, int PK = 0, int RE = 0>
+// CTX > 0 forces the co tiles per wave (1: waves split the co tiles, more pixel groups each)
+template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0, int PK = 0, int RE = 0,
+          int CTX = 0>
 __global__ void __launch_bounds__(NWV * 64)
 __attribute__((amdgpu_waves_per_eu(PREC ? 2 : (NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))))
 conv_fast_kernel(ConvArgs a) {
@@ -157,7 +159,7 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int TP = TH * W;                        // tile pixels
   constexpr int NPG = TP / 16;                      // pixel groups
   // co tiles per wave (odd NT: one per wave; packed last tile: all NT, so every wave carries the same work)
-  constexpr int CT = PK ? NT : ((NT >= 2 && NT % 2 == 0) ? 2 : 1);
+  constexpr int CT = CTX ? CTX : PK ? NT : ((NT >= 2 && NT % 2 == 0) ? 2 : 1);
   constexpr int WC = NT / CT;                       // waves along co
   constexpr int WP = NWV / WC;                        // waves along pixels
   constexpr int PG = NPG / WP;                      // pixel groups per wave
@@ -1315,6 +1317,25 @@ static int g_probe = 0;
 #define CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_)                               \
   CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_, 0)
 
+// one co tile per wave (CTX 1), fp32, register-direct epilogue
+#define CONV_FAST_LAUNCH_CT1(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                   \
+  {                                                                                                     \
+    if (g_probe) return 1000 + TH_;                                                                     \
+    dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
+    const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 1>::lds(a->epi_bf16 != 0);          \
+    auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 0, 1, 1>;                 \
+    lds_limit(fn, lds);                                                                                 \
+    hipLaunchKernelGGL(fn, grid, dim3(NWV_ * 64), lds, stream, *a);                                     \
+    return (int)hipGetLastError();                                                                      \
+  }
+
+// 1 (default): the S=(3,5) s2 input-conv dgrad (5x5, 50 -> 20) with one co tile per wave and 4 pixel groups
+// each instead of the packed tile's 2 tiles x 2 groups: 33 % more MFMAs but half the weight loads per MFMA;
+// same-box A/B 126 -> 114 us per launch at 25 groups, population step -1.6 % (profiles/conv_s2in_dgrad_ct1_ab_r3.txt)
+#ifndef GT_S2IN_DGRAD_CT1
+#define GT_S2IN_DGRAD_CT1 1
+#endif
+
 // fp32 register-direct epilogue in the tile kernel (A/B: GENTUN_F32_REGEPI=0 / 1, gt_conv_set_regepi):
 // no LDS output tile, no second barrier, the pool from lane shuffles
 static int g_regepi = -1;
@@ -1409,6 +1430,9 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
     // (a packed tile here needs every wave to own all 4 co tiles: 2x the weight traffic per MFMA,
     // measured 20 % slower than the 2 + 2 split -- profiles/conv_f32_packed_tile_ab_r2.txt)
     CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
+#if GT_S2IN_DGRAD_CT1
+    if (CONV_FAST_MATCH(5, 5, 7, 16, 8, 2, 3)) CONV_FAST_LAUNCH_CT1(5, 5, 7, 16, 8, 2, 3, 4)
+#endif
     CONV_FAST_CASE_F32_PK(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
     // deep S=(3,4,5) space, kernels (20, 50, 100): stage 3 at 8x8, one image per workgroup
     CONV_FAST_CASE_F32_NARROW(5, 5, 7, 8, 8, 7, 13, 7)   // s3 input conv (50 -> 100): one co tile per wave, 7 waves

@@ -5,6 +5,9 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export GENTUN_NO_AUTOBUILD=1
+# the 20-generation search first: resume from profiles/ga20_ckpt (generations 19-20)
+TAG=_part2 BUDGET=600 bash tools/gpu_ga20.sh > gpurun_out/ga20_part2.txt 2>&1 || { tail -5 gpurun_out/ga20_part2.txt; exit 1; }
+tail -3 gpurun_out/ga20_part2.txt | cut -c1-400
 mkdir -p gpurun_out/ct1; rm -f gpurun_out/ct1/*.log
 GENTUN_HIP_LIB=gentun_amd/_native/ab/s2in_ct1.so timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_hip_fp32.py -k "dgrad_fanout" > gpurun_out/ct1/tests.log 2>&1 || { tail -20 gpurun_out/ct1/tests.log; exit 1; }
 tail -1 gpurun_out/ct1/tests.log
@@ -28,5 +31,3 @@ cat gpurun_out/wide/bench.json
 timeout -k 10 400 python3 -u bench.py --gpus 1 --space deep --batch-norm --per-gpu 3 --steps 3 --warmup 1 \
   --json-out gpurun_out/wide/bench_deep.json > gpurun_out/wide/bench_deep.out 2> gpurun_out/wide/bench_deep.err || { tail -5 gpurun_out/wide/bench_deep.err; exit 1; }
 cat gpurun_out/wide/bench_deep.json
-# the 20-generation search: resume from profiles/ga20_ckpt (generations 19-20)
-TAG=_part2 BUDGET=600 bash tools/gpu_ga20.sh
