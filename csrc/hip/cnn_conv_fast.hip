@@ -1329,11 +1329,14 @@ static int g_probe = 0;
     return (int)hipGetLastError();                                                                      \
   }
 
-// 1 (default): the S=(3,5) s2 input-conv dgrad (5x5, 50 -> 20) with one co tile per wave and 4 pixel groups
-// each instead of the packed tile's 2 tiles x 2 groups: 33 % more MFMAs but half the weight loads per MFMA;
-// same-box A/B 126 -> 114 us per launch at 25 groups, population step -1.6 % (profiles/conv_s2in_dgrad_ct1_ab_r3.txt)
+// 1: the S=(3,5) s2 input-conv dgrad (5x5, 50 -> 20) with one co tile per wave and 4 pixel groups each
+// instead of the packed tile's 2 tiles x 2 groups: 33 % more MFMAs but half the weight loads per MFMA;
+// same-box A/B 126 -> 114 us per launch at 25 groups, population step -1.6 % (profiles/conv_s2in_dgrad_ct1_ab_r3.txt).
+// Off by default: with it, tests/test_hip_dp.py's 2-rank data-parallel trajectory drifted 3.6e-4 (relative) from
+// the single-process one, past the test's 1e-4 bound (the packed tile's nine-term products: within it) -- not
+// understood yet, so the measured-safe kernel stays the default
 #ifndef GT_S2IN_DGRAD_CT1
-#define GT_S2IN_DGRAD_CT1 1
+#define GT_S2IN_DGRAD_CT1 0
 #endif
 
 // fp32 register-direct epilogue in the tile kernel (A/B: GENTUN_F32_REGEPI=0 / 1, gt_conv_set_regepi):
