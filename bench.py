@@ -243,7 +243,9 @@ def run(args):
                  "random-init weights)").format(args.samples // 1000),
         "config": {"model": "Genetic-CNN {} dense 500".format(space), "global_batch": 32 * args.nfold,
                    "seq_len": None,
-                   "parallelism": ("population-dp{} (RCCL genome bcast / score all_gather over xGMI)".format(N)
+                   "parallelism": ("population-dp{} ({} genome bcast / score all_gather)".format(
+                                       N, "RCCL over xGMI" if getattr(comm, "backend", "") == "nccl"
+                                       else getattr(comm, "backend", "?"))
                                    if N > 1 else "population-dp1 (single evaluator, no collectives)"),
                    "algorithm": "RussianRouletteGA pC0.2 pM0.8 qC0.3 qM0.1", "population": population,
                    "population_total": population, "max_candidates_per_round": round_size,
