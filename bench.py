@@ -155,18 +155,20 @@ def run(args):
     evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch,
                                     torch_pop=not args.torch_unbatched)
     N = comm.world_size
-    round_size = per_gpu * N
+    slack = 1                 # evaluate_round: up to one more per rank when that saves a round
+    round_size = (per_gpu + slack) * N
 
     if comm.rank != 0:
         # evaluator rank: serves EVAL / SYNC (timing fence) / STOP from rank 0
-        GentunWorker(GeneticCnnIndividual, x, y, comm=comm, evaluator=evaluator).work()
+        GentunWorker(GeneticCnnIndividual, x, y, comm=comm, evaluator=evaluator, verbose=False).work()
         _teardown(comm)
         return None
 
     grng.seed(args.seed)
     population = args.pop_per_gpu * N if args.pop_per_gpu else args.population
     pop = DistributedPopulation(GeneticCnnIndividual, x, y, size=population, crossover_rate=0.3,
-                                mutation_rate=0.1, additional_parameters=extra, comm=comm, evaluator=evaluator)
+                                mutation_rate=0.1, additional_parameters=extra, comm=comm, evaluator=evaluator,
+                                verbose=False)
     ga = RussianRouletteGA(pop, crossover_probability=0.2, mutation_probability=0.8, seed=args.seed,
                            verbose=False)
     completed = []          # per completed generation: fittest's fitness / categorical accuracy
@@ -196,7 +198,8 @@ def run(args):
     def one_round():
         if not ga.population.pending():
             advance()
-        n = ga.population.evaluate_round(per_gpu)
+        ga.population.ga_generation = ga.generation
+        n = ga.population.evaluate_round(per_gpu, slack=slack)
         track()
         return n
 

@@ -24,6 +24,15 @@ def _floats(s):
     return tuple(float(v) for v in s.split(",")) if s else ()
 
 
+class SearchFailed(SystemExit):
+    """A search that cannot continue (every evaluation failed): exit code
+    parallel.fault.EXIT_SEARCH_FAILED, which the restart supervisor does not retry."""
+
+    def __init__(self):
+        from .parallel.fault import EXIT_SEARCH_FAILED
+        super(SearchFailed, self).__init__(EXIT_SEARCH_FAILED)
+
+
 def _common(ap):
     from .config import RunConfig
     d = RunConfig.from_env()          # GENTUN_* environment over the defaults; flags win over both
@@ -108,7 +117,19 @@ def _run_search(args, species, x, y, extra, maximize):
         pop = DistributedPopulation(species, x, y, size=args.pop, maximize=maximize, additional_parameters=extra,
                                     comm=comm, evaluator=evaluator, schedule=cfg.schedule)
         ga = cls(pop, seed=cfg.seed, checkpoint_dir=cfg.checkpoint_dir, event_log=log, **ga_kw)
-    best = ga.run(args.gens)
+    try:
+        best = ga.run(args.gens)
+    except Exception:
+        import traceback
+        traceback.print_exc()
+        # every evaluator rank still waits in the dispatch broadcast: release them (CMD_STOP) before
+        # failing, and exit with a code the restart supervisor does not retry (a failed search is
+        # not a transient rank fault: resuming from the checkpoint would fail the same way)
+        try:
+            ga.population.shutdown()
+        finally:
+            sys.stderr.write("[gentun] search failed; evaluators released\n")
+        raise SearchFailed()
     ga.population.shutdown()
     out = {"best_fitness": best.get_fitness(), "best_genes": best.get_genes(),
            "history": [{k: h[k] for k in ("generation", "best_fitness", "evals", "wall_s", "candidates_per_hour")}

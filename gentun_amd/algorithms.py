@@ -39,6 +39,9 @@ class GeneticAlgorithm(object):
         self.seed = seed
         self.checkpoint_dir = checkpoint_dir
         self.event_log = event_log
+        if event_log is not None and getattr(population, "event_log", False) is None:
+            # a distributed population writes its per-unit evaluation events into the GA's log
+            population.event_log = event_log
         self.verbose = verbose
         self.history = []
         self.best_individual = None
@@ -60,6 +63,7 @@ class GeneticAlgorithm(object):
         record history. Returns the fittest individual."""
         self._say("Evaluating generation #{}...".format(self.generation))
         pending = len(self.population.pending())
+        self.population.ga_generation = self.generation       # tags distributed evaluation events
         t0 = time.perf_counter()
         fittest = self.population.get_fittest()
         wall = time.perf_counter() - t0

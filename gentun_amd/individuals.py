@@ -274,7 +274,9 @@ class GeneticCnnIndividual(Individual):
     the kernels, or 'all' = concurrent folds from fresh weights) and
     ``batching`` ('keras' = short last batch, or 'wrap') and ``batch_norm``
     (False = the reference network; True = conv -> BatchNorm -> ReLU in every
-    node, Keras BatchNormalization defaults).
+    node, Keras BatchNormalization defaults) and ``verbose`` (print the
+    reference's "KFold i/n" / "Training N epochs with learning rate lr" lines,
+    keras_models.py:134,137).
     """
 
     def __init__(self, x_train, y_train, genome=None, genes=None, crossover_rate=0.3, mutation_rate=0.1,
@@ -282,7 +284,7 @@ class GeneticCnnIndividual(Individual):
                  kernel_sizes=((5, 5), (5, 5)), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
                  loss='bce_compat', dtype='fp32', seed=0, backend=None, device=None, optimizer='adam',
-                 momentum=0.9, reset='kernels', batching='keras', batch_norm=False):
+                 momentum=0.9, reset='kernels', batching='keras', batch_norm=False, verbose=False):
         if genome is None:
             genome = {'S_{}'.format(i + 1): k * (k - 1) // 2 for i, k in enumerate(nodes)}
         if genes is None:
@@ -314,6 +316,7 @@ class GeneticCnnIndividual(Individual):
         self.reset = reset
         self.batching = batching
         self.batch_norm = batch_norm
+        self.verbose = verbose
 
     @staticmethod
     def generate_random_genes(genome):
@@ -331,7 +334,8 @@ class GeneticCnnIndividual(Individual):
                                self.learning_rate, self.batch_size, loss=self.loss, dtype=self.dtype,
                                seed=self.seed, backend=self.backend, device=device or self.device,
                                optimizer=self.optimizer, momentum=self.momentum, reset=self.reset,
-                               batching=self.batching, batch_norm=self.batch_norm)
+                               batching=self.batching, batch_norm=self.batch_norm,
+                               verbose=self.verbose)
 
     def cost(self):
         """Relative training cost (forward FLOPs/sample); LPT scheduling key."""
@@ -368,6 +372,7 @@ class GeneticCnnIndividual(Individual):
             'reset': self.reset,
             'batching': self.batching,
             'batch_norm': self.batch_norm,
+            'verbose': self.verbose,
         }
 
     def mutate(self):

@@ -28,7 +28,8 @@ class GeneticCnnModel(GentunModel):
     def __init__(self, x_train, y_train, genes, nodes, input_shape, kernels_per_layer, kernel_sizes, dense_units,
                  dropout_probability, classes, nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
                  loss="bce_compat", dtype="fp32", seed=0, backend=None, device=None, fold_parallel=True,
-                 optimizer="adam", momentum=0.9, reset="kernels", batching="keras", batch_norm=False):
+                 optimizer="adam", momentum=0.9, reset="kernels", batching="keras", batch_norm=False,
+                 verbose=False):
         super(GeneticCnnModel, self).__init__(x_train, y_train)
         self.genes = dict(genes)
         self.name = '-'.join(self.genes[k] for k in sorted(self.genes))
@@ -58,12 +59,13 @@ class GeneticCnnModel(GentunModel):
         self.cfg = _eng.TrainConfig(epochs=epochs, learning_rate=learning_rate, batch_size=batch_size,
                                     dropout=dropout_probability, loss=loss, dtype=dtype, seed=seed,
                                     optimizer=optimizer, momentum=momentum, reset=reset, batching=batching,
-                                    batch_norm=batch_norm)
+                                    batch_norm=batch_norm, verbose=verbose, nfold=nfold)
         self.fold_parallel = fold_parallel
         self.model = self.build_model(self.genes, self.nodes, self.input_shape, self.kernels_per_layer,
                                       self.kernel_sizes, self.dense_units, self.dropout_probability, self.classes)
         self.fold_scores = []
         self.fold_metrics = None
+        self.jobs = []               # the trained job(s) of the last cross_validate (reset_weights)
 
     # ------------------------------------------------------------ structure
     def build_model(self, genes, nodes, input_shape, kernels_per_layer, kernel_sizes, dense_units,
@@ -88,22 +90,37 @@ class GeneticCnnModel(GentunModel):
         return body, " + ".join(names[i] for i in outputs)
 
     def reset_weights(self):
-        """Per-fold re-initialisation policy of the engine (keras_models.py:
-        120-125): with ``reset="kernels"`` (default) each fold re-draws only
-        the Glorot kernels and keeps the biases of the previous fold
-        (models/cnn_engine.py SequentialFoldJob); ``reset="all"`` trains the
-        folds concurrently from fresh kernels and zero biases. Returns the
-        active policy (the engine applies it; there is no live Keras model
-        to mutate here)."""
-        return self.cfg.reset
+        """keras_models.py:120-125: re-run the kernel initialisers of the
+        model's live weights, keeping the biases (and BatchNorm state). The
+        weights live in the job(s) the last :meth:`cross_validate` trained
+        (one per fold with the reference's sequential folds); before any
+        training there is nothing to reset -- every job draws fresh Glorot
+        kernels when it starts, which is the same policy. Returns the number
+        of jobs whose kernels were re-drawn."""
+        n = 0
+        for job in self._live_jobs():
+            job.reset_kernels()
+            n += 1
+        return n
+
+    def _live_jobs(self):
+        out = []
+        for job in self.jobs:
+            out.extend(getattr(job, "jobs", None) or [job])     # SequentialFoldJob: one job per fold
+        return out
 
     def plot(self, path=None):
-        """Write the decoded topology as text (Keras' plot_model needs
-        graphviz; keras_models.py:41-44)."""
-        path = path or "{}.txt".format(self.name)
-        with open(path, "w") as f:
-            f.write(self.model.describe() + "\n")
-        return path
+        """Draw the decoded network to validate gene-to-DAG (keras_models.py:
+        41-44 writes ``<name>.png`` with Keras' plot_model). ``path`` suffix
+        ``.png`` (default), ``.svg`` or ``.dot``; ``.txt`` writes the textual
+        topology. Returns the path."""
+        from ..utils.plot import plot_plan
+        path = path or "{}.png".format(self.name)
+        if path.lower().endswith(".txt"):
+            with open(path, "w") as f:
+                f.write(self.model.describe() + "\n")
+            return path
+        return plot_plan(self.model, path)
 
     # ------------------------------------------------------------ training
     def make_folds(self):
@@ -144,4 +161,5 @@ class GeneticCnnModel(GentunModel):
         for job in jobs:
             job.launch()
             results.append(job.finish())
+        self.jobs = jobs
         return self.collect(results)

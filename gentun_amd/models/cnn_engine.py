@@ -55,7 +55,7 @@ class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
                  dtype="fp32", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9,
                  reset="kernels", batching="keras", batch_norm=False, bn_momentum=0.99, bn_eps=1e-3,
-                 dp_group=None):
+                 dp_group=None, verbose=False, nfold=None):
         if isinstance(epochs, int):
             epochs = (epochs,)
         if isinstance(learning_rate, (int, float)):
@@ -96,6 +96,10 @@ class TrainConfig(object):
         self.eval_batch = int(eval_batch)
         self.optimizer = optimizer
         self.momentum = float(momentum)
+        # the reference's progress lines (keras_models.py:134,137): "KFold i/n" as a fold's
+        # training is enqueued, "Training N epochs with learning rate lr" per stage
+        self.verbose = bool(verbose)
+        self.nfold = None if nfold is None else int(nfold)
 
     def total_epochs(self):
         return sum(self.epochs)
@@ -277,6 +281,22 @@ class FoldJob(object):
     def restore(self, snap):
         raise NotImplementedError
 
+    def bias_state(self):
+        """Clones of everything ``reset_weights`` keeps (biases; BatchNorm
+        gamma / beta / running statistics)."""
+        raise NotImplementedError
+
+    def load_bias_state(self, state):
+        raise NotImplementedError
+
+    def reset_kernels(self):
+        """keras_models.py:120-125 ``reset_weights``: re-run the kernel
+        initialisers (Glorot, keyed by run seed / genes / fold like a fresh
+        job) and keep the biases the job has trained."""
+        keep = self.bias_state()
+        self.init_params()
+        self.load_bias_state(keep)
+
     # -- driver --------------------------------------------------------------
     def graph_steps(self):
         """Train steps per graph replay: the largest divisor of the epoch's
@@ -328,7 +348,14 @@ class FoldJob(object):
             graph = self._capture() if use_graph else None
             if timed:
                 ev[1].record()
+            verbose = getattr(self.cfg, "verbose", False)
+            if verbose:
+                n = getattr(self.cfg, "nfold", None) or (max(self.fold_ids) + 1)
+                for fid in sorted(set(self.fold_ids)):
+                    print("KFold {}/{}".format(fid + 1, n))
             for epochs, lr in zip(self.cfg.epochs, self.cfg.learning_rate):
+                if verbose:
+                    print("Training {} epochs with learning rate {}".format(epochs, lr))
                 self.reset_optimizer(lr)
                 for _ in range(epochs):
                     self._new_epoch_order()
@@ -544,6 +571,20 @@ class TorchFoldJob(FoldJob):
                     a[name].copy_(b[name])
             for k, r in self.bn_run.items():
                 r.copy_(other.bn_run[k])
+
+    def bias_state(self):
+        with torch.no_grad():
+            a = self._views()
+            return ({name: a[name].clone() for name, _, kind, _ in self.shapes if kind in ("zero", "one")},
+                    {k: r.clone() for k, r in self.bn_run.items()})
+
+    def load_bias_state(self, state):
+        with torch.no_grad():
+            a = self._views()
+            for name, t in state[0].items():
+                a[name].copy_(t)
+            for k, r in state[1].items():
+                self.bn_run[k].copy_(r)
 
     def restore(self, snap):
         with torch.no_grad():

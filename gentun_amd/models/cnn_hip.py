@@ -54,6 +54,10 @@ from .cnn_engine import FoldJob
 from .pop_schedule import PopulationSchedule
 
 
+# bytes of forward-only activation twins an evaluation may allocate for all groups of a job
+EVAL_TWIN_BUDGET = 1 << 30
+
+
 def pad8(c):
     return (c + 7) // 8 * 8
 
@@ -125,6 +129,10 @@ class HipPopJob(FoldJob):
         # 907 vs 958 candidates/h with it on -- it competes with the dgrad chain,
         # profiles/bench_round_size_r2.txt)
         self.adam_overlap = os.environ.get("GENTUN_ADAM_OVERLAP", "0") == "1"
+        if self.dp is not None:
+            # X5: every update must see the all-reduced gradient; an in-backward conv
+            # update on side3 would run before _dp_allreduce and the ranks would diverge
+            self.adam_overlap = False
         self.side3 = torch.cuda.Stream(dev) if self.adam_overlap else None
         self._build_adam_table()
         self._build_args()
@@ -715,6 +723,22 @@ class HipPopJob(FoldJob):
         for name in ("b1", "b2"):
             self.views[name][0].copy_(other.views[name][0])
 
+    def _kept_tensors(self):
+        out = []
+        for L in self.layers:
+            out.append(L.b[0])
+            if self.bn:
+                out += [L.gamma[0], L.beta[0], L.bn_run]
+        return out + [self.views["b1"][0], self.views["b2"][0]]
+
+    def bias_state(self):
+        return [t.clone() for t in self._kept_tensors()]
+
+    def load_bias_state(self, state):
+        for t, v in zip(self._kept_tensors(), state):
+            t.copy_(v)
+        self._refresh_copies()          # bf16 / split-plane copies of the parameters
+
     def restore(self, snap):
         self.flat.copy_(snap[0])
         self.m.copy_(snap[1])
@@ -799,24 +823,34 @@ class HipPopJob(FoldJob):
             K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
 
     def eval_batch(self):
-        """Rows per evaluation launch (K13): ``cfg.eval_batch`` (1,000 by
-        default), capped at 256, at the validation fold size and by a 4 GB
-        budget for the forward-only activation slots of all Q groups; never
-        below the training batch. Larger eval launches fill the GPU with Q
-        groups x EB rows instead of Q x 32 (63 launches of 32 per 2,000-sample
-        fold become 8 of 256)."""
+        """Rows per evaluation launch (K13): ``cfg.eval_batch`` (default 256),
+        capped at 256, at the validation fold size and by a 1 GB budget for
+        the forward-only activation twins of ALL Q groups together (so a
+        40-group job takes fewer rows per launch instead of 40x the memory);
+        never below the training batch. Larger eval launches fill the GPU with
+        Q groups x EB rows instead of Q x 32 (63 launches of 32 per
+        2,000-sample fold become 8 of 256)."""
         per_img = sum(t[0, 0].numel() * t.element_size() for t in self.act.values())
         per_img += sum(t[0, 0].numel() * t.element_size() for t in self.zpre.values())
         per_img += self.Up * 4 * 2
         maxv = int(self.val_mat.shape[1])
         eb = min(int(getattr(self.cfg, "eval_batch", 256) or 256), 256, round_up(maxv, 32))
-        eb = min(eb, max(1, int(256e6 // max(1, per_img))) // 32 * 32)     # <= 256 MB per group
+        eb = min(eb, max(1, int(EVAL_TWIN_BUDGET // max(1, per_img * self.Q))) // 32 * 32)
         return max(self.B, eb)
 
     def _eval_ops(self, EB):
         """Forward-only argument copies at batch EB on their own activation
         buffers (pointers of the training buffers remapped), the dense / head
-        copies, and the buffers to keep alive."""
+        copies, and the buffers to keep alive. Built once per job and batch
+        size: every fold's evaluation reuses the same twins."""
+        cached = getattr(self, "_eval_cache", None)
+        if cached is not None and cached[0] == EB:
+            return cached[1]
+        built = self._build_eval_ops(EB)
+        self._eval_cache = (EB, built)
+        return built
+
+    def _build_eval_ops(self, EB):
         Q = self.Q
         remap, keep = {}, []
 

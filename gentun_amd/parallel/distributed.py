@@ -7,10 +7,11 @@ them. Here every rank is a persistent evaluator
 (one per GPU) and rank 0 also runs the GA:
 
 per generation (collectives X2/X3 of SURVEY.md §2.6)
-  1. rank 0 broadcasts ``int64[4]`` = (command, generation, P, nfold),
-     the species' ``additional_parameters`` as a JSON blob (X1), and the
-     genome table ``float64[U, 3 + width]`` = (candidate slot, owner rank,
-     fold mask, encoded genes) for the ``U`` work units;
+  1. rank 0 broadcasts ``int64[5]`` = (command, generation, P, nfold, blob?),
+     the species' ``additional_parameters`` as a JSON blob (X1, only when it
+     changed), and the genome table ``float64[U, 4 + width]`` = (candidate
+     slot, owner rank, fold mask, population index, encoded genes) for the
+     ``U`` work units;
   2. every rank evaluates the units it owns (several concurrently on its GPU,
      :class:`~gentun_amd.parallel.evaluators.LocalBatchEvaluator`);
   3. one ``all_gather`` of ``float64[U, 3 + 2 nfold]`` = (status, fitness,
@@ -19,6 +20,15 @@ per generation (collectives X2/X3 of SURVEY.md §2.6)
      KB, latency-bound on xGMI;
   4. rank 0 merges fold groups per candidate, re-evaluates failed units
      locally once (worst fitness if that fails too) and breeds.
+
+Observability: the reference's progress lines are kept --
+" [.] Evaluating individual i" on the evaluating rank (gentun/worker.py:43)
+and " [*] Got fitness for individual i" on rank 0 once the gather delivered
+it (gentun/master.py:72), ``i`` = the individual's population index -- and
+rank 0 writes one ``evaluation`` JSONL event per work unit of every rank
+(rank, GA generation, dispatch, population index, genes, folds, fold scores,
+fitness, wall_s) from the gathered table, so a distributed run's event log
+is as complete as a single-process one's.
 
 Failure handling (:mod:`gentun_amd.parallel.fault`):
 per-unit status codes with one local retry on rank 0; a per-rank watchdog
@@ -119,14 +129,16 @@ class _Unit(object):
         self.fold_ids = fold_ids
 
 
-def evaluate_units(units, evaluator, nfold, rank, generation):
+def evaluate_units(units, evaluator, nfold, rank, generation, on_take=None):
     """Evaluate this rank's units; returns ``{unit_index: row}``.
 
     ``units`` is a list of ``(unit_index, _Unit)`` (static schedule) or a
     :class:`UnitClaimer` (dynamic schedule: units are claimed from the job-wide
-    ticket counter one at a time, whenever this rank has a free slot)."""
+    ticket counter one at a time, whenever this rank has a free slot).
+    ``on_take(entry)`` is called as each unit is taken (progress lines)."""
     rows = {}
     source = units if isinstance(units, UnitClaimer) else _StaticSource(units)
+    source.on_take = on_take
     try:
         _fault_hook(rank, generation)
     except Exception as exc:     # noqa: BLE001
@@ -160,6 +172,8 @@ def evaluate_units(units, evaluator, nfold, rank, generation):
 class _StaticSource(object):
     """Pre-assigned units, most expensive first (so long jobs start early)."""
 
+    on_take = None
+
     def __init__(self, units):
         self.units = sorted(units, key=lambda e: -_unit_cost(e[1]))
         self._taken = []
@@ -170,6 +184,8 @@ class _StaticSource(object):
     def __iter__(self):
         for e in self.units:
             self._taken.append(e)
+            if self.on_take is not None:
+                self.on_take(e)
             yield e
 
     def taken(self):
@@ -184,6 +200,8 @@ class UnitClaimer(object):
     nobody has started whenever it has capacity (the pull-queue behaviour of
     the reference's RabbitMQ workers, gentun/worker.py:59-63, without a
     broker)."""
+
+    on_take = None
 
     def __init__(self, comm, key, n_units, make_unit, kind):
         self.comm = comm
@@ -203,6 +221,8 @@ class UnitClaimer(object):
                 return
             e = (k, self.make_unit(k))
             self._taken.append(e)
+            if self.on_take is not None:
+                self.on_take(e)
             yield e
 
     def taken(self):
@@ -243,6 +263,9 @@ def row_width(nfold):
     return 3 + 2 * nfold
 
 
+TABLE_HDR = 4       # genome table columns before the encoded genes: slot, owner, fold mask, population index
+
+
 def _row(status, fitness, wall, scores, nfold, fold_ids, aux=None):
     row = np.full(row_width(nfold), np.nan, np.float64)
     row[0], row[1], row[2] = status, fitness, wall
@@ -269,8 +292,12 @@ class DistributedPopulation(Population):
     def __init__(self, species, x_train=None, y_train=None, individual_list=None, size=None,
                  crossover_rate=0.5, mutation_rate=0.015, maximize=True, additional_parameters=None,
                  host='localhost', port=5672, user='guest', password='guest', rabbit_queue='rpc_queue',
-                 comm=None, evaluator=None, split_folds=True, schedule="auto"):
+                 comm=None, evaluator=None, split_folds=True, schedule="auto", event_log=None, verbose=True):
         self.comm = comm if comm is not None else _comm_from_args(host, port)
+        # JSONL sink for per-unit evaluation events (the GA attaches its own log when this is None)
+        self.event_log = event_log
+        self.verbose = verbose
+        self.ga_generation = None          # set by the GA: the generation being evaluated
         if evaluator is None:
             evaluator = LocalBatchEvaluator()
         if schedule not in ("auto", "dynamic", "lpt"):
@@ -301,6 +328,9 @@ class DistributedPopulation(Population):
         pop.credentials = dict(self.credentials)
         pop.generation_counter = self.generation_counter
         pop.last_dispatch = None
+        pop.event_log = self.event_log
+        pop.verbose = self.verbose
+        pop.ga_generation = self.ga_generation
         Population.__init__(pop, self.species, self.x_train, self.y_train,
                             individual_list=[] if individual_list is None else individual_list,
                             crossover_rate=self.crossover_rate, mutation_rate=self.mutation_rate,
@@ -357,6 +387,8 @@ class DistributedPopulation(Population):
                 ind.fold_scores = scores
                 if aux is not None:
                     ind.fold_metrics = dict(getattr(ind, "fold_metrics", None) or {}, categorical_accuracy=aux)
+            if self.verbose:
+                print(" [*] Got fitness for individual {}".format(self._pop_index(ind)))
         if len(todo) > 1 and nworst == len(todo):
             # nothing evaluated anywhere (a lost device, a broken build): a search on worst-fitness
             # placeholders is meaningless -- stop loudly instead of breeding from them
@@ -365,6 +397,12 @@ class DistributedPopulation(Population):
                               "wall_s": time.perf_counter() - t0, "schedule": info["schedule"],
                               "per_rank_units": info["per_rank_units"]}
         return len(todo)
+
+    def _pop_index(self, ind):
+        for i, x in enumerate(self.individuals):
+            if x is ind:
+                return i
+        return -1
 
     def _dispatch(self, todo, exclude=()):
         """One dispatch of ``todo`` over the ranks (not in ``exclude``):
@@ -394,12 +432,14 @@ class DistributedPopulation(Population):
             owner = [-1] * len(units)
         else:
             owner = [allowed[o] for o in lpt_assign(ucost, len(allowed))]
-        table = np.zeros((len(units), 3 + codec.width), np.float64)
+        table = np.zeros((len(units), TABLE_HDR + codec.width), np.float64)
+        pidx = [self._pop_index(ind) for ind in todo]
         for k, (slot, fids) in enumerate(units):
             table[k, 0] = slot
             table[k, 1] = owner[k]
             table[k, 2] = sum(1 << f for f in fids)
-            table[k, 3:] = codec.encode(todo[slot].get_genes())
+            table[k, 3] = pidx[slot]
+            table[k, TABLE_HDR:] = codec.encode(todo[slot].get_genes())
         wd = _fault.watchdog()
         if wd is not None:
             wd.arm("generation {} (rank 0)".format(self.generation_counter))
@@ -424,7 +464,8 @@ class DistributedPopulation(Population):
                                "cnn" if splittable else "other")
         else:
             mine = [(k, make_unit(k)) for k in range(len(units)) if owner[k] == comm.rank]
-        rows = evaluate_units(mine, self.local_evaluator, nfold, comm.rank, self.generation_counter)
+        rows = evaluate_units(mine, self.local_evaluator, nfold, comm.rank, self.generation_counter,
+                              on_take=_announcer(table) if self.verbose and comm.world_size > 1 else None)
         local = np.zeros((len(units), row_width(nfold)), np.float64)
         for k, row in rows.items():
             local[k] = row
@@ -432,6 +473,9 @@ class DistributedPopulation(Population):
         if wd is not None:
             wd.disarm()
         merged = _merge(gathered, units, len(todo), nfold)
+        log = self.event_log
+        if log is not None and comm.world_size > 1:
+            self._log_units(log, gathered, units, todo, table, nfold)
         # ranks to leave out of a retry: owners of units that came back empty, ranks that reported errors
         failed_ranks = set()
         for k in range(len(units)):
@@ -442,6 +486,19 @@ class DistributedPopulation(Population):
         info = {"units": len(units), "schedule": "dynamic" if dynamic else "lpt", "failed_ranks": failed_ranks,
                 "per_rank_units": [int(np.sum(g[:, 0] != ST_NONE)) for g in gathered]}
         return merged, info
+
+    def _log_units(self, log, gathered, units, todo, table, nfold):
+        """One ``evaluation`` event per work unit, from whichever rank returned it."""
+        for k, (slot, fids) in enumerate(units):
+            rank = next((r for r, g in enumerate(gathered) if g[k, 0] != ST_NONE), None)
+            row = gathered[rank][k] if rank is not None else None
+            ok = row is not None and row[0] == ST_OK
+            log.write("evaluation", rank=rank, generation=self.ga_generation, dispatch=self.generation_counter,
+                      i=int(table[k, 3]), genes=todo[slot].get_genes(), folds=list(fids),
+                      status="ok" if ok else ("error" if row is not None else "missing"),
+                      fitness=float(row[1]) if ok else None,
+                      fold_scores=[float(row[3 + f]) for f in fids] if ok else None,
+                      wall_s=float(row[2]) if row is not None else None)
 
     def evaluate_round(self, per_rank, slack=1):
         """One balanced evaluation round: about ``per_rank`` candidates per
@@ -534,8 +591,9 @@ class GentunWorker(object):
     rank 0 until it broadcasts STOP."""
 
     def __init__(self, individual, x_train, y_train, host='localhost', port=5672, user='guest',
-                 password='guest', rabbit_queue='rpc_queue', comm=None, evaluator=None):
+                 password='guest', rabbit_queue='rpc_queue', comm=None, evaluator=None, verbose=True):
         self.individual = individual
+        self.verbose = verbose
         self.x_train = x_train
         self.y_train = y_train
         self.comm = comm if comm is not None else _comm_from_args(host, port)
@@ -576,7 +634,7 @@ class GentunWorker(object):
         codec = GenomeCodec(genome)
 
         def make_unit(k):
-            genes = codec.decode(table[k, 3:])
+            genes = codec.decode(table[k, TABLE_HDR:])
             fids = [f for f in range(nfold) if (int(table[k, 2]) >> f) & 1]
             ind = self.individual(self.x_train, self.y_train, genes=genes, **extra)
             return _Unit(int(table[k, 0]), ind, fids)
@@ -587,7 +645,8 @@ class GentunWorker(object):
             mine = UnitClaimer(comm, "steal/{}".format(generation), n_units, make_unit, kind)
         else:
             mine = [(k, make_unit(k)) for k in range(n_units) if int(table[k, 1]) == comm.rank]
-        rows = evaluate_units(mine, self.evaluator, nfold, comm.rank, generation)
+        rows = evaluate_units(mine, self.evaluator, nfold, comm.rank, generation,
+                              on_take=_announcer(table) if self.verbose else None)
         local = np.zeros((table.shape[0], row_width(nfold)), np.float64)
         for k, row in rows.items():
             local[k] = row
@@ -605,6 +664,19 @@ class GentunWorker(object):
         except KeyboardInterrupt:
             print()
         print("Good bye!")
+
+
+def _announcer(table):
+    """The reference worker's line per job (gentun/worker.py:43), printed when
+    a rank takes a candidate (a candidate split into fold units prints once)."""
+    seen = set()
+
+    def on_take(entry):
+        i = int(table[entry[0], 3])
+        if i not in seen:
+            seen.add(i)
+            print(" [.] Evaluating individual {}".format(i), flush=True)
+    return on_take
 
 
 def _comm_from_args(host, port):

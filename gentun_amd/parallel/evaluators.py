@@ -74,8 +74,8 @@ class LocalBatchEvaluator(SequentialEvaluator):
 
     def __init__(self, device=None, streams=2, cache=False, event_log=None, pop_batch=16, torch_pop=None):
         super(LocalBatchEvaluator, self).__init__(cache=cache, event_log=event_log)
-        # population-batch the torch executor too (TorchPopJob, comparator (a)); default
-        # GENTUN_TORCH_POP=1, else the torch oracle trains one candidate per job
+        # population-batch the torch executor too (TorchPopJob, comparator (a)): off unless
+        # GENTUN_TORCH_POP=1 (or torch_pop=True); otherwise the torch oracle trains one candidate per job
         if torch_pop is None:
             torch_pop = os.environ.get("GENTUN_TORCH_POP", "0") == "1"
         self.torch_pop = bool(torch_pop)

@@ -35,6 +35,8 @@ import time
 import warnings
 
 EXIT_WATCHDOG = 75
+# a search that cannot continue (every evaluation failed): never restarted by supervise()
+EXIT_SEARCH_FAILED = 78
 
 
 def parse_fault(spec=None):
@@ -170,6 +172,8 @@ def supervise(cmd, max_restarts=3, env=None, restart_codes=None):
         rc = subprocess.call(cmd, env=e)
         if rc == 0:
             return 0
+        if rc == EXIT_SEARCH_FAILED:
+            return rc
         if attempt >= max_restarts or (restart_codes is not None and rc not in restart_codes):
             return rc
         warnings.warn("child exited with {}; restart {} of {}".format(rc, attempt + 1, max_restarts))

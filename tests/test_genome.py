@@ -100,3 +100,49 @@ def test_epochs_learning_rate_rules():
         GeneticCnnModel(*args, epochs=(2,), learning_rate=1e-3, device='cpu')
     with pytest.raises(ValueError):
         GeneticCnnModel(*args, epochs=(2, 1), learning_rate=(1e-3,), device='cpu')
+
+
+def test_plot_writes_graph_images(tmp_path):
+    """plot(): the reference writes <name>.png (keras_models.py:41-44); PNG, SVG and DOT here."""
+    import zlib
+    m = GeneticCnnModel(None, None, {'S_1': '111', 'S_2': '0101110011'}, (3, 5), (32, 32, 3), (20, 50),
+                        ((5, 5), (5, 5)), 500, 0.5, 10, device='cpu')
+    png = open(m.plot(str(tmp_path / "net.png")), "rb").read()
+    assert png[:8] == b"\x89PNG\r\n\x1a\n"
+    import struct
+    w, h = struct.unpack(">II", png[16:24])
+    idat = png[png.index(b"IDAT") + 4:png.index(b"IEND") - 8]
+    raw = zlib.decompress(idat)
+    assert len(raw) == h * (w + 1) and w > 100 and h > 100
+    assert 0 in raw[1:] and 255 in raw                                  # ink on a white canvas
+    svg = open(m.plot(str(tmp_path / "net.svg"))).read()
+    # s2 node 3 sums n0 + n1 + n2 through an add node; 12 convs + 2 pools + head
+    assert "s2_n3_add" not in svg and svg.count("<rect") == 1 + svg.count("<text")
+    dot = open(m.plot(str(tmp_path / "net.dot"))).read()
+    for e in ('"s2_n0" -> "s2_n3_add"', '"s2_n1" -> "s2_n3_add"', '"s2_n2" -> "s2_n3_add"', '"s2_n3_add" -> "s2_n3"',
+              '"s1_out" -> "s1_pool"', '"dense1" -> "dropout"'):
+        assert e in dot, e
+
+
+def test_reset_weights_redraws_kernels_keeps_biases():
+    """reset_weights (keras_models.py:120-125): kernels re-drawn, biases kept."""
+    import torch
+    from gentun_amd.utils.data import make_cifar_like
+    x, y = make_cifar_like(n=48, seed=1)
+    m = GeneticCnnModel(x, y, {'S_1': '1', 'S_2': '1'}, (2, 2), x.shape[1:], (4, 4), ((3, 3), (3, 3)), 8, 0.5, 10,
+                        nfold=2, epochs=(1,), learning_rate=(1e-2,), batch_size=16, backend="torch",
+                        device=torch.device("cpu"), reset="all")
+    assert m.reset_weights() == 0                     # nothing trained yet
+    m.cross_validate()
+    job = m.jobs[0]
+    views = job._views()
+    before = {k: v.clone() for k, v in views.items()}
+    assert m.reset_weights() == 1
+    after = job._views()
+    kinds = {name: kind for name, _, kind, _ in job.shapes}
+    for name, kind in kinds.items():
+        if kind == "glorot":
+            assert not torch.equal(before[name], after[name]), name
+        else:
+            assert torch.equal(before[name], after[name]), name
+    assert any(before[n].abs().sum() > 0 for n, k in kinds.items() if k == "zero")    # trained biases kept

@@ -54,7 +54,11 @@ def _worker(rank, port, out):
         dist.destroy_process_group()
 
 
-def test_two_rank_hip_data_parallel_matches_single_process():
+@pytest.mark.parametrize("adam_overlap", ["0", "1"])
+def test_two_rank_hip_data_parallel_matches_single_process(adam_overlap, monkeypatch):
+    # GENTUN_ADAM_OVERLAP=1 puts per-layer conv updates inside the backward loop; with X5 the
+    # executor must turn that off, or each rank would update from its own partial gradient
+    monkeypatch.setenv("GENTUN_ADAM_OVERLAP", adam_overlap)
     single, sres = _train(_job())
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

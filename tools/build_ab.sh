@@ -1,10 +1,10 @@
 #!/bin/bash
 # Alternative build of the kernel library for same-box A/B runs (GENTUN_HIP_LIB=<path>):
-#   bash tools/build_ab.sh NAME -DMACRO=VALUE ...   ->  gentun_amd/_native/ab/NAME.so
+#   bash tools/build_ab.sh NAME -DMACRO=VALUE ...   ->  ab_libs/NAME.so
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-mkdir -p build/ab_$name gentun_amd/_native/ab
+mkdir -p build/ab_$name ab_libs
 objs=()
 for f in csrc/hip/*.hip; do
   o=build/ab_$name/$(basename $f).o
@@ -12,5 +12,5 @@ for f in csrc/hip/*.hip; do
   objs+=($o)
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o gentun_amd/_native/ab/$name.so "${objs[@]}"
-echo gentun_amd/_native/ab/$name.so
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ab_libs/$name.so "${objs[@]}"
+echo ab_libs/$name.so

@@ -7,6 +7,9 @@ generations population-batched. Resumable: ``--resume`` continues from
 back), so a run longer than one GPU session is split over calls.
 
 usage: python tools/ga_run.py --gens 20 --ckpt DIR [--resume] [--data hard] [--fold-reset all]
+                             [--space deep [--kernels 20,50,100] [--batch-norm]]
+``--space deep`` is BASELINE config 4's search space: S=(3,4,5), 5x5 stage
+convs, kernels (20,50,100) unless ``--kernels`` overrides them.
 Prints one JSON line: best categorical / binary val-acc per generation.
 """
 import argparse
@@ -26,6 +29,9 @@ ap.add_argument("--data", choices=("hard", "glyph"), default="hard")
 ap.add_argument("--fold-reset", choices=("all", "kernels"), default="all")
 ap.add_argument("--pop-batch", type=int, default=32)
 ap.add_argument("--seed", type=int, default=1234)
+ap.add_argument("--space", choices=("default", "deep"), default="default")
+ap.add_argument("--kernels", default=None, help="kernels per stage, e.g. 20,50,100")
+ap.add_argument("--batch-norm", action="store_true")
 ap.add_argument("--time-budget", type=float, default=0.0, help="stop after the generation that passes this many s")
 args = ap.parse_args()
 
@@ -39,10 +45,13 @@ from gentun_amd.utils.data import make_cifar_hard, make_cifar_like  # noqa: E402
 
 dev = torch.device("cuda", 0)
 x, y = (make_cifar_hard if args.data == "hard" else make_cifar_like)(n=10000, seed=0)
-extra = dict(nodes=(3, 5), input_shape=(32, 32, 3), kernels_per_layer=(20, 50), kernel_sizes=((5, 5), (5, 5)),
+nodes, kernels = ((3, 4, 5), (20, 50, 100)) if args.space == "deep" else ((3, 5), (20, 50))
+if args.kernels:
+    kernels = tuple(int(k) for k in args.kernels.split(","))
+extra = dict(nodes=nodes, input_shape=(32, 32, 3), kernels_per_layer=kernels, kernel_sizes=((5, 5),) * len(nodes),
              dense_units=500, dropout_probability=0.5, classes=10, nfold=5, epochs=(20, 4, 1),
              learning_rate=(1e-3, 1e-4, 1e-5), batch_size=32, dtype="fp32", loss="bce_compat", seed=args.seed,
-             reset=args.fold_reset, batching="keras")
+             reset=args.fold_reset, batching="keras", batch_norm=args.batch_norm)
 ev = LocalBatchEvaluator(device=dev, streams=1, pop_batch=args.pop_batch)
 comm = LocalComm()
 latest = os.path.join(args.ckpt, "latest.json")
@@ -73,6 +82,8 @@ wall = sum(h["wall_s"] for h in ga.history)
 print(json.dumps({"generations": len(ga.history), "evals": evals, "eval_wall_s": round(wall, 1),
                   "candidates_per_hour": round(3600 * evals / wall, 1) if wall else None,
                   "data": args.data, "fold_reset": args.fold_reset, "population": args.pop,
+                  "space": "S=({}) kernels ({})".format(",".join(map(str, nodes)), ",".join(map(str, kernels))),
+                  "batch_norm": args.batch_norm,
                   "best_val_cat_acc_by_gen": [round(h.get("best_cat_acc") or 0.0, 4) for h in ga.history],
                   "best_val_binary_acc_by_gen": [round(h["best_fitness"], 5) for h in ga.history],
                   "evals_by_gen": [h["evals"] for h in ga.history],
