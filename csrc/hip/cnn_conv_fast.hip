@@ -1329,15 +1329,22 @@ static int g_probe = 0;
     return (int)hipGetLastError();                                                                      \
   }
 
-// 1: the S=(3,5) s2 input-conv dgrad (5x5, 50 -> 20) with one co tile per wave and 4 pixel groups each
+// The S=(3,5) s2 input-conv dgrad (5x5, 50 -> 20) with one co tile per wave and 4 pixel groups each
 // instead of the packed tile's 2 tiles x 2 groups: 33 % more MFMAs but half the weight loads per MFMA;
 // same-box A/B 126 -> 114 us per launch at 25 groups, population step -1.6 % (profiles/conv_s2in_dgrad_ct1_ab_r3.txt).
-// Off by default: with it, tests/test_hip_dp.py's 2-rank data-parallel trajectory drifted 3.6e-4 (relative) from
-// the single-process one, past the test's 1e-4 bound (the packed tile's nine-term products: within it) -- not
-// understood yet, so the measured-safe kernel stays the default
-#ifndef GT_S2IN_DGRAD_CT1
-#define GT_S2IN_DGRAD_CT1 0
-#endif
+// Runtime switch (GENTUN_S2IN_CT1, gt_conv_set_s2in_ct1) so both variants are compared against the fp64
+// oracle on one launch in one process (tests/test_hip_fp32.py::test_s2in_dgrad_variants).
+static int g_s2in_ct1 = -1;
+static bool s2in_ct1_on() {
+  if (g_s2in_ct1 < 0) g_s2in_ct1 = std::getenv("GENTUN_S2IN_CT1") ? std::atoi(std::getenv("GENTUN_S2IN_CT1")) : 0;
+  return g_s2in_ct1 != 0;
+}
+extern "C" int gt_conv_set_s2in_ct1(int on) {
+  s2in_ct1_on();
+  const int old = g_s2in_ct1;
+  g_s2in_ct1 = on;
+  return old;
+}
 
 // fp32 register-direct epilogue in the tile kernel (A/B: GENTUN_F32_REGEPI=0 / 1, gt_conv_set_regepi):
 // no LDS output tile, no second barrier, the pool from lane shuffles
@@ -1433,9 +1440,7 @@ extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
     // (a packed tile here needs every wave to own all 4 co tiles: 2x the weight traffic per MFMA,
     // measured 20 % slower than the 2 + 2 split -- profiles/conv_f32_packed_tile_ab_r2.txt)
     CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
-#if GT_S2IN_DGRAD_CT1
-    if (CONV_FAST_MATCH(5, 5, 7, 16, 8, 2, 3)) CONV_FAST_LAUNCH_CT1(5, 5, 7, 16, 8, 2, 3, 4)
-#endif
+    if (s2in_ct1_on() && CONV_FAST_MATCH(5, 5, 7, 16, 8, 2, 3)) CONV_FAST_LAUNCH_CT1(5, 5, 7, 16, 8, 2, 3, 4)
     CONV_FAST_CASE_F32_PK(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
     // deep S=(3,4,5) space, kernels (20, 50, 100): stage 3 at 8x8, one image per workgroup
     CONV_FAST_CASE_F32_NARROW(5, 5, 7, 8, 8, 7, 13, 7)   // s3 input conv (50 -> 100): one co tile per wave, 7 waves

@@ -158,6 +158,8 @@ def lib():
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
         L.gt_conv_set_nwv.argtypes = [I]
+        L.gt_conv_set_s2in_ct1.restype = I
+        L.gt_conv_set_s2in_ct1.argtypes = [I]
         L.gt_conv_set_nwv.restype = I
         if os.environ.get("GENTUN_CONV_NWV"):
             L.gt_conv_set_nwv(int(os.environ["GENTUN_CONV_NWV"]))

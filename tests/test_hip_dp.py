@@ -4,9 +4,19 @@ GPU 0 -- the multi-GPU path is RCCL with the same code) each train rows
 gradients (conv weight gradients after their split-K reduce, dW1 from the
 dense weight-gradient kernel in gradient-only mode, dW2 / db2 / db1) are
 summed by one all-reduce, and the identical optimizer step follows. The
-trajectory equals the single-process run of the same job (fp32 up to the
-gradient summation order; dropout keyed by the full-batch row, Keras short
-last batch normalised by the full batch; SGD-momentum -- see _job)."""
+trajectory equals the single-process run of the same job up to the gradient
+summation order (dropout keyed by the full-batch row, Keras short last batch
+normalised by the full batch; SGD-momentum -- see _job).
+
+The bound is derived, not ad hoc: data parallelism changes only the ORDER in
+which every gradient is summed (two half-batch sums, then the all-reduce).
+The reference scale for that is the same single-process job with its conv
+weight gradients summed in a different split-K order (``GENTUN_WGRAD_SPLITS``:
+another split count = another fp32 summation order of the same terms, nothing
+else changes). The data-parallel trajectory must stay within a small multiple
+of that reordering drift (ReLU decisions near zero turn rounding-level
+differences into larger parameter differences over the steps; both drifts see
+the same amplification)."""
 
 import os
 import socket
@@ -18,6 +28,9 @@ import torch
 import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
+
+# data-parallel drift allowed, in units of the single-process reordering drift (see module docstring)
+DP_ORDER_FACTOR = 8.0
 
 
 def _job(dp_group=None):
@@ -33,6 +46,17 @@ def _job(dp_group=None):
     cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-2,), batch_size=32, dtype="fp32", loss="bce_compat",
                         reset="all", optimizer="sgd", momentum=0.9, dp_group=dp_group)
     return E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg, torch.device("cuda", 0))
+
+
+def _reordered_single():
+    """The single-process run with every specialised conv wgrad summed in another split order."""
+    from gentun_amd.ops import cnn_kernels as K
+    old = K.WGRAD_FAST_SPLITS
+    K.WGRAD_FAST_SPLITS = 4
+    try:
+        return _train(_job())
+    finally:
+        K.WGRAD_FAST_SPLITS = old
 
 
 def _train(job):
@@ -54,12 +78,26 @@ def _worker(rank, port, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("adam_overlap", ["0", "1"])
-def test_two_rank_hip_data_parallel_matches_single_process(adam_overlap, monkeypatch):
+@pytest.mark.parametrize("adam_overlap,ct1", [("0", "0"), ("1", "0"), ("0", "1")])
+def test_two_rank_hip_data_parallel_matches_single_process(adam_overlap, ct1, monkeypatch):
     # GENTUN_ADAM_OVERLAP=1 puts per-layer conv updates inside the backward loop; with X5 the
-    # executor must turn that off, or each rank would update from its own partial gradient
+    # executor must turn that off, or each rank would update from its own partial gradient.
+    # ct1: the stage-2 input-conv dgrad variant with one co tile per wave (GENTUN_S2IN_CT1).
+    from gentun_amd.ops import cnn_kernels as K
     monkeypatch.setenv("GENTUN_ADAM_OVERLAP", adam_overlap)
+    monkeypatch.setenv("GENTUN_S2IN_CT1", ct1)              # the spawned ranks read it at first launch
+    old = K.lib().gt_conv_set_s2in_ct1(int(ct1))
+    try:
+        _compare()
+    finally:
+        K.lib().gt_conv_set_s2in_ct1(old)
+
+
+def _compare():
     single, sres = _train(_job())
+    again, _ = _train(_job())
+    assert torch.equal(single, again)                       # the executor itself is deterministic
+    reorder, _ = _reordered_single()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -68,7 +106,11 @@ def test_two_rank_hip_data_parallel_matches_single_process(adam_overlap, monkeyp
         r0 = torch.load(os.path.join(d, "rank0.pt"), weights_only=True)
         r1 = torch.load(os.path.join(d, "rank1.pt"), weights_only=True)
     assert torch.equal(r0["flat"], r1["flat"])              # identical optimizer steps on every rank
-    scale = single.abs().max()
-    assert (r0["flat"] - single).abs().max() <= 1e-4 * scale, (r0["flat"] - single).abs().max()
+    scale = single.abs().max().item()
+    d_dp = (r0["flat"] - single).abs().max().item() / scale
+    d_order = (reorder - single).abs().max().item() / scale
+    print("[dp] relative drift: data-parallel {:.2e}, single-process split reorder {:.2e}".format(d_dp, d_order))
+    assert d_order > 0                                      # the reorder really changed the summation
+    assert d_dp <= DP_ORDER_FACTOR * max(d_order, 2.0 ** -23), (d_dp, d_order)
     for a, b in zip(r0["cat"], [r["categorical_accuracy"] for r in sres]):
         assert np.allclose(a, b, atol=0.02)

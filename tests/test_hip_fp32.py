@@ -436,3 +436,106 @@ def test_adam_segments_fp32_planes(tiled):
     w = p.view(G, co, kh, kw, ci)
     assert torch.equal(bfT, _split(w.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous()))
     del ctypes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["write_acc_mask", "unpool"])
+def test_s2in_dgrad_variants(mode):
+    """The S=(3,5) stage-2 input-conv data gradient (5x5, 50 -> 20, 16x16) at
+    the bench launch (25 groups x batch 32) in both kernel variants: the
+    packed last co tile (default: channels 16-19 as 9-term plane rows) and one
+    co tile per wave (GENTUN_S2IN_CT1: six-term products everywhere).
+
+    * both are fp32-level against the fp64 oracle (<= TOL of the output range,
+      reported next to torch fp32's own error);
+    * channels 0-15 run the SAME k order and MFMA sequence in both -> bitwise
+      equal (an indexing fault or race at a tile edge would break this);
+    * every variant is deterministic launch to launch (bitwise)."""
+    Km = K()
+    L = Km.lib()
+    torch.manual_seed(21)
+    G, B, H, W, k = 25, 32, 16, 16, 5
+    cin, cout = 20, 50                       # forward conv: 20 -> 50; its dgrad maps dz (50) to dx (20)
+    cinp, coutp = 24, 56
+    w = torch.randn(G, cout, cin, k, k) / math.sqrt(cout * k * k)
+    dz = torch.randn(G, B, cout, H, W)
+    ref = torch.stack([torch.nn.grad.conv2d_input((B, cin, H, W), w[g].double(), dz[g].double(), padding=2)
+                       for g in range(G)])                                    # [G, B, cin, H, W]
+    r32 = torch.stack([torch.nn.grad.conv2d_input((B, cin, H, W), w[g], dz[g], padding=2) for g in range(G)])
+    wp = torch.stack([pack_w(w[g], coutp, cinp) for g in range(G)]).to(DEV)
+    wT = _split(wp.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous()).contiguous()
+    dz_p = torch.stack([nhwc_pad(dz[g], coutp) for g in range(G)]).to(DEV).contiguous()
+    prev = torch.randn(G, B, H, W, cinp, device=DEV)
+    prev[..., cin:] = 0
+    pmask = torch.randn(G, B, H, W, cinp, device=DEV)
+    pm = torch.randint(0, 8, (G * B, H, W, cinp), dtype=torch.uint8, device=DEV)
+    sel = (torch.arange(G, dtype=torch.int32, device=DEV) % 2).contiguous()
+    outs = {}
+    for variant in (0, 1, 0, 1):
+        o0 = torch.zeros(G, B, H, W, cinp, device=DEV)
+        o1 = prev.clone()
+        x0 = torch.full((G, B, 2 * H, 2 * W, cinp), 4.0, device=DEV)
+        x1 = torch.full((G, B, 2 * H, 2 * W, cinp), 6.0, device=DEV)
+        a = Km.ConvArgs()
+        a.inp[0] = dz_p.data_ptr()
+        if mode == "unpool":
+            rows = torch.tensor([[g, 1, 1 | (1 << 25), 0] for g in range(G)], dtype=torch.int32, device=DEV)
+            a.out[0] = o0.data_ptr()
+            a.pool_y, a.pool_mask, a.unpool_x1, a.unpool_sel = x0.data_ptr(), pm.data_ptr(), x1.data_ptr(), \
+                sel.data_ptr()
+        else:
+            rows = torch.tensor([[g, 1, 0b11 | (0b10 << 8) | (0b10 << 16), 0] for g in range(G)], dtype=torch.int32,
+                                device=DEV)
+            a.out[0], a.out[1] = o0.data_ptr(), o1.data_ptr()
+            a.out_mask[1] = pmask.data_ptr()
+        a.gtab, a.ngroups, a.relu, a.epi_bf16 = rows.data_ptr(), G, 0, 0
+        a.w, a.bias, a.wps = wT.data_ptr(), 0, wT[0].numel()
+        a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, coutp, cinp, k, k
+        a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cin
+        old = L.gt_conv_set_s2in_ct1(variant)
+        try:
+            Km.check(L.gt_conv_fwd(a, stream()), "dgrad")
+            torch.cuda.synchronize()
+        finally:
+            L.gt_conv_set_s2in_ct1(old)
+        got = (x0, x1) if mode == "unpool" else (o0, o1)
+        if variant in outs:                                  # second launch of the same variant: bitwise
+            for t0, t1 in zip(outs[variant], got):
+                assert torch.equal(t0, t1), ("nondeterministic", variant)
+        outs[variant] = got
+    e32 = rel(r32, ref)
+    if mode == "unpool":
+        # un-pooled gradient: value at the argmax cell of each 2x2 cell when bit 2 (max > 0) is set
+        mk = pm.view(G, B, H, W, cinp)[..., :cin].long().cpu()
+        refn = ref.permute(0, 1, 3, 4, 2)                                       # [G, B, H, W, cin]
+        for variant in (0, 1):
+            x0, x1 = outs[variant]
+            for g in range(G):
+                dst = (x1 if sel[g].item() else x0)[g].cpu().double()[..., :cin]        # [B, 2H, 2W, cin]
+                cell = dst.view(B, H, 2, W, 2, cin).permute(0, 1, 3, 2, 4, 5).reshape(B, H, W, 4, cin)
+                want = torch.zeros(B, H, W, 4, cin, dtype=torch.float64)
+                hit = (mk[g] & 4) > 0
+                idx = (mk[g] & 3)
+                want.scatter_(3, idx.unsqueeze(3), torch.where(hit, refn[g], torch.zeros_like(refn[g])).unsqueeze(3))
+                e = ((cell - want).abs().max() / refn.abs().max()).item()
+                assert e < TOL, (variant, g, e)
+            report("s2in dgrad unpool variant {}".format(variant), e, e32)
+        other = (outs[0][0] != 4.0) | (outs[0][1] != 6.0)
+        assert other.any()
+        c0 = [t.view(G, B, 2 * H, 2 * W, cinp)[..., :16] for t in outs[0]]
+        c1 = [t.view(G, B, 2 * H, 2 * W, cinp)[..., :16] for t in outs[1]]
+        assert all(torch.equal(a0, a1) for a0, a1 in zip(c0, c1))
+        return
+    refm = (ref + prev[..., :cin].permute(0, 1, 4, 2, 3).double().cpu()) * \
+        (pmask[..., :cin] > 0).permute(0, 1, 4, 2, 3).cpu()
+    for variant in (0, 1):
+        o0, o1 = outs[variant]
+        e0 = rel(o0[..., :cin].permute(0, 1, 4, 2, 3), ref)
+        e1 = rel(o1[..., :cin].permute(0, 1, 4, 2, 3), refm)
+        report("s2in dgrad variant {} (write / acc+mask)".format(variant), max(e0, e1), e32)
+        assert e0 < TOL and e1 < TOL, (variant, e0, e1)
+        assert (o0[..., cin:] == 0).all()                                # padding channels stay zero
+    for i in range(2):
+        assert torch.equal(outs[0][i][..., :16], outs[1][i][..., :16])   # same k order: bitwise
+        d = (outs[0][i][..., 16:cin] - outs[1][i][..., 16:cin]).abs().max().item()
+        assert d <= 4 * e32 * ref.abs().max().item() + 1e-30, d         # 9- vs 6-term: rounding only
