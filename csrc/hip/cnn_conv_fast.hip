@@ -25,6 +25,7 @@
 // fan-out (accumulate, ReLU mask) for the data gradient.
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <type_traits>
 
@@ -40,6 +41,18 @@
 
 #ifndef GT_F32_NO_BPIPE
 #define GT_F32_NO_BPIPE 0      // 1: fp32 conv main loop without the patch-fragment pipeline (A/B builds)
+#endif
+
+// 1: the unrolled tile-kernel k loop takes each k-step's patch offset from per-lane arithmetic
+// (no LDS table lookup + lgkmcnt(0) drain in the middle of the MFMA stream); 0: the LDS coff table.
+// Measured 4-7 % SLOWER on the stage-2 3x3 fwd / dgrad (profiles/conv_f32_regoff_pf_ab_r4.txt), as was a
+// 3- or 4-deep weight prefetch (GT_F32_PFM): both stay A/B builds
+#ifndef GT_F32_REGOFF
+#define GT_F32_REGOFF 0
+#endif
+// weight (A operand) prefetch depth of the fp32 tile kernel, in k-steps (3 planes each)
+#ifndef GT_F32_PFM
+#define GT_F32_PFM 2
 #endif
 
 // LDS bytes of one launch: the patch (NPL bf16 planes) or the output tile
@@ -163,7 +176,7 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int WC = NT / CT;                       // waves along co
   constexpr int WP = NWV / WC;                        // waves along pixels
   constexpr int PG = NPG / WP;                      // pixel groups per wave
-  constexpr int PFM = PREC ? 2 : 4;                 // weight prefetch depth (k-steps; 3 planes each in prec 1)
+  constexpr int PFM = PREC ? (NKS > 64 ? 2 : GT_F32_PFM) : 4;   // weight prefetch depth (k-steps; 3 planes each in prec 1)
   constexpr int PF = NKS < PFM ? NKS : PFM;
   static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == NWV, "tile shape");
   static_assert(!PK || (PREC == 1 && WC == 1), "packed last tile: fp32, every wave owns all co tiles");
@@ -181,6 +194,9 @@ conv_fast_kernel(ConvArgs a) {
   const int nbx = gridDim.x;
   const int total = nbx * gridDim.y;
   int lin = blockIdx.y * nbx + blockIdx.x;
+  if (PREC && a.stagger > 0 &&
+      (a.stagger_lo >= 0 ? (lin >= a.stagger_lo && lin < a.stagger_hi) : (((lin >> 3) & 1) == 1 && lin < a.stagger_hi)))
+    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(32);     // 32 x 64 = 2048 cycles each
   if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
   const int by = lin / nbx, bx = lin - by * nbx;
   const int nband = (a.H + TH - 1) / TH;
@@ -371,8 +387,14 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
     for (int h = 0; h < PG; ++h) acc[t][h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  // chunk c of the reduction -> patch offset of its (kh, kw, cb) (the coff table, computed in registers)
+  auto koff = [&](int s) {
+    const int c = s * 4 + kq;
+    const int kk = c / NCBI, cb = c - kk * NCBI;
+    return c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
+  };
   auto load_b = [&](int s, uint4 (*dst)[NPL]) {
-    const uint4* pb = patch + lbase + gbase + coff[s * 4 + kq];
+    const uint4* pb = patch + lbase + gbase + ((GT_F32_REGOFF && PREC && NKS <= 64) ? koff(s) : coff[s * 4 + kq]);
 #pragma unroll
     for (int h = 0; h < PG; ++h) {
       const int p = h * 16;                        // relative to the wave's first group
@@ -1333,10 +1355,13 @@ static int g_probe = 0;
 // instead of the packed tile's 2 tiles x 2 groups: 33 % more MFMAs but half the weight loads per MFMA;
 // same-box A/B 126 -> 114 us per launch at 25 groups, population step -1.6 % (profiles/conv_s2in_dgrad_ct1_ab_r3.txt).
 // Runtime switch (GENTUN_S2IN_CT1, gt_conv_set_s2in_ct1) so both variants are compared against the fp64
-// oracle on one launch in one process (tests/test_hip_fp32.py::test_s2in_dgrad_variants).
+// oracle on one launch in one process (tests/test_hip_fp32.py::test_s2in_dgrad_variants): both 1.3e-6 of
+// the output range (torch fp32: 7.1e-7), channels 0-15 bitwise equal, deterministic; the 2-rank DP
+// trajectory stays within the derived summation-order bound (tests/test_hip_dp.py). On by default since
+// round 4 (profiles/conv_s2in_dgrad_ct1_r4.txt).
 static int g_s2in_ct1 = -1;
 static bool s2in_ct1_on() {
-  if (g_s2in_ct1 < 0) g_s2in_ct1 = std::getenv("GENTUN_S2IN_CT1") ? std::atoi(std::getenv("GENTUN_S2IN_CT1")) : 0;
+  if (g_s2in_ct1 < 0) g_s2in_ct1 = std::getenv("GENTUN_S2IN_CT1") ? std::atoi(std::getenv("GENTUN_S2IN_CT1")) : 1;
   return g_s2in_ct1 != 0;
 }
 extern "C" int gt_conv_set_s2in_ct1(int on) {
@@ -1422,7 +1447,29 @@ static bool pk_ok(const ConvArgs* a, int nt) {
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
   }
 
-extern "C" int gt_conv_fast(const ConvArgs* a, hipStream_t stream) {
+// start-phase stagger of the fp32 tile kernel (see ConvArgs::stagger): GENTUN_CONV_STAGGER="n[:lo:hi]"
+static int g_stagger[3] = {-1, 256, 512};
+extern "C" int gt_conv_set_stagger(int n, int lo, int hi) {
+  const int old = g_stagger[0];
+  g_stagger[0] = n; g_stagger[1] = lo; g_stagger[2] = hi;
+  return old;
+}
+static void stagger_init() {
+  if (g_stagger[0] >= 0) return;
+  g_stagger[0] = 0;
+  if (const char* e = std::getenv("GENTUN_CONV_STAGGER")) {
+    int n = 0, lo = 256, hi = 512;
+    if (std::sscanf(e, "%d:%d:%d", &n, &lo, &hi) >= 1) { g_stagger[0] = n; g_stagger[1] = lo; g_stagger[2] = hi; }
+  }
+}
+
+extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
+  stagger_init();
+  ConvArgs lc = *a_in;
+  lc.stagger = g_stagger[0];
+  lc.stagger_lo = g_stagger[1];
+  lc.stagger_hi = g_stagger[2];
+  const ConvArgs* a = &lc;
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
   if (a->prec == 1) {
     // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs

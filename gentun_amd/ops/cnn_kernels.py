@@ -37,7 +37,7 @@ class ConvArgs(C.Structure):
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
                 ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long),
                 ("cbb", I), ("pool_y", P), ("pool_mask", P), ("unpool_x1", P), ("unpool_sel", P),
-                ("cout_real", I)]
+                ("cout_real", I), ("stagger", I), ("stagger_lo", I), ("stagger_hi", I)]
 
 
 class WgradArgs(C.Structure):
