@@ -321,6 +321,14 @@ __global__ void __launch_bounds__(256) dense_fwd_stream_kernel(DenseFwdArgs a) {
   }
 }
 
+// plane q (0..2) of the exact split of p (q = 0: the bf16 rounding)
+__device__ __forceinline__ void split3(float p, uint16_t* h) {
+  h[0] = f2bf(p);
+  const float r1 = p - bf2f(h[0]);
+  h[1] = f2bf(r1);
+  h[2] = f2bf(r1 - bf2f(h[1]));
+}
+
 // ---------------------------------------------------------------------------
 struct HeadArgs {
   const void* h;           // [G][B][Up] (post-dropout activations), bf16 or fp32 (prec)
@@ -343,6 +351,8 @@ struct HeadArgs {
   int prec;
   const int* valid;        // [steps][G] real rows of each training batch (Keras short batch) or null = B
   const int* valid_norm;   // X5: [steps][G] real rows of the FULL batch (loss mean over all ranks' rows) or null
+  uint16_t* dHp;           // optional [NPL][G][B][Up] bf16 planes of dH (prec 1: the exact 3-way split; prec 0:
+                           // the bf16 rounding), written once here so dense_dgrad does not re-split per wave
 };
 
 #define HEAD_MAXB 64
@@ -451,7 +461,20 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(HeadArgs a) {
       float s = 0.f;
       for (int c = 0; c < C; ++c) s += dzs[b * C + c] * w2s[j * C + c];
       const float d = hsl[b][j] > 0.f ? s * a.drop_scale : 0.f;
-      if (u0 + j < Up) a.dH[((long)g * B + b) * Up + u0 + j] = d;
+      if (u0 + j < Up) {
+        const long o = ((long)g * B + b) * Up + u0 + j;
+        a.dH[o] = d;
+        if (a.dHp) {
+          if (a.prec) {
+            uint16_t hq[3];
+            split3(d, hq);
+            const long ps = (long)a.G * B * Up;
+            a.dHp[o] = hq[0]; a.dHp[ps + o] = hq[1]; a.dHp[2 * ps + o] = hq[2];
+          } else {
+            a.dHp[o] = f2bf(d);
+          }
+        }
+      }
       sb += d;
     }
     colsum[q][j] = sb;
@@ -491,6 +514,7 @@ struct DenseDgradArgs {
   const int* unpool_sel;        // [G]
   int Hs, Ws, Cp;
   const float* w1;              // fp32 master W1 [G][Fp][Up]: streaming kernel (null: the copy + LDS transpose)
+  const uint16_t* dHp;          // optional: head_bwd's bf16 planes of dH [NPL][G][B][Up] -> dense_dgrad_stream2
 };
 
 // dx (or, with an unpool mask, the fused pool backward) of one 16-feature x
@@ -667,6 +691,85 @@ __global__ void __launch_bounds__(256) dense_dgrad_stream_kernel(DenseDgradArgs 
   dense_dgrad_epilogue<PREC>(a, g, f_t, b0, acc, lane);
 }
 
+// Data gradient v2 (the default when head_bwd wrote the dH planes): every
+// wave carries TWO 16-feature tiles (32 features) and takes dH as the
+// pre-split bf16 planes head_bwd stored once, instead of loading fp32 dH and
+// splitting it again in every wave of every workgroup (the v1 kernel spent 2/3
+// of its vector instructions on that). Per k-step a wave issues two W1 row
+// loads (split in registers) and 2 x NPL plane loads for 2 x 2 x 6 MFMAs. Same
+// k-step order and the same split values as dense_dgrad_stream_kernel: dx is
+// bit-identical. Grid (Fp/128, ceil(B/32), G), XCD-grouped.
+template <int PREC>
+__global__ void __launch_bounds__(256) dense_dgrad_stream2_kernel(DenseDgradArgs a) {
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  int bx, g;
+  xcd_tile(bx, g);
+  const int f_t = bx * 128 + wave * 32;
+  const int b0 = blockIdx.y * 32;
+  const float* wrow[2];
+  bool fok[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int fa = f_t + 16 * m + l16;
+    fok[m] = fa < a.Fp;
+    wrow[m] = a.w1 + ((long)g * a.Fp + (fok[m] ? fa : 0)) * a.Up;
+  }
+  const long ps = (long)a.G * a.B * a.Up;               // plane stride of dHp
+  const int br[2] = {b0 + l16, b0 + 16 + l16};
+  const uint16_t* hp[2];
+  bool bok[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bok[h] = br[h] < a.B;
+    hp[h] = a.dHp + ((long)g * a.B + (bok[h] ? br[h] : 0)) * a.Up;
+  }
+  const int nchunks = a.Up >> 3;
+  const int nks = (nchunks + 3) >> 2;
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) acc[m][0] = acc[m][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float rw[2][2][8];
+  uint4 rh[2][2][NPL];
+  const uint4* zero4 = reinterpret_cast<const uint4*>(gt_zero8);
+  auto load = [&](int j, int buf) {
+    const int c = 4 * j + kq;
+    const bool cok = c < nchunks;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) ld8_raw(wrow[m] + c * 8, cok && fok[m], rw[buf][m]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int p = 0; p < NPL; ++p)
+        rh[buf][h][p] = *((cok && bok[h]) ? reinterpret_cast<const uint4*>(hp[h] + p * ps + c * 8) : zero4);
+  };
+  auto step = [&](int buf) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      uint4 af[NPL];
+      planes8<PREC>(rw[buf][m], af);
+      acc[m][0] = mfma_np<NPL>(af, rh[buf][0], acc[m][0]);
+      acc[m][1] = mfma_np<NPL>(af, rh[buf][1], acc[m][1]);
+    }
+  };
+  load(0, 0);                              // (unconditional loads, ordered: see dense_fwd_stream_kernel)
+  __builtin_amdgcn_sched_barrier(0);
+  load(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
+  for (int j = 0; j < nks; j += 2) {
+    step(0);
+    __builtin_amdgcn_sched_barrier(0);
+    load(j + 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    step(1);
+    __builtin_amdgcn_sched_barrier(0);
+    load(j + 3, 1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) dense_dgrad_epilogue<PREC>(a, g, f_t + 16 * m, b0, acc[m], lane);
+}
+
 // ---------------------------------------------------------------------------
 struct DenseWgradAdamArgs {
   const void* x;       // [G][B][Fp] bf16 or fp32 (prec)
@@ -836,13 +939,6 @@ struct AdamSeg {
   long pstride_bf, pstride_bfT;   // plane strides (elements)
 };
 
-// plane q (0..2) of the exact split of p (q = 0: the bf16 rounding)
-__device__ __forceinline__ void split3(float p, uint16_t* h) {
-  h[0] = f2bf(p);
-  const float r1 = p - bf2f(h[0]);
-  h[1] = f2bf(r1);
-  h[2] = f2bf(r1 - bf2f(h[1]));
-}
 
 #define ADAM_TK 64
 
@@ -933,7 +1029,21 @@ static bool dense_stream_on() {
   return g_dense_stream != 0;
 }
 
+// A/B: GENTUN_DENSE_DGRAD2=0 keeps the v1 streaming data gradient even when the dH planes exist
+static int g_dgrad2 = -1;
+static bool dgrad2_on() {
+  if (g_dgrad2 < 0) g_dgrad2 = std::getenv("GENTUN_DENSE_DGRAD2") ? std::atoi(std::getenv("GENTUN_DENSE_DGRAD2")) : 1;
+  return g_dgrad2 != 0;
+}
+
 extern "C" {
+
+int gt_dense_set_dgrad2(int on) {
+  dgrad2_on();
+  const int old = g_dgrad2;
+  g_dgrad2 = on;
+  return old;
+}
 
 int gt_dense_set_stream(int on) {
   dense_stream_on();
@@ -984,6 +1094,12 @@ int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
     return -1;
   if (a->Up % 8) return -1;
   if (a->prec != 0 && a->prec != 1) return -1;
+  if (a->w1 && a->dHp && dense_stream_on() && dgrad2_on()) {
+    dim3 grid2((a->Fp + 127) / 128, (a->B + 31) / 32, a->G);
+    if (a->prec) hipLaunchKernelGGL(dense_dgrad_stream2_kernel<1>, grid2, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL(dense_dgrad_stream2_kernel<0>, grid2, dim3(256), 0, stream, *a);
+    return (int)hipGetLastError();
+  }
   dim3 grid((a->Fp + 63) / 64, (a->B + 31) / 32, a->G);
   if (a->w1 && dense_stream_on()) {
     if (a->prec) hipLaunchKernelGGL(dense_dgrad_stream_kernel<1>, grid, dim3(256), 0, stream, *a);

@@ -259,6 +259,8 @@ class HipPopJob(FoldJob):
         self.Up = round_up(p0.dense_units, 64)
         self.hdrop = torch.zeros((Q, B, self.Up), dtype=self.adt, device=dev)
         self.dH = torch.zeros((Q, B, self.Up), dtype=torch.float32, device=dev)
+        # bf16 planes of dH written by head_bwd, read by the dense data gradient (no per-wave re-split)
+        self.dHp = torch.zeros((self.npl, Q, B, self.Up), dtype=torch.int16, device=dev)
         self.dz_head = torch.zeros((Q, B, self.classes), dtype=torch.float32, device=dev)
         self.plog = torch.zeros((Q, self.Up // 16, B, self.classes), dtype=torch.float32, device=dev)
         segs = []
@@ -503,9 +505,11 @@ class HipPopJob(FoldJob):
         hd.drop_scale = 1.0 / (1.0 - self.cfg.dropout) if self.cfg.dropout < 1 else 0.0
         hd.eval = 0
         hd.prec = prec
+        hd.dHp = self.dHp.data_ptr()
         self.head_args = hd
         dd = K.DenseDgradArgs()
         dd.dH, dd.wt, dd.dx = self.dH.data_ptr(), self.w1t.data_ptr(), self.grad[self.last].data_ptr()
+        dd.dHp = self.dHp.data_ptr()
         dd.G, dd.B, dd.Fp, dd.Up = Q, B, self.Fp, self.Up
         dd.prec, dd.wps = prec, self.w1t.numel()
         dd.w1 = self.views["W1"][0].data_ptr()      # the fp32 master (updated after dgrad): streaming kernel

@@ -57,13 +57,13 @@ class HeadArgs(C.Structure):
     _fields_ = [("h", P), ("w2", P), ("b2", P), ("labels", P), ("gather", P), ("st", P), ("dH", P),
                 ("gw2", P), ("gb2", P), ("gb1", P), ("eval_out", P), ("dz", P), ("plog", P),
                 ("G", I), ("B", I), ("Up", I), ("C", I), ("loss_ce", I), ("drop_scale", C.c_float), ("eval", I),
-                ("prec", I), ("valid", P), ("valid_norm", P)]
+                ("prec", I), ("valid", P), ("valid_norm", P), ("dHp", P)]
 
 
 class DenseDgradArgs(C.Structure):
     _fields_ = [("dH", P), ("wt", P), ("dx", P), ("G", I), ("B", I), ("Fp", I), ("Up", I), ("prec", I),
                 ("wps", C.c_long), ("unpool_mask", P), ("unpool_x0", P), ("unpool_x1", P), ("unpool_sel", P),
-                ("Hs", I), ("Ws", I), ("Cp", I), ("w1", P)]
+                ("Hs", I), ("Ws", I), ("Cp", I), ("w1", P), ("dHp", P)]
 
 
 class DenseWgradAdamArgs(C.Structure):

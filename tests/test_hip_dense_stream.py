@@ -19,6 +19,8 @@ def _lib():
     L = Km.lib()
     L.gt_dense_set_stream.argtypes = [ctypes.c_int]
     L.gt_dense_set_stream.restype = ctypes.c_int
+    L.gt_dense_set_dgrad2.argtypes = [ctypes.c_int]
+    L.gt_dense_set_dgrad2.restype = ctypes.c_int
     return L
 
 
@@ -43,9 +45,11 @@ def test_dense_stream_bit_identical(prec, G, B, Fp, Up):
     st = torch.zeros(8, dtype=torch.int32, device=DEV)
     fids = torch.arange(G, dtype=torch.int32, device=DEV)
     dH = torch.randn(G, B, Up, device=DEV)
+    from gentun_amd.models.cnn_hip import split_planes
+    dHp = split_planes(dH, 3 if prec else 1).view(torch.int16).contiguous()     # head_bwd's planes
     outs = []
-    for mode in (0, 1):
-        old = L.gt_dense_set_stream(mode)
+    for mode in (0, 1, 2):                   # round-2 kernels, streaming v1, streaming v2 (dH planes)
+        old = L.gt_dense_set_stream(1 if mode else 0)
         try:
             out = torch.zeros(G, B, Up, dtype=adt, device=DEV)
             plog = torch.zeros(G, Up // 16, B, C, device=DEV)
@@ -60,13 +64,15 @@ def test_dense_stream_bit_identical(prec, G, B, Fp, Up):
             d.dH, d.wt, d.dx, d.G, d.B, d.Fp, d.Up, d.prec = dH.data_ptr(), wt.data_ptr(), dx.data_ptr(), \
                 G, B, Fp, Up, prec
             d.w1 = w1.data_ptr() if mode else 0
+            d.dHp = dHp.data_ptr() if mode == 2 else 0
             Km.check(L.gt_dense_dgrad(d, _stream()), "dense_dgrad")
             torch.cuda.synchronize()
             outs.append((out.clone(), plog.clone(), dx.clone()))
         finally:
             L.gt_dense_set_stream(old)
-    for name, r0, r1 in zip(("h", "plog", "dx"), outs[0], outs[1]):
-        assert torch.equal(r0, r1), "{} differs: max {}".format(name, (r0.float() - r1.float()).abs().max().item())
+    for k in (1, 2):
+        for name, r0, r1 in zip(("h", "plog", "dx"), outs[0], outs[k]):
+            assert torch.equal(r0, r1), "{} {} differs: max {}".format(k, name, (r0.float() - r1.float()).abs().max().item())
     # and against the math (fp32: split-MFMA level; bf16: bf16 level)
     ref = torch.bmm(dH.double(), w1.double().transpose(1, 2))
     err = (outs[1][2].double() - ref).abs().max().item() / ref.abs().max().item()

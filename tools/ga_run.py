@@ -58,13 +58,13 @@ latest = os.path.join(args.ckpt, "latest.json")
 if args.resume and os.path.exists(latest):
     def factory(inds):
         return DistributedPopulation(GeneticCnnIndividual, x, y, individual_list=inds, additional_parameters=extra,
-                                     comm=comm, evaluator=ev)
+                                     comm=comm, evaluator=ev, verbose=False)
     ga = RussianRouletteGA.resume(latest, GeneticCnnIndividual, x, y, population_factory=factory,
                                   checkpoint_dir=args.ckpt)
 else:
     grng.seed(args.seed)
     pop = DistributedPopulation(GeneticCnnIndividual, x, y, size=args.pop, crossover_rate=0.3, mutation_rate=0.1,
-                                additional_parameters=extra, comm=comm, evaluator=ev)
+                                additional_parameters=extra, comm=comm, evaluator=ev, verbose=False)
     ga = RussianRouletteGA(pop, crossover_probability=0.2, mutation_probability=0.8, seed=args.seed,
                            checkpoint_dir=args.ckpt, verbose=False)
 t0 = time.perf_counter()

@@ -48,7 +48,7 @@ timeline)
   WARM=0 timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/tl -o run --output-format csv -- \
     python3 tools/probe_pop.py ${P:-5} ${P:-5} 1 1 ${SAMPLES:-2000} > gpurun_out/timeline/run${TAG:-}.log 2>&1 \
     || { tail -5 gpurun_out/timeline/run${TAG:-}.log; exit 1; }
-  python3 tools/timeline.py "$(find /tmp/tl -name '*kernel_trace.csv' | head -1)" > gpurun_out/timeline/summary${TAG:-}.txt
+  TIMELINE_DUMP=${DUMP:-1} python3 tools/timeline.py "$(find /tmp/tl -name "*kernel_trace.csv" | head -1)" > gpurun_out/timeline/summary${TAG:-}.txt
   head -30 gpurun_out/timeline/summary${TAG:-}.txt ;;
 prof)
   name=$1; shift; shift
@@ -96,7 +96,7 @@ qcurve)
     echo "== RESET=$1 P=$2 $(grep '^{' gpurun_out/qc/run.log | cut -c1-200)" | tee -a gpurun_out/qc/qcurve.txt
   done ;;
 ga)
-  heartbeat; ck=${CKPT:-gpurun_out/ga/ckpt}; mkdir -p gpurun_out/ga
+  heartbeat; ck=${CKPT:-gpurun_out/ga/ckpt}; mkdir -p gpurun_out/ga "$(dirname "$ck")"
   if [ -n "${SEED_CKPT:-}" ] && [ -d "$SEED_CKPT" ] && [ ! -d "$ck" ]; then cp -r "$SEED_CKPT" "$ck"; fi
   timeout -k 10 ${TIME:-1080} python3 -u tools/ga_run.py --gens ${GENS:-20} --ckpt "$ck" --resume \
     --time-budget ${BUDGET:-900} ${GA_ARGS:-} > gpurun_out/ga/run${TAG:-}.json 2> gpurun_out/ga/run${TAG:-}.err; rc=$?

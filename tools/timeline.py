@@ -53,3 +53,14 @@ for s in steps:
 for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
     print("{:62s} {:8.1f} us/step {:5.1f}% of wall  {:5.1f} calls/step {:7.1f} us/call".format(
         k, v / n / 1e3, 100 * v / n / wall, tcnt[k] / n, v / max(1, tcnt[k]) / 1e3))
+
+# one steady-state step in detail: TIMELINE_DUMP=k prints the k-th analysed step's launches
+import os  # noqa: E402
+if os.environ.get("TIMELINE_DUMP"):
+    k = int(os.environ["TIMELINE_DUMP"])
+    a, b = starts[5 + k], starts[6 + k]
+    t0 = ks[a][0]
+    print("\n# step {} in detail: start / end us relative to step_begin, queue, kernel".format(k))
+    for s, e, name, q in ks[a:b]:
+        print("{:8.1f} {:8.1f} {:7.1f}  q{:<3s} {}".format((s - t0) / 1e3, (e - t0) / 1e3, (e - s) / 1e3, str(q),
+                                                        name.split("(")[0][:70]))
