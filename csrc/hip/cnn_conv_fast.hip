@@ -1463,6 +1463,32 @@ static void stagger_init() {
   }
 }
 
+// Small launches (few groups per launch: the reference's sequential folds, one
+// rank's share of a config-3 generation): at 2 groups the 8-row tiles of the
+// 16x16 stage make 128 workgroups for 256 CUs. Shorter tiles (4 or 2 rows;
+// 2 rows = one co tile per wave, so a wave still holds whole row pairs for the
+// fused pool) multiply the grid. Every output's k loop (order of k-steps and
+// of the six split terms) is the same for any tile height: results are
+// bit-identical to the 8-row tiles (tests/test_hip_kernels.py), so a
+// candidate's result still does not depend on how many groups share its
+// launch. GENTUN_CONV_SMALLQ=0 disables (A/B).
+static int g_smallq = -1;
+extern "C" int gt_conv_set_smallq(int on) {
+  const int old = g_smallq;
+  g_smallq = on;
+  return old;
+}
+// tile rows for a launch whose default tile has TH rows: halve while the grid
+// is below SMALLQ_WG workgroups, down to THMIN
+#define SMALLQ_WG 512
+static int smallq_th(const ConvArgs* a, int TH, int THMIN) {
+  if (g_smallq < 0) g_smallq = std::getenv("GENTUN_CONV_SMALLQ") ? std::atoi(std::getenv("GENTUN_CONV_SMALLQ")) : 1;
+  if (!g_smallq) return TH;
+  int th = TH;
+  while (th > THMIN && (long)a->ngroups * a->B * (a->H / th) < SMALLQ_WG) th >>= 1;
+  return th;
+}
+
 extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
   stagger_init();
   ConvArgs lc = *a_in;
@@ -1472,6 +1498,27 @@ extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
   const ConvArgs* a = &lc;
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
   if (a->prec == 1) {
+    // small launches: shorter tiles of the S=(3,5) shapes (see smallq_th)
+    if (CONV_FAST_MATCH(5, 5, 1, 32, 8, 2, 3) && smallq_th(a, 8, 4) == 4) {      // s1 input conv
+      if (pk_ok(a, 2)) CONV_FAST_LAUNCH_PK(5, 5, 1, 32, 4, 2, 3, 2, 1, 1)
+      CONV_FAST_LAUNCH(5, 5, 1, 32, 4, 2, 3, 2, 1)
+    }
+    if (CONV_FAST_MATCH(3, 3, 3, 32, 8, 2, 3) && smallq_th(a, 8, 4) == 4) {      // s1 nodes / dgrad
+      if (pk_ok(a, 2)) CONV_FAST_LAUNCH_PK(3, 3, 3, 32, 4, 2, 3, 2, 1, 1)
+      CONV_FAST_LAUNCH(3, 3, 3, 32, 4, 2, 3, 2, 1)
+    }
+    if (CONV_FAST_MATCH(5, 5, 3, 16, 8, 4, 7)) {                                  // s2 input conv
+      const int th = smallq_th(a, 8, 2);
+      if (th == 4) CONV_FAST_LAUNCH(5, 5, 3, 16, 4, 4, 7, 4, 1)
+      if (th == 2) CONV_FAST_LAUNCH_CT1(5, 5, 3, 16, 2, 4, 7, 4)
+    }
+    if (CONV_FAST_MATCH(3, 3, 7, 16, 8, 4, 7)) {                                  // s2 nodes / dgrad
+      const int th = smallq_th(a, 8, 2);
+      if (th == 4) CONV_FAST_LAUNCH(3, 3, 7, 16, 4, 4, 7, 4, 1)
+      if (th == 2) CONV_FAST_LAUNCH_CT1(3, 3, 7, 16, 2, 4, 7, 4)
+    }
+    if (s2in_ct1_on() && CONV_FAST_MATCH(5, 5, 7, 16, 8, 2, 3) && smallq_th(a, 8, 4) == 4)   // s2 input dgrad
+      CONV_FAST_LAUNCH_CT1(5, 5, 7, 16, 4, 2, 3, 4)
     // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
     CONV_FAST_CASE_F32_PK(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
     CONV_FAST_CASE_F32_PK(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)

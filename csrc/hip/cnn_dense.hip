@@ -959,11 +959,16 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
     // thread scattered 2-byte stores over a 1-2 KB stride instead (every store
     // its own L2 transaction: the kernel's old bottleneck)
     __shared__ __attribute__((aligned(16))) uint16_t tile[GT_NPL_F32][ADAM_TK][128 + 8];
-    const int Co = sg.tCo, Ci = sg.tCi, KH = sg.tKH, KW = sg.tKW;
+    // Co > 128 (wide nodes): the weight is cut into 128-row co bands, one
+    // block per (group, band, column tile); bfT runs stay 16-byte aligned
+    const int CoF = sg.tCo, Ci = sg.tCi, KH = sg.tKH, KW = sg.tKW;
     const int Kd = KH * KW * Ci;
     const int nkt = (Kd + ADAM_TK - 1) / ADAM_TK;
-    const int gg = blk.y / nkt, k0 = (blk.y - gg * nkt) * ADAM_TK;
-    const long base = (long)gg * Co * Kd;
+    const int ncot = (CoF + 127) >> 7;
+    const int gb = blk.y / nkt, k0 = (blk.y - gb * nkt) * ADAM_TK;
+    const int gg = gb / ncot, c0 = (gb - gg * ncot) << 7;
+    const int Co = min(128, CoF - c0);
+    const long base = ((long)gg * CoF + c0) * Kd;
     const float lr_t = a.st->lr_t;
     for (int idx = threadIdx.x; idx < Co * ADAM_TK; idx += 256) {
       const int co = idx / ADAM_TK, kk = idx % ADAM_TK, k = k0 + kk;
@@ -987,7 +992,7 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
       const int kk = idx / nc8, c8 = idx - kk * nc8, k = k0 + kk;
       if (k >= Kd) continue;
       const int ci = k % Ci, r = k / Ci, kw = r % KW, kh = r / KW;
-      const long o = ((((long)gg * Ci + ci) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * Co + c8 * 8;
+      const long o = ((((long)gg * Ci + ci) * KH + (KH - 1 - kh)) * KW + (KW - 1 - kw)) * CoF + c0 + c8 * 8;
       for (int q = 0; q < npl; ++q)
         *reinterpret_cast<uint4*>(sg.bfT + q * sg.pstride_bfT + o) = *reinterpret_cast<const uint4*>(&tile[q][kk][c8 * 8]);
     }

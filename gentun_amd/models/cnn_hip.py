@@ -119,6 +119,12 @@ class HipPopJob(FoldJob):
         # optimizer run concurrently with the data-gradient chain (fork / join
         # edges inside the captured step graph)
         self.side = torch.cuda.Stream(dev)
+        # the conv wgrads of different layers are independent (own dz, own
+        # partial buffers): round-robin over GENTUN_WGRAD_STREAMS streams so a
+        # small launch (few groups: 64 workgroups) does not serialise the
+        # backward tail behind one wgrad at a time
+        nws = max(1, int(os.environ.get("GENTUN_WGRAD_STREAMS", "2")))
+        self.wg_streams = [self.side] + [torch.cuda.Stream(dev) for _ in range(nws - 1)]
         # the dense W1 optimizer (the largest single launch) on a stream of its
         # own, so it does not sit in front of the first conv wgrads
         self.side2 = torch.cuda.Stream(dev)
@@ -795,12 +801,16 @@ class HipPopJob(FoldJob):
         # layer L's update waits for its wgrad (side) and for its last
         # main-stream op (the dgrad reading its flipped weights / BN backward)
         side3 = self.side3 if (self.overlap and self.adam_overlap) else None
+        wgs = self.wg_streams if (self.overlap and side3 is None) else [side]
+        nwg = 0
         for i, (kind, a, Lr) in enumerate(self.bwd_ops):
             if kind == "wgrad":
-                fork(side)
-                K.check(L.gt_conv_wgrad(a, ss), "conv_wgrad")
+                ws = wgs[nwg % len(wgs)]
+                nwg += 1
+                fork(ws)
+                K.check(L.gt_conv_wgrad(a, ws.cuda_stream), "conv_wgrad")
                 if Lr.wred:
-                    K.check(L.gt_wgrad_reduce(a, ss), "wgrad_reduce")
+                    K.check(L.gt_wgrad_reduce(a, ws.cuda_stream), "wgrad_reduce")
             elif kind == "conv":
                 K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
             elif kind == "bn_bwd":
@@ -813,7 +823,7 @@ class HipPopJob(FoldJob):
                     ev.record(stream)
                     side3.wait_event(ev)
                 K.check(L.gt_adam_segments(Lr.adam_part[0], Lr.adam_part[1], side3.cuda_stream), "adam")
-        for stream in (side, side2, side3):
+        for stream in [side2, side3] + list(wgs):
             if stream is not None and stream is not main:
                 ev = torch.cuda.Event()
                 ev.record(stream)

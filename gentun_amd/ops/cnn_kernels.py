@@ -83,10 +83,10 @@ ADAM_TK = 64        # adam_segments transpose tiles: tCo rows x ADAM_TK reductio
 def adam_tiles(tG, tCo, tKH, tKW, tCi):
     """Blocks of a tiled conv-weight segment (csrc/hip/cnn_dense.hip, tiled
     path), or 0 when the segment cannot be tiled (then: 256-element blocks)."""
-    if tCo > 128 or tCo % 8:
+    if tCo % 8:
         return 0
     kd = tKH * tKW * tCi
-    return tG * (-(-kd // ADAM_TK))
+    return tG * (-(-tCo // 128)) * (-(-kd // ADAM_TK))
 
 
 class BnArgs(C.Structure):
@@ -159,6 +159,8 @@ def lib():
         L.gt_conv_set_fast.restype = I
         L.gt_conv_set_nwv.argtypes = [I]
         L.gt_conv_set_s2in_ct1.restype = I
+        L.gt_conv_set_smallq.argtypes = [I]
+        L.gt_conv_set_smallq.restype = I
         L.gt_conv_set_s2in_ct1.argtypes = [I]
         L.gt_conv_set_nwv.restype = I
         if os.environ.get("GENTUN_CONV_NWV"):

@@ -465,11 +465,14 @@ def test_head(loss):
 
 
 @pytest.mark.parametrize("tiled,dims", [(False, (2, 16, 3, 3, 8)), (True, (2, 16, 3, 3, 8)),
-                                        (True, (1, 104, 3, 3, 104)), (True, (2, 56, 5, 5, 24))])
+                                        (True, (1, 104, 3, 3, 104)), (True, (2, 56, 5, 5, 24)),
+                                        (False, (1, 256, 3, 3, 24)), (True, (2, 256, 3, 3, 40)),
+                                        (True, (1, 200, 3, 3, 16))])
 def test_adam_segments_with_partials_and_transpose(tiled, dims):
     """Multi-tensor Adam over split-K partials, bf16 copy and the flipped /
-    transposed dgrad copy; ``tiled``: (group, 64-column) tile blocks with the
-    transposed copy staged through LDS."""
+    transposed dgrad copy; ``tiled``: (group, 128-row co band, 64-column) tile
+    blocks with the transposed copy staged through LDS (Co > 128: several
+    bands, the last one partial)."""
     Km = K()
     import ctypes
     torch.manual_seed(7)

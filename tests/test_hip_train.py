@@ -175,6 +175,100 @@ def test_fused_pool_matches_separate_pool_kernel(dtype, bn, monkeypatch):
         assert torch.equal(a, b)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("bn", [False, True])
+def test_small_launch_tiles_bit_identical(bn, monkeypatch):
+    """Small launches (2 groups) take shorter conv tiles (4 / 2 rows, one co
+    tile per wave at 2) and more wgrad streams; training is bit-identical to
+    the default 8-row tiles on one wgrad stream (every output keeps its k-loop
+    order; the wgrads of different layers are independent)."""
+    import numpy as np
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.cnn_hip import HipPopJob
+    from gentun_amd.models.genome import make_plan
+    from gentun_amd.ops import cnn_kernels as Km
+    from gentun_amd.utils.data import make_cifar_like, stratified_kfold
+    x, y = make_cifar_like(n=400, seed=2)
+    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
+    genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '111', 'S_2': '0000000001'}]
+    members = [(make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10), [folds[0]], [0])
+               for g in genes]
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="fp32", reset="all",
+                        use_graph=False, batch_norm=bn)
+    out = {}
+    lib = Km.lib()
+    try:
+        for small in (1, 0):
+            lib.gt_conv_set_smallq(small)
+            monkeypatch.setenv("GENTUN_WGRAD_STREAMS", "3" if small else "1")
+            job = HipPopJob(None, x, y, None, cfg, torch.device("cuda", 0), members=members)
+            job.init_params()
+            job.reset_optimizer(1e-3)
+            job._new_epoch_order()
+            for _ in range(4):
+                job.train_step()
+            ev = job.evaluate()
+            torch.cuda.synchronize()
+            out[small] = (job.flat.detach().clone(), [t.detach().clone() for t in ev])
+    finally:
+        lib.gt_conv_set_smallq(1)
+    assert torch.equal(out[1][0], out[0][0])
+    for a, b in zip(out[1][1], out[0][1]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bn", [False, True])
+def test_inactive_node_params_untouched(bn):
+    """A population job lays out the superset of its members' layers; a node
+    a group's genome leaves out (no edges: the reference never builds it,
+    keras_models.py:114-117,138) has parameter slots for that group which the
+    optimizer must skip: weights, biases, BatchNorm affine and Adam moments of
+    inactive groups stay exactly as initialised while active groups move.
+    Stage 2 is 256 wide so its weights take the banded (Co > 128) Adam tiles."""
+    import numpy as np
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.cnn_hip import HipPopJob
+    from gentun_amd.models.genome import make_plan
+    from gentun_amd.utils.data import make_cifar_like, stratified_kfold
+    x, y = make_cifar_like(n=400, seed=2)
+    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
+    genes = [{'S_1': '111', 'S_2': '1111111111'}, {'S_1': '000', 'S_2': '0000000000'}]
+    members = [(make_plan(g, (3, 5), (32, 32, 3), (32, 256), ((5, 5), (3, 3)), 500, 10), folds, [0, 1])
+               for g in genes]
+    cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype="fp32", reset="all",
+                        use_graph=False, batch_norm=bn)
+    job = HipPopJob(None, x, y, None, cfg, torch.device("cuda", 0), members=members)
+    job.init_params()
+    job.reset_optimizer(1e-3)
+    job._new_epoch_order()
+    torch.cuda.synchronize()
+
+    def params(L):
+        ts = list(L.w) + list(L.b)
+        if bn:
+            ts += list(L.gamma) + list(L.beta)
+        return ts
+
+    before = [[t.detach().clone() for t in params(L)] for L in job.layers]
+    for _ in range(3):
+        job.train_step()
+    torch.cuda.synchronize()
+    n_inactive = n_wide = 0
+    for L, old in zip(job.layers, before):
+        active = {q for q, _ in L.rows}
+        n_wide += L.coutp > 128
+        for q in range(job.Q):
+            new = [t[q] for t in params(L)]
+            if q in active:
+                assert not torch.equal(new[0], old[0][q])            # the weights were updated
+            else:
+                n_inactive += 1
+                for a, b in zip(new, old):
+                    assert torch.equal(a, b[q])
+    assert n_inactive > 0 and n_wide > 0
+
+
 @pytest.mark.parametrize("bn", [False, True])
 def test_eval_batch_does_not_change_metrics(bn):
     """K13: the validation forward runs ``eval_batch()`` rows per launch on
