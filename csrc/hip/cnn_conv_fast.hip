@@ -1479,13 +1479,15 @@ extern "C" int gt_conv_set_smallq(int on) {
   return old;
 }
 // tile rows for a launch whose default tile has TH rows: halve while the grid
-// is below SMALLQ_WG workgroups, down to THMIN
-#define SMALLQ_WG 512
+// is below SMALLQ_WG workgroups (GENTUN_CONV_SMALLQ_WG, default 512), down to THMIN
+static long g_smallq_wg = -1;
 static int smallq_th(const ConvArgs* a, int TH, int THMIN) {
   if (g_smallq < 0) g_smallq = std::getenv("GENTUN_CONV_SMALLQ") ? std::atoi(std::getenv("GENTUN_CONV_SMALLQ")) : 1;
+  if (g_smallq_wg < 0)
+    g_smallq_wg = std::getenv("GENTUN_CONV_SMALLQ_WG") ? std::atol(std::getenv("GENTUN_CONV_SMALLQ_WG")) : 512;
   if (!g_smallq) return TH;
   int th = TH;
-  while (th > THMIN && (long)a->ngroups * a->B * (a->H / th) < SMALLQ_WG) th >>= 1;
+  while (th > THMIN && (long)a->ngroups * a->B * (a->H / th) < g_smallq_wg) th >>= 1;
   return th;
 }
 

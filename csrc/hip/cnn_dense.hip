@@ -62,6 +62,12 @@ struct DenseFwdArgs {
   int prec;                // 0: bf16 tensors, bf16 MFMA; 1: fp32 tensors, split-fp32 MFMA (common.h)
   long wps;                // unused (kept for the ABI)
   int row_off;             // data parallelism (X5): this rank's first row of the full batch (dropout keys)
+  // split-K forward (dense_fwd_sk_kernel): W1 read from the fp32 master [G][Fp][Up] itself, KS
+  // feature splits per output tile, partial tiles in `part`, per-tile arrival counters in `cnt`
+  const float* w1;
+  float* part;             // [G][ceil(B/32)][Up/64][KS][4][2][64] f32x4 range partials
+  int* cnt;                // unused (reserved)
+  int ks;
 };
 
 // an MFMA A operand of 8 consecutive weights of the transposed W1 copy: bf16
@@ -328,6 +334,153 @@ __device__ __forceinline__ void split3(float p, uint16_t* h) {
   h[1] = f2bf(r1);
   h[2] = f2bf(r1 - bf2f(h[1]));
 }
+
+// Split-K forward (the default): one workgroup = 4 unit tiles (64 units) x 32
+// rows x ONE of KS contiguous ranges of the feature k-steps, so a launch is
+// (Up/64) x KS x G workgroups instead of (Up/64) x G -- the streaming kernel
+// ran 8 workgroups per group, 16 at 2 groups and 200 at 25 (latency-bound at
+// every population size, each wave walking 25 of the 100 k-steps). W1 comes
+// from the fp32 master [G][Fp][Up] (the transposed copy the optimizer used to
+// write every step is gone): per k-step the workgroup stages the [32 f][64 u]
+// W1 tile (16-byte loads along u) and the [32 rows][32 f] activation tile
+// into LDS as exact bf16 planes, and each wave reads its unit tile's A operand
+// with ds_read_b64_tr_b16 (transposing reads: k = feature runs down the rows
+// of the natural layout). Wave w owns unit tile w over the whole range; the
+// KS range partials go to `part` and dense_fwd_skred_kernel sums them in
+// range order and runs the bias / ReLU / dropout / partial-logit epilogue.
+// Every sum has a fixed order: deterministic, and independent of how many
+// groups share the launch (KS is a per-shape constant).
+#define DSK_WLD 72            // W1 tile row stride (bf16): 64 units + 8 (16-byte aligned rows)
+#define DSK_XLD 40            // activation tile row stride (bf16): 32 features + 8
+typedef __attribute__((ext_vector_type(4))) short dsk_short4;
+
+__device__ __forceinline__ uint4 dsk_tr_frag(const uint16_t* tile, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  typedef __attribute__((address_space(3))) dsk_short4 lds_s4;
+  const uint16_t* r0 = tile + (8 * g + q) * DSK_WLD + col0 + 4 * p;
+  const uint16_t* r1 = r0 + 4 * DSK_WLD;
+  const dsk_short4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(r0));
+  const dsk_short4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(r1));
+  typedef __attribute__((ext_vector_type(8))) short short8_t;
+  return __builtin_bit_cast(uint4, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+template <int PREC>
+__global__ void __launch_bounds__(256) dense_fwd_sk_kernel(DenseFwdArgs a) {
+  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
+  typedef typename ActT<PREC>::T AT;
+  __shared__ __attribute__((aligned(16))) uint16_t wl[2][NPL][32 * DSK_WLD];
+  __shared__ __attribute__((aligned(16))) uint16_t xl[2][NPL][32 * DSK_XLD];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  int bx, g;
+  xcd_tile(bx, g);
+  const int KS = a.ks, nut = a.Up / 64, nby = gridDim.y;
+  const int ut = bx / KS, s = bx - ut * KS;
+  const int u_t = ut * 64;
+  const int b0 = blockIdx.y * 32;
+  const int nks = (a.Fp + 31) >> 5;                         // k-steps of 32 features
+  const int per = (nks + KS - 1) / KS;
+  const int j0 = s * per, j1 = min(nks, j0 + per);
+  // staging lanes: W1 row f = tid / 8 of the k-step, units u_t + 8 (tid % 8) .. +7;
+  // activations row b0 + tid / 8, features 4 (tid % 8) .. +3
+  const int wf = tid >> 3, wu = (tid & 7) * 8;
+  const float* w1 = a.w1 + (long)g * a.Fp * a.Up + u_t + wu;
+  const int xr = b0 + (tid >> 3), xf = (tid & 7) * 4;
+  const bool xok = xr < a.B;
+  const AT* xg = static_cast<const AT*>(a.x) + ((long)g * a.B + (xok ? xr : 0)) * a.Fp + xf;
+  float rw[8], rx[4];
+  auto load = [&](int j) {
+    const int f = 32 * j + wf;
+    const bool ok = j < j1 && f < a.Fp;
+    const float* src = ok ? w1 + (long)f * a.Up : gt_zero8;
+    const float4 q0 = *reinterpret_cast<const float4*>(src);
+    const float4 q1 = *reinterpret_cast<const float4*>(src + (ok ? 4 : 0));
+    rw[0] = q0.x; rw[1] = q0.y; rw[2] = q0.z; rw[3] = q0.w;
+    rw[4] = q1.x; rw[5] = q1.y; rw[6] = q1.z; rw[7] = q1.w;
+    const int fx = 32 * j + xf;
+    const bool okx = j < j1 && xok && fx < a.Fp;            // Fp % 8 == 0: a 4-run never straddles the end
+    if constexpr (PREC != 0) {
+      const float4 v = *reinterpret_cast<const float4*>(okx ? reinterpret_cast<const float*>(xg + 32 * j) : gt_zero8);
+      rx[0] = v.x; rx[1] = v.y; rx[2] = v.z; rx[3] = v.w;
+    } else {
+      const uint2 v = *reinterpret_cast<const uint2*>(okx ? reinterpret_cast<const void*>(xg + 32 * j)
+                                                          : reinterpret_cast<const void*>(gt_zero8));
+      rx[0] = __uint_as_float(v.x << 16); rx[1] = __uint_as_float(v.x & 0xffff0000u);
+      rx[2] = __uint_as_float(v.y << 16); rx[3] = __uint_as_float(v.y & 0xffff0000u);
+    }
+  };
+  auto stage = [&](int buf) {
+    uint4 wp[NPL];
+    planes8<PREC>(rw, wp);
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) *reinterpret_cast<uint4*>(&wl[buf][p][wf * DSK_WLD + wu]) = wp[p];
+    if constexpr (PREC != 0) {
+      uint16_t h[4][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) split3(rx[i], h[i]);
+#pragma unroll
+      for (int p = 0; p < NPL; ++p)
+        *reinterpret_cast<uint2*>(&xl[buf][p][(tid >> 3) * DSK_XLD + xf]) =
+            make_uint2(h[0][p] | ((uint32_t)h[1][p] << 16), h[2][p] | ((uint32_t)h[3][p] << 16));
+    } else {
+      *reinterpret_cast<uint2*>(&xl[buf][0][(tid >> 3) * DSK_XLD + xf]) = pack4(rx);
+    }
+  };
+  f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  load(j0);
+  for (int j = j0; j < j1; ++j) {
+    const int buf = (j - j0) & 1;
+    stage(buf);
+    __syncthreads();                    // buf complete; the other buffer's readers are done (previous step)
+    load(j + 1);                        // next k-step's raw values in flight during the MFMAs
+    uint4 af[NPL], b0f[NPL], b1f[NPL];
+#pragma unroll
+    for (int p = 0; p < NPL; ++p) {
+      af[p] = dsk_tr_frag(wl[buf][p], wave * 16, lane);
+      b0f[p] = *reinterpret_cast<const uint4*>(&xl[buf][p][l16 * DSK_XLD + kq * 8]);
+      b1f[p] = *reinterpret_cast<const uint4*>(&xl[buf][p][(16 + l16) * DSK_XLD + kq * 8]);
+    }
+    acc[0] = mfma_np<NPL>(af, b0f, acc[0]);
+    acc[1] = mfma_np<NPL>(af, b1f, acc[1]);
+  }
+  if (KS > 1) {                        // range partial; dense_fwd_skred_kernel sums the ranges
+    const long tile = ((long)g * nby + blockIdx.y) * nut + ut;
+    f32x4_t* pt = reinterpret_cast<f32x4_t*>(a.part) + (((tile * KS + s) * 4 + wave) * 2) * 64 + lane;
+    pt[0] = acc[0];
+    pt[64] = acc[1];
+    return;
+  }
+  f32x4_t r2[2] = {acc[0], acc[1]};
+  dense_fwd_epilogue<PREC>(a, g, u_t + wave * 16, b0, r2, lane, u_t / 16 + wave);
+}
+
+// the KS range partials of a split-K forward tile summed in range order (a
+// launch of its own: visibility of the partials comes with the kernel
+// boundary -- a last-arriving-workgroup protocol needed a device-scope L2
+// write-back per workgroup and ran 10x slower), then the epilogue.
+// Grid (Up/64, ceil(B/32), G), wave w = unit tile w.
+template <int PREC>
+__global__ void __launch_bounds__(256) dense_fwd_skred_kernel(DenseFwdArgs a) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int ut, g;
+  xcd_tile(ut, g);
+  const int KS = a.ks, nut = a.Up / 64, nby = gridDim.y;
+  const long tile = ((long)g * nby + blockIdx.y) * nut + ut;
+  const f32x4_t* pt = reinterpret_cast<const f32x4_t*>(a.part) + ((tile * KS * 4 + wave) * 2) * 64 + lane;
+  f32x4_t v[2][16];
+  f32x4_t r2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (int q0 = 0; q0 < KS; q0 += 16) {      // all loads of a batch in flight, then the ordered sum
+    const int n = min(16, KS - q0);
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (q < n) { v[0][q] = pt[(long)(q0 + q) * 4 * 2 * 64]; v[1][q] = pt[(long)(q0 + q) * 4 * 2 * 64 + 64]; }
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (q < n) { r2[0] += v[0][q]; r2[1] += v[1][q]; }
+  }
+  dense_fwd_epilogue<PREC>(a, g, ut * 64 + wave * 16, blockIdx.y * 32, r2, lane, ut * 4 + wave);
+}
+
 
 // ---------------------------------------------------------------------------
 struct HeadArgs {
@@ -908,7 +1061,9 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
     }
 #endif
   }
-  if (a.mode == 1) return;                            // (uniform) no update, no copy
+  // (uniform) no update, or no transposed copy: every W1 reader takes the master (split-K dense_fwd,
+  // streaming dense_dgrad)
+  if (a.mode == 1 || a.wt == nullptr) return;
   __syncthreads();
   // transposed copy: wt[u][f0 .. f0+15] (32 / 64 contiguous bytes per unit), 8 values per store
   const int nu = a.Ur > 0 ? ((a.Ur + 3) >> 2) << 2 : a.Up;
@@ -1062,8 +1217,40 @@ int gt_step_begin(StepState* s, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// split-K forward from the W1 master (default; GENTUN_DENSE_SK=0: the streaming kernel on the transposed copy)
+static int g_dense_sk = -1;
+static bool dense_sk_on() {
+  if (g_dense_sk < 0) g_dense_sk = std::getenv("GENTUN_DENSE_SK") ? std::atoi(std::getenv("GENTUN_DENSE_SK")) : 1;
+  return g_dense_sk != 0;
+}
+
+int gt_dense_set_sk(int on) {
+  dense_sk_on();
+  const int old = g_dense_sk;
+  g_dense_sk = on;
+  return old;
+}
+
+// feature ranges per output tile of the split-K forward: a per-shape constant (~12 k-steps of
+// 32 features per range), never a function of the number of groups
+int gt_dense_fwd_splits(int Fp) {
+  const int nks = (Fp + 31) / 32;
+  return std::max(1, std::min(16, nks / 12));
+}
+
 int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
   if (a->Fp % 8 || a->Up % 64 || a->C > HEAD_MAXC_FWD || (a->prec != 0 && a->prec != 1)) return -1;
+  if (a->w1 && a->ks >= 1 && (a->ks == 1 || a->part) && dense_sk_on()) {
+    dim3 grid(a->Up / 64 * a->ks, (a->B + 31) / 32, a->G);
+    if (a->prec) hipLaunchKernelGGL(dense_fwd_sk_kernel<1>, grid, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL(dense_fwd_sk_kernel<0>, grid, dim3(256), 0, stream, *a);
+    if (a->ks > 1) {
+      dim3 rgrid(a->Up / 64, (a->B + 31) / 32, a->G);
+      if (a->prec) hipLaunchKernelGGL(dense_fwd_skred_kernel<1>, rgrid, dim3(256), 0, stream, *a);
+      else hipLaunchKernelGGL(dense_fwd_skred_kernel<0>, rgrid, dim3(256), 0, stream, *a);
+    }
+    return (int)hipGetLastError();
+  }
   if (dense_stream_on()) {
     // unit tiles per workgroup (A/B: GENTUN_DENSE_UT = 1 / 2 / 4; 4: 53 vs 67 us at 25 groups, W1 in MALL)
     static const int ut = std::getenv("GENTUN_DENSE_UT") ? std::atoi(std::getenv("GENTUN_DENSE_UT")) : 4;

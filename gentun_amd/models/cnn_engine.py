@@ -37,6 +37,7 @@ Backends: ``hip`` (MI355X kernels, :mod:`gentun_amd.models.cnn_hip`) and
 ``torch`` (autograd oracle / comparator path (a) of SURVEY.md §6).
 """
 
+import copy
 import math
 import os
 
@@ -241,6 +242,58 @@ class FoldJob(object):
         self.step_ctr = torch.zeros((1,), dtype=torch.int64, device=self.device)
         self.result = None
 
+    # -- sequential folds: one job, re-pointed at the next fold ---------------
+    can_rebind = False          # executors whose device state survives a rebind set this
+
+    def rebind(self, folds, fold_ids):
+        """Point the job at other folds of the same members (one fold per
+        group, in group order) without rebuilding it: index tables, shuffle
+        streams and fold ids change; buffers, argument tables and the captured
+        step graph stay. Returns False (nothing changed) when the new folds
+        need another step count per epoch; the caller then builds a new job."""
+        if not self.can_rebind or len(folds) != self.G or len(fold_ids) != self.G:
+            return False
+        ntr = [len(tr) for tr, _ in folds]
+        if int(math.ceil(max(ntr) / self.B)) != self.steps_per_epoch:
+            return False
+        # the previous fold's launches may still read the old tables: keep them alive
+        self._retired = getattr(self, "_retired", []) + [self.train_mat, self.ntrain_t, self.val_mat,
+                                                         self.val_mask]
+        self.folds = list(folds)
+        self.fold_ids = [int(f) for f in fold_ids]
+        self.ntrain = ntr
+        self.nval = [len(va) for _, va in folds]
+        tm = np.zeros((self.G, max(ntr)), np.int64)
+        for g, (tr, _) in enumerate(folds):
+            tm[g, :len(tr)] = tr
+        self.train_mat = torch.from_numpy(tm).to(self.device)
+        self.ntrain_t = torch.tensor(ntr, dtype=torch.int64, device=self.device)
+        maxv = max(self.nval)
+        vm = np.zeros((self.G, maxv), np.int64)
+        vmask = np.zeros((self.G, maxv), np.float32)
+        for g, (_, va) in enumerate(folds):
+            vm[g, :len(va)] = va
+            vmask[g, :len(va)] = 1.0
+        self.val_mat = torch.from_numpy(vm).to(self.device)
+        self.val_mask = torch.from_numpy(vmask).to(self.device)
+        self.shuffle_gens = []
+        for g, fid in enumerate(self.fold_ids):
+            gen = torch.Generator(device=self.device)
+            gen.manual_seed(_rng.stable_hash(self.member_seeds[self.gmember[g]], "shuffle", fid) & 0x7FFFFFFF)
+            self.shuffle_gens.append(gen)
+        if self.cfg.batching == "keras":      # in place: the captured step reads these rows
+            v = np.zeros((self.steps_per_epoch, self.G), np.int32)
+            for g, n in enumerate(ntr):
+                for st in range(self.steps_per_epoch):
+                    v[st, g] = max(0, min(self.B, n - st * self.B))
+            self.epoch_valid.copy_(torch.from_numpy(v))
+        self._rebind_device()
+        self.result = None
+        return True
+
+    def _rebind_device(self):
+        """Executor state keyed by fold id (init seeds, dropout keys)."""
+
     # -- shuffling -----------------------------------------------------------
     def _new_epoch_order(self):
         G, maxn = self.train_mat.shape
@@ -345,7 +398,13 @@ class FoldJob(object):
             if self.after_init is not None:
                 self.after_init(self)
             self._k_steps = self.graph_steps() if use_graph else 1
-            graph = self._capture() if use_graph else None
+            keep = getattr(self, "_graph_keep", None)
+            if use_graph and keep is not None and keep[0] == self._k_steps:
+                graph = keep[1]                  # rebound job: same launches, same buffers
+            else:
+                graph = self._capture() if use_graph else None
+                if graph is not None and self.can_rebind:
+                    self._graph_keep = (self._k_steps, graph)
             if timed:
                 ev[1].record()
             verbose = getattr(self.cfg, "verbose", False)
@@ -410,21 +469,40 @@ class SequentialFoldJob(object):
     trained (``reset_weights`` re-runs kernel initialisers only,
     keras_models.py:120-125). ``make(fold_index)`` builds the job of one
     fold (all candidates, one group each); everything is enqueued on the
-    jobs' stream, so ``launch()`` does not block."""
+    jobs' stream, so ``launch()`` does not block.
 
-    def __init__(self, make, nfolds, multi):
+    With ``spec(fold_index) -> (folds, fold_ids)`` (one fold per group) an
+    executor that can rebind (the HIP one) trains every fold on ONE job: the
+    buffers, argument tables and captured step graph of fold 0 are reused,
+    only the index tables and fold-keyed seeds change, and the biases are
+    carried in place (``GENTUN_FOLD_REUSE=0``: a new job per fold; results are
+    bit-identical either way, tests/test_hip_train.py)."""
+
+    def __init__(self, make, nfolds, multi, spec=None):
         self.make = make
         self.nfolds = nfolds
         self.multi = multi
+        self.spec = spec if os.environ.get("GENTUN_FOLD_REUSE", "1") != "0" else None
         self.jobs = []
         self.phase_ms = None
 
     def launch(self):
         prev = None
         for f in range(self.nfolds):
-            job = self.make(f)
-            if prev is not None:
-                job.after_init = _carry_biases(prev)
+            job = None
+            if prev is not None and self.spec is not None and prev.can_rebind:
+                # fold f-1's results stay with a shallow copy (its own eval tensors / events / sizes)
+                self.jobs[-1] = copy.copy(prev)
+                ctx = torch.cuda.stream(prev.stream) if prev.stream is not None else _nullctx()
+                with ctx:                       # ordered after fold f-1's launches on the job stream
+                    kept = prev.bias_state()
+                    if prev.rebind(*self.spec(f)):
+                        job = prev
+                        job.after_init = _load_biases(kept)
+            if job is None:
+                job = self.make(f)
+                if prev is not None:
+                    job.after_init = _carry_biases(prev)
             job.launch()
             self.jobs.append(job)
             prev = job
@@ -443,6 +521,12 @@ class SequentialFoldJob(object):
 def _carry_biases(prev):
     def hook(job):
         job.copy_biases_from(prev)
+    return hook
+
+
+def _load_biases(kept):
+    def hook(job):
+        job.load_bias_state(kept)
     return hook
 
 
@@ -888,7 +972,7 @@ def make_job(backend, plan, x, y, folds, cfg, device, fold_ids=None, stream=None
     if cfg.reset == "all" or len(folds) == 1:
         return _one_job(backend, plan, x, y, folds, cfg, device, ids, stream)
     return SequentialFoldJob(lambda f: _one_job(backend, plan, x, y, [folds[f]], cfg, device, [ids[f]], stream),
-                             len(folds), multi=False)
+                             len(folds), multi=False, spec=lambda f: ([folds[f]], [ids[f]]))
 
 
 def make_population_job(backend, members, x, y, cfg, device, stream=None):
@@ -913,7 +997,10 @@ def make_population_job(backend, members, x, y, cfg, device, stream=None):
     def make(k):
         return Job(None, x, y, None, cfg, device, stream=stream,
                    members=[(p, [f[k]], [ids[k]]) for p, f, ids in members])
-    return SequentialFoldJob(make, nf.pop(), multi=True)
+
+    def spec(k):
+        return [f[k] for _, f, _ in members], [ids[k] for _, _, ids in members]
+    return SequentialFoldJob(make, nf.pop(), multi=True, spec=spec)
 
 
 def default_backend(device):

@@ -372,6 +372,16 @@ class HipPopJob(FoldJob):
         self.adam_nblocks = len(blocks)
         self.adam_head_range = (self.adam_head_range[0], len(blocks))
 
+    def _dense_sk_buffers(self, df, rows):
+        """Range partials and arrival counters of a split-K dense forward at
+        ``rows`` batch rows (training and evaluation launches get their own)."""
+        nby, nut = -(-rows // 32), self.Up // 64
+        part = torch.empty((self.Q * nby * nut * max(1, df.ks) * 4 * 2 * 64 * 4,), dtype=torch.float32,
+                           device=self.device)
+        cnt = torch.zeros((self.Q * nby * nut,), dtype=torch.int32, device=self.device)
+        self._keep += [part, cnt]
+        df.part, df.cnt = part.data_ptr(), cnt.data_ptr()
+
     def _conv_args(self, L, in_ptrs, out_ptrs, mask_ptrs, w, bias, relu, rows, gather=None, Cinp=None, Coutp=None):
         a = K.ConvArgs()
         for i, p in enumerate(in_ptrs):
@@ -497,6 +507,16 @@ class HipPopJob(FoldJob):
         df.drop_p, df.train, df.seed = self.cfg.dropout, 1, 0
         df.w2, df.plog, df.C = self.views["W2"][0].data_ptr(), self.plog.data_ptr(), self.classes
         df.prec, df.wps = prec, self.w1t.numel()
+        # split-K forward straight from the fp32 W1 master (csrc/hip/cnn_dense.hip dense_fwd_sk_kernel);
+        # with the streaming data gradient also on the master, nothing reads the transposed copy and
+        # the W1 optimizer stops writing it (GENTUN_DENSE_SK=0: the copy and the streaming forward)
+        self.dense_sk = (os.environ.get("GENTUN_DENSE_SK", "1") != "0" and
+                         os.environ.get("GENTUN_DENSE_STREAM", "1") != "0" and
+                         os.environ.get("GENTUN_DENSE_DGRAD2", "1") != "0" and self.Up % 64 == 0)
+        if self.dense_sk:
+            df.w1 = self.views["W1"][0].data_ptr()
+            df.ks = int(self.L.gt_dense_fwd_splits(self.Fp))
+            self._dense_sk_buffers(df, B)
         self.dense_fwd_args = df
         hd = K.HeadArgs()
         hd.h, hd.w2, hd.b2 = self.hdrop.data_ptr(), self.views["W2"][0].data_ptr(), self.views["b2"][0].data_ptr()
@@ -524,7 +544,7 @@ class HipPopJob(FoldJob):
         p, m, v = self.views["W1"]
         dw.x, dw.dH, dw.p, dw.m, dw.v = self.act[self.last].data_ptr(), self.dH.data_ptr(), p.data_ptr(), \
             m.data_ptr(), v.data_ptr()
-        dw.wt, dw.st = self.w1t.data_ptr(), self.state.data_ptr()
+        dw.wt, dw.st = (0 if self.dense_sk else self.w1t.data_ptr()), self.state.data_ptr()
         dw.G, dw.B, dw.Fp, dw.Up = Q, B, self.Fp, self.Up
         dw.Cp, dw.Cr, dw.Ur = self.final_cp, self.plan.kernels_per_layer[-1], self.plan.dense_units
         dw.prec, dw.wps = prec, self.w1t.numel()
@@ -717,6 +737,20 @@ class HipPopJob(FoldJob):
         return (self.flat.clone(), self.m.clone(), self.v.clone(), self.state.clone(),
                 [L.bn_run.clone() for L in self.layers] if self.bn else [])
 
+    @property
+    def can_rebind(self):
+        # sequential folds on one job (SequentialFoldJob); the data-parallel
+        # executor runs eagerly across ranks and is rebuilt per fold
+        return self.dp is None
+
+    def _rebind_device(self):
+        # dropout keys read through this pointer by the captured step: in place
+        self.fold_ids_t.copy_(torch.tensor(self.fold_ids, dtype=torch.int32))
+        self.init_args = None            # Glorot seeds are keyed by fold id: rebuilt by init_params
+        # a fresh job's step state: global_step keys the dropout masks of every step
+        self.state.zero_()
+        self.eval_state.zero_()
+
     def copy_biases_from(self, other):
         """Everything ``reset_weights`` keeps (keras_models.py:120-125 re-runs
         kernel initialisers only): conv / dense biases and, with BatchNorm,
@@ -907,6 +941,8 @@ class HipPopJob(FoldJob):
         df = K.DenseFwdArgs.from_buffer_copy(self.dense_fwd_args)
         df.x, df.out, df.plog = rp(df.x), hdrop.data_ptr(), plog.data_ptr()
         df.B, df.train = EB, 0
+        if self.dense_sk:
+            self._dense_sk_buffers(df, EB)
         hd = K.HeadArgs.from_buffer_copy(self.head_args)
         hd.h, hd.plog = hdrop.data_ptr(), plog.data_ptr()
         hd.B, hd.eval, hd.st = EB, 1, self.eval_state.data_ptr()

@@ -50,7 +50,8 @@ class WgradArgs(C.Structure):
 class DenseFwdArgs(C.Structure):
     _fields_ = [("x", P), ("wt", P), ("bias", P), ("out", P), ("w2", P), ("plog", P), ("st", P), ("fold_ids", P),
                 ("seeds", P), ("G", I), ("B", I), ("Fp", I), ("Up", I), ("drop_p", C.c_float), ("train", I),
-                ("seed", C.c_uint), ("C", I), ("prec", I), ("wps", C.c_long), ("row_off", I)]
+                ("seed", C.c_uint), ("C", I), ("prec", I), ("wps", C.c_long), ("row_off", I),
+                ("w1", P), ("part", P), ("cnt", P), ("ks", I)]
 
 
 class HeadArgs(C.Structure):
@@ -159,6 +160,10 @@ def lib():
         L.gt_conv_set_fast.restype = I
         L.gt_conv_set_nwv.argtypes = [I]
         L.gt_conv_set_s2in_ct1.restype = I
+        L.gt_dense_fwd_splits.argtypes = [I]
+        L.gt_dense_fwd_splits.restype = I
+        L.gt_dense_set_sk.argtypes = [I]
+        L.gt_dense_set_sk.restype = I
         L.gt_conv_set_smallq.argtypes = [I]
         L.gt_conv_set_smallq.restype = I
         L.gt_conv_set_s2in_ct1.argtypes = [I]

@@ -77,3 +77,60 @@ def test_dense_stream_bit_identical(prec, G, B, Fp, Up):
     ref = torch.bmm(dH.double(), w1.double().transpose(1, 2))
     err = (outs[1][2].double() - ref).abs().max().item() / ref.abs().max().item()
     assert err < (1e-5 if prec else 2e-2)
+
+
+@pytest.mark.parametrize("prec", [1, 0])
+@pytest.mark.parametrize("G,B,Fp,Up,ks", [(5, 32, 3584, 512, None), (3, 20, 392, 128, 3), (2, 64, 392, 128, 1)])
+def test_dense_fwd_split_k(prec, G, B, Fp, Up, ks):
+    """Split-K forward from the fp32 W1 master (dense_fwd_sk_kernel, the
+    default): same dropout mask as the streaming kernel, values at the
+    split-MFMA level of an fp64 reference, bitwise deterministic across
+    launches and independent of how many groups share the launch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L = _lib()
+    torch.manual_seed(1)
+    adt = torch.float32 if prec else torch.bfloat16
+    C = 10
+    w1 = torch.randn(G, Fp, Up, device=DEV) * 0.05
+    if not prec:
+        w1 = w1.to(torch.bfloat16).float()                         # the bf16 path multiplies RNE roundings
+    wt = w1.transpose(1, 2).contiguous().to(adt)
+    x = torch.randn(G, B, Fp, device=DEV).to(adt)
+    b1 = torch.randn(G, Up, device=DEV) * 0.1
+    w2 = torch.randn(G, Up, C, device=DEV) * 0.05
+    st = torch.zeros(8, dtype=torch.int32, device=DEV)
+    fids = torch.arange(G, dtype=torch.int32, device=DEV)
+    ks = ks or L.gt_dense_fwd_splits(Fp)
+
+    def run(g, sk):
+        out = torch.zeros(g, B, Up, dtype=adt, device=DEV)
+        plog = torch.zeros(g, Up // 16, B, C, device=DEV)
+        a = Km.DenseFwdArgs()
+        a.x, a.wt, a.bias, a.out, a.st, a.fold_ids = x.data_ptr(), wt.data_ptr(), b1.data_ptr(), \
+            out.data_ptr(), st.data_ptr(), fids.data_ptr()
+        a.G, a.B, a.Fp, a.Up, a.drop_p, a.train, a.seed = g, B, Fp, Up, 0.5, 1, 7
+        a.w2, a.plog, a.C, a.prec = w2.data_ptr(), plog.data_ptr(), C, prec
+        keep = []
+        if sk:
+            nby, nut = -(-B // 32), Up // 64
+            part = torch.empty(g * nby * nut * ks * 4 * 2 * 64 * 4, device=DEV)
+            cnt = torch.zeros(g * nby * nut, dtype=torch.int32, device=DEV)
+            keep = [part, cnt]
+            a.w1, a.part, a.cnt, a.ks = w1.data_ptr(), part.data_ptr(), cnt.data_ptr(), ks
+        Km.check(L.gt_dense_fwd(a, _stream()), "dense_fwd")
+        torch.cuda.synchronize()
+        return out.clone(), plog.clone()
+
+    ref_h, ref_p = run(G, False)
+    h1, p1 = run(G, True)
+    h2, p2 = run(G, True)
+    assert torch.equal(h1, h2) and torch.equal(p1, p2)
+    hs, ps = run(2, True)                                          # groups 0-1 alone
+    assert torch.equal(hs, h1[:2]) and torch.equal(ps, p1[:2])
+    assert ((h1 == 0) != (ref_h == 0)).float().mean().item() < 1e-4   # same dropout mask (ReLU ties aside)
+    z = torch.relu(torch.bmm(x.double(), w1.double()) + b1.double()[:, None, :])
+    keep_mask = (ref_h != 0)
+    dense = (z * 2.0 * keep_mask).float()                          # inverted dropout, p = 0.5
+    err = ((h1.float() - dense).abs().max() / dense.abs().max()).item()
+    assert err < (1e-5 if prec else 2e-2), err

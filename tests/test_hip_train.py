@@ -176,6 +176,33 @@ def test_fused_pool_matches_separate_pool_kernel(dtype, bn, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype,bn", [("fp32", False), ("bf16", False), ("fp32", True)])
+def test_sequential_folds_job_reuse_bit_identical(dtype, bn, monkeypatch):
+    """Reference fold protocol on ONE rebound job (index tables, fold-keyed
+    seeds and carried biases swapped in place, the captured step graph
+    replayed again) gives exactly the results of a fresh job per fold."""
+    import numpy as np
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.genome import make_plan
+    from gentun_amd.utils.data import make_cifar_like, stratified_kfold
+    x, y = make_cifar_like(n=500, seed=4)
+    folds = stratified_kfold(np.argmax(y, 1), 3, seed=1)
+    genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '111', 'S_2': '1000000001'}]
+    plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
+    cfg = E.TrainConfig(epochs=(1, 1), learning_rate=(1e-3, 5e-4), batch_size=32, dtype=dtype, loss="ce",
+                        batch_norm=bn)
+    out = {}
+    for reuse in ("1", "0"):
+        monkeypatch.setenv("GENTUN_FOLD_REUSE", reuse)
+        job = E.make_population_job("hip", [(p, folds, [0, 1, 2]) for p in plans], x, y, cfg,
+                                    torch.device("cuda", 0))
+        out[reuse] = job.launch().finish()
+        if reuse == "1":
+            assert len({j.flat.data_ptr() for j in job.jobs}) == 1         # one job's buffers for all folds
+    assert out["1"] == out["0"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bn", [False, True])
 def test_small_launch_tiles_bit_identical(bn, monkeypatch):
     """Small launches (2 groups) take shorter conv tiles (4 / 2 rows, one co
