@@ -63,11 +63,16 @@ struct FastCfg {
   static constexpr int NPL = PREC ? GT_NPL_F32 : 1;
   static constexpr int PW = W + KW - 1;
   static constexpr int NP = (TH + KH - 1) * PW * NCBI;
+  // LDS pixel stride of the patch in 16-byte chunks: odd (an even stride -- 8, 16, 32 chunks of
+  // the wide deep space -- put every lane of a ds_read_b128 pass on the same banks: 8-16 way
+  // conflicts, PMC LDSbc 0.7-0.86 on those launches); the S=(3,5) / (20,50,100) strides are odd already
+  static constexpr int NCBP = NCBI + ((NCBI & 1) ? 0 : 1);
+  static constexpr int NPP = (TH + KH - 1) * PW * NCBP;
   static constexpr int TP = TH * W;
   static constexpr int OROW = NT * 16 + 4;          // fp32 tile row (floats; conflict-free float4 writes)
   static constexpr int OROWB = NT * 16 + 8;         // bf16 tile row (elements; conflict-free 8-byte writes)
   static size_t lds(bool fwd) {
-    const size_t p = (size_t)NP * 16 * NPL;
+    const size_t p = (size_t)NPP * 16 * NPL;
     const size_t o = (fwd && !PREC) ? (size_t)TP * OROWB * 2 : (size_t)TP * OROW * 4;
     return p > o ? p : o;
   }
@@ -166,6 +171,13 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int NTH = NWV * 64;                     // threads
   constexpr int PH = TH + KH - 1, PW = W + KW - 1;
   constexpr int NP = PH * PW * NCBI;                // patch chunks (8 channels) per plane
+  constexpr int NCBP = FastCfg<KH, KW, NCBI, W, TH, NT, NCO, PREC>::NCBP;   // LDS chunks per patch pixel
+  constexpr int NPP = PH * PW * NCBP;               // LDS plane stride (chunks)
+  // staged chunk i (pixel i / NCBI, chunk i % NCBI) -> its LDS slot
+  auto pslot = [&](int i) {
+    if constexpr (NCBP == NCBI) return i;
+    else return (i / NCBI) * NCBP + i % NCBI;
+  };
   constexpr int NPT = (NP + NTH - 1) / NTH;             // patch chunks per thread
   constexpr int NCH = KH * KW * NCBI;               // reduction chunks
   constexpr int NKS = (NCH + 3) / 4;                // k-steps (32 k each)
@@ -264,7 +276,7 @@ conv_fast_kernel(ConvArgs a) {
     for (int j = 0; j < NPT; ++j)
 #pragma unroll
       for (int p = 0; p < NPL; ++p)
-        if (tid + NTH * j < NP) patch[p * NP + tid + NTH * j] = make_uint4(0, 0, 0, 0);
+        if (tid + NTH * j < NP) patch[p * NPP + pslot(tid + NTH * j)] = make_uint4(0, 0, 0, 0);
   } else if (!PREC && n_src == 1) {
     uint4 v[NPT];
 #pragma unroll
@@ -272,7 +284,7 @@ conv_fast_kernel(ConvArgs a) {
       v[j] = *reinterpret_cast<const uint4*>(pok[j] ? (const void*)(src0 + poff[j]) : (const void*)gt_zero8);
 #pragma unroll
     for (int j = 0; j < NPT; ++j)
-      if (tid + NTH * j < NP) patch[tid + NTH * j] = v[j];
+      if (tid + NTH * j < NP) patch[pslot(tid + NTH * j)] = v[j];
   } else {
     // chunks in batches of JB with the batch's loads in flight; N-ary DAG
     // input summed in fp32 (prec 0: one rounding to bf16 at the end; prec 1:
@@ -326,11 +338,11 @@ conv_fast_kernel(ConvArgs a) {
         if (PREC) {
           uint4 p0, p1, p2;
           split8(acc8[j], p0, p1, p2);
-          patch[i] = p0;
-          patch[NP + i] = p1;
-          patch[2 * NP + i] = p2;
+          patch[pslot(i)] = p0;
+          patch[NPP + pslot(i)] = p1;
+          patch[2 * NPP + pslot(i)] = p2;
         } else {
-          patch[i] = pack8(acc8[j]);
+          patch[pslot(i)] = pack8(acc8[j]);
         }
       }
     }
@@ -343,10 +355,10 @@ conv_fast_kernel(ConvArgs a) {
       const int cb = i % NCBI, pix = i / NCBI;
       const int r = pix / W, c = pix % W;
       if (h0 + r >= a.H) continue;
-      const int pi = ((r + KH / 2) * PW + c + KW / 2) * NCBI + cb;
+      const int pi = ((r + KH / 2) * PW + c + KW / 2) * NCBP + cb;
       if (PREC) {
         float f[8];
-        join8(patch[pi], patch[NP + pi], patch[2 * NP + pi], f);   // exact: the fp32 sum
+        join8(patch[pi], patch[NPP + pi], patch[2 * NPP + pi], f);   // exact: the fp32 sum
         st_chunk(xo + (long)i * 8, f);
       } else {
         *reinterpret_cast<uint4*>(xo + (long)i * 8) = patch[pi];
@@ -356,7 +368,7 @@ conv_fast_kernel(ConvArgs a) {
   // chunk c -> patch offset of its (kh, kw, cb) relative to the output pixel
   for (int c = tid; c < NKS * 4; c += NTH) {
     const int kk = c / NCBI, cb = c % NCBI;
-    coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
+    coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBP + cb : 0;
   }
   // first PF k-steps of weights in flight before the barrier (after the patch
   // staging: its registers are dead by now -- lower peak register pressure)
@@ -375,11 +387,11 @@ conv_fast_kernel(ConvArgs a) {
 
   // ---- MFMA main loop ------------------------------------------------------
   // lane's pixel within a group: (l16 / W) rows down, l16 % W across (W >= 16: same row)
-  const int lbase = ((l16 / W) * PW + (l16 % W)) * NCBI;
+  const int lbase = ((l16 / W) * PW + (l16 % W)) * NCBP;
   int gbase;
   {
     const int p = pgw * 16;
-    gbase = ((p / W) * PW + (p % W)) * NCBI;
+    gbase = ((p / W) * PW + (p % W)) * NCBP;
   }
   f32x4_t acc[CT][PG];
 #pragma unroll
@@ -391,7 +403,7 @@ conv_fast_kernel(ConvArgs a) {
   auto koff = [&](int s) {
     const int c = s * 4 + kq;
     const int kk = c / NCBI, cb = c - kk * NCBI;
-    return c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
+    return c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBP + cb : 0;
   };
   auto load_b = [&](int s, uint4 (*dst)[NPL]) {
     const uint4* pb = patch + lbase + gbase + ((GT_F32_REGOFF && PREC && NKS <= 64) ? koff(s) : coff[s * 4 + kq]);
@@ -399,7 +411,7 @@ conv_fast_kernel(ConvArgs a) {
     for (int h = 0; h < PG; ++h) {
       const int p = h * 16;                        // relative to the wave's first group
 #pragma unroll
-      for (int q = 0; q < NPL; ++q) dst[h][q] = pb[q * NP + ((p / W) * PW + (p % W)) * NCBI];
+      for (int q = 0; q < NPL; ++q) dst[h][q] = pb[q * NPP + ((p / W) * PW + (p % W)) * NCBP];
     }
   };
   if (!(a.dbg & 1)) {
@@ -1479,12 +1491,13 @@ extern "C" int gt_conv_set_smallq(int on) {
   return old;
 }
 // tile rows for a launch whose default tile has TH rows: halve while the grid
-// is below SMALLQ_WG workgroups (GENTUN_CONV_SMALLQ_WG, default 512), down to THMIN
+// is below GENTUN_CONV_SMALLQ_WG workgroups (default 300: about one per CU; at 5 and 10 groups the
+// 8-row tiles measured faster than 4-row ones, profiles/conv_tile_threshold_ab_r4.txt), down to THMIN
 static long g_smallq_wg = -1;
 static int smallq_th(const ConvArgs* a, int TH, int THMIN) {
   if (g_smallq < 0) g_smallq = std::getenv("GENTUN_CONV_SMALLQ") ? std::atoi(std::getenv("GENTUN_CONV_SMALLQ")) : 1;
   if (g_smallq_wg < 0)
-    g_smallq_wg = std::getenv("GENTUN_CONV_SMALLQ_WG") ? std::atol(std::getenv("GENTUN_CONV_SMALLQ_WG")) : 512;
+    g_smallq_wg = std::getenv("GENTUN_CONV_SMALLQ_WG") ? std::atol(std::getenv("GENTUN_CONV_SMALLQ_WG")) : 300;
   if (!g_smallq) return TH;
   int th = TH;
   while (th > THMIN && (long)a->ngroups * a->B * (a->H / th) < g_smallq_wg) th >>= 1;
@@ -1816,12 +1829,27 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
   constexpr int XCH = PR * PW * NCBI;              // staged input chunks per band (per plane)
   constexpr int DCH = R * W * NCBO;                // staged dz chunks per band (per plane)
   constexpr int XT = (XCH + NT_ - 1) / NT_, DT = (DCH + NT_ - 1) / NT_;
-  constexpr int XROW = NCBI * 16, DROW = NCBO * 16;   // LDS bytes per pixel (one plane)
+  // LDS pixel strides in 16-byte chunks, odd: an even stride (8 / 16 / 32 chunks, the wide deep
+  // space) put the 8 pixels of a ds_read_b64_tr_b16 pass on the same banks (PMC LDSbc 0.7-0.8)
+  // (kept unpadded when the padded double buffers would not fit the 160 KB of LDS)
+  constexpr int NCBIP0 = NCBI + ((NCBI & 1) ? 0 : 1), NCBOP0 = NCBO + ((NCBO & 1) ? 0 : 1);
+  constexpr bool PADOK = (long)NB * NPL * (PR * PW * NCBIP0 + R * W * NCBOP0) * 16 + (long)NB * R * W * 32 <= 160 * 1024;
+  constexpr int NCBIP = PADOK ? NCBIP0 : NCBI, NCBOP = PADOK ? NCBOP0 : NCBO;
+  constexpr int XCHL = PR * PW * NCBIP, DCHL = R * W * NCBOP;   // LDS chunks per band (per plane)
+  constexpr int XROW = NCBIP * 16, DROW = NCBOP * 16;   // LDS bytes per pixel (one plane)
+  auto xslot = [&](int i) {
+    if constexpr (NCBIP == NCBI) return i;
+    else return (i / NCBI) * NCBIP + i % NCBI;
+  };
+  auto dslot = [&](int i) {
+    if constexpr (NCBOP == NCBO) return i;
+    else return (i / NCBO) * NCBOP + i % NCBO;
+  };
   constexpr bool MOUT = NZ > 1;                    // co tiles in the outer loop
   static_assert(R * W % 32 == 0 && (W == 8 || W == 16 || W == 32), "bands must be whole 32-pixel K-steps");
 
-  __shared__ __attribute__((aligned(16))) uint4 xs[NB][NPL][XCH];
-  __shared__ __attribute__((aligned(16))) uint4 ds[NB][NPL][DCH];
+  __shared__ __attribute__((aligned(16))) uint4 xs[NB][NPL][XCHL];
+  __shared__ __attribute__((aligned(16))) uint4 ds[NB][NPL][DCHL];
   constexpr int PKC = 2 * (MT - 1);                // dz chunk holding the packed tile's channels
   constexpr int PKR = PK ? R * W : 1;
   __shared__ __attribute__((aligned(16))) uint4 dpk[NB][PKR][2];   // packed plane rows per pixel (PK)
@@ -1892,7 +1920,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < XT; ++j) {
       const int i = tid + NT_ * j;
-      if (i < XCH) split8(xr[j], xs[buf][0][i], xs[buf][1][i], xs[buf][2][i]);
+      if (i < XCH) split8(xr[j], xs[buf][0][xslot(i)], xs[buf][1][xslot(i)], xs[buf][2][xslot(i)]);
     }
 #pragma unroll
     for (int j = 0; j < DT; ++j) {
@@ -1900,9 +1928,9 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
       if (i >= DCH) continue;
       uint4 q0, q1, q2;
       split8(dr[j], q0, q1, q2);
-      ds[buf][0][i] = q0;
-      ds[buf][1][i] = q1;
-      ds[buf][2][i] = q2;
+      ds[buf][0][dslot(i)] = q0;
+      ds[buf][1][dslot(i)] = q1;
+      ds[buf][2][dslot(i)] = q2;
       if (PK && i % NCBO == PKC) {
         // channels 16 (MT-1) + c, c < 4: plane p at element 4c + p (element 4c + 3 = 0)
         const int creal = a.cout_real - 16 * (MT - 1);

@@ -6,6 +6,7 @@
 #   bash tools/gpu.sh timeline                kernel timeline of a population step (P=5 SAMPLES=2000 SPACE= KERNELS= BN=)
 #   bash tools/gpu.sh prof NAME -- CMD...     rocprofv3 --kernel-trace --stats, keeps the stats CSVs
 #   bash tools/gpu.sh pmc NAME "CTRS" -- CMD  one PMC pass (kernel-trace only) + tools/pmc_summary.py
+#   bash tools/gpu.sh profstep                stats + 3 PMC passes of a population step -> tools/pmc_table.py (P= SPACE= KERNELS= BN= OUT=)
 #   bash tools/gpu.sh conv                    conv microbench tools/bench_conv.py (GS="25" ONLY= DBGS=0), fp32 tests first
 #   bash tools/gpu.sh ab                      tests + population-step A/B: ab_old/ (built previous tree) vs this tree
 #   bash tools/gpu.sh qcurve                  groups per launch vs throughput, both fold protocols
@@ -64,6 +65,23 @@ pmc)
     > gpurun_out/pmc_$name/run.log 2>&1 || { tail -5 gpurun_out/pmc_$name/run.log; exit 1; }
   python3 tools/pmc_summary.py /tmp/pmc_$name > gpurun_out/pmc_$name/summary.txt
   head -30 gpurun_out/pmc_$name/summary.txt ;;
+profstep)
+  out=gpurun_out/${OUT:-profstep}; mkdir -p $out; rocprof_env; export WARM=0
+  cmd="python3 tools/probe_pop.py ${P:-5} ${P:-5} 1 1 ${SAMPLES:-2000}"
+  rm -rf /tmp/ps_stats
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats -d /tmp/ps_stats -o run --output-format csv -- $cmd \
+    > $out/stats_run.log 2>&1 || { tail -5 $out/stats_run.log; exit 1; }
+  find /tmp/ps_stats -name "*kernel_stats.csv" -exec cp {} $out/kernel_stats.csv \;
+  i=0
+  for ctr in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE" \
+             "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE" \
+             "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+    i=$((i+1)); rm -rf /tmp/ps_pmc$i
+    timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctr -d /tmp/ps_pmc$i -o run --output-format csv -- $cmd \
+      > $out/pmc$i.log 2>&1 || { tail -5 $out/pmc$i.log; exit 1; }
+    python3 tools/pmc_summary.py /tmp/ps_pmc$i > $out/pmc$i.txt
+  done
+  python3 tools/pmc_table.py $out > $out/table.txt; head -24 $out/table.txt ;;
 conv)
   timeout -k 10 300 python -u -m pytest tests/test_hip_fp32.py -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/fp32_tests.log 2>&1 || { tail -30 gpurun_out/fp32_tests.log; exit 1; }
