@@ -54,6 +54,10 @@
 #ifndef GT_F32_PFM
 #define GT_F32_PFM 2
 #endif
+// 1: the double-buffered fp32 wgrad's two wave halves stage and multiply in opposite orders (see the kernel)
+#ifndef GT_WGRAD_HALVES
+#define GT_WGRAD_HALVES 1
+#endif
 
 // LDS bytes of one launch: the patch (NPL bf16 planes) or the output tile
 // (fp32, or bf16 for prec-0 forward launches -- measured 7-9 % faster: more
@@ -1973,15 +1977,29 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 #pragma unroll
     for (int t = 0; t < TPW; ++t) acc[m][t] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
+  // Two buffers: the two halves of the workgroup (waves w and w + NW/2 share a SIMD) take
+  // opposite orders inside a band -- the first half multiplies, then stages the next band; the
+  // second half stages first (from registers loaded one band earlier), then multiplies -- so on
+  // every SIMD one wave's split + LDS stores run beside the other wave's MFMAs instead of all
+  // waves staging while the matrix pipe idles. Same per-wave MFMA order: bit-identical.
+  const bool early = NB == 2 && GT_WGRAD_HALVES && wave >= NW / 2;
   if (band0 < band1) {
     load(band0);
     store(0);
+    if (early && band0 + 1 < band1) load(band0 + 1);
   }
   int cur = 0;
   for (int band = band0; band < band1; ++band, cur ^= (NB - 1)) {
     __syncthreads();                      // band `cur` staged everywhere; the other buffer no longer read
     const bool more = band + 1 < band1;
-    if (more) load(band + 1);             // global loads in flight during the MFMAs
+    if (early) {
+      if (more) {
+        store(cur ^ 1);                   // band + 1, loaded during the previous band
+        if (band + 2 < band1) load(band + 2);
+      }
+    } else if (more) {
+      load(band + 1);                     // global loads in flight during the MFMAs
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int xrow_off = ((ks * 32) / W) * PW * XROW;        // compile-time after unrolling
@@ -2050,7 +2068,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
         }
       }
     }
-    if (more) {
+    if (more && !early) {
       if (NB == 1) __syncthreads();       // every wave is done reading the single buffer
       store(cur ^ (NB - 1));
     }

@@ -1,5 +1,9 @@
 # step PMC profile at the bench round size (25 groups), and the separate-vs-fused wgrad split reduction A/B
 set -o pipefail
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_hip_kernels.py tests/test_hip_train.py tests/test_hip_dense_stream.py > gpurun_out/r4c11_tests.log 2>&1 \
+  || { tail -30 gpurun_out/r4c11_tests.log; exit 1; }
+tail -1 gpurun_out/r4c11_tests.log
 P=5 OUT=profstep_p5 bash tools/gpu.sh profstep || exit 1
 for spec in "kernels 2" "all 5" "all 2"; do
   set -- $spec

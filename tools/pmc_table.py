@@ -3,7 +3,7 @@
 usage: python tools/pmc_table.py DIR   (DIR holds kernel_stats.csv and pmc1.txt .. pmc3.txt)
 
 Columns: mean us per call (kernel stats); MFMA% = SQ_VALU_MFMA_BUSY_CYCLES per CU-cycle
-(GRBM_GUI_ACTIVE x 256 CUs, x4 SIMDs -> a busy pipe on every SIMD = 100 %); LDSbc =
+(GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs: a busy pipe on every SIMD = 100 %); LDSbc =
 SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; issue-stall = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES;
 L2 hit = TCC_HIT / (TCC_HIT + TCC_MISS); rd / wr MB = TCC_EA0_RDREQ / WRREQ x 64 B (upper bound:
 128-B reads tallied at 64 B).
@@ -41,7 +41,7 @@ print("{:48s} {:>8s} {:>6s} {:>6s} {:>6s} {:>6s} {:>8s} {:>8s}".format(
 for name in sorted(pm, key=lambda n: -us.get(n, 0.0)):
     c = pm[name]
     g = c.get("GRBM_GUI_ACTIVE", 0.0)
-    mf = 100.0 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (g * ncu * 4) if g else 0.0
+    mf = 100.0 * c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (g / 8 * ncu * 4) if g else 0.0   # GRBM summed over 8 XCDs
     lds = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"] if c.get("SQ_LDS_IDX_ACTIVE") else 0.0
     stall = c.get("SQ_WAIT_INST_ANY", 0.0) / c["SQ_WAVE_CYCLES"] if c.get("SQ_WAVE_CYCLES") else 0.0
     h, m = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
