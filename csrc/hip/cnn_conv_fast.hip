@@ -39,6 +39,11 @@
 #define GT_STAGE_SELECT 0
 #endif
 
+// 1: multi-input (N-ary Add) patch staging loads two inputs per round trip (see conv_fast_kernel)
+#ifndef GT_STAGE_PAIRS
+#define GT_STAGE_PAIRS 1
+#endif
+
 #ifndef GT_F32_NO_BPIPE
 #define GT_F32_NO_BPIPE 0      // 1: fp32 conv main loop without the patch-fragment pipeline (A/B builds)
 #endif
@@ -53,6 +58,11 @@
 // weight (A operand) prefetch depth of the fp32 tile kernel, in k-steps (3 planes each)
 #ifndef GT_F32_PFM
 #define GT_F32_PFM 2
+#endif
+// 1: the fp32 tile kernel keeps every k-step's patch offset in registers (read once from the LDS table);
+// measured neutral at 25 groups (profiles/conv_f32_kreg_ab_r4.txt): off
+#ifndef GT_F32_KREG
+#define GT_F32_KREG 0
 #endif
 // 1: the double-buffered fp32 wgrad's two wave halves stage and multiply in opposite orders (see the kernel)
 #ifndef GT_WGRAD_HALVES
@@ -241,7 +251,8 @@ conv_fast_kernel(ConvArgs a) {
   }
   uint4 areg[PF][CT][NPL];
   auto load_a = [&](int s, uint4 (*dst)[NPL]) {
-    const int c = s * 4 + kq;
+    // (dbg bit 8, diagnostics only: every k-step re-reads k-step 0's weights -- L1-resident operands)
+    const int c = ((a.dbg & 8) ? 0 : s * 4) + kq;
 #pragma unroll
     for (int t = 0; t < CT; ++t)
 #pragma unroll
@@ -313,6 +324,40 @@ conv_fast_kernel(ConvArgs a) {
 #else
           if (j0 + j < NPT && pok[j0 + j]) ld_chunk(src0 + poff[j0 + j], acc8[j]);
 #endif
+      } else if (GT_STAGE_PAIRS) {
+        // DAG inputs two at a time: both inputs' chunk loads are in flight before either is
+        // summed (one input at a time waited a global round trip per input). Still summed in
+        // increasing slot order: bit-identical.
+        int m = gr.in_mask & 0xff;
+        while (m) {
+          const int k0 = __builtin_ctz(m);
+          m &= m - 1;
+          const bool two = m != 0;
+          const int k1 = two ? __builtin_ctz(m) : k0;
+          if (two) m &= m - 1;
+          const AT* s0 = static_cast<const AT*>(a.in[k0]) + gimg;
+          const AT* s1 = static_cast<const AT*>(a.in[k1]) + gimg;
+          float t0[JB][8], t1[JB][8];
+#pragma unroll
+          for (int j = 0; j < JB; ++j) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t0[j][e] = t1[j][e] = 0.f;
+            if (j0 + j < NPT && pok[j0 + j]) {
+              ld_chunk(s0 + poff[j0 + j], t0[j]);
+              if (two) ld_chunk(s1 + poff[j0 + j], t1[j]);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < JB; ++j)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc8[j][e] += t0[j][e];
+          if (two) {
+#pragma unroll
+            for (int j = 0; j < JB; ++j)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) acc8[j][e] += t1[j][e];
+          }
+        }
       } else {
 #pragma unroll
         for (int k = 0; k < GT_MAXSLOT; ++k) {
@@ -409,8 +454,17 @@ conv_fast_kernel(ConvArgs a) {
     const int kk = c / NCBI, cb = c - kk * NCBI;
     return c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBP + cb : 0;
   };
+  // fp32, unrolled k loop: every k-step's patch offset read from the LDS table ONCE, up front, into
+  // registers (NKS VGPRs) -- no table lookup + lgkmcnt drain in front of each k-step's B reads
+  constexpr bool KREG = GT_F32_KREG && PREC != 0 && NKS <= 64 && !GT_F32_REGOFF;
+  int kreg[KREG ? NKS : 1];
+  if constexpr (KREG) {
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) kreg[s] = lbase + gbase + coff[s * 4 + kq];
+  }
   auto load_b = [&](int s, uint4 (*dst)[NPL]) {
-    const uint4* pb = patch + lbase + gbase + ((GT_F32_REGOFF && PREC && NKS <= 64) ? koff(s) : coff[s * 4 + kq]);
+    const uint4* pb = KREG ? patch + kreg[KREG ? s : 0]
+                           : patch + lbase + gbase + ((GT_F32_REGOFF && PREC && NKS <= 64) ? koff(s) : coff[s * 4 + kq]);
 #pragma unroll
     for (int h = 0; h < PG; ++h) {
       const int p = h * 16;                        // relative to the wave's first group
