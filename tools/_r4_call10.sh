@@ -1,4 +1,6 @@
 # config-3 share on one GPU (about 2 candidates per rank per generation: 10 groups concurrent folds, 2 reference
+( while sleep 50; do date >> gpurun_out/heartbeat; done ) & HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
 # folds), then the Q-curve republished at this tree
 set -o pipefail
 mkdir -p gpurun_out/c3share
