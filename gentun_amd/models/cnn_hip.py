@@ -118,16 +118,18 @@ class HipPopJob(FoldJob):
         # weight-gradient side stream: every conv wgrad and the dense W1
         # optimizer run concurrently with the data-gradient chain (fork / join
         # edges inside the captured step graph)
-        self.side = torch.cuda.Stream(dev)
+        # GENTUN_SIDE_PRIO: priority of the side streams (A/B; HIP: lower = higher priority)
+        sprio = int(os.environ.get("GENTUN_SIDE_PRIO", "0"))
+        self.side = torch.cuda.Stream(dev, priority=sprio)
         # the conv wgrads of different layers are independent (own dz, own
         # partial buffers): round-robin over GENTUN_WGRAD_STREAMS streams so a
         # small launch (few groups: 64 workgroups) does not serialise the
         # backward tail behind one wgrad at a time
         nws = max(1, int(os.environ.get("GENTUN_WGRAD_STREAMS", "2")))
-        self.wg_streams = [self.side] + [torch.cuda.Stream(dev) for _ in range(nws - 1)]
+        self.wg_streams = [self.side] + [torch.cuda.Stream(dev, priority=sprio) for _ in range(nws - 1)]
         # the dense W1 optimizer (the largest single launch) on a stream of its
         # own, so it does not sit in front of the first conv wgrads
-        self.side2 = torch.cuda.Stream(dev)
+        self.side2 = torch.cuda.Stream(dev, priority=sprio)
         # GENTUN_OVERLAP=0: one stream (A/B of the fork / join edges at small launches)
         self.overlap = os.environ.get("GENTUN_OVERLAP", "1") != "0"
         self.w1_stream = os.environ.get("GENTUN_W1_STREAM", "1") != "0"

@@ -40,7 +40,7 @@ for _ in range(P):
     plans.append(make_plan(g, nodes, (32, 32, 3), kernels, ((5, 5),) * len(nodes), 500, 10))
 cfg = E.TrainConfig(epochs=(epochs,), learning_rate=(1e-3,), batch_size=32, dtype=os.environ.get("DTYPE", "fp32"),
                     loss="ce", reset=os.environ.get("RESET", "all"), batch_norm=os.environ.get("BN", "0") == "1")
-streams = [torch.cuda.Stream(dev) for _ in range(ns)]
+streams = [torch.cuda.Stream(dev, priority=int(os.environ.get("MAIN_PRIO", "0"))) for _ in range(ns)]
 # warm-up (allocator, code objects); WARM=0 keeps profiles free of the small warm-up job
 if os.environ.get("WARM", "1") != "0":
     E.make_population_job("hip", [(plans[0], folds, list(range(5)))], x, y, cfg, dev).launch().finish()
