@@ -60,9 +60,11 @@
 #define GT_F32_PFM 2
 #endif
 // 1: the stage-2 3x3 fp32 shape (7 input chunks, 16 wide) reduces its chunks PART-MAJOR -- (kh, kw, cb)
-// for cb 0-3, then for cb 4-6 -- in every kernel that runs it, so the split-staging kernel
-// (conv_s2split_kernel: the second part's loads overlap the first part's MFMAs) and the small-launch
-// tiles stay bit-identical to each other
+// for cb 0-3, then for cb 4-6 -- in every kernel that runs it (so the small-launch tiles stay
+// bit-identical to the 8-row one): +2.6 % per population step over the kk-major order
+// (profiles/conv_s2_parts_split_ab_r4.txt). A two-part staging kernel built on it (part-1 loads in
+// flight during the part-0 k-steps) and a bank-paired order were measured slower and removed
+// (same file; profiles/conv_s2_bank_order_ab_r4.txt).
 #ifndef GT_S2_PARTS
 #define GT_S2_PARTS 1
 #endif
@@ -677,225 +679,6 @@ conv_fast_kernel(ConvArgs a) {
     if (a.pool_y && ((gr.out_mask >> 24) & 1))
       fused_pool<TH, W, NCO, NTH, PREC>(
           a, [&](int p, int cb, float* f) { load8f(otile + p * OROW + cb * 8, f); }, g, b, h0, tid);
-}
-
-// ---------------------------------------------------------------------------
-// Stage-2 3x3 fp32 conv / data gradient with the patch staged in TWO channel
-// parts (the tile kernel stages the whole patch, then multiplies: ~a third of
-// its time is the staging phase with the matrix pipe idle, tools/bench_conv.py
-// dbg 6). Part 0 = chunks 0-3 of every patch pixel is staged; then the global
-// loads of part 1 (chunks 4-6) are issued, the 9 k-steps that read only part 0
-// run (part-major order, GT_S2_PARTS) while they are in flight, part 1 is
-// split into planes and stored (other LDS slots: no barrier before it), and
-// the 7 remaining k-steps run. Same k order, same epilogue as the tile kernel
-// with GT_S2_PARTS: bit-identical to it. Shape: 3x3, 7 chunks in, 16 wide,
-// 8-row tiles, 4 co tiles (2 per wave) x 8 pixel groups (4 per wave), 4 waves.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-conv_s2split_kernel(ConvArgs a) {
-  constexpr int KW = 3, NCBI = 7, W = 16, TH = 8, NCO = 7, NTH = 256;
-  constexpr int NPL = GT_NPL_F32;
-  constexpr int PW = W + 2, NPIX = (TH + 2) * PW, NCBP = NCBI, NPP = NPIX * NCBP;
-  constexpr int C0 = 4, C1 = NCBI - C0;
-  constexpr int NP0 = NPIX * C0, NP1 = NPIX * C1;
-  constexpr int NPT0 = (NP0 + NTH - 1) / NTH, NPT1 = (NP1 + NTH - 1) / NTH;
-  constexpr int NCH = 9 * NCBI;
-  constexpr int KS0 = 9, NKS = (NCH + 3) / 4;      // 9 part-0 k-steps of 16
-  constexpr int CT = 2, WC = 2, PG = 4, PF = 2;
-  static_assert(S2P_E0 == KS0 * 4, "part 0 = whole k-steps");
-  static_assert(NPT0 == NPT1, "one register layout for both parts' chunks");
-  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-  uint4* patch = smem;
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
-  const int nbx = gridDim.x, total = nbx * gridDim.y;
-  int lin = blockIdx.y * nbx + blockIdx.x;
-  if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
-  const int by = lin / nbx, bx = lin - by * nbx;
-  const int nband = a.H / TH;
-  const int b = bx / nband, h0 = (bx - b * nband) * TH;
-  const GroupRec gr = group_rec(a.gtab, by, a.n_in, a.n_out, a.acc_flags, a.out_mask);
-  const int g = gr.g;
-  const long img = (long)a.H * W * NCBI * 8;
-
-  // ---- weights (A): entry e = 4 s + kq of the part-major chunk list
-  const int wco = (wave % WC) * CT, pgw = (wave / WC) * PG;
-  const uint16_t* wrow[CT];
-  bool wok[CT];
-#pragma unroll
-  for (int t = 0; t < CT; ++t) {
-    const int co = (wco + t) * 16 + l16;
-    wok[t] = co < NCO * 8;
-    wrow[t] = a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8);
-  }
-  auto ent = [&](int e, int& kk, int& cb) {
-    if (e < S2P_E0) { kk = e >> 2; cb = e & 3; }
-    else { const int e1 = e - S2P_E0; kk = e1 / 3; cb = 4 + e1 - kk * 3; }
-  };
-  uint4 areg[PF][CT][NPL];
-  auto load_a = [&](int s, uint4 (*dst)[NPL]) {
-    const int e = s * 4 + kq;
-    int kk, cb;
-    ent(e, kk, cb);
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int p = 0; p < NPL; ++p)
-        dst[t][p] = *reinterpret_cast<const uint4*>((wok[t] && e < NCH) ? (const void*)(wrow[t] + p * a.wps + (kk * NCBI + cb) * 8)
-                                                                          : (const void*)gt_zero8);
-  };
-  // this lane's patch offset of every k-step (registers; part 0: (kk = s, cb = kq))
-  int koff[NKS];
-#pragma unroll
-  for (int s = 0; s < NKS; ++s) {
-    int kk, cb;
-    ent(s * 4 + kq, kk, cb);
-    koff[s] = s * 4 + kq < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBP + cb : 0;
-  }
-
-  // ---- patch staging of one part: chunk i -> (pixel i / C, chunk CB0 + i % C)
-  const long gimg = ((long)g * a.B + b) * img;
-  const int n_src = a.gather ? 1 : __builtin_popcount(gr.in_mask);
-  const float* src0 = a.gather ? static_cast<const float*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + g) * a.B + b] * img
-                               : static_cast<const float*>(a.in[__builtin_ctz(gr.in_mask | 0x100) & 7]) + gimg;
-  auto geo = [&](int i, int C, int CB0, long& off, bool& ok, int& slot) {
-    const int pix = i / C, cb = CB0 + (i - (i / C) * C);
-    const int pr = pix / PW, pc = pix - pr * PW;
-    const int hh = h0 - 1 + pr, ww = pc - 1;
-    ok = hh >= 0 && hh < a.H && ww >= 0 && ww < W;
-    off = ((long)hh * W + ww) * (NCBI * 8) + cb * 8;
-    slot = pix * NCBP + cb;
-  };
-  // the other DAG inputs of chunk sets already holding the first input's values, two per round trip
-  auto add_rest = [&](auto& r, const long* off, const bool* ok, int nj) {
-    int m = (gr.in_mask & 0xff) & ((gr.in_mask & 0xff) - 1);      // every input but the first
-    while (m) {
-      const int k0 = __builtin_ctz(m);
-      m &= m - 1;
-      const bool two = m != 0;
-      const int k1 = two ? __builtin_ctz(m) : k0;
-      if (two) m &= m - 1;
-      const float* s0 = static_cast<const float*>(a.in[k0]) + gimg;
-      const float* s1 = static_cast<const float*>(a.in[k1]) + gimg;
-      float t0[NPT0][8], t1[NPT0][8];
-#pragma unroll
-      for (int j = 0; j < NPT0; ++j) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) t0[j][e] = t1[j][e] = 0.f;
-        if (j < nj && ok[j]) {
-          load8f(s0 + off[j], t0[j]);
-          if (two) load8f(s1 + off[j], t1[j]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NPT0; ++j)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) r[j][e] += t0[j][e];
-      if (two) {
-#pragma unroll
-        for (int j = 0; j < NPT0; ++j)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) r[j][e] += t1[j][e];
-      }
-    }
-  };
-  auto store = [&](auto& r, const int* slot, const bool* live, int nj) {
-#pragma unroll
-    for (int j = 0; j < NPT0; ++j) {
-      if (j >= nj || !live[j]) continue;
-      uint4 p0, p1, p2;
-      split8(r[j], p0, p1, p2);
-      patch[slot[j]] = p0;
-      patch[NPP + slot[j]] = p1;
-      patch[2 * NPP + slot[j]] = p2;
-    }
-  };
-  auto write_xsum = [&](int C, int CB0) {        // this part's chunks of the summed input (for the wgrad)
-    float* xo = static_cast<float*>(a.xsum) + gimg + (long)h0 * W * NCBI * 8;
-    for (int i = tid; i < TH * W * C; i += NTH) {
-      const int pix = i / C, cb = CB0 + i % C;
-      const int r = pix / W, c = pix % W;
-      const int pi = ((r + 1) * PW + c + 1) * NCBP + cb;
-      float f[8];
-      join8(patch[pi], patch[NPP + pi], patch[2 * NPP + pi], f);
-      st_chunk(xo + ((long)pix * NCBI + cb) * 8, f);
-    }
-  };
-
-  // part 0: staged before any MFMA
-  {
-    float r[NPT0][8];
-    long off[NPT0];
-    bool ok[NPT0], live[NPT0];
-    int slot[NPT0];
-#pragma unroll
-    for (int j = 0; j < NPT0; ++j) {
-      const int i = tid + NTH * j;
-      geo(i < NP0 ? i : 0, C0, 0, off[j], ok[j], slot[j]);
-      live[j] = i < NP0;
-      ok[j] = ok[j] && live[j];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) r[j][e] = 0.f;
-      if (ok[j]) load8f(src0 + off[j], r[j]);
-    }
-    if (n_src > 1) add_rest(r, off, ok, NPT0);
-    store(r, slot, live, NPT0);
-  }
-#pragma unroll
-  for (int s = 0; s < PF; ++s) load_a(s, areg[s]);
-  __syncthreads();                                // (the register epilogue reads the bias itself)
-  if (a.xsum && n_src > 1) write_xsum(C0, 0);
-
-  // part 1: global loads in flight during the part-0 k-steps (first input only; the others after)
-  float r1[NPT1][8];
-  long off1[NPT1];
-  bool ok1[NPT1], live1[NPT1];
-  int slot1[NPT1];
-#pragma unroll
-  for (int j = 0; j < NPT1; ++j) {
-    const int i = tid + NTH * j;
-    geo(i < NP1 ? i : 0, C1, C0, off1[j], ok1[j], slot1[j]);
-    live1[j] = i < NP1;
-    ok1[j] = ok1[j] && live1[j];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) r1[j][e] = 0.f;
-    if (ok1[j]) load8f(src0 + off1[j], r1[j]);
-  }
-
-  // ---- MFMA k loop: part 0, then part 1 after its staging
-  const int pbase = (l16 + pgw * PW) * NCBP;      // lane pixel (W = 16: one row per group) + wave's first row
-  f32x4_t acc[CT][PG];
-#pragma unroll
-  for (int t = 0; t < CT; ++t)
-#pragma unroll
-    for (int h = 0; h < PG; ++h) acc[t][h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  auto load_b = [&](int s, uint4 (*dst)[NPL]) {
-    const uint4* pb = patch + pbase + koff[s];
-#pragma unroll
-    for (int h = 0; h < PG; ++h)
-#pragma unroll
-      for (int q = 0; q < NPL; ++q) dst[h][q] = pb[q * NPP + h * PW * NCBP];
-  };
-  uint4 bfr[2][PG][NPL];
-  auto kstep = [&](int s) {
-    if (s + 1 < NKS && s + 1 != KS0) load_b(s + 1, bfr[(s + 1) & 1]);
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int h = 0; h < PG; ++h) acc[t][h] = mfma_np<NPL>(areg[s % PF][t], bfr[s & 1][h], acc[t][h]);
-    if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
-  };
-  load_b(0, bfr[0]);
-#pragma unroll
-  for (int s = 0; s < KS0; ++s) kstep(s);
-  if (n_src > 1) add_rest(r1, off1, ok1, NPT1);
-  store(r1, slot1, live1, NPT1);
-  __syncthreads();
-  if (a.xsum && n_src > 1) write_xsum(C1, C0);
-  load_b(KS0, bfr[KS0 & 1]);
-#pragma unroll
-  for (int s = KS0; s < NKS; ++s) kstep(s);
-
-  f32_epi_regs<CT, PG, 0, W, NCO, true>(a, gr, b, h0, acc, wco, pgw, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -1816,20 +1599,6 @@ static int smallq_th(const ConvArgs* a, int TH, int THMIN) {
   return th;
 }
 
-// the two-part staging kernel of the stage-2 3x3 fp32 shape (A/B: GENTUN_S2_SPLIT=0, gt_conv_set_s2split)
-static int g_s2split = -1;
-static bool s2split_on() {
-  // off by default: slower than the tile kernel in the same order (profiles/conv_s2_parts_split_ab_r4.txt)
-  if (g_s2split < 0) g_s2split = std::getenv("GENTUN_S2_SPLIT") ? std::atoi(std::getenv("GENTUN_S2_SPLIT")) : 0;
-  return g_s2split != 0;
-}
-extern "C" int gt_conv_set_s2split(int on) {
-  s2split_on();
-  const int old = g_s2split;
-  g_s2split = on;
-  return old;
-}
-
 extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
   stagger_init();
   ConvArgs lc = *a_in;
@@ -1860,15 +1629,6 @@ extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
     }
     if (s2in_ct1_on() && CONV_FAST_MATCH(5, 5, 7, 16, 8, 2, 3) && smallq_th(a, 8, 4) == 4)   // s2 input dgrad
       CONV_FAST_LAUNCH_CT1(5, 5, 7, 16, 4, 2, 3, 4)
-    // s2 nodes / dgrad, 8-row tiles: the two-part staging kernel (bit-identical to the tile kernel)
-    if (GT_S2_PARTS && CONV_FAST_MATCH(3, 3, 7, 16, 8, 4, 7) && s2split_on() && regepi_on() && !a->dbg) {
-      if (g_probe) return 1000 + 8;
-      dim3 grid(a->B * (a->H / 8), a->ngroups);
-      const size_t lds = FastCfg<3, 3, 7, 16, 8, 4, 7, 1>::lds(a->epi_bf16 != 0);
-      lds_limit(conv_s2split_kernel, lds);
-      hipLaunchKernelGGL(conv_s2split_kernel, grid, dim3(256), lds, stream, *a);
-      return (int)hipGetLastError();
-    }
     // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
     CONV_FAST_CASE_F32_PK(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
     CONV_FAST_CASE_F32_PK(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)

@@ -540,74 +540,3 @@ def test_s2in_dgrad_variants(mode):
         d = (outs[0][i][..., 16:cin] - outs[1][i][..., 16:cin]).abs().max().item()
         assert d <= 4 * e32 * ref.abs().max().item() + 1e-30, d         # 9- vs 6-term: rounding only
 
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("nin", [1, 2, 3])
-def test_s2_split_staging_bit_identical(nin):
-    """The two-part staging kernel of the stage-2 3x3 conv (conv_s2split_kernel:
-    part-1 loads in flight during the part-0 k-steps) against the tile kernel
-    with the same part-major reduction order: forward (bias, ReLU, fused pool,
-    the summed-input copy for the wgrad) and data gradient (fan-out: write,
-    accumulate + ReLU mask) bitwise equal, both within fp32 level of fp64."""
-    Km = K()
-    L = Km.lib()
-    torch.manual_seed(21)
-    G, B, H, W, cin, cout, k = 5, 32, 16, 16, 50, 50, 3          # 320 workgroups: the 8-row tiles
-    cinp, coutp = 56, 56
-    xs = [torch.randn(G, B, cin, H, W) for _ in range(nin)]
-    w = torch.randn(G, cout, cin, k, k) * (1.0 / math.sqrt(cin * k * k))
-    bvec = torch.randn(G, cout) * 0.1
-    x_in = [torch.stack([nhwc_pad(x[g], cinp) for g in range(G)]).to(DEV).contiguous() for x in xs]
-    wp = torch.stack([pack_w(w[g], coutp, cinp) for g in range(G)]).to(DEV)
-    wpl = _split(wp).contiguous()
-    wT = _split(wp.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous()).contiguous()
-    bp = torch.zeros(G, coutp, device=DEV)
-    bp[:, :cout] = bvec.to(DEV)
-    dz = torch.stack([nhwc_pad(torch.randn(B, cout, H, W), coutp) for _ in range(G)]).to(DEV).contiguous()
-    prev = torch.randn(G, B, H, W, cinp, device=DEV)
-    prev[..., cin:] = 0
-    pmask = torch.randn(G, B, H, W, cinp, device=DEV)
-    out = {}
-    try:
-        for split in (1, 0):
-            L.gt_conv_set_s2split(split)
-            y = torch.zeros(G, B, H, W, coutp, device=DEV)
-            xsum = torch.zeros(G, B, H, W, cinp, device=DEV)
-            py = torch.zeros(G * B, H // 2, W // 2, coutp, device=DEV)
-            pm = torch.zeros(G * B, H // 2, W // 2, coutp, dtype=torch.uint8, device=DEV)
-            rows = torch.tensor([[g, (1 << nin) - 1, 1 | (1 << 24), 0] for g in range(G)], dtype=torch.int32, device=DEV)
-            a = Km.ConvArgs()
-            for i, t in enumerate(x_in):
-                a.inp[i] = t.data_ptr()
-            a.out[0] = y.data_ptr()
-            a.gtab, a.ngroups, a.relu, a.epi_bf16 = rows.data_ptr(), G, 1, 1
-            a.w, a.bias, a.wps = wpl.data_ptr(), bp.data_ptr(), wpl[0].numel()
-            a.xsum = xsum.data_ptr() if nin > 1 else 0
-            a.pool_y, a.pool_mask = py.data_ptr(), pm.data_ptr()
-            a.G, a.B, a.H, a.W, a.Cinp, a.Coutp, a.KH, a.KW = G, B, H, W, cinp, coutp, k, k
-            a.TH, a.prec, a.cout_real = 8, 1, cout
-            Km.check(L.gt_conv_fwd(a, stream()), "fwd")
-            o0 = torch.zeros(G, B, H, W, cinp, device=DEV)
-            o1 = prev.clone()
-            drows = torch.tensor([[g, 1, 0b11 | (0b10 << 8) | (0b10 << 16), 0] for g in range(G)], dtype=torch.int32,
-                                 device=DEV)
-            d = Km.ConvArgs()
-            d.inp[0] = dz.data_ptr()
-            d.out[0], d.out[1] = o0.data_ptr(), o1.data_ptr()
-            d.out_mask[1] = pmask.data_ptr()
-            d.gtab, d.ngroups, d.relu = drows.data_ptr(), G, 0
-            d.w, d.bias, d.wps = wT.data_ptr(), 0, wT[0].numel()
-            d.G, d.B, d.H, d.W, d.Cinp, d.Coutp, d.KH, d.KW = G, B, H, W, coutp, cinp, k, k
-            d.TH, d.prec, d.cout_real = 8, 1, cin
-            Km.check(L.gt_conv_fwd(d, stream()), "dgrad")
-            torch.cuda.synchronize()
-            out[split] = (y.clone(), xsum.clone(), py.clone(), pm.clone(), o0.clone(), o1.clone())
-    finally:
-        L.gt_conv_set_s2split(0)
-    for u, v in zip(out[1], out[0]):
-        assert torch.equal(u, v)
-    x32 = sum(xs)
-    g = 1
-    ref = F.relu(F.conv2d(x32[g].double(), w[g].double(), bvec[g].double(), padding=1))
-    got = out[1][0][g, ..., :cout].permute(0, 3, 1, 2)
-    assert rel(got, ref) < TOL
