@@ -81,9 +81,11 @@
 // the part-major reduction order of the stage-2 3x3 fp32 shape (GT_S2_PARTS)
 template <int KH, int KW, int NCBI, int W, int PREC>
 struct S2Parts {
-  static constexpr bool on = GT_S2_PARTS && PREC == 1 && KH == 3 && KW == 3 && NCBI == 7 && W == 16;
+  // 3x3 nodes / output convs and their dgrad; GT_S2_PARTS >= 2 also the 5x5 input-conv dgrad (50 -> 20)
+  static constexpr bool on = GT_S2_PARTS && PREC == 1 && NCBI == 7 && W == 16 &&
+                             ((KH == 3 && KW == 3) || (GT_S2_PARTS >= 2 && KH == 5 && KW == 5));
+  static constexpr int e0 = KH * KW * 4;     // chunk-list entries of part 0 (every tap x chunks 0-3)
 };
-#define S2P_E0 36            // chunk-list entries of part 0 (9 kernel taps x chunks 0-3)
 
 // LDS bytes of one launch: the patch (NPL bf16 planes) or the output tile
 // (fp32, or bf16 for prec-0 forward launches -- measured 7-9 % faster: more
@@ -216,8 +218,9 @@ conv_fast_kernel(ConvArgs a) {
   constexpr bool PARTS = S2Parts<KH, KW, NCBI, W, PREC>::on;
   auto ent = [&](int e, int& kk, int& cb) {
     if constexpr (PARTS) {
-      if (e < S2P_E0) { kk = e >> 2; cb = e & 3; }
-      else { const int e1 = e - S2P_E0; kk = e1 / 3; cb = 4 + e1 - kk * 3; }
+      constexpr int E0 = S2Parts<KH, KW, NCBI, W, PREC>::e0;
+      if (e < E0) { kk = e >> 2; cb = e & 3; }
+      else { const int e1 = e - E0; kk = e1 / 3; cb = 4 + e1 - kk * 3; }
     } else {
       kk = e / NCBI; cb = e - kk * NCBI;
     }
