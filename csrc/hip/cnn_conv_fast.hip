@@ -2277,6 +2277,12 @@ extern "C" int gt_wgrad_set_nb(int nb) {
                                     dim3(NW_ * 64), 0, stream, *a);                                      \
         else hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, NB_, 0, 2>), gz,     \
                                 dim3(NW_ * 64), 0, stream, *a);                                          \
+      } else if (nz_ == 8) {                                                                             \
+        /* tiny launches (< 32 split x group blocks): 8 slices of 4-wave workgroups */                   \
+        if (pkz) hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, 4, 1, 1, 8>), gz, \
+                                    dim3(256), 0, stream, *a);                                           \
+        else hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, 4, 1, 0, 8>), gz,     \
+                                dim3(256), 0, stream, *a);                                               \
       } else {                                                                                           \
         if (pkz) hipLaunchKernelGGL((wgrad_fast_f32_kernel<KH_, KW_, NCBI_, NCBO_, W_, R_, NW_, 1, 1, 4>), gz, \
                                     dim3(NW_ * 64), 0, stream, *a);                                      \
@@ -2317,7 +2323,7 @@ extern "C" int gt_wgrad_set_nb(int nb) {
 // grid fills more CUs and each workgroup's serial band loop carries 1/NZ of
 // the MFMAs. Every weight's sum runs in the same band / k-step order in any
 // slice: results are bit-identical for any NZ (tests/test_hip_kernels.py).
-// GENTUN_WGRAD_NZ: 0 auto (default), 1 / 2 / 4 forced.
+// GENTUN_WGRAD_NZ: 0 auto (default), 1 / 2 / 4 / 8 forced (8: 4-wave workgroups).
 static int g_wgrad_nz = -1;
 
 extern "C" int gt_wgrad_set_nz(int nz) {
@@ -2326,12 +2332,16 @@ extern "C" int gt_wgrad_set_nz(int nz) {
   return old;
 }
 
+// blocks below which the 8-slice variant runs (GENTUN_WGRAD_NZ8; default 0 = never: measured neutral at
+// 2 groups, profiles/wgrad_nz8_ab_r4.txt)
+static int g_wgrad_nz8 = std::getenv("GENTUN_WGRAD_NZ8") ? std::atoi(std::getenv("GENTUN_WGRAD_NZ8")) : 0;
+
 static int wgrad_nz(const WgradArgs* a) {
   if (g_wgrad_nz < 0) g_wgrad_nz = std::getenv("GENTUN_WGRAD_NZ") ? std::atoi(std::getenv("GENTUN_WGRAD_NZ")) : 0;
   const int force = g_wgrad_nz;
-  if (force == 1 || force == 2 || force == 4) return force;
+  if (force == 1 || force == 2 || force == 4 || force == 8) return force;
   const int blocks = a->S * a->ngroups;
-  return blocks < 64 ? 4 : blocks < 160 ? 2 : 1;
+  return blocks < g_wgrad_nz8 ? 8 : blocks < 64 ? 4 : blocks < 160 ? 2 : 1;
 }
 
 // packed last co tile of the fp32 wgrad (A/B switch GENTUN_WGRAD_PK=0 disables)

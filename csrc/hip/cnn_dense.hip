@@ -519,6 +519,11 @@ __global__ void __launch_bounds__(64) head_fwd_kernel(HeadArgs a) {
   const int idx = blockIdx.x, lane = threadIdx.x;
   const int g = idx / a.B, b = idx % a.B;
   const int C = a.C, nt = a.Up / 16;
+  // the label chain (step -> sample id -> label: three dependent loads) issued first, so it runs
+  // beside the partial-logit loads instead of after the reduction
+  const int step = a.st ? a.st->cur_step : 0;
+  const long sid = a.gather[((long)step * a.G + g) * a.B + b];
+  const int y = (int)a.labels[sid];
   float acc[HEAD_MAXC];
   const float* pl = a.plog + ((long)g * nt * a.B + b) * C;
 #pragma unroll
@@ -542,9 +547,6 @@ __global__ void __launch_bounds__(64) head_fwd_kernel(HeadArgs a) {
   if (lane != 0) return;
   float logit[HEAD_MAXC];
   for (int c = 0; c < C; ++c) logit[c] = acc[c] + a.b2[(long)g * C + c];
-  const int step = a.st ? a.st->cur_step : 0;
-  const long sid = a.gather[((long)step * a.G + g) * a.B + b];
-  const int y = (int)a.labels[sid];
   float p[HEAD_MAXC];
   float mx = -INFINITY;
   for (int c = 0; c < C; ++c) mx = fmaxf(mx, logit[c]);

@@ -178,10 +178,10 @@ def test_duo_unpool_bit_identical(H, W, cin, cout, k):
 @pytest.mark.parametrize("H,W,cin,cout,k", SHAPES[:4])
 @pytest.mark.parametrize("nin", [1, 2])
 def test_wgrad_column_slices_bit_identical(H, W, cin, cout, k, nin):
-    """Small launches slice the fp32 wgrad's k-column tiles over NZ = 2 / 4
-    workgroups per (split, group): every weight gradient (and the bias
-    column) is bit-identical to the one-workgroup kernel, for single and
-    summed (DAG) inputs and the packed last co tile."""
+    """Small launches slice the fp32 wgrad's k-column tiles over NZ = 2 / 4 / 8
+    workgroups per (split, group) (8: 4-wave workgroups): every weight
+    gradient (and the bias column) is bit-identical to the one-workgroup
+    kernel, for single and summed (DAG) inputs and the packed last co tile."""
     import ctypes
     Km = K()
     L = Km.lib()
@@ -202,7 +202,7 @@ def test_wgrad_column_slices_bit_identical(H, W, cin, cout, k, nin):
     rows = torch.tensor([[g, (1 << nin) - 1, 0, 0] for g in range(G)], dtype=torch.int32, device=DEV)
     st = torch.zeros(8, dtype=torch.int32, device=DEV)
     res = {}
-    for nz in (1, 2, 4):
+    for nz in (1, 2, 4, 8):
         pw = torch.full((S, G, coutp, kd), 9.0, device=DEV)
         pb = torch.full((S, G, coutp), 9.0, device=DEV)
         a = Km.WgradArgs()
@@ -219,7 +219,7 @@ def test_wgrad_column_slices_bit_identical(H, W, cin, cout, k, nin):
         finally:
             L.gt_wgrad_set_nz(old)
         res[nz] = (pw, pb)
-    for nz in (2, 4):
+    for nz in (2, 4, 8):
         assert torch.equal(res[1][0], res[nz][0]), nz
         assert torch.equal(res[1][1], res[nz][1]), nz
     assert not torch.equal(res[1][0], torch.full_like(res[1][0], 9.0))
