@@ -2406,8 +2406,12 @@ extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
   if (a->prec == 1) {
     WGRAD_FAST_CASE_F32(5, 5, 1, 3, 32, 8, 4, 1)      // s1 input conv (3 -> 20)
     WGRAD_FAST_CASE_F32(3, 3, 3, 3, 32, 4, 4, 1)      // s1 nodes / output conv (20 -> 20)
-    WGRAD_FAST_CASE_F32(5, 5, 3, 7, 16, 4, 8, 2)      // s2 input conv (20 -> 50)
-    WGRAD_FAST_CASE_F32(3, 3, 7, 7, 16, 4, 8, 2)      // s2 nodes / output conv (50 -> 50)
+    // s2: ONE band buffer (57 KB of LDS instead of 115): in the population step the wgrads run beside the
+    // data-gradient convs, and a single-buffered wgrad workgroup leaves room on its CU for a conv
+    // workgroup (60 KB) -- 1.1-1.6 % per step from 25 groups up although the wgrad alone is slower
+    // (profiles/wgrad_nb_ab_r4.txt)
+    WGRAD_FAST_CASE_F32(5, 5, 3, 7, 16, 4, 8, 1)      // s2 input conv (20 -> 50)
+    WGRAD_FAST_CASE_F32(3, 3, 7, 7, 16, 4, 8, 1)      // s2 nodes / output conv (50 -> 50)
     WGRAD_FAST_CASE_F32Z(5, 5, 7, 13, 8, 4, 8, 4)     // deep s3 input conv (50 -> 100)
     WGRAD_FAST_CASE_F32Z(3, 3, 13, 13, 8, 4, 8, 4)    // deep s3 nodes / output conv (100 -> 100)
     // wide deep space (64, 128, 256): column slices so each workgroup's dW slice fits its registers
