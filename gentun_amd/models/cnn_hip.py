@@ -133,15 +133,17 @@ class HipPopJob(FoldJob):
         # GENTUN_OVERLAP=0: one stream (A/B of the fork / join edges at small launches)
         self.overlap = os.environ.get("GENTUN_OVERLAP", "1") != "0"
         self.w1_stream = os.environ.get("GENTUN_W1_STREAM", "1") != "0"
-        # conv-layer optimizer updates per layer on a third stream (A/B switch, off:
-        # 907 vs 958 candidates/h with it on -- it competes with the dgrad chain,
-        # profiles/bench_round_size_r2.txt)
-        self.adam_overlap = os.environ.get("GENTUN_ADAM_OVERLAP", "0") == "1"
+        # GENTUN_ADAM_OVERLAP=1: each conv layer's optimizer update runs on the
+        # W1 optimizer stream as soon as its wgrad and its last data-gradient op
+        # are done, instead of in one launch after the backward (A/B switch, off:
+        # 7-45 % slower, profiles/adam_overlap_w1stream_ab_r4.txt -- the
+        # two-parent update nodes serialise the captured graph's streams; a
+        # third-stream variant lost 5 %, stream_priority_adam_overlap_ab_r4.txt)
+        self.adam_overlap = os.environ.get("GENTUN_ADAM_OVERLAP", "0") == "1" and self.w1_stream
         if self.dp is not None:
             # X5: every update must see the all-reduced gradient; an in-backward conv
-            # update on side3 would run before _dp_allreduce and the ranks would diverge
+            # update would run before _dp_allreduce and the ranks would diverge
             self.adam_overlap = False
-        self.side3 = torch.cuda.Stream(dev) if self.adam_overlap else None
         self._build_adam_table()
         self._build_args()
 
@@ -833,17 +835,20 @@ class HipPopJob(FoldJob):
         # (unchanged) inputs: it overlaps the layer's dgrad and everything after.
         fork(side2)
         K.check(L.gt_dense_wgrad_adam(self.dense_wgrad_args, side2.cuda_stream), "dense_wgrad_adam")
-        # per-layer optimizer updates on a third stream (off the dgrad chain):
-        # layer L's update waits for its wgrad (side) and for its last
-        # main-stream op (the dgrad reading its flipped weights / BN backward)
-        side3 = self.side3 if (self.overlap and self.adam_overlap) else None
-        wgs = self.wg_streams if (self.overlap and side3 is None) else [side]
+        # per-layer optimizer updates on side2 (off the dgrad chain, behind the
+        # W1 update): layer L's update waits for its wgrad (+ reduce) stream and
+        # for its last main-stream op (the dgrad reading its flipped weights /
+        # its BN backward)
+        ovl = self.overlap and self.adam_overlap
+        wgs = self.wg_streams if self.overlap else [side]
+        wg_of = {}
         nwg = 0
         for i, (kind, a, Lr) in enumerate(self.bwd_ops):
             if kind == "wgrad":
                 ws = wgs[nwg % len(wgs)]
                 nwg += 1
                 fork(ws)
+                wg_of[Lr.name] = ws
                 K.check(L.gt_conv_wgrad(a, ws.cuda_stream), "conv_wgrad")
                 if Lr.wred:
                     K.check(L.gt_wgrad_reduce(a, ws.cuda_stream), "wgrad_reduce")
@@ -853,21 +858,21 @@ class HipPopJob(FoldJob):
                 K.check(L.gt_bn_bwd(a, s), "bn_bwd")
             else:
                 K.check(L.gt_pool_bwd_mask(*a, s), "pool_bwd")
-            if side3 is not None and Lr is not None and self.bwd_last.get(Lr.name) == i and Lr.adam_part[1] > 0:
-                for stream in (main, side):
+            if ovl and Lr is not None and self.bwd_last.get(Lr.name) == i and Lr.adam_part[1] > 0:
+                for stream in {main, wg_of.get(Lr.name, main)}:
                     ev = torch.cuda.Event()
                     ev.record(stream)
-                    side3.wait_event(ev)
-                K.check(L.gt_adam_segments(Lr.adam_part[0], Lr.adam_part[1], side3.cuda_stream), "adam")
-        for stream in [side2, side3] + list(wgs):
-            if stream is not None and stream is not main:
+                    side2.wait_event(ev)
+                K.check(L.gt_adam_segments(Lr.adam_part[0], Lr.adam_part[1], side2.cuda_stream), "adam")
+        for stream in [side2] + list(wgs):
+            if stream is not main:
                 ev = torch.cuda.Event()
                 ev.record(stream)
                 main.wait_event(ev)
         if self.dp is not None:
             self._dp_allreduce()
             K.check(L.gt_dense_wgrad_adam(self.dense_apply_args, s), "dense_wgrad_adam(apply)")
-        if side3 is not None:
+        if ovl:
             K.check(L.gt_adam_segments(self.adam_head[0], self.adam_head[1], s), "adam")
         else:
             K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")

@@ -246,6 +246,32 @@ def test_small_launch_tiles_bit_identical(bn, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bn", [False, True])
+def test_per_layer_adam_overlap_bit_identical(bn, monkeypatch):
+    """GENTUN_ADAM_OVERLAP=1 runs each conv layer's optimizer update on the W1
+    optimizer stream inside the backward (after its wgrad and its last
+    data-gradient op): the same results as the one update launch after the
+    backward, through the captured step graph of a population job."""
+    import numpy as np
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.genome import make_plan
+    from gentun_amd.utils.data import make_cifar_like, stratified_kfold
+    x, y = make_cifar_like(n=400, seed=3)
+    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
+    genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '111', 'S_2': '0000000001'}]
+    plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
+    cfg = E.TrainConfig(epochs=(1, 1), learning_rate=(1e-3, 5e-4), batch_size=32, dtype="fp32", reset="all",
+                        batch_norm=bn)
+    out = {}
+    for ovl in ("1", "0"):
+        monkeypatch.setenv("GENTUN_ADAM_OVERLAP", ovl)
+        job = E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg,
+                                    torch.device("cuda", 0))
+        out[ovl] = job.launch().finish()
+    assert out["1"] == out["0"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bn", [False, True])
 def test_inactive_node_params_untouched(bn):
     """A population job lays out the superset of its members' layers; a node
     a group's genome leaves out (no edges: the reference never builds it,
