@@ -54,7 +54,7 @@ CLIP_EPS = 1e-7
 
 class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
-                 dtype="fp32", seed=0, use_graph=True, eval_batch=1000, optimizer="adam", momentum=0.9,
+                 dtype="fp32", seed=0, use_graph=None, eval_batch=1000, optimizer="adam", momentum=0.9,
                  reset="kernels", batching="keras", batch_norm=False, bn_momentum=0.99, bn_eps=1e-3,
                  dp_group=None, verbose=False, nfold=None):
         if isinstance(epochs, int):
@@ -387,7 +387,14 @@ class FoldJob(object):
         return graph
 
     def launch(self):
-        use_graph = self.cfg.use_graph and self.device.type == "cuda" and getattr(self, "capture_ok", True)
+        # use_graph None (default): the captured step graph unless GENTUN_GRAPH=0 (eager
+        # launches: 2-12 % faster on the GPU in a bare population step, but 2.5 % slower
+        # in bench.py, where the Python launch path competes with the host side of the
+        # search -- profiles/graph_vs_eager_ab_r4.txt)
+        ug = self.cfg.use_graph
+        if ug is None:
+            ug = os.environ.get("GENTUN_GRAPH", "1") != "0"
+        use_graph = ug and self.device.type == "cuda" and getattr(self, "capture_ok", True)
         ctx = torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
         timed = self.device.type == "cuda"
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None

@@ -39,7 +39,8 @@ for _ in range(P):
     g = {"S_{}".format(s + 1): "".join(rnd.choice("01") for _ in range(k * (k - 1) // 2)) for s, k in enumerate(nodes)}
     plans.append(make_plan(g, nodes, (32, 32, 3), kernels, ((5, 5),) * len(nodes), 500, 10))
 cfg = E.TrainConfig(epochs=(epochs,), learning_rate=(1e-3,), batch_size=32, dtype=os.environ.get("DTYPE", "fp32"),
-                    loss="ce", reset=os.environ.get("RESET", "all"), batch_norm=os.environ.get("BN", "0") == "1")
+                    loss="ce", reset=os.environ.get("RESET", "all"), batch_norm=os.environ.get("BN", "0") == "1",
+                    use_graph=os.environ.get("GRAPH", "1") != "0")
 streams = [torch.cuda.Stream(dev, priority=int(os.environ.get("MAIN_PRIO", "0"))) for _ in range(ns)]
 # warm-up (allocator, code objects); WARM=0 keeps profiles free of the small warm-up job
 if os.environ.get("WARM", "1") != "0":
