@@ -386,11 +386,16 @@ class FoldJob(object):
         self.restore(snap)
         return graph
 
+    def train_steps(self, n):
+        """``n`` eager training steps (executors may issue them natively)."""
+        for _ in range(n):
+            self.train_step()
+
     def launch(self):
         # use_graph None (default): the captured step graph unless GENTUN_GRAPH=0 (eager
-        # launches: 2-12 % faster on the GPU in a bare population step, but 2.5 % slower
-        # in bench.py, where the Python launch path competes with the host side of the
-        # search -- profiles/graph_vs_eager_ab_r4.txt)
+        # launches, through the native step program: -2..+12 % in a bare population
+        # step depending on the box, 2.5 % slower in bench.py on two boxes --
+        # profiles/graph_vs_eager_ab_r4.txt)
         ug = self.cfg.use_graph
         if ug is None:
             ug = os.environ.get("GENTUN_GRAPH", "1") != "0"
@@ -429,8 +434,7 @@ class FoldJob(object):
                         for _ in range(self.steps_per_epoch // self._k_steps):
                             graph.replay()
                     else:
-                        for _ in range(self.steps_per_epoch):
-                            self.train_step()
+                        self.train_steps(self.steps_per_epoch)
             if timed:
                 ev[2].record()
             self._graph = graph

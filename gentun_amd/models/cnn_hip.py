@@ -811,30 +811,47 @@ class HipPopJob(FoldJob):
             else:
                 K.check(L.gt_pool_fwd(*a, self.prec, s), "pool_fwd")
 
-    def train_step(self):
-        L = self.L
-        main = torch.cuda.current_stream(self.device)
-        s = main.cuda_stream
-        K.check(L.gt_step_begin(self.state.data_ptr(), s), "step_begin")
-        self._run_fwd(s, self.fwd_ops)
-        K.check(L.gt_dense_fwd(self.dense_fwd_args, s), "dense_fwd")
-        K.check(L.gt_head(self.head_args, s), "head")
-        K.check(L.gt_dense_dgrad(self.dense_dgrad_args, s), "dense_dgrad")   # reads W1 before its update
+    def _fwd_plan(self, ops):
+        plan = []
+        for kind, a, mk in ops:
+            if kind == "conv":
+                plan.append(("k", "gt_conv_fwd", (a,), None, "conv_fwd"))
+            elif kind == "bn":
+                plan.append(("k", "gt_bn_fwd", (a,), None, "bn_fwd"))
+            elif mk is not None:
+                plan.append(("k", "gt_pool_fwd_mask", tuple(a) + (mk, self.prec), None, "pool_fwd"))
+            else:
+                plan.append(("k", "gt_pool_fwd", tuple(a) + (self.prec,), None, "pool_fwd"))
+        return plan
+
+    def _step_plan(self):
+        """One training step up to the join of its streams, as launches
+        ``("k", entry point, operands, stream, what)`` and event edges
+        ``("rec" | "wait", stream, event id)``; stream ``None`` is the caller's
+        (main) stream. Issued by :meth:`_exec_plan` (Python; also what a
+        captured step graph records) or compiled once into a native
+        :class:`~gentun_amd.ops.cnn_kernels.StepProgram`."""
+        main = None
+        plan = [("k", "gt_step_begin", (self.state.data_ptr(),), main, "step_begin")]
+        plan += self._fwd_plan(self.fwd_ops)
+        plan += [("k", "gt_dense_fwd", (self.dense_fwd_args,), main, "dense_fwd"),
+                 ("k", "gt_head", (self.head_args,), main, "head"),
+                 ("k", "gt_dense_dgrad", (self.dense_dgrad_args,), main, "dense_dgrad")]   # reads W1 before its update
         side = self.side if self.overlap else main
         side2 = (self.side2 if self.w1_stream else side) if self.overlap else main
-        ss = side.cuda_stream
+        nev = [0]
 
-        def fork(stream):
-            if stream is not main:
-                ev = torch.cuda.Event()
-                ev.record(main)
-                stream.wait_event(ev)
+        def edge(src, dst):
+            if src is not dst:
+                plan.append(("rec", src, nev[0]))
+                plan.append(("wait", dst, nev[0]))
+                nev[0] += 1
 
         # W1 gradient + Adam only needs dH and the pooled features: it overlaps
         # the whole conv backward. Each layer's wgrad reads its final dz and its
         # (unchanged) inputs: it overlaps the layer's dgrad and everything after.
-        fork(side2)
-        K.check(L.gt_dense_wgrad_adam(self.dense_wgrad_args, side2.cuda_stream), "dense_wgrad_adam")
+        edge(main, side2)
+        plan.append(("k", "gt_dense_wgrad_adam", (self.dense_wgrad_args,), side2, "dense_wgrad_adam"))
         # per-layer optimizer updates on side2 (off the dgrad chain, behind the
         # W1 update): layer L's update waits for its wgrad (+ reduce) stream and
         # for its last main-stream op (the dgrad reading its flipped weights /
@@ -847,35 +864,66 @@ class HipPopJob(FoldJob):
             if kind == "wgrad":
                 ws = wgs[nwg % len(wgs)]
                 nwg += 1
-                fork(ws)
+                edge(main, ws)
                 wg_of[Lr.name] = ws
-                K.check(L.gt_conv_wgrad(a, ws.cuda_stream), "conv_wgrad")
+                plan.append(("k", "gt_conv_wgrad", (a,), ws, "conv_wgrad"))
                 if Lr.wred:
-                    K.check(L.gt_wgrad_reduce(a, ws.cuda_stream), "wgrad_reduce")
+                    plan.append(("k", "gt_wgrad_reduce", (a,), ws, "wgrad_reduce"))
             elif kind == "conv":
-                K.check(L.gt_conv_fwd(a, s), "conv_dgrad")
+                plan.append(("k", "gt_conv_fwd", (a,), main, "conv_dgrad"))
             elif kind == "bn_bwd":
-                K.check(L.gt_bn_bwd(a, s), "bn_bwd")
+                plan.append(("k", "gt_bn_bwd", (a,), main, "bn_bwd"))
             else:
-                K.check(L.gt_pool_bwd_mask(*a, s), "pool_bwd")
+                plan.append(("k", "gt_pool_bwd_mask", tuple(a), main, "pool_bwd"))
             if ovl and Lr is not None and self.bwd_last.get(Lr.name) == i and Lr.adam_part[1] > 0:
-                for stream in {main, wg_of.get(Lr.name, main)}:
-                    ev = torch.cuda.Event()
-                    ev.record(stream)
-                    side2.wait_event(ev)
-                K.check(L.gt_adam_segments(Lr.adam_part[0], Lr.adam_part[1], side2.cuda_stream), "adam")
+                edge(main, side2)
+                if wg_of.get(Lr.name) is not None:
+                    edge(wg_of[Lr.name], side2)
+                plan.append(("k", "gt_adam_segments", Lr.adam_part, side2, "adam"))
         for stream in [side2] + list(wgs):
-            if stream is not main:
+            edge(stream, main)
+        return plan
+
+    def _adam_plan(self):
+        if self.overlap and self.adam_overlap:
+            return [("k", "gt_adam_segments", self.adam_head, None, "adam")]
+        return [("k", "gt_adam_segments", (self.adam_args, self.adam_nblocks), None, "adam")]
+
+    def _exec_plan(self, plan):
+        L = self.L
+        main = torch.cuda.current_stream(self.device)
+        evs = {}
+        for op in plan:
+            st = op[3] if op[0] == "k" else op[1]
+            st = main if st is None else st
+            if op[0] == "k":
+                K.check(getattr(L, op[1])(*op[2], st.cuda_stream), op[4])
+            elif op[0] == "rec":
                 ev = torch.cuda.Event()
-                ev.record(stream)
-                main.wait_event(ev)
+                ev.record(st)
+                evs[op[2]] = ev
+            else:
+                st.wait_event(evs[op[2]])
+
+    def train_step(self):
+        self._exec_plan(self._step_plan())
         if self.dp is not None:
             self._dp_allreduce()
-            K.check(L.gt_dense_wgrad_adam(self.dense_apply_args, s), "dense_wgrad_adam(apply)")
-        if ovl:
-            K.check(L.gt_adam_segments(self.adam_head[0], self.adam_head[1], s), "adam")
-        else:
-            K.check(L.gt_adam_segments(self.adam_args, self.adam_nblocks, s), "adam")
+            K.check(self.L.gt_dense_wgrad_adam(self.dense_apply_args, self._stream()), "dense_wgrad_adam(apply)")
+        self._exec_plan(self._adam_plan())
+
+    def train_steps(self, n):
+        """``n`` training steps issued eagerly: through the native step program
+        (one host call; GENTUN_NATIVE_STEPS=0 or X5 data parallelism: the
+        Python issue path per step)."""
+        if self.dp is None and os.environ.get("GENTUN_NATIVE_STEPS", "1") != "0":
+            prog = getattr(self, "_prog", None)
+            if prog is None:
+                prog = self._prog = K.StepProgram(self._step_plan() + self._adam_plan())
+            prog.run(self._stream(), n)
+            return
+        for _ in range(n):
+            self.train_step()
 
     def eval_batch(self):
         """Rows per evaluation launch (K13): ``cfg.eval_batch`` (default 256),

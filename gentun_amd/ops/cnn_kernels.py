@@ -106,6 +106,19 @@ class AdamArgs(C.Structure):
     _fields_ = [("segs", P), ("blocks", P), ("st", P)]
 
 
+class ProgOp(C.Structure):
+    """One op of a native step program (csrc/hip/step_prog.hip GtProgOp)."""
+    _fields_ = [("kind", C.c_int32), ("stream", C.c_int32), ("event", C.c_int32), ("pad", C.c_int32),
+                ("v", C.c_int64 * 14)]
+
+
+# op kinds of csrc/hip/step_prog.hip, by the name of the launch entry point
+PROG_OPS = {"record": 0, "wait": 1, "gt_step_begin": 2, "gt_conv_fwd": 3, "gt_conv_wgrad": 4,
+            "gt_wgrad_reduce": 5, "gt_bn_fwd": 6, "gt_bn_bwd": 7, "gt_dense_fwd": 8, "gt_head": 9,
+            "gt_dense_dgrad": 10, "gt_dense_wgrad_adam": 11, "gt_adam_segments": 12, "gt_pool_fwd": 13,
+            "gt_pool_fwd_mask": 14, "gt_pool_bwd_mask": 15}
+
+
 class InitSeg(C.Structure):
     _fields_ = [("p", P), ("seeds", P), ("d", I * 4), ("r", I * 4), ("G", I), ("tag", I), ("limit", C.c_float),
                 ("pad", I)]
@@ -178,6 +191,14 @@ def lib():
         L.gt_glorot_init.restype = I
         L.gt_glorot_ref.argtypes = [C.c_uint64, C.c_uint64, I, C.c_float]
         L.gt_glorot_ref.restype = C.c_float
+        L.gt_prog_create.argtypes = [C.POINTER(ProgOp), I, I, I]
+        L.gt_prog_create.restype = P
+        L.gt_prog_run.argtypes = [P, P, I, C.POINTER(I)]
+        L.gt_prog_run.restype = I
+        L.gt_prog_destroy.argtypes = [P]
+        L.gt_prog_destroy.restype = None
+        L.gt_sizeof_prog_op.restype = C.c_size_t
+        assert L.gt_sizeof_prog_op() == C.sizeof(ProgOp), "ProgOp ABI mismatch"
         for name in ("gt_sizeof_conv_args", "gt_sizeof_wgrad_args", "gt_sizeof_adam_seg", "gt_sizeof_init_seg",
                      "gt_sizeof_dense_fwd_args", "gt_sizeof_head_args", "gt_sizeof_dense_dgrad_args",
                      "gt_sizeof_dense_wgrad_args", "gt_sizeof_bn_args"):
@@ -197,6 +218,69 @@ def lib():
 def check(rc, what):
     if rc != 0:
         raise RuntimeError("HIP kernel launch {} failed with code {}".format(what, rc))
+
+
+class StepProgram(object):
+    """A native step program (csrc/hip/step_prog.hip): ``plan`` is a list of
+    ``("k", entry_point, args, stream_key, what)`` launches and ``("rec" |
+    "wait", stream_key, event_id)`` edges; stream key ``None`` is the caller's
+    stream at :meth:`run` time. Launch operands are ctypes argument structs
+    (passed by address) or ints (pool launches)."""
+
+    def __init__(self, plan):
+        L = lib()
+        self.L = L
+        keys, nev = [None], 0
+        ops = (ProgOp * len(plan))()
+        for o, op in zip(ops, plan):
+            st = op[3] if op[0] == "k" else op[1]
+            if not any(st is k for k in keys):
+                keys.append(st)
+            o.stream = next(i for i, k in enumerate(keys) if k is st)
+            if op[0] in ("rec", "wait"):
+                o.kind = PROG_OPS["record" if op[0] == "rec" else "wait"]
+                o.event = int(op[2])
+                nev = max(nev, o.event + 1)
+                continue
+            o.kind = PROG_OPS[op[1]]
+            vals = []
+            for a in op[2]:
+                if isinstance(a, C.Structure):
+                    vals.append(C.addressof(a))
+                elif a is None:
+                    vals.append(0)
+                elif isinstance(a, C.c_void_p):
+                    vals.append(a.value or 0)
+                else:
+                    vals.append(int(a))
+            if len(vals) > len(o.v):
+                raise ValueError("step program: too many operands for " + op[1])
+            for i, x in enumerate(vals):
+                o.v[i] = x
+        self._ops = ops
+        self._structs = [a for op in plan if op[0] == "k" for a in op[2] if isinstance(a, C.Structure)]
+        self.keys = keys
+        self.h = L.gt_prog_create(ops, len(plan), nev, len(keys))
+        if not self.h:
+            raise RuntimeError("gt_prog_create rejected the step program")
+        self._streams = (C.c_void_p * len(keys))()
+
+    def run(self, main_stream, nsteps):
+        self._streams[0] = main_stream
+        for i, k in enumerate(self.keys[1:], 1):
+            self._streams[i] = k.cuda_stream
+        bad = I(-1)
+        rc = self.L.gt_prog_run(self.h, self._streams, int(nsteps), C.byref(bad))
+        if rc != 0:
+            raise RuntimeError("HIP step program op {} failed with code {}".format(bad.value, rc))
+
+    def __del__(self):
+        h, self.h = getattr(self, "h", None), None
+        if h:
+            try:
+                self.L.gt_prog_destroy(h)
+            except Exception:          # interpreter shutdown
+                pass
 
 
 def ptr(t):

@@ -246,6 +246,34 @@ def test_small_launch_tiles_bit_identical(bn, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bn", [False, True])
+def test_native_step_program_bit_identical(bn, monkeypatch):
+    """The native step runner (csrc/hip/step_prog.hip: the step's launches and
+    stream edges issued from C++, a whole epoch per host call), the Python
+    issue path and the captured step graph give the same results."""
+    import numpy as np
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models.genome import make_plan
+    from gentun_amd.utils.data import make_cifar_like, stratified_kfold
+    x, y = make_cifar_like(n=400, seed=5)
+    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
+    genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '111', 'S_2': '1000000001'}]
+    plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
+    cfg = E.TrainConfig(epochs=(1, 1), learning_rate=(1e-3, 5e-4), batch_size=32, dtype="fp32", batch_norm=bn)
+    out = {}
+    for mode in ("native", "python", "graph"):
+        monkeypatch.setenv("GENTUN_GRAPH", "1" if mode == "graph" else "0")
+        monkeypatch.setenv("GENTUN_NATIVE_STEPS", "1" if mode == "native" else "0")
+        job = E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg,
+                                    torch.device("cuda", 0))
+        out[mode] = job.launch().finish()
+        if mode == "native":
+            assert all(getattr(j, "_prog", None) is not None for j in job.jobs)
+    assert out["native"] == out["python"]
+    assert out["native"] == out["graph"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bn", [False, True])
 def test_per_layer_adam_overlap_bit_identical(bn, monkeypatch):
     """GENTUN_ADAM_OVERLAP=1 runs each conv layer's optimizer update on the W1
     optimizer stream inside the backward (after its wgrad and its last
