@@ -140,7 +140,9 @@ class HipPopJob(FoldJob):
         # two-parent update nodes serialise the captured graph's streams; a
         # third-stream variant lost 5 %, stream_priority_adam_overlap_ab_r4.txt)
         self.adam_overlap = os.environ.get("GENTUN_ADAM_OVERLAP", "0") == "1" and self.w1_stream
+        self.adam_split = os.environ.get("GENTUN_ADAM_SPLIT", "0") == "1" and self.w1_stream and not self.adam_overlap
         if self.dp is not None:
+            self.adam_split = False
             # X5: every update must see the all-reduced gradient; an in-backward conv
             # update would run before _dp_allreduce and the ranks would diverge
             self.adam_overlap = False
@@ -659,6 +661,18 @@ class HipPopJob(FoldJob):
         for i, (kind, a, Lr) in enumerate(self.bwd_ops):
             if Lr is not None:
                 self.bwd_last[Lr.name] = i
+        # GENTUN_ADAM_SPLIT=1: the last stage's conv updates and the head's run on
+        # side2 once that stage's backward (dgrads, BN backward, wgrads) is done,
+        # the earlier stages' after the join (A/B switch)
+        self.adam_split_at = None
+        last = max(Ly.stage for Ly in self.layers)
+        late = [Ly for Ly in self.layers if Ly.stage == last]
+        b0 = min(Ly.adam_range[0] for Ly in late)
+        if (all((Ly.stage == last) == (Ly.adam_range[0] >= b0) for Ly in self.layers)
+                and all(Ly.name in self.bwd_last for Ly in late)):
+            self.adam_late = adam_part((b0, self.adam_head_range[1]))
+            self.adam_early = adam_part((0, b0))
+            self.adam_split_at = max(self.bwd_last[Ly.name] for Ly in late)
 
     # -------------------------------------------------------------- protocol
     def _build_init_table(self):
@@ -857,6 +871,7 @@ class HipPopJob(FoldJob):
         # for its last main-stream op (the dgrad reading its flipped weights /
         # its BN backward)
         ovl = self.overlap and self.adam_overlap
+        split = self.overlap and self.adam_split and self.adam_split_at is not None
         wgs = self.wg_streams if self.overlap else [side]
         wg_of = {}
         nwg = 0
@@ -875,6 +890,11 @@ class HipPopJob(FoldJob):
                 plan.append(("k", "gt_bn_bwd", (a,), main, "bn_bwd"))
             else:
                 plan.append(("k", "gt_pool_bwd_mask", tuple(a), main, "pool_bwd"))
+            if split and i == self.adam_split_at:
+                edge(main, side2)
+                for ws in wgs[:min(nwg, len(wgs))]:
+                    edge(ws, side2)
+                plan.append(("k", "gt_adam_segments", self.adam_late, side2, "adam"))
             if ovl and Lr is not None and self.bwd_last.get(Lr.name) == i and Lr.adam_part[1] > 0:
                 edge(main, side2)
                 if wg_of.get(Lr.name) is not None:
@@ -885,6 +905,8 @@ class HipPopJob(FoldJob):
         return plan
 
     def _adam_plan(self):
+        if self.overlap and self.adam_split and self.adam_split_at is not None:
+            return [("k", "gt_adam_segments", self.adam_early, None, "adam")] if self.adam_early[1] > 0 else []
         if self.overlap and self.adam_overlap:
             return [("k", "gt_adam_segments", self.adam_head, None, "adam")]
         return [("k", "gt_adam_segments", (self.adam_args, self.adam_nblocks), None, "adam")]

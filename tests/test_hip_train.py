@@ -274,11 +274,13 @@ def test_native_step_program_bit_identical(bn, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("bn", [False, True])
-def test_per_layer_adam_overlap_bit_identical(bn, monkeypatch):
+@pytest.mark.parametrize("switch", ["GENTUN_ADAM_OVERLAP", "GENTUN_ADAM_SPLIT"])
+def test_per_layer_adam_overlap_bit_identical(bn, switch, monkeypatch):
     """GENTUN_ADAM_OVERLAP=1 runs each conv layer's optimizer update on the W1
     optimizer stream inside the backward (after its wgrad and its last
-    data-gradient op): the same results as the one update launch after the
-    backward, through the captured step graph of a population job."""
+    data-gradient op); GENTUN_ADAM_SPLIT=1 updates the last stage and the head
+    there once that stage's backward is done. Both give the results of the one
+    update launch after the backward (captured step graph of a population job)."""
     import numpy as np
     from gentun_amd.models import cnn_engine as E
     from gentun_amd.models.genome import make_plan
@@ -291,7 +293,7 @@ def test_per_layer_adam_overlap_bit_identical(bn, monkeypatch):
                         batch_norm=bn)
     out = {}
     for ovl in ("1", "0"):
-        monkeypatch.setenv("GENTUN_ADAM_OVERLAP", ovl)
+        monkeypatch.setenv(switch, ovl)
         job = E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg,
                                     torch.device("cuda", 0))
         out[ovl] = job.launch().finish()

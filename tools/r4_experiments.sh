@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments (A/B runs, searches), one function per gpurun call; every
 # profiles/*_r4* file names the experiment that produced it: bash tools/r4_experiments.sh NAME
-#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep
+#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35
 # Run from the repository root on the GPU box (tools/gpu.sh has the shared tasks).
 set -o pipefail
 
@@ -507,6 +507,19 @@ exp_ga_deep() {
     GA_ARGS="--space deep --batch-norm" bash tools/gpu.sh ga
 }
 
+exp_call35() {
+  # the last stage's conv Adam + head Adam on the W1 stream once that stage's backward is done (GENTUN_ADAM_SPLIT=1) vs one update after the join
+  timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_hip_train.py -k "adam_overlap" \
+    > gpurun_out/r4c35_test.log 2>&1 || { tail -30 gpurun_out/r4c35_test.log; exit 1; }
+  grep -E "passed|failed" gpurun_out/r4c35_test.log | tail -2
+  for v in "all 5 0" "all 5 1" "all 5 0" "all 5 1" "kernels 2 0" "kernels 2 1" "all 2 0" "all 2 1"; do
+    set -- $v
+    GENTUN_ADAM_SPLIT=$3 DTYPE=fp32 RESET=$1 timeout -k 10 200 python -u tools/probe_pop.py $2 $2 1 4 \
+      > gpurun_out/r4c35_run.log 2>&1 || { tail -5 gpurun_out/r4c35_run.log; exit 1; }
+    echo "RESET=$1 P=$2 adam_split=$3 $(grep -o '"ms_per_step": [0-9.]*, "ms_per_cand_step": [0-9.]*, "cand_per_hour_full_protocol": [0-9.]*' gpurun_out/r4c35_run.log)"
+  done
+}
+
 case "${1:-}" in
   call4) exp_call4 ;;
   call5) exp_call5 ;;
@@ -541,5 +554,6 @@ case "${1:-}" in
   call34) exp_call34 ;;
   dense) exp_dense ;;
   ga_deep) exp_ga_deep ;;
+  call35) exp_call35 ;;
   *) sed -n 2,5p "$0"; exit 2 ;;
 esac
