@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments (A/B runs, searches), one function per gpurun call; every
 # profiles/*_r4* file names the experiment that produced it: bash tools/r4_experiments.sh NAME
-#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35
+#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35 call36
 # Run from the repository root on the GPU box (tools/gpu.sh has the shared tasks).
 set -o pipefail
 
@@ -520,6 +520,16 @@ exp_call35() {
   done
 }
 
+exp_call36() {
+  # reference folds (reset kernels) at 2 candidates: one 2-group population job vs two 1-group jobs on two streams
+  for v in "2 1 4 2" "1 2 4 2" "1 2 4 1" "2 1 4 2" "1 2 4 2"; do
+    set -- $v
+    GENTUN_WGRAD_STREAMS=$4 DTYPE=fp32 RESET=kernels timeout -k 10 200 python -u tools/probe_pop.py 2 $1 $2 $3 \
+      > gpurun_out/r4c36_run.log 2>&1 || { tail -5 gpurun_out/r4c36_run.log; exit 1; }
+    echo "RESET=kernels P=2 pop_batch=$1 job_streams=$2 wgrad_streams=$4 $(grep -o '"ms_per_step": [0-9.]*, "ms_per_cand_step": [0-9.]*, "cand_per_hour_full_protocol": [0-9.]*' gpurun_out/r4c36_run.log)"
+  done
+}
+
 case "${1:-}" in
   call4) exp_call4 ;;
   call5) exp_call5 ;;
@@ -555,5 +565,6 @@ case "${1:-}" in
   dense) exp_dense ;;
   ga_deep) exp_ga_deep ;;
   call35) exp_call35 ;;
+  call36) exp_call36 ;;
   *) sed -n 2,5p "$0"; exit 2 ;;
 esac
