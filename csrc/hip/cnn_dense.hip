@@ -30,6 +30,9 @@
 #define ADAM_B2 0.999f
 #define ADAM_EPS 1e-7f
 #define CLIP_EPS 1e-7f
+#ifndef GT_ADAM_UNROLL
+#define GT_ADAM_UNROLL 1   // adam_segments_kernel tiled path: elements per thread whose loads issue together (4: neutral, profiles/adam_unroll_ab_r4.txt)
+#endif
 #ifndef GT_WADAM_HOIST
 #define GT_WADAM_HOIST 0   // dense_wgrad_adam_kernel: 1 = optimizer-state loads hoisted above the row branches (A/B build)
 #endif
@@ -968,6 +971,7 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
   }
   __syncthreads();
   const float lr_t = a.st->lr_t;
+  const bool cp = a.wt != nullptr;                      // (uniform) transposed copy wanted: stage its tile
   const float* dH = a.dH + (long)g * a.B * a.Up;
   const int nq = a.Ur > 0 ? (a.Ur + 3) >> 2 : a.Up >> 2;
   const int fr = tid >> 7;
@@ -1026,7 +1030,8 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
       if (f >= a.Fp) continue;
       if (!ok[r]) {                            // padded channel: weights stay 0, only the copy tile
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
+        for (int i = 0; i < 4; ++i)
+          if (cp) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
         continue;
       }
       const long off = ((long)g * a.Fp + f) * a.Up + u0;
@@ -1034,8 +1039,10 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         P[i] = opt_update(a.st, P[i], acc[r][i], M[i], V[i], lr_t);
-        if constexpr (PREC != 0) tt[(u0 + i) * 16 + fr + 2 * r] = P[i];
-        else tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
+        if (cp) {
+          if constexpr (PREC != 0) tt[(u0 + i) * 16 + fr + 2 * r] = P[i];
+          else tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
+        }
       }
       *reinterpret_cast<float4*>(a.p + off) = pp[r];
       *reinterpret_cast<float4*>(a.m + off) = mm[r];
@@ -1048,7 +1055,8 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
       if (f >= a.Fp) continue;
       if (a.Cp > 0 && f % a.Cp >= a.Cr) {      // padded channel: weights stay 0, only the copy tile
 #pragma unroll
-        for (int i = 0; i < 4; ++i) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
+        for (int i = 0; i < 4; ++i)
+          if (cp) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
         continue;
       }
       const long off = ((long)g * a.Fp + f) * a.Up + u0;
@@ -1059,8 +1067,10 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         P[i] = opt_update(a.st, P[i], acc[r][i], M[i], V[i], lr_t);
-        if constexpr (PREC != 0) tt[(u0 + i) * 16 + fr + 2 * r] = P[i];
-        else tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
+        if (cp) {
+          if constexpr (PREC != 0) tt[(u0 + i) * 16 + fr + 2 * r] = P[i];
+          else tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
+        }
       }
       *reinterpret_cast<float4*>(a.p + off) = pp;
       *reinterpret_cast<float4*>(a.m + off) = mm;
@@ -1132,20 +1142,41 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
     const int Co = min(128, CoF - c0);
     const long base = ((long)gg * CoF + c0) * Kd;
     const float lr_t = a.st->lr_t;
-    for (int idx = threadIdx.x; idx < Co * ADAM_TK; idx += 256) {
-      const int co = idx / ADAM_TK, kk = idx % ADAM_TK, k = k0 + kk;
-      if (k >= Kd) continue;
-      const long i = base + (long)co * Kd + k;
-      float gr = 0.f;
-      for (int s = 0; s < sg.S; ++s) gr += sg.g[(long)s * sg.gstride + i];
-      float m = sg.m[i], v = sg.v[i];
-      const float p = opt_update(a.st, sg.p[i], gr, m, v, lr_t);
-      sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
-      uint16_t h[3];
-      split3(p, h);
-      for (int q = 0; q < npl; ++q) {
-        if (sg.bf) sg.bf[q * sg.pstride_bf + i] = h[q];
-        tile[q][kk][co] = h[q];
+    // GT_ADAM_UNROLL elements per thread: all their loads issue before the first
+    // update (4 measured neutral: the kernel moves ~260 MB at 25 groups, 12 B of
+    // every parameter's 24 written being the exact bf16 planes of the two copies)
+    constexpr int U = GT_ADAM_UNROLL;
+    for (int idx0 = threadIdx.x; idx0 < Co * ADAM_TK; idx0 += 256 * U) {
+      float gr[U], mv[U], vv[U], pv[U];
+      long iv[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = idx0 + 256 * u;
+        const int co = idx / ADAM_TK, kk = idx % ADAM_TK, k = k0 + kk;
+        ok[u] = idx < Co * ADAM_TK && k < Kd;
+        iv[u] = base + (long)co * Kd + (ok[u] ? k : 0);
+        gr[u] = 0.f; mv[u] = vv[u] = pv[u] = 0.f;
+        if (ok[u]) {
+          for (int s = 0; s < sg.S; ++s) gr[u] += sg.g[(long)s * sg.gstride + iv[u]];
+          mv[u] = sg.m[iv[u]]; vv[u] = sg.v[iv[u]]; pv[u] = sg.p[iv[u]];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (!ok[u]) continue;
+        const int idx = idx0 + 256 * u;
+        const int co = idx / ADAM_TK, kk = idx % ADAM_TK;
+        const long i = iv[u];
+        float m = mv[u], v = vv[u];
+        const float p = opt_update(a.st, pv[u], gr[u], m, v, lr_t);
+        sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
+        uint16_t h[3];
+        split3(p, h);
+        for (int q = 0; q < npl; ++q) {
+          if (sg.bf) sg.bf[q * sg.pstride_bf + i] = h[q];
+          tile[q][kk][co] = h[q];
+        }
       }
     }
     __syncthreads();
