@@ -30,6 +30,9 @@
 #define ADAM_B2 0.999f
 #define ADAM_EPS 1e-7f
 #define CLIP_EPS 1e-7f
+#ifndef GT_DGRAD_BUF
+#define GT_DGRAD_BUF 2     // dense_dgrad_stream2_kernel: k-steps in flight per wave (4: 3 % slower, profiles/dense_dgrad_buf_ab_r4.txt)
+#endif
 #ifndef GT_ADAM_UNROLL
 #define GT_ADAM_UNROLL 1   // adam_segments_kernel tiled path: elements per thread whose loads issue together (4: neutral, profiles/adam_unroll_ab_r4.txt)
 #endif
@@ -892,8 +895,10 @@ __global__ void __launch_bounds__(256) dense_dgrad_stream2_kernel(DenseDgradArgs
   f32x4_t acc[2][2];
 #pragma unroll
   for (int m = 0; m < 2; ++m) acc[m][0] = acc[m][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float rw[2][2][8];
-  uint4 rh[2][2][NPL];
+  constexpr int NBUF = GT_DGRAD_BUF;                   // k-steps in flight per wave (grid-limited occupancy:
+                                                        // ~2.7 waves per SIMD, so registers are free)
+  float rw[NBUF][2][8];
+  uint4 rh[NBUF][2][NPL];
   const uint4* zero4 = reinterpret_cast<const uint4*>(gt_zero8);
   auto load = [&](int j, int buf) {
     const int c = 4 * j + kq;
@@ -915,19 +920,22 @@ __global__ void __launch_bounds__(256) dense_dgrad_stream2_kernel(DenseDgradArgs
       acc[m][1] = mfma_np<NPL>(af, rh[buf][1], acc[m][1]);
     }
   };
-  load(0, 0);                              // (unconditional loads, ordered: see dense_fwd_stream_kernel)
-  __builtin_amdgcn_sched_barrier(0);
-  load(1, 1);
-  __builtin_amdgcn_sched_barrier(0);
-  for (int j = 0; j < nks; j += 2) {
-    step(0);
+  // (unconditional loads, ordered: see dense_fwd_stream_kernel)
+#pragma unroll
+  for (int t = 0; t < NBUF; ++t) {
+    load(t, t);
     __builtin_amdgcn_sched_barrier(0);
-    load(j + 2, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    step(1);
-    __builtin_amdgcn_sched_barrier(0);
-    load(j + 3, 1);
-    __builtin_amdgcn_sched_barrier(0);
+  }
+  const int nks2 = (nks + 1) & ~1;      // the k-steps NBUF 2 runs (an odd count ends on a zero-loaded step)
+  for (int j = 0; j < nks; j += NBUF) {
+#pragma unroll
+    for (int t = 0; t < NBUF; ++t) {
+      // the same k-steps in the same order at any NBUF (bit-identical dx)
+      if (j + t < nks2) step(t);
+      __builtin_amdgcn_sched_barrier(0);
+      load(j + NBUF + t, t);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 #pragma unroll
   for (int m = 0; m < 2; ++m) dense_dgrad_epilogue<PREC>(a, g, f_t + 16 * m, b0, acc[m], lane);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments (A/B runs, searches), one function per gpurun call; every
 # profiles/*_r4* file names the experiment that produced it: bash tools/r4_experiments.sh NAME
-#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35 call36 call37
+#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35 call36 call37 call38
 # Run from the repository root on the GPU box (tools/gpu.sh has the shared tasks).
 set -o pipefail
 
@@ -549,6 +549,29 @@ exp_call37() {
   grep -E "adam" gpurun_out/r4c37_kernel_stats.csv | cut -c1-160
 }
 
+exp_call38() {
+  # dense data gradient v2 with 4 k-steps in flight per wave (GT_DGRAD_BUF=4, default) vs 2 (ab_libs/dgrad_b2.so)
+  timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_hip_dense_stream.py tests/test_hip_train.py tests/test_hip_fp32.py tests/test_hip_dp.py \
+    > gpurun_out/r4c38_test.log 2>&1 || { tail -30 gpurun_out/r4c38_test.log; exit 1; }
+  tail -1 gpurun_out/r4c38_test.log
+  for v in "b2 5" "b4 5" "b2 5" "b4 5" "b2 2" "b4 2"; do
+    set -- $v
+    lib=""; [ "$1" = "b2" ] && lib=ab_libs/dgrad_b2.so
+    GENTUN_HIP_LIB=$lib DTYPE=fp32 RESET=all timeout -k 10 200 python -u tools/probe_pop.py $2 $2 1 4 \
+      > gpurun_out/r4c38_run.log 2>&1 || { tail -5 gpurun_out/r4c38_run.log; exit 1; }
+    echo "P=$2 dgrad=$1 $(grep -o '"ms_per_step": [0-9.]*, "ms_per_cand_step": [0-9.]*, "cand_per_hour_full_protocol": [0-9.]*' gpurun_out/r4c38_run.log)"
+  done
+  cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+  for v in b2 b4; do
+    lib=""; [ "$v" = "b2" ] && lib=ab_libs/dgrad_b2.so
+    rm -rf /tmp/a38$v
+    GENTUN_HIP_LIB=$lib WARM=0 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d /tmp/a38$v -o run --output-format csv -- python3 tools/probe_pop.py 5 5 1 1 2000 > gpurun_out/r4c38_prof.log 2>&1 \
+      || { tail -5 gpurun_out/r4c38_prof.log; exit 1; }
+    find /tmp/a38$v -name "*kernel_stats.csv" -exec cp {} gpurun_out/r4c38_kernel_stats_$v.csv \;
+    echo "$v: $(grep -E "dense_dgrad" gpurun_out/r4c38_kernel_stats_$v.csv | cut -c1-120)"
+  done
+}
+
 case "${1:-}" in
   call4) exp_call4 ;;
   call5) exp_call5 ;;
@@ -586,5 +609,6 @@ case "${1:-}" in
   call35) exp_call35 ;;
   call36) exp_call36 ;;
   call37) exp_call37 ;;
+  call38) exp_call38 ;;
   *) sed -n 2,5p "$0"; exit 2 ;;
 esac
