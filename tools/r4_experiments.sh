@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments (A/B runs, searches), one function per gpurun call; every
 # profiles/*_r4* file names the experiment that produced it: bash tools/r4_experiments.sh NAME
-#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35 call36 call37 call38
+#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35 call36 call37 call38 call39 call40 call41
 # Run from the repository root on the GPU box (tools/gpu.sh has the shared tasks).
 set -o pipefail
 
@@ -572,6 +572,36 @@ exp_call38() {
   done
 }
 
+exp_call39() {
+  # wgrad streams 2 vs 3 at small launches (2 and 10 groups)
+  for v in "kernels 2 2" "kernels 2 3" "kernels 2 2" "kernels 2 3" "all 2 2" "all 2 3" "all 2 2" "all 2 3"; do
+    set -- $v
+    GENTUN_WGRAD_STREAMS=$3 DTYPE=fp32 RESET=$1 timeout -k 10 200 python -u tools/probe_pop.py $2 $2 1 4 \
+      > gpurun_out/r4c39_run.log 2>&1 || { tail -5 gpurun_out/r4c39_run.log; exit 1; }
+    echo "RESET=$1 P=$2 wgrad_streams=$3 $(grep -o '"ms_per_step": [0-9.]*, "ms_per_cand_step": [0-9.]*, "cand_per_hour_full_protocol": [0-9.]*' gpurun_out/r4c39_run.log)"
+  done
+}
+
+exp_call40() {
+  # hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4) x wgrad streams
+  for v in "4 2 all 5" "8 2 all 5" "8 3 all 5" "4 2 all 5" "8 2 all 5" "8 3 all 5" "4 2 kernels 2" "8 2 kernels 2" "8 3 kernels 2"; do
+    set -- $v
+    GPU_MAX_HW_QUEUES=$1 GENTUN_WGRAD_STREAMS=$2 DTYPE=fp32 RESET=$3 timeout -k 10 200 python -u tools/probe_pop.py $4 $4 1 4 \
+      > gpurun_out/r4c40_run.log 2>&1 || { tail -5 gpurun_out/r4c40_run.log; exit 1; }
+    echo "hwq=$1 wgrad_streams=$2 RESET=$3 P=$4 $(grep -o '"ms_per_step": [0-9.]*, "ms_per_cand_step": [0-9.]*, "cand_per_hour_full_protocol": [0-9.]*' gpurun_out/r4c40_run.log)"
+  done
+}
+
+exp_call41() {
+  # hardware queues per process below the default (GPU_MAX_HW_QUEUES 2 / 3 / 4)
+  for v in "4 all 5" "3 all 5" "2 all 5" "4 all 5" "3 all 5" "2 all 5" "4 kernels 2" "3 kernels 2" "2 kernels 2"; do
+    set -- $v
+    GPU_MAX_HW_QUEUES=$1 DTYPE=fp32 RESET=$2 timeout -k 10 200 python -u tools/probe_pop.py $3 $3 1 4 \
+      > gpurun_out/r4c41_run.log 2>&1 || { tail -5 gpurun_out/r4c41_run.log; exit 1; }
+    echo "hwq=$1 RESET=$2 P=$3 $(grep -o '"ms_per_step": [0-9.]*, "ms_per_cand_step": [0-9.]*, "cand_per_hour_full_protocol": [0-9.]*' gpurun_out/r4c41_run.log)"
+  done
+}
+
 case "${1:-}" in
   call4) exp_call4 ;;
   call5) exp_call5 ;;
@@ -610,5 +640,8 @@ case "${1:-}" in
   call36) exp_call36 ;;
   call37) exp_call37 ;;
   call38) exp_call38 ;;
+  call39) exp_call39 ;;
+  call40) exp_call40 ;;
+  call41) exp_call41 ;;
   *) sed -n 2,5p "$0"; exit 2 ;;
 esac
