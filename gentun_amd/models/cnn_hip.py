@@ -53,6 +53,20 @@ from ..utils import rng as _rng
 from .cnn_engine import FoldJob
 from .pop_schedule import PopulationSchedule
 
+_SIDE_STREAMS = {}
+
+
+def _side_streams(dev, prio, n, main):
+    """The side streams of every job issued on stream ``main``, created once
+    per process: a stream gets its hardware queue (4 per process) when it is
+    created, so fresh per-job streams from torch's pool can land on the main
+    stream's queue in some jobs and not in others (profiles/stream_cache_ab_r4.txt).
+    GENTUN_STREAM_CACHE=1 (A/B, not yet measured on the GPU; default: fresh streams per job)."""
+    key = (str(dev), prio, n, main.cuda_stream if main is not None else 0)
+    if key not in _SIDE_STREAMS:
+        _SIDE_STREAMS[key] = [torch.cuda.Stream(dev, priority=prio) for _ in range(n)]
+    return _SIDE_STREAMS[key]
+
 
 # bytes of forward-only activation twins an evaluation may allocate for all groups of a job
 EVAL_TWIN_BUDGET = 1 << 30
@@ -120,16 +134,20 @@ class HipPopJob(FoldJob):
         # edges inside the captured step graph)
         # GENTUN_SIDE_PRIO: priority of the side streams (A/B; HIP: lower = higher priority)
         sprio = int(os.environ.get("GENTUN_SIDE_PRIO", "0"))
-        self.side = torch.cuda.Stream(dev, priority=sprio)
         # the conv wgrads of different layers are independent (own dz, own
         # partial buffers): round-robin over GENTUN_WGRAD_STREAMS streams so a
         # small launch (few groups: 64 workgroups) does not serialise the
-        # backward tail behind one wgrad at a time
+        # backward tail behind one wgrad at a time; the dense W1 optimizer (the
+        # largest single launch) on a stream of its own, so it does not sit in
+        # front of the first conv wgrads
         nws = max(1, int(os.environ.get("GENTUN_WGRAD_STREAMS", "2")))
-        self.wg_streams = [self.side] + [torch.cuda.Stream(dev, priority=sprio) for _ in range(nws - 1)]
-        # the dense W1 optimizer (the largest single launch) on a stream of its
-        # own, so it does not sit in front of the first conv wgrads
-        self.side2 = torch.cuda.Stream(dev, priority=sprio)
+        if os.environ.get("GENTUN_STREAM_CACHE", "0") == "1":
+            ss = _side_streams(dev, sprio, nws + 1, getattr(self, "stream", None))
+        else:
+            ss = [torch.cuda.Stream(dev, priority=sprio) for _ in range(nws + 1)]
+        self.side = ss[0]
+        self.wg_streams = list(ss[:nws])
+        self.side2 = ss[nws]
         # GENTUN_OVERLAP=0: one stream (A/B of the fork / join edges at small launches)
         self.overlap = os.environ.get("GENTUN_OVERLAP", "1") != "0"
         self.w1_stream = os.environ.get("GENTUN_W1_STREAM", "1") != "0"

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 GPU experiments (A/B runs, searches), one function per gpurun call; every
 # profiles/*_r4* file names the experiment that produced it: bash tools/r4_experiments.sh NAME
-#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35 call36 call37 call38 call39 call40 call41
+#   NAME: call4 call5 call6 call7 call8 call9 call10 call11 call12 call13 call14 call15 call16 call17 call18 call19 call20 call21 call22 call23 call24 call25 call26 call27 call28 call29 call30 call31 call32 call33 call34 dense ga_deep call35 call36 call37 call38 call39 call40 call41 call42
 # Run from the repository root on the GPU box (tools/gpu.sh has the shared tasks).
 set -o pipefail
 
@@ -602,6 +602,26 @@ exp_call41() {
   done
 }
 
+exp_call42() {
+  # side streams created once per process (GENTUN_STREAM_CACHE=1) vs fresh streams per job (0): tests, population step, bench.py
+  ( while true; do sleep 50; echo hb > gpurun_out/heartbeat; done ) & HB=$!
+  trap "kill $HB" EXIT
+  timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_hip_train.py \
+    > gpurun_out/r4c42_test.log 2>&1 || { tail -30 gpurun_out/r4c42_test.log; exit 1; }
+  tail -1 gpurun_out/r4c42_test.log
+  for v in "0 all 5" "1 all 5" "0 kernels 2" "1 kernels 2"; do
+    set -- $v
+    GENTUN_STREAM_CACHE=$1 DTYPE=fp32 RESET=$2 timeout -k 10 200 python -u tools/probe_pop.py $3 $3 1 4 \
+      > gpurun_out/r4c42_run.log 2>&1 || { tail -5 gpurun_out/r4c42_run.log; exit 1; }
+    echo "cache=$1 RESET=$2 P=$3 $(grep -o '"ms_per_step": [0-9.]*, "ms_per_cand_step": [0-9.]*, "cand_per_hour_full_protocol": [0-9.]*' gpurun_out/r4c42_run.log)"
+  done
+  for c in 0 1 0 1; do
+    GENTUN_STREAM_CACHE=$c timeout -k 10 300 python3 -u bench.py --gpus 1 --steps 8 --warmup 2 > gpurun_out/r4c42_c$c.json 2> gpurun_out/r4c42_c$c.err \
+      || { tail -5 gpurun_out/r4c42_c$c.err; exit 1; }
+    echo "bench cache=$c $(grep -o '"value": [0-9.]*, "unit": "[a-z/]*", "n_gpus": 1, "steps": 8, "warmup": 2, "ms_per_step": [0-9.]*' gpurun_out/r4c42_c$c.json)"
+  done
+}
+
 case "${1:-}" in
   call4) exp_call4 ;;
   call5) exp_call5 ;;
@@ -643,5 +663,6 @@ case "${1:-}" in
   call39) exp_call39 ;;
   call40) exp_call40 ;;
   call41) exp_call41 ;;
+  call42) exp_call42 ;;
   *) sed -n 2,5p "$0"; exit 2 ;;
 esac
