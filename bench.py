@@ -178,9 +178,11 @@ def run(args):
         fittest = ga._evaluate_and_report()
         fm = getattr(fittest, "fold_metrics", None) or {}
         cat = fm.get("categorical_accuracy")
+        h = ga.history[-1]
         completed.append({"generation": ga.generation, "best_fitness": fittest.get_fitness(),
                           "best_cat_acc": float(sum(cat) / len(cat)) if cat else None,
-                          "best_genes": dict(fittest.get_genes())})
+                          "best_genes": dict(fittest.get_genes()),
+                          "mean_cat_acc": h.get("mean_cat_acc"), "mean_fitness": h.get("mean_fitness_finite")})
         ga.breed()
         ga.generation += 1
 
@@ -271,6 +273,12 @@ def run(args):
         "best_genes": last["best_genes"] if last else None,
         "best_val_cat_acc_by_gen": [round(c["best_cat_acc"], 4) if c["best_cat_acc"] is not None else None
                                     for c in completed],
+        # population means per completed generation (the search signal: RR-GA keeps no elite, so the
+        # best-by-generation curve is not monotone; the mean shows whether selection moves the population)
+        "mean_val_cat_acc_by_gen": [round(c["mean_cat_acc"], 4) if c["mean_cat_acc"] is not None else None
+                                    for c in completed],
+        "mean_fitness_by_gen": [round(c["mean_fitness"], 5) if c["mean_fitness"] is not None else None
+                                for c in completed],
         # the fittest individual evaluated in the run (also when no generation completed)
         "best_val_acc_evaluated": round(best_seen["cat"], 5) if best_seen else None,
         "best_genes_evaluated": best_seen.get("genes"),

@@ -117,14 +117,17 @@ def _run_search(args, species, x, y, extra, maximize):
         pop = DistributedPopulation(species, x, y, size=args.pop, maximize=maximize, additional_parameters=extra,
                                     comm=comm, evaluator=evaluator, schedule=cfg.schedule)
         ga = cls(pop, seed=cfg.seed, checkpoint_dir=cfg.checkpoint_dir, event_log=log, **ga_kw)
+    from .parallel.distributed import AllEvaluationsFailed
     try:
         best = ga.run(args.gens)
-    except Exception:
+    except AllEvaluationsFailed:
         import traceback
         traceback.print_exc()
-        # every evaluator rank still waits in the dispatch broadcast: release them (CMD_STOP) before
+        # every evaluator rank waits in the next dispatch broadcast: release them (CMD_STOP) before
         # failing, and exit with a code the restart supervisor does not retry (a failed search is
-        # not a transient rank fault: resuming from the checkpoint would fail the same way)
+        # not a transient rank fault: resuming from the checkpoint would fail the same way). Any
+        # other exception (a HIP launch failure, a checkpoint OSError, a dead peer's collective
+        # error) propagates: a non-zero exit the supervisor restarts from the last checkpoint.
         try:
             ga.population.shutdown()
         finally:

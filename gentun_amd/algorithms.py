@@ -83,6 +83,13 @@ class GeneticAlgorithm(object):
         if cat:
             # Genetic-CNN: the fitness is the reference's binary accuracy; record categorical too
             rec["best_cat_acc"] = float(sum(cat) / len(cat))
+        # population means over the members that evaluated (a failed one carries +-inf)
+        finite = [f for f in fits if math.isfinite(f)]
+        rec["mean_fitness_finite"] = sum(finite) / len(finite) if finite else None
+        cats = [(getattr(ind, "fold_metrics", None) or {}).get("categorical_accuracy") for ind in self.population]
+        cats = [float(sum(c) / len(c)) for c in cats if c]
+        if cats:
+            rec["mean_cat_acc"] = sum(cats) / len(cats)
         self.history.append(rec)
         if self.best_individual is None or self._better(fittest.get_fitness(), self.best_individual.get_fitness()):
             self.best_individual = fittest

@@ -31,6 +31,15 @@ class Communicator(object):
         by receivers; pass ``None`` there)."""
         raise NotImplementedError
 
+    def broadcast_arrays(self, arrays, src=0):
+        """Broadcast a list of arrays from ``src`` as one message (receivers
+        pass ``None``). Default: one broadcast per array."""
+        if self.rank == src:
+            self.broadcast_array(np.array([len(arrays)], np.int64), src)
+            return [self.broadcast_array(a, src) for a in arrays]
+        n = int(self.broadcast_array(None, src)[0])
+        return [self.broadcast_array(None, src) for _ in range(n)]
+
     def all_gather_array(self, arr):
         """Return a list of every rank's array (same shape on every rank)."""
         raise NotImplementedError
@@ -71,6 +80,14 @@ class LocalComm(Communicator):
 
 _DTYPES = [np.float64, np.float32, np.int64, np.int32, np.uint8]
 
+# One dispatch message (X1 + X2: command header, optional config blob, genome table) travels as ONE
+# fixed-size byte tensor: a 64-word int64 header (array count, per array dtype / ndim / shape, total
+# payload bytes) followed by the arrays' bytes, each 8-byte aligned. A message larger than the
+# fixed capacity sends its remainder in a second broadcast whose size the header announces.
+_MSG_WORDS = 64
+_MSG_CAP = 32768            # bytes per message tensor (header included): every dispatch of the bench fits
+_MSG_MAX_ARRAYS = 7         # 1 + 8 words per array within the 64-word header
+
 
 def _attempt_store(timeout):
     """Under torchrun's static rendezvous the agent's TCPStore outlives a
@@ -91,27 +108,85 @@ def _attempt_store(timeout):
     return dist.PrefixStore("gentun/attempt_{}".format(os.environ["TORCHELASTIC_RESTART_COUNT"]), base)
 
 
+def _own_store(timeout):
+    """The rendezvous store of a launch without torchrun's agent store (plain
+    ``MASTER_ADDR`` / ``MASTER_PORT`` / ``RANK`` / ``WORLD_SIZE``): rank 0
+    hosts it, exactly what ``init_process_group("env://")`` would create --
+    but created here, so the communicator keeps the handle (the ticket
+    counter of dynamic scheduling, X6) instead of fishing it out of
+    torch.distributed's private state."""
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    return dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world,
+                         is_master=(rank == 0), timeout=timeout)
+
+
+def pack_message(arrays):
+    """numpy arrays -> (int64 header words, payload bytes) of one message."""
+    if len(arrays) > _MSG_MAX_ARRAYS:
+        raise ValueError("at most {} arrays per message".format(_MSG_MAX_ARRAYS))
+    hdr = np.zeros(_MSG_WORDS, np.int64)
+    hdr[1] = len(arrays)
+    parts = []
+    for i, arr in enumerate(arrays):
+        arr = np.ascontiguousarray(arr)
+        code = [c for c, d in enumerate(_DTYPES) if np.dtype(d) == arr.dtype]
+        if not code:
+            raise TypeError("unsupported dtype {}".format(arr.dtype))
+        if arr.ndim > 6:
+            raise ValueError("at most 6 dims")
+        w = 2 + 8 * i
+        hdr[w] = code[0]
+        hdr[w + 1] = arr.ndim
+        hdr[w + 2:w + 2 + arr.ndim] = arr.shape
+        b = arr.tobytes()
+        parts.append(b + b"\0" * (-len(b) % 8))
+    payload = b"".join(parts)
+    hdr[0] = len(payload)
+    return hdr, payload
+
+
+def unpack_message(hdr, payload):
+    """The inverse of :func:`pack_message`: a list of (copied) numpy arrays."""
+    out, off = [], 0
+    for i in range(int(hdr[1])):
+        w = 2 + 8 * i
+        dtype = np.dtype(_DTYPES[int(hdr[w])])
+        shape = tuple(int(s) for s in hdr[w + 2:w + 2 + int(hdr[w + 1])])
+        n = int(np.prod(shape, dtype=np.int64)) * dtype.itemsize
+        out.append(np.frombuffer(payload, dtype, count=n // dtype.itemsize, offset=off).reshape(shape).copy())
+        off += n + (-n % 8)
+    return out
+
+
 class DistComm(Communicator):
     """``torch.distributed`` collectives on small numpy arrays.
 
     With the ``nccl`` (RCCL) backend arrays travel as device tensors on this
-    rank's GPU; with ``gloo`` as CPU tensors. Headers (dtype, ndim, shape)
-    are broadcast as a fixed 8-int64 vector first so receivers need no
-    out-of-band shape knowledge.
+    rank's GPU; with ``gloo`` as CPU tensors. A broadcast message (one or
+    several arrays) is ONE fixed-size byte tensor with a self-describing
+    header, so receivers need no out-of-band shape knowledge and pay one
+    collective and one host synchronisation per message.
+
+    The process group is initialised on a store this object creates (or
+    receives as ``store=`` together with ``init=False``); :meth:`ticket`
+    counts on it.
     """
 
-    def __init__(self, backend=None, timeout_s=1800, init=True, device=None):
+    def __init__(self, backend=None, timeout_s=1800, init=True, device=None, store=None):
         import torch.distributed as dist
         self.dist = dist
+        self.store = store
         if init and not dist.is_initialized():
             if backend is None:
                 backend = "nccl" if torch.cuda.is_available() else "gloo"
-            kwargs = {"backend": backend, "timeout": datetime.timedelta(seconds=timeout_s)}
+            timeout = datetime.timedelta(seconds=timeout_s)
+            kwargs = {"backend": backend, "timeout": timeout}
             if backend == "nccl" and device is not None:
                 kwargs["device_id"] = torch.device(device)
-            store = _attempt_store(kwargs["timeout"])
-            if store is not None:
-                kwargs.update(store=store, rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
+            if self.store is None:
+                self.store = _attempt_store(timeout) or _own_store(timeout)
+            kwargs.update(store=self.store, rank=int(os.environ["RANK"]), world_size=int(os.environ["WORLD_SIZE"]))
             dist.init_process_group(**kwargs)
         self.backend = dist.get_backend()
         self.rank = dist.get_rank()
@@ -121,34 +196,39 @@ class DistComm(Communicator):
                 torch.device("cuda", torch.cuda.current_device())
         else:
             self.device = torch.device("cpu")
+        self.messages = 0               # broadcast messages sent / received (tests count collectives)
 
     def _t(self, arr):
         return torch.from_numpy(np.ascontiguousarray(arr)).to(self.device)
 
+    def broadcast_arrays(self, arrays, src=0):
+        """Broadcast a list of numpy arrays from ``src`` as one message
+        (receivers pass ``None`` and get the list back)."""
+        buf = np.zeros(_MSG_CAP, np.uint8)
+        rest = b""
+        if self.rank == src:
+            hdr, payload = pack_message(list(arrays))
+            head = _MSG_CAP - 8 * _MSG_WORDS
+            buf[:8 * _MSG_WORDS] = hdr.view(np.uint8)
+            buf[8 * _MSG_WORDS:8 * _MSG_WORDS + min(head, len(payload))] = np.frombuffer(payload[:head], np.uint8)
+            rest = payload[head:]
+        t = self._t(buf)
+        self.dist.broadcast(t, src=src)
+        got = t.cpu().numpy()                         # the one host sync of a message
+        self.messages += 1
+        hdr = got[:8 * _MSG_WORDS].view(np.int64)
+        total = int(hdr[0])
+        head = _MSG_CAP - 8 * _MSG_WORDS
+        payload = got[8 * _MSG_WORDS:8 * _MSG_WORDS + min(head, total)].tobytes()
+        if total > head:                              # rare: a message beyond the fixed capacity
+            tail = self._t(np.frombuffer(rest, np.uint8)) if self.rank == src else \
+                torch.empty(total - head, dtype=torch.uint8, device=self.device)
+            self.dist.broadcast(tail, src=src)
+            payload += tail.cpu().numpy().tobytes()
+        return unpack_message(hdr, payload)
+
     def broadcast_array(self, arr, src=0):
-        hdr = np.zeros(8, np.int64)
-        if self.rank == src:
-            arr = np.ascontiguousarray(arr)
-            code = [i for i, d in enumerate(_DTYPES) if np.dtype(d) == arr.dtype]
-            if not code:
-                raise TypeError("unsupported dtype {}".format(arr.dtype))
-            if arr.ndim > 6:
-                raise ValueError("at most 6 dims")
-            hdr[0] = code[0]
-            hdr[1] = arr.ndim
-            hdr[2:2 + arr.ndim] = arr.shape
-        th = self._t(hdr)
-        self.dist.broadcast(th, src=src)
-        hdr = th.cpu().numpy()
-        dtype = _DTYPES[int(hdr[0])]
-        shape = tuple(int(s) for s in hdr[2:2 + int(hdr[1])])
-        if self.rank == src:
-            payload = self._t(arr.astype(dtype, copy=False))
-        else:
-            payload = torch.empty(shape, dtype=torch.from_numpy(np.zeros(0, dtype)).dtype, device=self.device)
-        if payload.numel():
-            self.dist.broadcast(payload, src=src)
-        return payload.cpu().numpy()
+        return self.broadcast_arrays([arr] if self.rank == src else None, src=src)[0]
 
     def all_gather_array(self, arr):
         t = self._t(arr)
@@ -163,10 +243,12 @@ class DistComm(Communicator):
             self.dist.barrier()
 
     def ticket(self, key):
-        # the rendezvous TCPStore of the process group: one round trip to the
-        # store host (rank 0's node), no collective, ranks proceed independently
-        store = self.dist.distributed_c10d._get_default_store()
-        return int(store.add("gentun/" + key, 1)) - 1
+        # the rendezvous store this communicator created: one round trip to the store host (rank 0's
+        # node), no collective, ranks proceed independently
+        if self.store is None:
+            raise RuntimeError("DistComm.ticket needs the rendezvous store: construct DistComm with init=True, "
+                               "or pass store= with init=False")
+        return int(self.store.add("gentun/" + key, 1)) - 1
 
     def destroy(self):
         if self.dist.is_initialized():
@@ -206,6 +288,10 @@ class ThreadComm(Communicator):
     def broadcast_array(self, arr, src=0):
         vals = self._exchange(np.array(arr, copy=True) if self.rank == src else None)
         return np.array(vals[src], copy=True)
+
+    def broadcast_arrays(self, arrays, src=0):
+        vals = self._exchange([np.array(a, copy=True) for a in arrays] if self.rank == src else None)
+        return [np.array(a, copy=True) for a in vals[src]]
 
     def all_gather_array(self, arr):
         return [np.array(v, copy=True) for v in self._exchange(np.array(arr, copy=True))]

@@ -280,6 +280,15 @@ def _row(status, fitness, wall, scores, nfold, fold_ids, aux=None):
 # master side
 # ---------------------------------------------------------------------------
 
+class AllEvaluationsFailed(RuntimeError):
+    """Every candidate of a dispatch failed, on its rank and on the retry
+    round: a search on worst-fitness placeholders is meaningless, and resuming
+    from the checkpoint would fail the same way (the CLI maps this, and only
+    this, to the non-restartable exit code). Raised after the round's
+    all_gather, so the evaluator ranks wait in the next broadcast and a STOP
+    message reaches them."""
+
+
 class DistributedPopulation(Population):
     """Population whose pending individuals are evaluated by all ranks.
 
@@ -392,7 +401,8 @@ class DistributedPopulation(Population):
         if len(todo) > 1 and nworst == len(todo):
             # nothing evaluated anywhere (a lost device, a broken build): a search on worst-fitness
             # placeholders is meaningless -- stop loudly instead of breeding from them
-            raise RuntimeError("every evaluation of dispatch {} failed (and its retry)".format(self.generation_counter))
+            raise AllEvaluationsFailed("every evaluation of dispatch {} failed (and its retry)".format(
+                self.generation_counter))
         self.last_dispatch = {"units": info["units"], "candidates": len(todo), "retried": len(failed),
                               "wall_s": time.perf_counter() - t0, "schedule": info["schedule"],
                               "per_rank_units": info["per_rank_units"]}
@@ -449,11 +459,11 @@ class DistributedPopulation(Population):
         # X1: the config blob travels once (and again only if it changes); the
         # evaluator ranks keep the last one
         send_blob = blob != getattr(comm, "_gentun_last_blob", None)
-        comm.broadcast_array(np.array([CMD_EVAL, self.generation_counter, len(todo), nfold, int(send_blob)], np.int64))
+        # X1 + X2 as ONE message: command header, the config blob when it changed, the genome table
+        hdr = np.array([CMD_EVAL, self.generation_counter, len(todo), nfold, int(send_blob)], np.int64)
+        comm.broadcast_arrays([hdr, np.frombuffer(blob, np.uint8), table] if send_blob else [hdr, table])
         if send_blob:
-            comm.broadcast_array(np.frombuffer(blob, np.uint8))
             comm._gentun_last_blob = blob
-        comm.broadcast_array(table)
 
         def make_unit(k):
             slot, fids = units[k]
@@ -512,14 +522,14 @@ class DistributedPopulation(Population):
     def sync_ranks(self):
         """Device-synchronise every rank and barrier (bench timing fence)."""
         if self.comm.world_size > 1:
-            self.comm.broadcast_array(np.array([CMD_SYNC, self.generation_counter, 0, 0, 0], np.int64))
+            self.comm.broadcast_arrays([np.array([CMD_SYNC, self.generation_counter, 0, 0, 0], np.int64)])
         _device_sync(self.local_evaluator)
         self.comm.barrier()
 
     def shutdown(self):
         """Release the evaluator ranks (they return from ``work()``)."""
         if self.comm.world_size > 1:
-            self.comm.broadcast_array(np.array([CMD_STOP, self.generation_counter, 0, 0, 0], np.int64))
+            self.comm.broadcast_arrays([np.array([CMD_STOP, self.generation_counter, 0, 0, 0], np.int64)])
 
 
 def _clone(ind):
@@ -607,8 +617,8 @@ class GentunWorker(object):
         wd = _fault.watchdog()
         if wd is not None:
             wd.arm("evaluator rank {} waiting / evaluating".format(comm.rank))
-        hdr = comm.broadcast_array(None)
-        cmd, generation, _ncand, nfold, has_blob = (int(v) for v in hdr)
+        msg = comm.broadcast_arrays(None)
+        cmd, generation, _ncand, nfold, has_blob = (int(v) for v in msg[0])
         if cmd == CMD_STOP:
             if wd is not None:
                 wd.disarm()
@@ -620,13 +630,12 @@ class GentunWorker(object):
                 wd.disarm()
             return True
         if has_blob:
-            blob = comm.broadcast_array(None)
-            self._meta = json.loads(bytes(blob.astype(np.uint8)).decode())
+            self._meta = json.loads(bytes(msg[1].astype(np.uint8)).decode())
         meta = self._meta
         if meta is None:
             raise RuntimeError("evaluator rank {}: generation {} arrived before the config blob".format(
                 comm.rank, generation))
-        table = comm.broadcast_array(None)
+        table = msg[-1]
         extra = {k: _tuplify(v) for k, v in meta["extra"].items()}
         # genome spec comes with the broadcast: building a throw-away individual
         # here would draw random genes from the GA stream

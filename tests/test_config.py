@@ -46,3 +46,29 @@ def test_cli_precedence(monkeypatch):
     args = ap.parse_args(["--pop-batch", "2"])
     cfg = cli._config(args)
     assert cfg.pop_batch == 2 and cfg.pairing == "disjoint" and cfg.streams == 1
+
+
+@pytest.mark.parametrize("exc,expect", [("all_failed", "search_failed"), ("oserror", "propagates")])
+def test_cli_maps_only_all_failed_to_the_final_exit(monkeypatch, tmp_path, exc, expect):
+    """Only AllEvaluationsFailed becomes the non-restartable exit code 78; any
+    other error (checkpoint OSError, HIP launch failure, dead peer) propagates,
+    so the supervisor restarts the run from its checkpoint."""
+    from gentun_amd import __main__ as cli
+    from gentun_amd.algorithms import GeneticAlgorithm
+    from gentun_amd.parallel.distributed import AllEvaluationsFailed
+    from gentun_amd.parallel.fault import EXIT_SEARCH_FAILED
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+
+    def boom(self, n):
+        raise AllEvaluationsFailed("x") if exc == "all_failed" else OSError("disk full")
+
+    monkeypatch.setattr(GeneticAlgorithm, "run", boom)
+    argv = ["xgb", "--data", "iris", "--pop", "2", "--gens", "1", "--algorithm", "tournament",
+            "--checkpoint-dir", str(tmp_path)]
+    if expect == "search_failed":
+        with pytest.raises(SystemExit) as e:
+            cli.main(argv)
+        assert e.value.code == EXIT_SEARCH_FAILED
+    else:
+        with pytest.raises(OSError):
+            cli.main(argv)

@@ -168,6 +168,81 @@ def test_gloo_processes_match_local_run():
     assert hist == _local(BitIndividual, RussianRouletteGA, 4, seed=77, size=10)
 
 
+def _msg_proc(rank, world, port, q):
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
+    os.environ.pop("TORCHELASTIC_USE_AGENT_STORE", None)
+    from gentun_amd.parallel import DistComm
+    comm = DistComm(backend="gloo", timeout_s=60)
+    big = np.arange(20000, dtype=np.float64).reshape(100, 200)            # 160 KB: beyond one message tensor
+    sent = [np.array([3, 1, 4], np.int64), np.frombuffer(b"blob", np.uint8).copy(), big,
+            np.zeros((0, 3), np.float32)]
+    got = comm.broadcast_arrays(sent if rank == 0 else None)
+    ok = len(got) == len(sent) and all(a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a, b)
+                                       for a, b in zip(sent, got))
+    one = comm.broadcast_array(np.array([7.5], np.float32) if rank == 0 else None)
+    ok = ok and one.dtype == np.float32 and float(one[0]) == 7.5 and comm.messages == 2
+    # X6 tickets on the communicator's own rendezvous store: every value taken exactly once
+    tickets = [comm.ticket("t") for _ in range(5)]
+    allt = comm.all_gather_array(np.array(tickets, np.int64))
+    ok = ok and sorted(np.concatenate(allt).tolist()) == list(range(5 * world))
+    comm.barrier()
+    q.put((rank, ok))
+    comm.destroy()
+
+
+def test_gloo_one_message_broadcast_and_own_store_tickets():
+    """A dispatch message (several arrays, also beyond the fixed 32 KB tensor)
+    arrives intact on every rank as one message; tickets count on the store
+    DistComm created itself (no private torch.distributed state)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_msg_proc, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: True, 1: True, 2: True}
+
+
+def test_dispatch_is_one_message_per_round():
+    """Rank 0 sends one broadcast message per evaluation round (header, config
+    blob and genome table together), not one per array."""
+    comms = ThreadComm.group(2)
+    counts = {"n": 0}
+    orig = ThreadComm.broadcast_arrays
+
+    def counting(self, arrays, src=0):
+        if self.rank == 0:
+            counts["n"] += 1
+        return orig(self, arrays, src)
+
+    ThreadComm.broadcast_arrays = counting
+    try:
+        t = threading.Thread(target=lambda: GentunWorker(BitIndividual, None, None, comm=comms[1],
+                                                         evaluator=SequentialEvaluator()).work(), daemon=True)
+        t.start()
+        rng.seed(5)
+        pop = DistributedPopulation(BitIndividual, None, None, size=6, comm=comms[0], evaluator=SequentialEvaluator())
+        pop.evaluate_in_parallel()
+        assert counts["n"] == 1
+        pop.shutdown()
+        t.join(timeout=30)
+        assert counts["n"] == 2
+    finally:
+        ThreadComm.broadcast_arrays = orig
+
+
+def test_comm_uses_no_private_torch_symbols():
+    import inspect
+    from gentun_amd.parallel import comm
+    src = inspect.getsource(comm)
+    assert "_get_default_store" not in src and "distributed_c10d" not in src
+
+
 def test_dynamic_and_static_schedules_agree():
     """Work stealing (ticket counter) and static LPT give the same GA run;
     every unit is evaluated exactly once."""

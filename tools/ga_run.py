@@ -86,5 +86,9 @@ print(json.dumps({"generations": len(ga.history), "evals": evals, "eval_wall_s":
                   "batch_norm": args.batch_norm,
                   "best_val_cat_acc_by_gen": [round(h.get("best_cat_acc") or 0.0, 4) for h in ga.history],
                   "best_val_binary_acc_by_gen": [round(h["best_fitness"], 5) for h in ga.history],
+                  "mean_val_cat_acc_by_gen": [round(h["mean_cat_acc"], 4) if h.get("mean_cat_acc") is not None
+                                              else None for h in ga.history],
+                  "mean_fitness_by_gen": [round(h.get("mean_fitness_finite", h["mean_fitness"]) or 0.0, 5)
+                                          for h in ga.history],
                   "evals_by_gen": [h["evals"] for h in ga.history],
                   "best_genes_by_gen": [h["best_genes"] for h in ga.history]}), flush=True)
