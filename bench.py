@@ -83,6 +83,12 @@ def parse():
     ap.add_argument("--kernels", default=None, help="override kernels per stage, e.g. 64,128,256")
     ap.add_argument("--batch-norm", action="store_true",
                     help="conv -> BatchNorm -> ReLU in every node (not in the reference network)")
+    ap.add_argument("--input-shape", default="32,32,3",
+                    help="H,W,C of the synthetic images; 28,28,1 is the reference's MNIST default "
+                         "(gentun/individuals.py:221, tests/test_mnist.py)")
+    ap.add_argument("--pad-images", type=int, default=1,
+                    help="1: a 28x28 image is stored zero-padded to 32x32 so every stage runs the "
+                         "shape-specialised kernels (ops/cnn_kernels.padded_hw); 0: the generic kernels")
     return ap.parse_args()
 
 
@@ -128,7 +134,8 @@ def run(args):
     from gentun_amd.parallel import DistComm, LocalComm
     from gentun_amd.parallel.distributed import DistributedPopulation, GentunWorker
     from gentun_amd.utils import rng as grng
-    from gentun_amd.utils.data import make_cifar_hard, make_cifar_like
+    from gentun_amd.utils.data import (make_cifar_hard, make_cifar_like, make_glyph_classification,
+                                       make_variant_classification)
 
     if world > 1:
         # RCCL (backend "nccl") over xGMI between GPUs; GENTUN_DIST_BACKEND=gloo for rehearsals
@@ -142,16 +149,23 @@ def run(args):
     # sequential folds (kernels) batch candidates only by fold position: a round takes the whole
     # pending generation (up to 16 per GPU) so every fold launch carries ~14-16 groups
     per_gpu = args.per_gpu or (16 if args.fold_reset == "kernels" else 5 if args.dtype == "fp32" else 8)
-    x, y = (make_cifar_hard if args.data == "hard" else make_cifar_like)(n=args.samples, seed=0)
+    shape = tuple(int(v) for v in args.input_shape.split(","))
+    if shape == (32, 32, 3):
+        x, y = (make_cifar_hard if args.data == "hard" else make_cifar_like)(n=args.samples, seed=0)
+    elif args.data == "hard":
+        x, y = make_variant_classification(n=args.samples, shape=shape, classes=10, seed=0, noise=0.7,
+                                           label_noise=0.3)
+    else:
+        x, y = make_glyph_classification(n=args.samples, shape=shape, classes=10, seed=0, noise=1.0)
     nodes, kernels = ((3, 4, 5), (20, 50, 100)) if args.space == "deep" else ((3, 5), (20, 50))
     if args.kernels:
         kernels = tuple(int(k) for k in args.kernels.split(","))
     space = "S=({}) kernels ({})".format(",".join(map(str, nodes)), ",".join(map(str, kernels)))
-    extra = dict(nodes=nodes, input_shape=(32, 32, 3), kernels_per_layer=kernels,
+    extra = dict(nodes=nodes, input_shape=shape, kernels_per_layer=kernels,
                  kernel_sizes=((5, 5),) * len(nodes), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=args.nfold, epochs=epochs, learning_rate=lrs, batch_size=32, dtype=args.dtype,
                  loss=args.loss, seed=args.seed, backend=args.backend, reset=args.fold_reset, batching="keras",
-                 batch_norm=args.batch_norm)
+                 batch_norm=args.batch_norm, pad_images=bool(args.pad_images))
     evaluator = LocalBatchEvaluator(device=device, streams=args.streams, pop_batch=args.pop_batch,
                                     torch_pop=not args.torch_unbatched)
     N = comm.world_size
@@ -242,10 +256,11 @@ def run(args):
         "scaling": "weak" if args.pop_per_gpu else "strong",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": ("synthetic (CIFAR-10-shaped {}k x 32x32x3: 5 stroke glyphs x 2 tick variants + clutter + noise, "
+        "data": ("synthetic ({}-shaped {}k x {}: 5 stroke glyphs x 2 tick variants + clutter + noise, "
                  "30% variant-label noise; random-init weights)" if args.data == "hard" else
-                 "synthetic (CIFAR-10-shaped {}k x 32x32x3 coloured stroke glyphs + clutter + noise; "
-                 "random-init weights)").format(args.samples // 1000),
+                 "synthetic ({}-shaped {}k x {} stroke glyphs + clutter + noise; "
+                 "random-init weights)").format("CIFAR-10" if shape == (32, 32, 3) else "MNIST" if shape == (28, 28, 1)
+                                                else "image", args.samples // 1000, "x".join(map(str, shape))),
         "config": {"model": "Genetic-CNN {} dense 500".format(space), "global_batch": 32 * args.nfold,
                    "seq_len": None,
                    "parallelism": ("population-dp{} ({} genome bcast / score all_gather)".format(

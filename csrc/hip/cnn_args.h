@@ -56,10 +56,12 @@ struct ConvArgs {
   void* unpool_x1;                  // un-pool: gradient of the pool source, slot 1 (groups with sel[g] = 1)
   const int* unpool_sel;            // un-pool: [Q] pool source per group (pop_schedule.pool_source)
   int cout_real;                    // real output channels (<= Coutp; 0 = unknown): prec-1 packed last co tile
-  // fp32 tile kernel: workgroups whose hardware id is in [stagger_lo, stagger_hi) start `stagger` x 2048
-  // cycles late, so the two workgroups sharing a CU run out of phase (one stages while the other runs its
-  // MFMA loop) instead of in lock-step; set by the launcher (GENTUN_CONV_STAGGER), 0 = off
-  int stagger, stagger_lo, stagger_hi;
+  // real extent of a zero-padded ("virtual") image (0: not padded). A layer whose real H x W is stored
+  // in a larger tensor (MNIST's 28 x 28 in 32 x 32, right / bottom padding, so every layer runs the 32 /
+  // 16 / 8-wide shape-specialised kernels) writes exact zeros outside the real rows / columns from its
+  // FORWARD epilogue; every other kernel then sees zeros there (the data gradient's ReLU / pool masks
+  // zero the gradient, the dense W1 rows of padded pixels stay 0), so results equal the unpadded network
+  int Hr, Wr;
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

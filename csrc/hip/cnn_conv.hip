@@ -262,12 +262,14 @@ conv_fwd_kernel(ConvArgs a) {
       const int co0 = co_blk + t * 16 + kq * 4;
       if (co0 >= a.Coutp) continue;
       float v[4];
+      // zero-padded image (ConvArgs::Hr / Wr): exact zeros outside the real rows / columns
+      const bool pad0 = a.Hr > 0 && (h0 + pyy[h] >= a.Hr || pxx[h] >= a.Wr);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float x = acc[h][t][i];
         if (a.bias) x += a.bias[(long)g * a.Coutp + co0 + i];
         if (a.relu) x = fmaxf(x, 0.f);
-        v[i] = x;
+        v[i] = pad0 ? 0.f : x;
       }
       for (int k = 0; k < GT_MAXSLOT; ++k) {
         if (!((gr.out_mask >> k) & 1)) continue;

@@ -31,59 +31,26 @@
 
 #include "cnn_args.h"
 
-// 1: staging loads without per-chunk branches (halo / padding chunks read a
-// zero chunk; the loads of a batch all issue before the first wait). Measured
-// same-box 2-3 % SLOWER per population step than the per-chunk branches, so
-// 0 is the default (profiles/conv_stage_select_ab_r3.txt)
-#ifndef GT_STAGE_SELECT
-#define GT_STAGE_SELECT 0
-#endif
+// Rejected variants are recorded in profiles/ and were removed from the source (round 5): branch-free
+// staging selects (conv_stage_select_ab_r3.txt), register-computed / register-held patch offsets and deeper
+// weight prefetch (conv_f32_regoff_pf_ab_r4.txt, conv_f32_kreg_ab_r4.txt), the unpipelined fp32 loop, the
+// round-3 two-team "duo" and persistent kernels and the round-5 fixed-role "pipe" kernel
+// (conv_f32_duo_ab_r3.txt, conv_f32_persistent_ab_r2.txt, r5/conv_f32_sched_pipe_ab_r5.txt).
 
-// 1: multi-input (N-ary Add) patch staging loads two inputs per round trip (see conv_fast_kernel)
-#ifndef GT_STAGE_PAIRS
-#define GT_STAGE_PAIRS 1
-#endif
+// a value the compiler cannot see through (nor hoist computations on it out of a loop)
+__device__ __forceinline__ int opaque_i(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 
-#ifndef GT_F32_NO_BPIPE
-#define GT_F32_NO_BPIPE 0      // 1: fp32 conv main loop without the patch-fragment pipeline (A/B builds)
-#endif
-
-// 1: the unrolled tile-kernel k loop takes each k-step's patch offset from per-lane arithmetic
-// (no LDS table lookup + lgkmcnt(0) drain in the middle of the MFMA stream); 0: the LDS coff table.
-// Measured 4-7 % SLOWER on the stage-2 3x3 fwd / dgrad (profiles/conv_f32_regoff_pf_ab_r4.txt), as was a
-// 3- or 4-deep weight prefetch (GT_F32_PFM): both stay A/B builds
-#ifndef GT_F32_REGOFF
-#define GT_F32_REGOFF 0
-#endif
-// weight (A operand) prefetch depth of the fp32 tile kernel, in k-steps (3 planes each)
-#ifndef GT_F32_PFM
-#define GT_F32_PFM 2
-#endif
-// 1: the stage-2 3x3 fp32 shape (7 input chunks, 16 wide) reduces its chunks PART-MAJOR -- (kh, kw, cb)
+// The stage-2 3x3 fp32 shape (7 input chunks, 16 wide) reduces its chunks PART-MAJOR -- (kh, kw, cb)
 // for cb 0-3, then for cb 4-6 -- in every kernel that runs it (so the small-launch tiles stay
 // bit-identical to the 8-row one): +2.6 % per population step over the kk-major order
-// (profiles/conv_s2_parts_split_ab_r4.txt). A two-part staging kernel built on it (part-1 loads in
-// flight during the part-0 k-steps) and a bank-paired order were measured slower and removed
-// (same file; profiles/conv_s2_bank_order_ab_r4.txt).
-#ifndef GT_S2_PARTS
-#define GT_S2_PARTS 1
-#endif
-// 1: the fp32 tile kernel keeps every k-step's patch offset in registers (read once from the LDS table);
-// measured neutral at 25 groups (profiles/conv_f32_kreg_ab_r4.txt): off
-#ifndef GT_F32_KREG
-#define GT_F32_KREG 0
-#endif
-// 1: the double-buffered fp32 wgrad's two wave halves stage and multiply in opposite orders (see the kernel)
-#ifndef GT_WGRAD_HALVES
-#define GT_WGRAD_HALVES 1
-#endif
-
-// the part-major reduction order of the stage-2 3x3 fp32 shape (GT_S2_PARTS)
+// (profiles/conv_s2_parts_split_ab_r4.txt; a two-part staging kernel built on it and a bank-paired order
+// were slower, same file and conv_s2_bank_order_ab_r4.txt).
 template <int KH, int KW, int NCBI, int W, int PREC>
 struct S2Parts {
-  // 3x3 nodes / output convs and their dgrad; GT_S2_PARTS >= 2 also the 5x5 input-conv dgrad (50 -> 20)
-  static constexpr bool on = GT_S2_PARTS && PREC == 1 && NCBI == 7 && W == 16 &&
-                             ((KH == 3 && KW == 3) || (GT_S2_PARTS >= 2 && KH == 5 && KW == 5));
+  static constexpr bool on = PREC == 1 && NCBI == 7 && W == 16 && KH == 3 && KW == 3;
   static constexpr int e0 = KH * KW * 4;     // chunk-list entries of part 0 (every tap x chunks 0-3)
 };
 
@@ -186,15 +153,20 @@ __device__ __forceinline__ void unpool_chunk(const ConvArgs& a, int g, long n, i
 // one accumulator) give every row a_p (b0 + b1 + b2), and the epilogue sums
 // the plane rows of a channel -- all nine split terms in 3 MFMAs instead of
 // six terms in 6.
-// forward declaration: the register-direct fp32 epilogue (defined with the duo kernel below)
+// forward declaration: the register-direct fp32 epilogue (defined below)
 template <int CT, int PG, int PK, int W, int NCO, bool POOLABLE>
 __device__ __forceinline__ void f32_epi_regs(const ConvArgs& a, const GroupRec& gr, int b, int h0,
                                              const f32x4_t (&acc)[CT][PG], int wco, int pgw, int lane);
 
 // RE (fp32 only): 1 = register-direct epilogue (f32_epi_regs), 0 = through the LDS output tile
 // CTX > 0 forces the co tiles per wave (1: waves split the co tiles, more pixel groups each)
+// SCH (fp32): 1 = the unrolled k loop as an ENFORCED software pipeline (sched_barrier between the patch
+// reads of k-step s+1, the MFMAs of k-step s and the weight loads of k-step s+2, a 3-slot weight ring).
+// hipcc's own schedule sinks every prefetch next to its first use; that is hidden where two MFMA waves
+// share a SIMD (neutral on the 2-tile shapes, slower on stage 1) but not on the one-co-tile-per-wave
+// s2 input-conv data gradient (-13 %): r5/conv_f32_sched_pipe_ab_r5.txt
 template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV = 4, int PREC = 0, int PK = 0, int RE = 0,
-          int CTX = 0>
+          int CTX = 0, int SCH = 0>
 __global__ void __launch_bounds__(NWV * 64)
 __attribute__((amdgpu_waves_per_eu(PREC ? 2 : (NWV == 8 ? 4 : (NT >= 4 ? (NCBI >= 7 ? 2 : 3) : 4)))))
 conv_fast_kernel(ConvArgs a) {
@@ -214,7 +186,7 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int NCH = KH * KW * NCBI;               // reduction chunks
   constexpr int NKS = (NCH + 3) / 4;                // k-steps (32 k each)
   // reduction order: entry e of the chunk list -> (kk = kh * KW + kw, cb); part-major for the
-  // stage-2 3x3 fp32 shape (GT_S2_PARTS), else kk-major
+  // stage-2 3x3 fp32 shape (S2Parts), else kk-major
   constexpr bool PARTS = S2Parts<KH, KW, NCBI, W, PREC>::on;
   auto ent = [&](int e, int& kk, int& cb) {
     if constexpr (PARTS) {
@@ -232,8 +204,12 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int WC = NT / CT;                       // waves along co
   constexpr int WP = NWV / WC;                        // waves along pixels
   constexpr int PG = NPG / WP;                      // pixel groups per wave
-  constexpr int PFM = PREC ? (NKS > 64 ? 2 : GT_F32_PFM) : 4;   // weight prefetch depth (k-steps; 3 planes each in prec 1)
+  constexpr int PFM = PREC ? 2 : 4;                 // weight prefetch depth (k-steps; 3 planes each in prec 1)
   constexpr int PF = NKS < PFM ? NKS : PFM;
+  // fp32 enforced pipeline (SCH): the weights of k-step s+PF load into the ring slot k-step s-1 used, so
+  // no load waits for an MFMA still reading its registers
+  constexpr bool SCHED = SCH && PREC != 0 && NKS <= 64;
+  constexpr int RA = SCHED ? PF + 1 : PF;
   static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == NWV, "tile shape");
   static_assert(!PK || (PREC == 1 && WC == 1), "packed last tile: fp32, every wave owns all co tiles");
   static_assert(W % 16 == 0 || 16 % W == 0, "pixel groups must tile image rows");
@@ -250,9 +226,6 @@ conv_fast_kernel(ConvArgs a) {
   const int nbx = gridDim.x;
   const int total = nbx * gridDim.y;
   int lin = blockIdx.y * nbx + blockIdx.x;
-  if (PREC && a.stagger > 0 &&
-      (a.stagger_lo >= 0 ? (lin >= a.stagger_lo && lin < a.stagger_hi) : (((lin >> 3) & 1) == 1 && lin < a.stagger_hi)))
-    for (int i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(32);     // 32 x 64 = 2048 cycles each
   if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
   const int by = lin / nbx, bx = lin - by * nbx;
   const int nband = (a.H + TH - 1) / TH;
@@ -279,7 +252,7 @@ conv_fast_kernel(ConvArgs a) {
     wok[t] = co < NCO * 8;
     wrow[t] = a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8);
   }
-  uint4 areg[PF][CT][NPL];
+  uint4 areg[RA][CT][NPL];
   auto load_a = [&](int s, uint4 (*dst)[NPL]) {
     // (dbg bit 8, diagnostics only: every k-step re-reads k-step 0's weights -- L1-resident operands)
     const int e = ((a.dbg & 8) ? 0 : s * 4) + kq;
@@ -348,19 +321,11 @@ conv_fast_kernel(ConvArgs a) {
       for (int j = 0; j < JB; ++j)
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc8[j][e] = 0.f;
-      // every chunk load is unconditional (halo / padding chunks read the zero
-      // chunk): a load under a per-chunk branch made hipcc wait for it at the
-      // branch, serialising the staging into one global round trip per chunk
-      const AT* zc = reinterpret_cast<const AT*>(gt_zero8);
       if (n_src == 1) {
 #pragma unroll
         for (int j = 0; j < JB; ++j)
-#if GT_STAGE_SELECT
-          if (j0 + j < NPT) ld_chunk(pok[j0 + j] ? src0 + poff[j0 + j] : zc, acc8[j]);
-#else
           if (j0 + j < NPT && pok[j0 + j]) ld_chunk(src0 + poff[j0 + j], acc8[j]);
-#endif
-      } else if (GT_STAGE_PAIRS) {
+      } else {
         // DAG inputs two at a time: both inputs' chunk loads are in flight before either is
         // summed (one input at a time waited a global round trip per input). Still summed in
         // increasing slot order: bit-identical.
@@ -393,27 +358,6 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) acc8[j][e] += t1[j][e];
           }
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < GT_MAXSLOT; ++k) {
-          if (!((gr.in_mask >> k) & 1)) continue;
-          const AT* sk = static_cast<const AT*>(a.in[k]) + gimg;
-          float t8[JB][8];
-#pragma unroll
-          for (int j = 0; j < JB; ++j) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) t8[j][e] = 0.f;
-#if GT_STAGE_SELECT
-            if (j0 + j < NPT) ld_chunk(pok[j0 + j] ? sk + poff[j0 + j] : zc, t8[j]);
-#else
-            if (j0 + j < NPT && pok[j0 + j]) ld_chunk(sk + poff[j0 + j], t8[j]);
-#endif
-          }
-#pragma unroll
-          for (int j = 0; j < JB; ++j)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc8[j][e] += t8[j][e];
         }
       }
 #pragma unroll
@@ -492,17 +436,10 @@ conv_fast_kernel(ConvArgs a) {
     ent(c, kk, cb);
     return c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBP + cb : 0;
   };
-  // fp32, unrolled k loop: every k-step's patch offset read from the LDS table ONCE, up front, into
-  // registers (NKS VGPRs) -- no table lookup + lgkmcnt drain in front of each k-step's B reads
-  constexpr bool KREG = GT_F32_KREG && PREC != 0 && NKS <= 64 && !GT_F32_REGOFF;
-  int kreg[KREG ? NKS : 1];
-  if constexpr (KREG) {
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) kreg[s] = lbase + gbase + coff[s * 4 + kq];
-  }
+  // the patch fragments of k-step s: the offset from the LDS table, or (pipelined loop) computed in
+  // registers so no table read drains lgkmcnt in the middle of the MFMA stream
   auto load_b = [&](int s, uint4 (*dst)[NPL]) {
-    const uint4* pb = KREG ? patch + kreg[KREG ? s : 0]
-                           : patch + lbase + gbase + ((GT_F32_REGOFF && PREC && NKS <= 64) ? koff(s) : coff[s * 4 + kq]);
+    const uint4* pb = patch + lbase + gbase + (SCHED ? koff(s) : coff[s * 4 + kq]);
 #pragma unroll
     for (int h = 0; h < PG; ++h) {
       const int p = h * 16;                        // relative to the wave's first group
@@ -511,7 +448,7 @@ conv_fast_kernel(ConvArgs a) {
     }
   };
   if (!(a.dbg & 1)) {
-    if constexpr (PREC != 0 && !GT_F32_NO_BPIPE && NKS > 64) {
+    if constexpr (PREC != 0 && NKS > 64) {
       // long reductions (wide layers: 72-100 k-steps): a runtime loop over k-step PAIRS, so the
       // register sets stay compile-time indexed (a fully unrolled loop this long is not unrolled
       // by hipcc and its dynamically indexed operand arrays went to scratch); the prefetches are
@@ -532,7 +469,30 @@ conv_fast_kernel(ConvArgs a) {
         kstep(s, std::integral_constant<int, 0>());
         if (s + 1 < NKS) kstep(s + 1, std::integral_constant<int, 1>());
       }
-    } else if constexpr (PREC != 0 && !GT_F32_NO_BPIPE) {
+    } else if constexpr (SCHED) {
+      // fp32, unrolled k loop as an explicit software pipeline. Left alone, hipcc sinks every prefetch
+      // next to its first use (round-4 ISA: a k-step's weight loads were waited on 2-4 MFMAs after they
+      // issued, its patch reads right before the MFMAs), so both waves of a SIMD stall on L2 / LDS
+      // latency in the middle of the MFMA stream. Per k-step s, fenced by sched_barrier:
+      //   1. LDS reads of k-step s+1's patch fragments (double buffer; offsets held in registers)
+      //   2. the 6 x CT x PG MFMAs of k-step s
+      //   3. global loads of k-step s+PF's weights into the ring slot k-step s-1 used
+      // The MFMA order (and so every accumulator's summation order) is the unpipelined loop's.
+      uint4 bfr[2][PG][NPL];
+      load_b(0, bfr[0]);
+#pragma unroll
+      for (int s = 0; s < NKS; ++s) {
+        if (s + 1 < NKS) load_b(s + 1, bfr[(s + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int h = 0; h < PG; ++h) acc[t][h] = mma(t, areg[s % RA][t], bfr[s & 1][h], acc[t][h]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + PF < NKS) load_a(s + PF, areg[(s + PF) % RA]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (PREC != 0) {
       // fp32: the next k-step's patch fragments are read while this step's 6 x CT x PG
       // MFMAs run (the unpipelined loop waited for its LDS reads before every k-step)
       uint4 bfr[2][PG][NPL];
@@ -547,6 +507,7 @@ conv_fast_kernel(ConvArgs a) {
         if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
       }
     } else {
+      // bf16
 #pragma unroll
       for (int s = 0; s < NKS; ++s) {
         uint4 bfr[PG][NPL];
@@ -581,11 +542,13 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
       for (int h = 0; h < PG; ++h) {
         const int p = (pgw + h) * 16 + l16;
+        const bool pad0 = a.Hr > 0 && (h0 + p / W >= a.Hr || p % W >= a.Wr);   // zero-padded image
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           v[i] = acc[t][h][i] + bias_v[t][i];
           if (a.relu) v[i] = fmaxf(v[i], 0.f);
+          if (pad0) v[i] = 0.f;
         }
         *reinterpret_cast<uint2*>(ot + p * OROWB + co0) = pack4(v);
       }
@@ -621,10 +584,12 @@ conv_fast_kernel(ConvArgs a) {
 #pragma unroll
     for (int h = 0; h < PG; ++h) {
       const int p = (pgw + h) * 16 + l16;
+      const bool pad0 = a.Hr > 0 && (h0 + p / W >= a.Hr || p % W >= a.Wr);   // zero-padded image
       if (PK && t == CT - 1) {
         // channel (wco + t) * 16 + kq = sum of its three plane rows; the tile's other columns are 0
         float s0 = acc[t][h][0] + acc[t][h][1] + acc[t][h][2] + bias_v[t][0];
         if (a.relu) s0 = fmaxf(s0, 0.f);
+        if (pad0) s0 = 0.f;
         float* orow = otile + p * OROW + (wco + t) * 16;
         orow[kq] = s0;
         orow[4 + kq] = 0.f;
@@ -638,6 +603,7 @@ conv_fast_kernel(ConvArgs a) {
       v.z = acc[t][h][2] + bias_v[t][2];
       v.w = acc[t][h][3] + bias_v[t][3];
       if (a.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+      if (pad0) v = make_float4(0.f, 0.f, 0.f, 0.f);
       *reinterpret_cast<float4*>(otile + p * OROW + co0) = v;
     }
   }
@@ -684,273 +650,7 @@ conv_fast_kernel(ConvArgs a) {
           a, [&](int p, int cb, float* f) { load8f(otile + p * OROW + cb * 8, f); }, g, b, h0, tid);
 }
 
-// ---------------------------------------------------------------------------
-// fp32 (prec 1), persistent and software-pipelined. The tile kernel above
-// runs stage -> MFMA -> epilogue back to back, and with 2 workgroups per CU
-// (60 KB of 3-plane patch, ~180 VGPRs) its memory phases barely overlap the
-// matrix work (tools/bench_conv.py: time ~= skip-MFMA time + MFMA time).
-// Here a workgroup loops over tiles (tile = blockIdx.x + i * gridDim.x) and
-// issues the global loads of its NEXT tile's patch into registers before the
-// current tile's MFMA loop, splitting and writing them to LDS after it (the
-// async-STAGE split); the epilogue stores straight from the accumulators
-// (16 contiguous bytes = 4 fp32 channels per lane) instead of through an LDS
-// tile, so a tile costs one LDS refill and two barriers. Only the first input
-// slot is prefetched; further DAG inputs are added after the MFMA loop.
-// ---------------------------------------------------------------------------
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int NWV>
-__global__ void __launch_bounds__(NWV * 64) __attribute__((amdgpu_waves_per_eu(2)))
-conv_f32p_kernel(ConvArgs a, int ntiles) {
-  constexpr int NPL = GT_NPL_F32;
-  constexpr int NTH = NWV * 64;
-  constexpr int PH = TH + KH - 1, PW = W + KW - 1;
-  constexpr int NP = PH * PW * NCBI;
-  constexpr int NPT = (NP + NTH - 1) / NTH;
-  constexpr int NCH = KH * KW * NCBI;
-  constexpr int NKS = (NCH + 3) / 4;
-  constexpr int TP = TH * W;
-  constexpr int NPG = TP / 16;
-  constexpr int CT = (NT >= 2 && NT % 2 == 0) ? 2 : 1;
-  constexpr int WC = NT / CT;
-  constexpr int WP = NWV / WC;
-  constexpr int PG = NPG / WP;
-  constexpr int PF = NKS < 2 ? NKS : 2;
-  static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == NWV, "tile shape");
-  static_assert(W % 16 == 0, "pixel groups must tile image rows");
-  extern __shared__ __attribute__((aligned(16))) uint4 smem[];
-  uint4* patch = smem;                               // [NPL][NP]
-  __shared__ int coff[NKS * 4];
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
-  const int nband = a.H / TH;
-  const int tiles_per_group = a.B * nband;
-  const long img = (long)a.H * W * NCBI * 8;
-  const long oimg = (long)a.H * W * NCO * 8;
-  for (int c = tid; c < NKS * 4; c += NTH) {
-    const int kk = c / NCBI, cb = c % NCBI;
-    coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
-  }
-  // per-thread patch chunk geometry (tile independent)
-  int pdh[NPT], pdw[NPT], pcb[NPT];
-#pragma unroll
-  for (int j = 0; j < NPT; ++j) {
-    const int i = tid + NTH * j;
-    const int pix = i / NCBI;
-    pcb[j] = i % NCBI;
-    pdh[j] = pix / PW - KH / 2;
-    pdw[j] = pix % PW - KW / 2;
-  }
-  struct Tile { GroupRec gr; int b, h0; };
-  auto tile_of = [&](int t) {
-    Tile x;
-    const int q = t / tiles_per_group, r = t - q * tiles_per_group;
-    x.gr = group_rec(a.gtab, q, a.n_in, a.n_out, a.acc_flags, a.out_mask);
-    x.b = r / nband;
-    x.h0 = (r - x.b * nband) * TH;
-    return x;
-  };
-  float xr[NPT][8];
-  // loads of the first input slot (or the gathered dataset image) of tile x
-  auto load_first = [&](const Tile& x) {
-    const float* src = a.gather
-        ? static_cast<const float*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + x.gr.g) * a.B + x.b] * img
-        : static_cast<const float*>(a.in[__builtin_ctz(x.gr.in_mask | 0x100) & 7]) + ((long)x.gr.g * a.B + x.b) * img;
-#pragma unroll
-    for (int j = 0; j < NPT; ++j) {
-      const int hh = x.h0 + pdh[j], ww = pdw[j];
-      const bool ok = tid + NTH * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
-      if (ok) load8f(src + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, xr[j]);
-    }
-  };
-  // remaining DAG input slots of tile x, added into xr; the split planes to
-  // LDS; the exact fp32 sum of N-ary tiles to xsum (interior chunks)
-  auto finish_stage = [&](const Tile& x) {
-    const int first = __builtin_ctz(x.gr.in_mask | 0x100) & 7;
-    const bool multi = !a.gather && __builtin_popcount(x.gr.in_mask) > 1;
-    if (multi) {
-      const long gimg = ((long)x.gr.g * a.B + x.b) * img;
-      for (int k = first + 1; k < GT_MAXSLOT; ++k) {
-        if (!((x.gr.in_mask >> k) & 1)) continue;
-        const float* sk = static_cast<const float*>(a.in[k]) + gimg;
-#pragma unroll
-        for (int j = 0; j < NPT; ++j) {
-          const int hh = x.h0 + pdh[j], ww = pdw[j];
-          if (tid + NTH * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W) {
-            float t8[8];
-            load8f(sk + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, t8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) xr[j][e] += t8[e];
-          }
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NPT; ++j) {
-      const int i = tid + NTH * j;
-      if (i >= NP) continue;
-      split8(xr[j], patch[i], patch[NP + i], patch[2 * NP + i]);
-      if (multi && a.xsum) {
-        const int hh = x.h0 + pdh[j], ww = pdw[j];
-        if (pdh[j] >= 0 && pdh[j] < TH && hh < a.H && ww >= 0 && ww < W)     // band interior
-          store8f(static_cast<float*>(a.xsum) + ((long)x.gr.g * a.B + x.b) * img + ((long)hh * W + ww) * (NCBI * 8) +
-                      pcb[j] * 8, xr[j]);
-      }
-    }
-  };
-
-  const int wco = (wave % WC) * CT;
-  const int pgw = (wave / WC) * PG;
-  const int lbase = (l16 / W) * PW * NCBI + (l16 % W) * NCBI;
-  const int gbase = (((pgw * 16) / W) * PW + (pgw * 16) % W) * NCBI;
-
-  int t = blockIdx.x;
-  if (t >= ntiles) return;
-  Tile cur = tile_of(t);
-  load_first(cur);
-  finish_stage(cur);
-  __syncthreads();
-  while (true) {
-    const int tn = t + gridDim.x;
-    const bool more = tn < ntiles;
-    Tile nxt;
-    if (more) {
-      nxt = tile_of(tn);
-      load_first(nxt);                                 // in flight during this tile's MFMAs
-    }
-    // ---- weights of this tile's group
-    const int g = cur.gr.g;
-    const uint16_t* wrow[CT];
-    bool wok[CT];
-#pragma unroll
-    for (int tt = 0; tt < CT; ++tt) {
-      const int co = (wco + tt) * 16 + l16;
-      wok[tt] = co < NCO * 8;
-      wrow[tt] = a.w + ((long)g * (NCO * 8) + (wok[tt] ? co : 0)) * (NCH * 8);
-    }
-    uint4 areg[PF][CT][NPL];
-    auto load_a = [&](int s, uint4 (*dst)[NPL]) {
-      const int c = s * 4 + kq;
-#pragma unroll
-      for (int tt = 0; tt < CT; ++tt)
-#pragma unroll
-        for (int p = 0; p < NPL; ++p)
-          dst[tt][p] = (wok[tt] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[tt] + p * a.wps + c * 8)
-                                             : make_uint4(0, 0, 0, 0);
-    };
-#pragma unroll
-    for (int s = 0; s < PF; ++s) load_a(s, areg[s]);
-    f32x4_t acc[CT][PG];
-#pragma unroll
-    for (int tt = 0; tt < CT; ++tt)
-#pragma unroll
-      for (int h = 0; h < PG; ++h) acc[tt][h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      const uint4* pb = patch + lbase + gbase + coff[s * 4 + kq];
-      uint4 bfr[PG][NPL];
-#pragma unroll
-      for (int h = 0; h < PG; ++h) {
-        const int p = h * 16;
-#pragma unroll
-        for (int q = 0; q < NPL; ++q) bfr[h][q] = pb[q * NP + ((p / W) * PW + (p % W)) * NCBI];
-      }
-#pragma unroll
-      for (int tt = 0; tt < CT; ++tt)
-#pragma unroll
-        for (int h = 0; h < PG; ++h) acc[tt][h] = mfma_np<NPL>(areg[s % PF][tt], bfr[h], acc[tt][h]);
-      if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
-    }
-    // ---- epilogue straight from the accumulators: lane = 4 channels of one pixel
-    const long obase = ((long)g * a.B + cur.b) * oimg + (long)cur.h0 * W * (NCO * 8);
-#pragma unroll
-    for (int tt = 0; tt < CT; ++tt) {
-      const int co0 = (wco + tt) * 16 + kq * 4;
-      if (co0 >= NCO * 8) continue;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (a.bias) {
-        const float4 q = *reinterpret_cast<const float4*>(a.bias + (long)g * (NCO * 8) + co0);
-        bv[0] = q.x; bv[1] = q.y; bv[2] = q.z; bv[3] = q.w;
-      }
-#pragma unroll
-      for (int h = 0; h < PG; ++h) {
-        const int p = (pgw + h) * 16 + l16;
-        const long off = obase + (long)p * (NCO * 8) + co0;
-        float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          v[i] = acc[tt][h][i] + bv[i];
-          if (a.relu) v[i] = fmaxf(v[i], 0.f);
-        }
-        for (int k = 0; k < GT_MAXSLOT; ++k) {
-          if (!((cur.gr.out_mask >> k) & 1)) continue;
-          float* dst = static_cast<float*>(a.out[k]) + off;
-          float4 o = make_float4(v[0], v[1], v[2], v[3]);
-          if ((cur.gr.out_mask >> (8 + k)) & 1) {
-            const float4 q = *reinterpret_cast<const float4*>(dst);
-            o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
-          }
-          if ((cur.gr.out_mask >> (16 + k)) & 1) {
-            const float4 m = *reinterpret_cast<const float4*>(static_cast<const float*>(a.out_mask[k]) + off);
-            o.x = m.x > 0.f ? o.x : 0.f; o.y = m.y > 0.f ? o.y : 0.f;
-            o.z = m.z > 0.f ? o.z : 0.f; o.w = m.w > 0.f ? o.w : 0.f;
-          }
-          *reinterpret_cast<float4*>(dst) = o;
-        }
-      }
-    }
-    if (!more) break;
-    __syncthreads();                                   // every wave is done with this tile's patch
-    finish_stage(nxt);
-    __syncthreads();
-    cur = nxt;
-    t = tn;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// fp32 (prec 1), "duo": one persistent workgroup of 8 waves per CU = two
-// TEAMS of 4 waves, each the 4-wave geometry of conv_fast_kernel with its own
-// 3-plane patch buffer in LDS (2 x 60 KB for the 16-wide 3x3 stage), walking
-// the workgroup's tiles alternately (team 0: tiles 0, 2, 4, ...; team 1:
-// 1, 3, 5, ...) in lock-step PHASES separated by one s_barrier:
-//
-//   phase k:  team (k & 1) runs the MFMA loop of tile k from its buffer,
-//             the other team stores tile k-1 (straight from its accumulators)
-//             and stages tile k+1 (global loads -> exact 3-way split -> LDS)
-//             into the buffer it just finished reading.
-//
-// Every SIMD holds one wave of each team, so the matrix pipe runs one team's
-// k loop while the other team's loads, splits, LDS writes and stores use the
-// vector / memory pipes: the tile kernel ran those phases back to back (its
-// time ~= MFMA time + memory time, profiles/conv_f32_phases_r2.txt); here a
-// tile costs ~max of the two. No team-internal synchronisation is needed:
-// the epilogue is register-direct (16-byte stores of 4 channels per lane; the
-// fused 2x2 max-pool and its argmax mask from lane shuffles and the paired
-// pixel-group register -- a wave's pixel groups cover whole row pairs), and a
-// buffer is only written by the team that reads it, one barrier apart.
-// Results are bit-identical to conv_fast_kernel (same k order, same MFMA
-// sequence, same epilogue arithmetic): tests/test_hip_duo.py.
-// ---------------------------------------------------------------------------
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int PK>
-struct DuoCfg {
-  static constexpr int NPL = GT_NPL_F32;
-  static constexpr int PH = TH + KH - 1, PW = W + KW - 1;
-  static constexpr int NP = PH * PW * NCBI;          // patch chunks per plane
-  static constexpr int NCH = KH * KW * NCBI;
-  static constexpr int NKS = (NCH + 3) / 4;
-  static constexpr int BUF = NPL * NP;               // chunks per team buffer
-  static constexpr size_t LDS = (size_t)2 * BUF * 16 + (size_t)NKS * 4 * 4;
-  // the register-direct epilogue fuses the 2x2 pool when a wave's pixel groups cover whole row pairs
-  static constexpr bool poolable() {
-    constexpr int CT = PK ? NT : ((NT >= 2 && NT % 2 == 0) ? 2 : 1);
-    constexpr int PG = (TH * W / 16) / (4 / (NT / CT));
-    return TH % 2 == 0 && PG % (2 * (W / 16)) == 0;
-  }
-};
-
-// Register-direct fp32 epilogue of one output tile (shared by the duo and the
-// tile kernel): lane = 4 channels of pixel (pgw + h) * 16 + l16; bias / ReLU;
+// Register-direct fp32 epilogue of one output tile of the tile kernel: lane = 4 channels of pixel (pgw + h) * 16 + l16; bias / ReLU;
 // plain store, or the data gradient's DAG fan-out (accumulate, ReLU mask, up to
 // 8 slots) with every global load of a slot's read-modify-write issued before
 // its first use; the fused un-pool; the fused 2x2 max-pool + argmax mask from
@@ -1004,6 +704,19 @@ __device__ __forceinline__ void f32_epi_regs(const ConvArgs& a, const GroupRec& 
           if (a.relu) v = fmaxf(v, 0.f);
           val[t][h][i] = v;
         }
+      }
+    }
+  }
+  if (a.Hr > 0 && !unpool) {
+    // zero-padded image (ConvArgs::Hr / Wr): exact zeros outside the real rows / columns
+#pragma unroll
+    for (int h = 0; h < PG; ++h) {
+      const int p = (pgw + h) * 16 + l16;
+      if (h0 + p / W >= a.Hr || p % W >= a.Wr) {
+#pragma unroll
+        for (int t = 0; t < CT; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) val[t][h][i] = 0.f;
       }
     }
   }
@@ -1124,290 +837,6 @@ __device__ __forceinline__ void f32_epi_regs(const ConvArgs& a, const GroupRec& 
   }
 }
 
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int PK>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-conv_duo_f32_kernel(ConvArgs a, int ntiles) {
-  using DC = DuoCfg<KH, KW, NCBI, W, TH, NT, NCO, PK>;
-  constexpr int NPL = DC::NPL, PW = DC::PW, NP = DC::NP, NCH = DC::NCH, NKS = DC::NKS, BUF = DC::BUF;
-  constexpr int TNT = 256;                                 // threads per team
-  constexpr int NPT = (NP + TNT - 1) / TNT;                // patch chunks per thread
-  constexpr int TP = TH * W;
-  constexpr int NPG = TP / 16;
-  constexpr int CT = PK ? NT : ((NT >= 2 && NT % 2 == 0) ? 2 : 1);
-  constexpr int WC = NT / CT;
-  constexpr int WP = 4 / WC;
-  constexpr int PG = NPG / WP;
-  constexpr int PF = NKS < 2 ? NKS : 2;
-  constexpr int COP = NCO * 8;                             // padded output channels (tensor row)
-  static_assert(NPG % WP == 0 && NT % CT == 0 && WC * WP == 4, "tile shape");
-  static_assert(!PK || WC == 1, "packed last tile: every wave owns all co tiles");
-  static_assert(W % 16 == 0, "pixel groups of one image row");
-  // pool pairing: rows r, r+1 of a wave's pixel groups are groups h, h + W/16
-  constexpr int RG = W / 16;                               // pixel groups per image row
-  constexpr bool POOLABLE = DC::poolable();
-  static_assert(POOLABLE == ((PG % (2 * RG)) == 0 && TH % 2 == 0), "pool pairing");
-
-  extern __shared__ __attribute__((aligned(16))) uint4 smem[];   // [2][BUF] patch buffers, then coff
-  int* coff = reinterpret_cast<int*>(smem + 2 * BUF);
-
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
-  const int team = wave >> 2, twave = wave & 3, ttid = tid & (TNT - 1);
-  uint4* patch = smem + team * BUF;
-
-  for (int c = tid; c < NKS * 4; c += 512) {
-    const int kk = c / NCBI, cb = c % NCBI;
-    coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBI + cb : 0;
-  }
-  // XCD-aware: the hardware deals consecutive workgroups to consecutive XCDs;
-  // virtual id v gives every XCD a contiguous range of tiles (a few groups'
-  // weights per L2), and each workgroup a contiguous run of tiles
-  const int nwg = gridDim.x;
-  int v = blockIdx.x;
-  if ((nwg & 7) == 0) v = (v & 7) * (nwg >> 3) + (v >> 3);
-  const int t_begin = (int)(((long)v * ntiles) / nwg), t_end = (int)(((long)(v + 1) * ntiles) / nwg);
-  const int nloc = t_end - t_begin;
-
-  const int nband = a.H / TH;
-  const int tpg = a.B * nband;                             // tiles per launch group
-  const long img = (long)a.H * W * NCBI * 8;
-  const long oimg = (long)a.H * W * COP;
-  struct Tile { GroupRec gr; int b, h0; };
-  auto tile_of = [&](int t) {
-    Tile x;
-    const int q = t / tpg, r = t - q * tpg;
-    x.gr = group_rec(a.gtab, q, a.n_in, a.n_out, a.acc_flags, a.out_mask);
-    x.b = r / nband;
-    x.h0 = (r - x.b * nband) * TH;
-    return x;
-  };
-
-  // ---- staging (memory phase of a team) ------------------------------------
-  int pdh[NPT], pdw[NPT], pcb[NPT];
-#pragma unroll
-  for (int j = 0; j < NPT; ++j) {
-    const int i = ttid + TNT * j;
-    const int pix = i / NCBI;
-    pcb[j] = i % NCBI;
-    pdh[j] = pix / PW - KH / 2;
-    pdw[j] = pix % PW - KW / 2;
-  }
-  float xr[NPT][8];
-  auto stage_issue = [&](const Tile& x) {                 // first input slot / gathered image -> xr
-    if (a.dbg & 4) return;
-    const float* src = a.gather
-        ? static_cast<const float*>(a.in[0]) + a.gather[((long)a.st->cur_step * a.G + x.gr.g) * a.B + x.b] * img
-        : static_cast<const float*>(a.in[__builtin_ctz(x.gr.in_mask | 0x100) & 7]) + ((long)x.gr.g * a.B + x.b) * img;
-#pragma unroll
-    for (int j = 0; j < NPT; ++j) {
-      const int hh = x.h0 + pdh[j], ww = pdw[j];
-      const bool ok = ttid + TNT * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
-      load8f_or0(src + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, ok, xr[j]);
-    }
-  };
-  auto stage_finish = [&](const Tile& x, uint4* buf) {    // other DAG inputs, split, LDS, xsum
-    if (a.dbg & 4) return;
-    const int first = __builtin_ctz(x.gr.in_mask | 0x100) & 7;
-    const bool multi = !a.gather && __builtin_popcount(x.gr.in_mask) > 1;
-    const long gimg = ((long)x.gr.g * a.B + x.b) * img;
-    if (multi) {
-      for (int k = first + 1; k < GT_MAXSLOT; ++k) {
-        if (!((x.gr.in_mask >> k) & 1)) continue;
-        const float* sk = static_cast<const float*>(a.in[k]) + gimg;
-        float t8[NPT][8];
-#pragma unroll
-        for (int j = 0; j < NPT; ++j) {
-          const int hh = x.h0 + pdh[j], ww = pdw[j];
-          const bool ok = ttid + TNT * j < NP && hh >= 0 && hh < a.H && ww >= 0 && ww < W;
-          load8f_or0(sk + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, ok, t8[j]);
-        }
-#pragma unroll
-        for (int j = 0; j < NPT; ++j)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xr[j][e] += t8[j][e];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NPT; ++j) {
-      const int i = ttid + TNT * j;
-      if (i >= NP) continue;
-      split8(xr[j], buf[i], buf[NP + i], buf[2 * NP + i]);
-      if (multi && a.xsum) {
-        const int hh = x.h0 + pdh[j], ww = pdw[j];
-        if (pdh[j] >= 0 && pdh[j] < TH && hh < a.H && ww >= 0 && ww < W)      // band interior
-          store8f(static_cast<float*>(a.xsum) + gimg + ((long)hh * W + ww) * (NCBI * 8) + pcb[j] * 8, xr[j]);
-      }
-    }
-  };
-
-  // ---- MFMA phase -----------------------------------------------------------
-  const int wco = (twave % WC) * CT;
-  const int pgw = (twave / WC) * PG;
-  const int lbase = ((l16 / W) * PW + (l16 % W)) * NCBI;
-  const int gbase = (((pgw * 16) / W) * PW + (pgw * 16) % W) * NCBI;
-  f32x4_t acc[CT][PG];
-  auto compute = [&](const Tile& x, const uint4* buf) {
-    const int g = x.gr.g;
-    const uint16_t* wrow[CT];
-    bool wok[CT];
-#pragma unroll
-    for (int t = 0; t < CT; ++t) {
-      if (PK && t == CT - 1) {
-        const int co = (wco + t) * 16 + (l16 >> 2), pl = l16 & 3;
-        wok[t] = pl < 3 && co < a.cout_real;
-        wrow[t] = a.w + ((long)g * COP + (wok[t] ? co : 0)) * (NCH * 8) + (wok[t] ? pl : 0) * a.wps;
-        continue;
-      }
-      const int co = (wco + t) * 16 + l16;
-      wok[t] = co < COP;
-      wrow[t] = a.w + ((long)g * COP + (wok[t] ? co : 0)) * (NCH * 8);
-    }
-    uint4 areg[PF][CT][NPL];
-    auto load_a = [&](int s, uint4 (*dst)[NPL]) {
-      const int c = s * 4 + kq;
-#pragma unroll
-      for (int t = 0; t < CT; ++t)
-#pragma unroll
-        for (int p = 0; p < ((PK && t == CT - 1) ? 1 : NPL); ++p)
-          dst[t][p] = (wok[t] && c < NCH) ? *reinterpret_cast<const uint4*>(wrow[t] + p * a.wps + c * 8)
-                                           : make_uint4(0, 0, 0, 0);
-    };
-    auto mma = [&](int t, const uint4* af, const uint4* bf, f32x4_t c) {
-      if (PK && t == CT - 1) {
-        c = mfma16(af[0], bf[2], c);
-        c = mfma16(af[0], bf[1], c);
-        return mfma16(af[0], bf[0], c);
-      }
-      return mfma_np<NPL>(af, bf, c);
-    };
-    auto load_b = [&](int s, uint4 (*dst)[NPL]) {
-      const uint4* pb = buf + lbase + gbase + coff[s * 4 + kq];
-#pragma unroll
-      for (int h = 0; h < PG; ++h) {
-        const int p = h * 16;
-#pragma unroll
-        for (int q = 0; q < NPL; ++q) dst[h][q] = pb[q * NP + ((p / W) * PW + (p % W)) * NCBI];
-      }
-    };
-#pragma unroll
-    for (int s = 0; s < PF; ++s) load_a(s, areg[s]);
-#pragma unroll
-    for (int t = 0; t < CT; ++t)
-#pragma unroll
-      for (int h = 0; h < PG; ++h) acc[t][h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    if (a.dbg & 1) return;
-    uint4 bfr[2][PG][NPL];
-    load_b(0, bfr[0]);
-#pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      if (s + 1 < NKS) load_b(s + 1, bfr[(s + 1) & 1]);
-#pragma unroll
-      for (int t = 0; t < CT; ++t)
-#pragma unroll
-        for (int h = 0; h < PG; ++h) acc[t][h] = mma(t, areg[s % PF][t], bfr[s & 1][h], acc[t][h]);
-      if (s + PF < NKS) load_a(s + PF, areg[s % PF]);
-    }
-  };
-
-  // ---- epilogue straight from the accumulators -------------------------------
-  // lane: channels co0..co0+3 of pixel p = (pgw + h) * 16 + l16 of the tile
-  auto epilogue = [&](const Tile& x) {
-    f32_epi_regs<CT, PG, PK, W, NCO, POOLABLE>(a, x.gr, x.b, x.h0, acc, wco, pgw, lane);
-  };
-
-  // ---- phase loop ---------------------------------------------------------------
-  // prologue: team 0 stages local tile 0
-  Tile tc, tn, tp;                                         // this wave's compute / next / previous tiles
-  if (nloc > 0 && team == 0) {
-    tc = tile_of(t_begin);
-    stage_issue(tc);
-    stage_finish(tc, patch);
-  }
-  __syncthreads();
-  for (int k = 0; k <= nloc; ++k) {
-    if ((k & 1) == team) {
-      if (k < nloc) {                                      // this team's MFMA phase: tile k
-        compute(tc, patch);
-        tp = tc;
-      }
-    } else {
-      // memory phase: store tile k-1 (this team computed it last phase), stage tile k+1
-      const bool nxt = k + 1 < nloc;
-      if (nxt) {
-        tn = tile_of(t_begin + k + 1);
-        stage_issue(tn);
-      }
-      if (k >= 1) epilogue(tp);
-      if (nxt) {
-        stage_finish(tn, patch);
-        tc = tn;
-      }
-    }
-    if (k < nloc) __syncthreads();
-  }
-}
-
-// duo kernel dispatch: 0 off, 1 auto (>= 2 tiles per workgroup on every CU), 2 force
-static int g_f32_duo = -1;
-static int g_duo_wgs = 256;        // persistent workgroups (one per CU)
-
-extern "C" int gt_conv_set_duo(int mode, int wgs) {
-  if (g_f32_duo < 0) g_f32_duo = 0;
-  const int old = g_f32_duo;
-  g_f32_duo = mode;
-  if (wgs > 0) g_duo_wgs = wgs;
-  return old;
-}
-
-static bool duo_ok(int ntiles) {
-  // off by default: measured slower than the tile kernel (profiles/conv_f32_duo_ab_r3.txt -- the memory
-  // phases do overlap, but one MFMA wave per SIMD runs the k loop at ~80 % of the tile kernel's two)
-  if (g_f32_duo < 0) g_f32_duo = std::getenv("GENTUN_F32_DUO") ? std::atoi(std::getenv("GENTUN_F32_DUO")) : 0;
-  if (g_f32_duo == 0) return false;
-  return g_f32_duo == 2 || ntiles >= 2 * g_duo_wgs;
-}
-
-// -100: not launched (the LDS of two 3-plane patches does not fit, or the
-// launch is too small for two tiles per workgroup); the discarded branch is
-// never instantiated
-template <int KH, int KW, int NCBI, int W, int TH, int NT, int NCO, int PK>
-static int launch_duo(const ConvArgs* a, hipStream_t stream, int probe) {
-  using DC = DuoCfg<KH, KW, NCBI, W, TH, NT, NCO, PK>;
-  if constexpr (DC::LDS <= 163840) {
-    const int ntiles = a->ngroups * a->B * (a->H / TH);
-    if (!duo_ok(ntiles)) return -100;
-    if (probe) return 1000 + (DC::poolable() ? TH : 1);
-    const int wgs = std::min(ntiles, g_duo_wgs);
-    auto* fn = conv_duo_f32_kernel<KH, KW, NCBI, W, TH, NT, NCO, PK>;
-    if (DC::LDS > 65536)
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)DC::LDS);
-    hipLaunchKernelGGL(fn, dim3(wgs), dim3(512), DC::LDS, stream, *a, ntiles);
-    return (int)hipGetLastError();
-  } else {
-    (void)a; (void)stream; (void)probe;
-    return -100;
-  }
-}
-
-#define CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, PK_)                                         \
-  {                                                                                                     \
-    const int rc_ = launch_duo<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, PK_>(a, stream, g_probe);           \
-    if (rc_ != -100) return rc_;                                                                        \
-  }
-
-// persistent pipelined fp32 conv: measured no faster than the tile kernel on
-// the S=(3,5) shapes (profiles/conv_f32_persistent_ab_r2.txt: the k loop, not
-// the staging, sets the time), so off by default; kept as the A/B switch
-static int g_f32_persistent = 0;
-static int g_f32_grid = 0;         // workgroups of the persistent kernel (0: 2 per CU)
-
-extern "C" int gt_conv_set_f32p(int on, int grid) {
-  const int old = g_f32_persistent;
-  g_f32_persistent = on;
-  g_f32_grid = grid;
-  return old;
-}
-
 // ---------------------------------------------------------------------------
 // dispatch: (KH, KW, Cinp, W, Coutp-tiles) -> instantiation; -100 = no match
 // (the caller then uses the generic kernel)
@@ -1453,7 +882,7 @@ static int g_probe = 0;
     if (g_probe) return 1000 + TH_;                                                                     \
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
     const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 1>::lds(a->epi_bf16 != 0);          \
-    auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 0, 1, 1>;                 \
+    auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 0, 1, 1, 1>;              \
     lds_limit(fn, lds);                                                                                 \
     hipLaunchKernelGGL(fn, grid, dim3(NWV_ * 64), lds, stream, *a);                                     \
     return (int)hipGetLastError();                                                                      \
@@ -1520,26 +949,8 @@ static bool pk_ok(const ConvArgs* a, int nt) {
 #define CONV_FAST_CASE_NW(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                      \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 0)
 
-// fp32 tensors (prec 1): 3-plane patch -> bands of 8 rows (LDS), 4 waves;
-// the persistent pipelined kernel unless switched off
-#define CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                       \
-  {                                                                                                     \
-    if (g_probe) return 0;                                                                              \
-    const int ntiles = a->ngroups * a->B * (a->H / TH_);                                                \
-    const int grid = std::min(ntiles, g_f32_grid > 0 ? g_f32_grid : 512);                               \
-    const size_t lds = (size_t)(TH_ + KH_ - 1) * (W_ + KW_ - 1) * NCBI_ * 16 * GT_NPL_F32;              \
-    auto* fn = conv_f32p_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_>;                            \
-    lds_limit(fn, lds);                                                                                 \
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(NWV_ * 64), lds, stream, *a, ntiles);                       \
-    return (int)hipGetLastError();                                                                      \
-  }
-
 #define CONV_FAST_CASE_F32(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                     \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
-    /* (the persistent / duo variants keep the kk-major order: not for part-major shapes) */            \
-    constexpr bool parts_ = S2Parts<KH_, KW_, NCBI_, W_, 1>::on;                                        \
-    if (!parts_ && g_f32_persistent && (W_ % 16) == 0) CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_) \
-    if (!parts_ && NWV_ == 4) CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 0)                   \
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
   }
 // narrow images (W < 16: no persistent variant), and the wide deep-space shapes (tile kernel only)
@@ -1548,30 +959,11 @@ static bool pk_ok(const ConvArgs* a, int nt) {
 // shapes whose every wave owns all NT co tiles: packed last tile when the real channels allow
 #define CONV_FAST_CASE_F32_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                  \
   if (CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)) {                                           \
-    if (g_f32_persistent && (W_ % 16) == 0) CONV_F32P_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)   \
     if (pk_ok(a, NT_)) {                                                                                \
-      CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 1)                                           \
       CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 1)                              \
     }                                                                                                   \
-    CONV_DUO_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 0)                                             \
     CONV_FAST_LAUNCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)                                      \
   }
-
-// start-phase stagger of the fp32 tile kernel (see ConvArgs::stagger): GENTUN_CONV_STAGGER="n[:lo:hi]"
-static int g_stagger[3] = {-1, 256, 512};
-extern "C" int gt_conv_set_stagger(int n, int lo, int hi) {
-  const int old = g_stagger[0];
-  g_stagger[0] = n; g_stagger[1] = lo; g_stagger[2] = hi;
-  return old;
-}
-static void stagger_init() {
-  if (g_stagger[0] >= 0) return;
-  g_stagger[0] = 0;
-  if (const char* e = std::getenv("GENTUN_CONV_STAGGER")) {
-    int n = 0, lo = 256, hi = 512;
-    if (std::sscanf(e, "%d:%d:%d", &n, &lo, &hi) >= 1) { g_stagger[0] = n; g_stagger[1] = lo; g_stagger[2] = hi; }
-  }
-}
 
 // Small launches (few groups per launch: the reference's sequential folds, one
 // rank's share of a config-3 generation): at 2 groups the 8-row tiles of the
@@ -1602,13 +994,9 @@ static int smallq_th(const ConvArgs* a, int TH, int THMIN) {
   return th;
 }
 
+#ifndef GT_KERNELS_ONLY   // (tools/isa_one.sh: one explicit instantiation, no dispatch tables)
 extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
-  stagger_init();
-  ConvArgs lc = *a_in;
-  lc.stagger = g_stagger[0];
-  lc.stagger_lo = g_stagger[1];
-  lc.stagger_hi = g_stagger[2];
-  const ConvArgs* a = &lc;
+  const ConvArgs* a = a_in;
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
   if (a->prec == 1) {
     // small launches: shorter tiles of the S=(3,5) shapes (see smallq_th)
@@ -1697,6 +1085,8 @@ extern "C" int gt_conv_fast_probe_any(const ConvArgs* a) {
   g_probe = 0;
   return rc >= 1000 ? 1 : 0;
 }
+
+#endif  // GT_KERNELS_ONLY
 
 // ===========================================================================
 // Weight gradient, shape-specialised:
@@ -1983,13 +1373,9 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
       const long off = ((long)hh * W + ww) * (NCBI * 8) + cb * 8;
       // unconditional loads (zero chunk for the halo): see conv_fast_kernel's staging
       if (n_src == 1) {
-#if GT_STAGE_SELECT
-        load8f_or0(src0 + off, ok, xr[j]);
-#else
 #pragma unroll
         for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
         if (ok) load8f(src0 + off, xr[j]);
-#endif
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) xr[j][e] = 0.f;
@@ -2007,11 +1393,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < DT; ++j) {
       const int i = tid + NT_ * j;
-#if GT_STAGE_SELECT
-      load8f_or0(dsrc + (long)i * 8, i < DCH, dr[j]);
-#else
       if (i < DCH) load8f(dsrc + (long)i * 8, dr[j]);
-#endif
     }
   };
   auto store = [&](int buf) {
@@ -2076,7 +1458,7 @@ __global__ void __launch_bounds__(NW * 64) wgrad_fast_f32_kernel(WgradArgs a) {
   // second half stages first (from registers loaded one band earlier), then multiplies -- so on
   // every SIMD one wave's split + LDS stores run beside the other wave's MFMAs instead of all
   // waves staging while the matrix pipe idles. Same per-wave MFMA order: bit-identical.
-  const bool early = NB == 2 && GT_WGRAD_HALVES && wave >= NW / 2;
+  const bool early = NB == 2 && wave >= NW / 2;
   if (band0 < band1) {
     load(band0);
     store(0);
@@ -2402,6 +1784,7 @@ extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, 
   return W >= 32 ? 16 : 3;
 }
 
+#ifndef GT_KERNELS_ONLY
 extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
   if (a->prec == 1) {
     WGRAD_FAST_CASE_F32(5, 5, 1, 3, 32, 8, 4, 1)      // s1 input conv (3 -> 20)
@@ -2430,3 +1813,4 @@ extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
   WGRAD_FAST_CASE(3, 3, 7, 7, 16, 16, 8, 2)     // s2 nodes / output conv (50 -> 50)
   return -100;
 }
+#endif  // GT_KERNELS_ONLY

@@ -284,7 +284,8 @@ class GeneticCnnIndividual(Individual):
                  kernel_sizes=((5, 5), (5, 5)), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
                  loss='bce_compat', dtype='fp32', seed=0, backend=None, device=None, optimizer='adam',
-                 momentum=0.9, reset='kernels', batching='keras', batch_norm=False, verbose=False):
+                 momentum=0.9, reset='kernels', batching='keras', batch_norm=False, verbose=False,
+                 pad_images=True):
         if genome is None:
             genome = {'S_{}'.format(i + 1): k * (k - 1) // 2 for i, k in enumerate(nodes)}
         if genes is None:
@@ -317,6 +318,8 @@ class GeneticCnnIndividual(Individual):
         self.batching = batching
         self.batch_norm = batch_norm
         self.verbose = verbose
+        # HIP executor: 28 x 28 stored zero-padded to 32 x 32 for the shape-specialised kernels
+        self.pad_images = bool(pad_images)
 
     @staticmethod
     def generate_random_genes(genome):
@@ -335,7 +338,7 @@ class GeneticCnnIndividual(Individual):
                                seed=self.seed, backend=self.backend, device=device or self.device,
                                optimizer=self.optimizer, momentum=self.momentum, reset=self.reset,
                                batching=self.batching, batch_norm=self.batch_norm,
-                               verbose=self.verbose)
+                               verbose=self.verbose, pad_images=self.pad_images)
 
     def cost(self):
         """Relative training cost (forward FLOPs/sample); LPT scheduling key."""
@@ -373,6 +376,7 @@ class GeneticCnnIndividual(Individual):
             'batching': self.batching,
             'batch_norm': self.batch_norm,
             'verbose': self.verbose,
+            'pad_images': self.pad_images,
         }
 
     def mutate(self):

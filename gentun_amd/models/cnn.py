@@ -29,7 +29,7 @@ class GeneticCnnModel(GentunModel):
                  dropout_probability, classes, nfold=5, epochs=(3,), learning_rate=(1e-3,), batch_size=32,
                  loss="bce_compat", dtype="fp32", seed=0, backend=None, device=None, fold_parallel=True,
                  optimizer="adam", momentum=0.9, reset="kernels", batching="keras", batch_norm=False,
-                 verbose=False):
+                 verbose=False, pad_images=True):
         super(GeneticCnnModel, self).__init__(x_train, y_train)
         self.genes = dict(genes)
         self.name = '-'.join(self.genes[k] for k in sorted(self.genes))
@@ -59,7 +59,7 @@ class GeneticCnnModel(GentunModel):
         self.cfg = _eng.TrainConfig(epochs=epochs, learning_rate=learning_rate, batch_size=batch_size,
                                     dropout=dropout_probability, loss=loss, dtype=dtype, seed=seed,
                                     optimizer=optimizer, momentum=momentum, reset=reset, batching=batching,
-                                    batch_norm=batch_norm, verbose=verbose, nfold=nfold)
+                                    batch_norm=batch_norm, verbose=verbose, nfold=nfold, pad_images=pad_images)
         self.fold_parallel = fold_parallel
         self.model = self.build_model(self.genes, self.nodes, self.input_shape, self.kernels_per_layer,
                                       self.kernel_sizes, self.dense_units, self.dropout_probability, self.classes)

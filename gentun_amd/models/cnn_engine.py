@@ -56,7 +56,7 @@ class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
                  dtype="fp32", seed=0, use_graph=None, eval_batch=1000, optimizer="adam", momentum=0.9,
                  reset="kernels", batching="keras", batch_norm=False, bn_momentum=0.99, bn_eps=1e-3,
-                 dp_group=None, verbose=False, nfold=None):
+                 dp_group=None, verbose=False, nfold=None, pad_images=True):
         if isinstance(epochs, int):
             epochs = (epochs,)
         if isinstance(learning_rate, (int, float)):
@@ -101,6 +101,9 @@ class TrainConfig(object):
         # training is enqueued, "Training N epochs with learning rate lr" per stage
         self.verbose = bool(verbose)
         self.nfold = None if nfold is None else int(nfold)
+        # HIP executor: store a slightly-smaller-than-power-of-two image zero-padded so every stage
+        # runs the shape-specialised kernels (ops/cnn_kernels.padded_hw: MNIST 28 x 28 -> 32 x 32)
+        self.pad_images = bool(pad_images)
 
     def total_epochs(self):
         return sum(self.epochs)
@@ -111,7 +114,7 @@ class TrainConfig(object):
 # ---------------------------------------------------------------------------
 
 class DeviceData(object):
-    def __init__(self, x, y, device, layout):
+    def __init__(self, x, y, device, layout, pad_hw=None):
         x = np.asarray(x)
         y = np.asarray(y)
         self.n = x.shape[0]
@@ -127,10 +130,12 @@ class DeviceData(object):
         elif layout in ("nhwc8", "nhwc8f"):
             # channels padded to a multiple of 8 so one chunk = 8 channels
             # (nhwc8: bf16 tensors of the bf16 mode; nhwc8f: fp32)
-            c = xt.shape[-1]
+            # pad_hw: the images stored zero-padded at the bottom / right to (H, W) (cnn_kernels.padded_hw)
+            n, h, w, c = xt.shape
+            hp, wp = pad_hw or (h, w)
             cp = (c + 7) // 8 * 8
-            pad = torch.zeros(xt.shape[:-1] + (cp,), dtype=torch.float32)
-            pad[..., :c] = xt
+            pad = torch.zeros((n, hp, wp, cp), dtype=torch.float32)
+            pad[:, :h, :w, :c] = xt
             dt = torch.float32 if layout == "nhwc8f" else torch.bfloat16
             self.x = pad.to(device=device, dtype=dt).contiguous()
         else:
@@ -142,12 +147,13 @@ class DeviceData(object):
 _DATA_CACHE = []
 
 
-def device_data(x, y, device, layout):
+def device_data(x, y, device, layout, pad_hw=None):
+    key = (layout, tuple(pad_hw) if pad_hw else None)
     for ent in _DATA_CACHE:
-        if ent[0] is x and ent[1] is y and ent[2] == str(device) and ent[3] == layout:
+        if ent[0] is x and ent[1] is y and ent[2] == str(device) and ent[3] == key:
             return ent[4]
-    dd = DeviceData(x, y, device, layout)
-    _DATA_CACHE.append((x, y, str(device), layout, dd))
+    dd = DeviceData(x, y, device, layout, pad_hw)
+    _DATA_CACHE.append((x, y, str(device), key, dd))
     while len(_DATA_CACHE) > 3:
         _DATA_CACHE.pop(0)
     return dd
@@ -192,7 +198,7 @@ class FoldJob(object):
                 self.fold_ids.append(int(fid))
                 self.folds.append(fold)
         self.G = len(self.folds)
-        self.data = device_data(x, y, self.device, self.layout)
+        self.data = device_data(x, y, self.device, self.layout, getattr(self, "pad_hw", None))
         self.stream = stream if stream is not None else torch.cuda.current_stream(self.device) \
             if self.device.type == "cuda" else None
         self.B = cfg.batch_size

@@ -97,6 +97,12 @@ class HipPopJob(FoldJob):
         if cfg.dtype not in K.PREC:
             raise ValueError("HIP backend precision must be one of {}".format(sorted(K.PREC)))
         self.layout = "nhwc8f" if cfg.dtype == "fp32" else "nhwc8"
+        # zero-padded storage of a slightly-smaller-than-power-of-two image (MNIST 28 x 28 -> 32 x 32):
+        # every stage then runs the shape-specialised kernels (cnn_kernels.padded_hw)
+        p0 = plan if plan is not None else kw["members"][0][0]
+        h0r, w0r, _ = p0.input_shape
+        hw = K.padded_hw(h0r, w0r, len(p0.kernels_per_layer), bool(getattr(cfg, "batch_norm", False)))
+        self.pad_hw = hw if hw != (h0r, w0r) and getattr(cfg, "pad_images", True) else None
         super(HipPopJob, self).__init__(plan, x, y, folds, cfg, device, **kw)
         if self.device.type != "cuda":
             raise RuntimeError("the HIP backend needs a GPU device")
@@ -234,8 +240,9 @@ class HipPopJob(FoldJob):
         """Superset layers / per-group launch records (models/pop_schedule.py)
         plus the device geometry of every layer."""
         p0, Q = self.plan, self.Q
-        h0, w0, _ = p0.input_shape
-        self.sched = PopulationSchedule([self.members[self.gmember[q]][0] for q in range(Q)])
+        h0r, w0r, _ = p0.input_shape
+        h0, w0 = self.pad_hw or (h0r, w0r)
+        self.sched = PopulationSchedule([self.members[self.gmember[q]][0] for q in range(Q)], hw=self.pad_hw)
         self.stages, self.layers = self.sched.stages, self.sched.layers
         for L in self.layers:
             L.cinp, L.coutp = pad8(L.cin), pad8(L.cout)
@@ -252,6 +259,7 @@ class HipPopJob(FoldJob):
         if hs < 1 or ws < 1:
             raise ValueError("input too small for the pooling stages")
         self.final_hw = (hs, ws)
+        self.final_hw_real = (h0r >> len(p0.kernels_per_layer), w0r >> len(p0.kernels_per_layer))
         self.final_cp = pad8(p0.kernels_per_layer[-1])
 
     # ------------------------------------------------------------ buffers
@@ -469,6 +477,8 @@ class HipPopJob(FoldJob):
                                 gather=gather_train if first else None)
             if L.xin is not None:
                 a.xsum = self.act[L.xin].data_ptr()
+            if self.pad_hw is not None:
+                a.Hr, a.Wr = L.Hr, L.Wr       # exact zeros outside the real image
             a.epi_bf16 = 1            # forward outputs never accumulate: bf16 output tile
             if cpools:
                 a.pool_y, a.pool_mask = self.act[st.pool].data_ptr(), st.pmask.data_ptr()
@@ -720,8 +730,9 @@ class HipPopJob(FoldJob):
             add(L.w[0], (L.coutp, L.KH, L.KW, L.cinp), (L.cout, L.KH, L.KW, L.cin), L.cin * L.KH * L.KW,
                 L.cout * L.KH * L.KW, L.name + ".w")
         hs, ws = self.final_hw
+        hr, wr = self.final_hw_real          # W1 rows of padded pixels stay 0 (and get zero gradient)
         add(self.views["W1"][0], (hs, ws, self.final_cp, self.Up),
-            (hs, ws, self.plan.kernels_per_layer[-1], self.plan.dense_units),
+            (hr, wr, self.plan.kernels_per_layer[-1], self.plan.dense_units),
             self.plan.flatten, self.plan.dense_units, "dense1.w")
         w2 = self.views["W2"][0]
         add(w2, (1, 1, w2.shape[1], w2.shape[2]), (1, 1, self.plan.dense_units, self.plan.classes),

@@ -86,7 +86,10 @@ class PopulationSchedule(object):
     per group; the plans of one job share the search space, only genes
     differ)."""
 
-    def __init__(self, plans):
+    def __init__(self, plans, hw=None):
+        """``hw``: the (H, W) the layers run at when it differs from the plans' input
+        shape (a zero-padded image, cnn_kernels.padded_hw); stages also record
+        their real extent (``Hr`` / ``Wr``)."""
         self.Q = len(plans)
         p0 = plans[0]
         for p in plans:
@@ -102,7 +105,8 @@ class PopulationSchedule(object):
                 topo[key] = [stage_topology(p.genes["S_{}".format(s + 1)], p.nodes[s])
                              for s in range(len(p.kernels_per_layer))]
             per_group.append(topo[key])
-        h0, w0, c0 = p0.input_shape
+        h0r, w0r, c0 = p0.input_shape
+        h0, w0 = hw or (h0r, w0r)
         self.stages, self.layers = [], []
         cin, x_slot = c0, "input"
         for s, cout in enumerate(p0.kernels_per_layer):
@@ -113,10 +117,12 @@ class PopulationSchedule(object):
                 raise ValueError("only odd kernel sizes are supported ('same' padding)")
             pre = "s{}".format(s + 1)
             st = StageSpec(s, H, W, x_slot, pre, [per_group[q][s][0] for q in range(self.Q)])
+            st.Hr, st.Wr = h0r >> s, w0r >> s
 
             def add(name, kind, j, cin_, k_, slots, rows):
                 if rows:
                     L = LayerSpec(name, kind, j, s, H, W, cin_, cout, k_, slots, rows)
+                    L.Hr, L.Wr = st.Hr, st.Wr
                     st.layers.append(L)
                     self.layers.append(L)
 

@@ -37,7 +37,7 @@ class ConvArgs(C.Structure):
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
                 ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long),
                 ("cbb", I), ("pool_y", P), ("pool_mask", P), ("unpool_x1", P), ("unpool_sel", P),
-                ("cout_real", I), ("stagger", I), ("stagger_lo", I), ("stagger_hi", I)]
+                ("cout_real", I), ("Hr", I), ("Wr", I)]
 
 
 class WgradArgs(C.Structure):
@@ -299,6 +299,27 @@ def conv_tile_rows(H, W, tile_pixels=None):
     if W > tp:
         raise ValueError("image width > {} not supported by conv_fwd tiles".format(tp))
     return max(1, min(H, tp // W))
+
+
+def padded_hw(h, w, nstages, batch_norm=False):
+    """(H, W) the HIP executor stores and runs a Genetic-CNN image at.
+
+    The shape-specialised kernels exist for the power-of-two stage widths of
+    the search spaces (32 / 16 / 8). An image a little smaller than a power of
+    two -- the reference's own MNIST default, 28 x 28 (gentun/individuals.py:221)
+    -- is stored zero-padded at the bottom / right to that size, so every stage
+    runs those kernels (28 -> 32, 14 -> 16, final 7 x 7 in 8 x 8) instead of
+    the generic ones. The forward epilogues write exact zeros outside the real
+    rows / columns (ConvArgs::Hr / Wr) and the dense W1 rows of padded pixels
+    are initialised to 0 and receive zero gradient, so the padded network IS
+    the unpadded one (tests/test_hip_train.py::test_padded_mnist_geometry).
+    Conditions: square, every stage's real size even (no floor pooling inside
+    the padding), at most 25 % wider, no BatchNorm (its batch statistics would
+    count the padding)."""
+    p = 1 << max(0, int(w) - 1).bit_length()
+    if (h != w or p == w or batch_norm or p > 1.25 * w or w % (1 << nstages) or p >> nstages < 8):
+        return h, w
+    return p, p
 
 
 def wgrad_blocks(kdim, with_bias=True):

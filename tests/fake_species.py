@@ -78,3 +78,13 @@ class FlakyBitIndividual(BitIndividual):
             FlakyBitIndividual.FAILS[0] += 1
             raise RuntimeError("permanent evaluation failure")
         super(FlakyBitIndividual, self).evaluate_fitness()
+
+
+class SlowBitIndividual(BitIndividual):
+    """A BitIndividual whose evaluation takes 20 ms: under the dynamic (work-stealing) schedule every
+    rank then gets units to claim, however fast rank 0 leaves its broadcast."""
+
+    def evaluate_fitness(self):
+        import time
+        time.sleep(0.02)
+        super(SlowBitIndividual, self).evaluate_fitness()

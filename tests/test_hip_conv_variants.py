@@ -1,12 +1,13 @@
-"""The persistent two-team fp32 conv kernel (``conv_duo_f32_kernel``,
-csrc/hip/cnn_conv_fast.hip) against the one-tile kernel it replaces at
-population launch sizes: every output -- forward with bias / ReLU / N-ary
-input sum / ``xsum`` / fused 2x2 pool + argmax mask, data gradient with the
-DAG fan-out (accumulate, ReLU mask, several output slots) and the fused
-un-pool -- must be BIT-identical (same k order, same MFMA sequence, same
-epilogue arithmetic), for every shape-specialised fp32 layer of the S=(3,5)
-space incl. the packed last co tile, and for workgroups that walk an odd or
-even number of tiles (both teams finish)."""
+"""Variants of the shape-specialised fp32 conv against each other: the tile
+kernel's LDS-tile epilogue vs its register-direct epilogue (the default for
+16 / 32-wide images) must be BIT-identical for every output -- forward with
+bias / ReLU / N-ary input sum / ``xsum`` / fused 2x2 pool + argmax mask, data
+gradient with the DAG fan-out (accumulate, ReLU mask, several output slots)
+and the fused un-pool -- for every shape-specialised fp32 layer of the S=(3,5)
+space incl. the packed last co tile; and the fp32 wgrad's column slices vs
+one workgroup. (Round 3-5 persistent variants of this file -- two-team "duo",
+fixed-role "pipe" -- were measured slower and deleted:
+profiles/r5/conv_f32_sched_pipe_ab_r5.txt.)"""
 
 import pytest
 import torch
@@ -28,21 +29,17 @@ def pad8(c):
 
 
 def _run(Km, a, mode, wgs):
-    """mode 0: tile kernel (LDS-tile epilogue); 2: duo kernel forced; 3: tile kernel with the
-    register-direct epilogue (gt_conv_set_regepi)."""
+    """mode 0: tile kernel, LDS-tile epilogue; 3: tile kernel, register-direct epilogue
+    (gt_conv_set_regepi). ``wgs`` is unused (kept so the parametrisations stay comparable)."""
     import ctypes
     L = Km.lib()
-    L.gt_conv_set_duo.argtypes = [ctypes.c_int, ctypes.c_int]
-    L.gt_conv_set_duo.restype = ctypes.c_int
     L.gt_conv_set_regepi.argtypes = [ctypes.c_int]
     L.gt_conv_set_regepi.restype = ctypes.c_int
-    old = L.gt_conv_set_duo(2 if mode == 2 else 0, wgs)
     old_re = L.gt_conv_set_regepi(1 if mode == 3 else 0)
     try:
         Km.check(L.gt_conv_fwd(a, torch.cuda.current_stream().cuda_stream), "conv")
         torch.cuda.synchronize()
     finally:
-        L.gt_conv_set_duo(old, 256)
         L.gt_conv_set_regepi(old_re)
 
 
@@ -54,8 +51,7 @@ def _split(w):
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,cin,cout,k", SHAPES)
 @pytest.mark.parametrize("nin", [1, 3])
-@pytest.mark.parametrize("wgs", [5, 8])
-def test_duo_forward_bit_identical(H, W, cin, cout, k, nin, wgs):
+def test_epilogue_variants_forward_bit_identical(H, W, cin, cout, k, nin, wgs=0):
     Km = K()
     torch.manual_seed(H + cin + k + nin)
     G, B = 3, 8
@@ -75,7 +71,7 @@ def test_duo_forward_bit_identical(H, W, cin, cout, k, nin, wgs):
     rows = torch.tensor([[0, full, 1 | (1 << 24), 0], [1, 1, 1, 0], [2, full, 1 | (1 << 24), 0]],
                         dtype=torch.int32, device=DEV)
     outs = {}
-    for mode in (0, 2, 3):
+    for mode in (0, 3):
         out = torch.full((G, B, H, W, coutp), 7.0, device=DEV)
         xsum = torch.full((G, B, H, W, cinp), 3.0, device=DEV)
         py = torch.full((G, B, H // 2, W // 2, coutp), 5.0, device=DEV)
@@ -92,7 +88,7 @@ def test_duo_forward_bit_identical(H, W, cin, cout, k, nin, wgs):
         a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
         _run(Km, a, mode, wgs)
         outs[mode] = (out, xsum, py, pm)
-    for m in (2, 3):
+    for m in (3,):
         for name, t0, t2 in zip(("out", "xsum", "pool_y", "pool_mask"), outs[0], outs[m]):
             assert torch.equal(t0, t2), (m, name)
     # the reference kernel really pooled groups 0 and 2 (sanity of the comparison itself)
@@ -101,8 +97,7 @@ def test_duo_forward_bit_identical(H, W, cin, cout, k, nin, wgs):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,cin,cout,k", SHAPES)
-@pytest.mark.parametrize("wgs", [5, 8])
-def test_duo_data_gradient_bit_identical(H, W, cin, cout, k, wgs):
+def test_epilogue_variants_data_gradient_bit_identical(H, W, cin, cout, k, wgs=0):
     """Data-gradient launches (conv with flipped weights, no bias / ReLU):
     per group write / accumulate / ReLU-mask into up to two output slots."""
     Km = K()
@@ -120,7 +115,7 @@ def test_duo_data_gradient_bit_identical(H, W, cin, cout, k, wgs):
     rows = torch.tensor([[0, 1, 1 | (1 << 8) | (1 << 16), 0], [1, 1, 3 | (1 << 9) | (1 << 17), 0],
                          [2, 1, 2 | (1 << 16 + 1), 0]], dtype=torch.int32, device=DEV)
     outs = {}
-    for mode in (0, 2, 3):
+    for mode in (0, 3):
         o = [t.clone() for t in init]
         a = Km.ConvArgs()
         a.inp[0] = dz.data_ptr()
@@ -132,7 +127,7 @@ def test_duo_data_gradient_bit_identical(H, W, cin, cout, k, wgs):
         a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
         _run(Km, a, mode, wgs)
         outs[mode] = o
-    for m in (2, 3):
+    for m in (3,):
         for i in range(2):
             assert torch.equal(outs[0][i], outs[m][i]), (m, i)
     assert not torch.equal(outs[0][0], init[0])
@@ -140,7 +135,7 @@ def test_duo_data_gradient_bit_identical(H, W, cin, cout, k, wgs):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,cin,cout,k", [(16, 16, 50, 20, 5), (16, 16, 50, 50, 3)])
-def test_duo_unpool_bit_identical(H, W, cin, cout, k):
+def test_epilogue_variants_unpool_bit_identical(H, W, cin, cout, k):
     """A data gradient whose output is a pool's gradient scatters it to the
     forward's argmax cells of the pool source (slot chosen per group)."""
     Km = K()
@@ -156,7 +151,7 @@ def test_duo_unpool_bit_identical(H, W, cin, cout, k):
     sel = torch.tensor([0, 1, 0], dtype=torch.int32, device=DEV)
     rows = torch.tensor([[g, 1, 1 | (1 << 25), 0] for g in range(G)], dtype=torch.int32, device=DEV)
     outs = {}
-    for mode in (0, 2, 3):
+    for mode in (0, 3):
         x0 = torch.full((G, B, 2 * H, 2 * W, coutp), 4.0, device=DEV)
         x1 = torch.full((G, B, 2 * H, 2 * W, coutp), 6.0, device=DEV)
         dummy = torch.zeros(G, B, H, W, coutp, device=DEV)
@@ -169,7 +164,7 @@ def test_duo_unpool_bit_identical(H, W, cin, cout, k):
         a.TH, a.prec, a.cout_real = Km.conv_tile_rows(H, W), 1, cout
         _run(Km, a, mode, 6)
         outs[mode] = (x0, x1, dummy)
-    for m in (2, 3):
+    for m in (3,):
         for i in range(3):
             assert torch.equal(outs[0][i], outs[m][i]), (m, i)
 

@@ -35,7 +35,7 @@ def _proc(rank, world, port, outdir, schedule):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
                        "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank)})
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from fake_species import BitIndividual as Bit
+    from fake_species import SlowBitIndividual as Bit
     from gentun_amd import GeneticAlgorithm
     from gentun_amd.metrics import EventLog
     from gentun_amd.parallel import DistComm

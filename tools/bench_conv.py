@@ -25,10 +25,6 @@ G, B = int(os.environ.get("G", "80")), 32
 DBGS = [int(d) for d in os.environ.get("DBGS", "0,1,2,4,7").split(",")]
 dev = torch.device("cuda", 0)
 L = K.lib()
-L.gt_conv_set_f32p.argtypes = [__import__("ctypes").c_int, __import__("ctypes").c_int]
-L.gt_conv_set_f32p(int(os.environ.get("F32P", "0")), int(os.environ.get("F32P_GRID", "0")))
-L.gt_conv_set_duo.argtypes = [__import__("ctypes").c_int, __import__("ctypes").c_int]
-L.gt_conv_set_duo(int(os.environ.get("DUO", "0")), int(os.environ.get("DUO_WGS", "256")))
 L.gt_conv_set_regepi.argtypes = [__import__("ctypes").c_int]
 L.gt_conv_set_regepi(int(os.environ.get("REGEPI", "1")))
 
@@ -126,7 +122,6 @@ for name, H, cin, cout, k, nin in shapes:
                 a.cout_real = cout
                 fn = lambda s: K.check(L.gt_conv_wgrad(a, s), kind)    # noqa: E731
             us = timeit(fn)
-            print(json.dumps({"regepi": os.environ.get("REGEPI", "1"), "duo": os.environ.get("DUO", "0"), "f32p": os.environ.get("F32P", "0"), "grid": os.environ.get("F32P_GRID", "0"),
-                              "dtype": DT, "G": G, "kernel": kind, "shape": name, "dbg": dbg, "us": round(us, 1),
+            print(json.dumps({"regepi": os.environ.get("REGEPI", "1"), "dtype": DT, "G": G, "kernel": kind, "shape": name, "dbg": dbg, "us": round(us, 1),
                               "tflops_useful": round(flops / us / 1e6, 1),
                               "mfma_floor_us": round(floor_us, 1), "mfma_eff": round(floor_us / us, 3)}), flush=True)

@@ -2,6 +2,8 @@
 split into jobs of ``pop_batch`` on ``streams`` streams, 1 epoch each.
 
 usage: python tools/probe_pop.py [P] [pop_batch] [streams] [epochs] [samples]
+Env: SHAPE=28,28,1 (MNIST-shaped: the reference default, stored zero-padded to 32 x 32 unless PAD=0),
+SPACE=deep, KERNELS=, BN=1, DTYPE=, RESET=, GRAPH=0, WARM=0.
 """
 import json
 import os
@@ -15,7 +17,7 @@ import torch
 
 from gentun_amd.models import cnn_engine as E
 from gentun_amd.models.genome import make_plan
-from gentun_amd.utils.data import make_cifar_like, stratified_kfold
+from gentun_amd.utils.data import make_cifar_like, make_mnist_like, stratified_kfold
 
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 pb = int(sys.argv[2]) if len(sys.argv) > 2 else 8
@@ -26,7 +28,9 @@ dev = torch.device("cuda", 0)
 if os.environ.get("GENTUN_WGRAD_NB"):                 # A/B: force the wgrad band buffers
     from gentun_amd.ops import cnn_kernels as K
     K.lib().gt_wgrad_set_nb(int(os.environ["GENTUN_WGRAD_NB"]))
-x, y = make_cifar_like(n=n, seed=0)
+shape = tuple(int(v) for v in os.environ.get("SHAPE", "32,32,3").split(","))
+x, y = make_cifar_like(n=n, seed=0) if shape == (32, 32, 3) else make_mnist_like(n=n, seed=0)
+assert tuple(x.shape[1:]) == shape, (x.shape, shape)
 folds = stratified_kfold(np.argmax(y, 1), 5, seed=0)
 rnd = random.Random(0)
 plans = []
@@ -37,10 +41,10 @@ if os.environ.get("KERNELS"):
     kernels = tuple(int(v) for v in os.environ["KERNELS"].split(","))
 for _ in range(P):
     g = {"S_{}".format(s + 1): "".join(rnd.choice("01") for _ in range(k * (k - 1) // 2)) for s, k in enumerate(nodes)}
-    plans.append(make_plan(g, nodes, (32, 32, 3), kernels, ((5, 5),) * len(nodes), 500, 10))
+    plans.append(make_plan(g, nodes, shape, kernels, ((5, 5),) * len(nodes), 500, 10))
 cfg = E.TrainConfig(epochs=(epochs,), learning_rate=(1e-3,), batch_size=32, dtype=os.environ.get("DTYPE", "fp32"),
                     loss="ce", reset=os.environ.get("RESET", "all"), batch_norm=os.environ.get("BN", "0") == "1",
-                    use_graph=os.environ.get("GRAPH", "1") != "0")
+                    use_graph=os.environ.get("GRAPH", "1") != "0", pad_images=os.environ.get("PAD", "1") != "0")
 streams = [torch.cuda.Stream(dev, priority=int(os.environ.get("MAIN_PRIO", "0"))) for _ in range(ns)]
 # warm-up (allocator, code objects); WARM=0 keeps profiles free of the small warm-up job
 if os.environ.get("WARM", "1") != "0":
