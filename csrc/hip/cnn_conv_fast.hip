@@ -891,14 +891,14 @@ static int g_probe = 0;
 // The S=(3,5) s2 input-conv dgrad (5x5, 50 -> 20) with one co tile per wave and 4 pixel groups each
 // instead of the packed tile's 2 tiles x 2 groups: 33 % more MFMAs but half the weight loads per MFMA;
 // same-box A/B 126 -> 114 us per launch at 25 groups, population step -1.6 % (profiles/conv_s2in_dgrad_ct1_ab_r3.txt).
-// Runtime switch (GENTUN_S2IN_CT1, gt_conv_set_s2in_ct1) so both variants are compared against the fp64
+// Runtime setter (gt_conv_set_s2in_ct1, tests only) so both variants are compared against the fp64
 // oracle on one launch in one process (tests/test_hip_fp32.py::test_s2in_dgrad_variants): both 1.3e-6 of
 // the output range (torch fp32: 7.1e-7), channels 0-15 bitwise equal, deterministic; the 2-rank DP
 // trajectory stays within the derived summation-order bound (tests/test_hip_dp.py). On by default since
 // round 4 (profiles/conv_s2in_dgrad_ct1_r4.txt).
 static int g_s2in_ct1 = -1;
 static bool s2in_ct1_on() {
-  if (g_s2in_ct1 < 0) g_s2in_ct1 = std::getenv("GENTUN_S2IN_CT1") ? std::atoi(std::getenv("GENTUN_S2IN_CT1")) : 1;
+  if (g_s2in_ct1 < 0) g_s2in_ct1 = 1;
   return g_s2in_ct1 != 0;
 }
 extern "C" int gt_conv_set_s2in_ct1(int on) {
@@ -908,12 +908,12 @@ extern "C" int gt_conv_set_s2in_ct1(int on) {
   return old;
 }
 
-// fp32 register-direct epilogue in the tile kernel (A/B: GENTUN_F32_REGEPI=0 / 1, gt_conv_set_regepi):
+// fp32 register-direct epilogue in the tile kernel (gt_conv_set_regepi: tests compare it with the LDS tile):
 // no LDS output tile, no second barrier, the pool from lane shuffles
 static int g_regepi = -1;
 static bool regepi_on() {
   // on by default: 2-19 % faster per fp32 conv launch, bit-identical (profiles/conv_f32_regepi_ab_r3.txt)
-  if (g_regepi < 0) g_regepi = std::getenv("GENTUN_F32_REGEPI") ? std::atoi(std::getenv("GENTUN_F32_REGEPI")) : 1;
+  if (g_regepi < 0) g_regepi = 1;
   return g_regepi != 0;
 }
 extern "C" int gt_conv_set_regepi(int on) {
@@ -924,11 +924,9 @@ extern "C" int gt_conv_set_regepi(int on) {
 }
 
 // the packed last co tile applies: fp32, the real output channels leave <= 4 in the last 16-channel tile
-static int g_conv_pk = -1;     // A/B switch (GENTUN_CONV_PK=0 disables)
 static bool pk_ok(const ConvArgs* a, int nt) {
-  if (g_conv_pk < 0) g_conv_pk = std::getenv("GENTUN_CONV_PK") ? std::atoi(std::getenv("GENTUN_CONV_PK")) : 1;
   const int last = a->cout_real - 16 * (nt - 1);
-  return g_conv_pk && a->prec == 1 && a->cout_real > 0 && last >= 1 && last <= 4;
+  return a->prec == 1 && a->cout_real > 0 && last >= 1 && last <= 4;
 }
 
 #define CONV_FAST_MATCH(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_)                                             \
@@ -973,7 +971,7 @@ static bool pk_ok(const ConvArgs* a, int nt) {
 // of the six split terms) is the same for any tile height: results are
 // bit-identical to the 8-row tiles (tests/test_hip_kernels.py), so a
 // candidate's result still does not depend on how many groups share its
-// launch. GENTUN_CONV_SMALLQ=0 disables (A/B).
+// launch. gt_conv_set_smallq(0) disables (tests compare both).
 static int g_smallq = -1;
 extern "C" int gt_conv_set_smallq(int on) {
   const int old = g_smallq;
@@ -981,13 +979,13 @@ extern "C" int gt_conv_set_smallq(int on) {
   return old;
 }
 // tile rows for a launch whose default tile has TH rows: halve while the grid
-// is below GENTUN_CONV_SMALLQ_WG workgroups (default 300: about one per CU; at 5 and 10 groups the
+// is below 300 workgroups (default 300: about one per CU; at 5 and 10 groups the
 // 8-row tiles measured faster than 4-row ones, profiles/conv_tile_threshold_ab_r4.txt), down to THMIN
 static long g_smallq_wg = -1;
 static int smallq_th(const ConvArgs* a, int TH, int THMIN) {
-  if (g_smallq < 0) g_smallq = std::getenv("GENTUN_CONV_SMALLQ") ? std::atoi(std::getenv("GENTUN_CONV_SMALLQ")) : 1;
+  if (g_smallq < 0) g_smallq = 1;
   if (g_smallq_wg < 0)
-    g_smallq_wg = std::getenv("GENTUN_CONV_SMALLQ_WG") ? std::atol(std::getenv("GENTUN_CONV_SMALLQ_WG")) : 300;
+    g_smallq_wg = 300;
   if (!g_smallq) return TH;
   int th = TH;
   while (th > THMIN && (long)a->ngroups * a->B * (a->H / th) < g_smallq_wg) th >>= 1;
@@ -1024,14 +1022,6 @@ extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
     CONV_FAST_CASE_F32_PK(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
     CONV_FAST_CASE_F32_PK(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
     CONV_FAST_CASE_F32(5, 5, 3, 16, 8, 4, 7, 4)   // s2 input conv (20 -> 50)
-    {
-      // A/B (GENTUN_F32_S2): 1 = whole 16x16 image per workgroup, 4 waves (8 pixel groups per wave: half
-      // the weight traffic per MFMA); 2 = whole image, 8 waves
-      static const int s2 = std::getenv("GENTUN_F32_S2") ? std::atoi(std::getenv("GENTUN_F32_S2")) : 0;
-      if (s2 == 1) CONV_FAST_CASE_F32(3, 3, 7, 16, 16, 4, 7, 4)
-      if (s2 == 2) CONV_FAST_CASE_F32(3, 3, 7, 16, 16, 4, 7, 8)
-      if (s2 == 1) CONV_FAST_CASE_F32(5, 5, 3, 16, 16, 4, 7, 4)
-    }
     // (a packed tile here needs every wave to own all 4 co tiles: 2x the weight traffic per MFMA,
     // measured 20 % slower than the 2 + 2 split -- profiles/conv_f32_packed_tile_ab_r2.txt)
     CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
@@ -1624,7 +1614,7 @@ extern "C" int gt_wgrad_reduce(const WgradArgs* a, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-static int g_wgrad_nb = 0;   // 0: per-shape default, 1 / 2: force band buffers (A/B switch)
+static int g_wgrad_nb = 0;   // 0: per-shape default, 1 / 2: force band buffers (gt_wgrad_set_nb, tests)
 
 extern "C" int gt_wgrad_set_nb(int nb) {
   const int old = g_wgrad_nb;
@@ -1705,8 +1695,8 @@ extern "C" int gt_wgrad_set_nb(int nb) {
 // grid fills more CUs and each workgroup's serial band loop carries 1/NZ of
 // the MFMAs. Every weight's sum runs in the same band / k-step order in any
 // slice: results are bit-identical for any NZ (tests/test_hip_kernels.py).
-// GENTUN_WGRAD_NZ: 0 auto (default), 1 / 2 / 4 / 8 forced (8: 4-wave workgroups).
-static int g_wgrad_nz = -1;
+// gt_wgrad_set_nz (tests): 0 auto (default), 1 / 2 / 4 / 8 forced (8: 4-wave workgroups).
+static int g_wgrad_nz = 0;
 
 extern "C" int gt_wgrad_set_nz(int nz) {
   const int old = g_wgrad_nz;
@@ -1714,23 +1704,18 @@ extern "C" int gt_wgrad_set_nz(int nz) {
   return old;
 }
 
-// blocks below which the 8-slice variant runs (GENTUN_WGRAD_NZ8; default 0 = never: measured neutral at
-// 2 groups, profiles/wgrad_nz8_ab_r4.txt)
-static int g_wgrad_nz8 = std::getenv("GENTUN_WGRAD_NZ8") ? std::atoi(std::getenv("GENTUN_WGRAD_NZ8")) : 0;
-
 static int wgrad_nz(const WgradArgs* a) {
-  if (g_wgrad_nz < 0) g_wgrad_nz = std::getenv("GENTUN_WGRAD_NZ") ? std::atoi(std::getenv("GENTUN_WGRAD_NZ")) : 0;
   const int force = g_wgrad_nz;
   if (force == 1 || force == 2 || force == 4 || force == 8) return force;
+  // (an 8-slice variant below ~32 blocks measured neutral at 2 groups: profiles/wgrad_nz8_ab_r4.txt)
   const int blocks = a->S * a->ngroups;
-  return blocks < g_wgrad_nz8 ? 8 : blocks < 64 ? 4 : blocks < 160 ? 2 : 1;
+  return blocks < 64 ? 4 : blocks < 160 ? 2 : 1;
 }
 
-// packed last co tile of the fp32 wgrad (A/B switch GENTUN_WGRAD_PK=0 disables)
+// packed last co tile of the fp32 wgrad
 static bool wgrad_pk_ok(const WgradArgs* a, int mt) {
-  static const int on = std::getenv("GENTUN_WGRAD_PK") ? std::atoi(std::getenv("GENTUN_WGRAD_PK")) : 1;
   const int last = a->cout_real - 16 * (mt - 1);
-  return on && a->cout_real > 0 && last >= 1 && last <= 4;
+  return a->cout_real > 0 && last >= 1 && last <= 4;
 }
 
 // band rows of the specialised wgrad per precision (the host sizes the split
@@ -1777,9 +1762,8 @@ extern "C" int gt_wgrad_fast_band(int KH, int KW, int Cinp, int Coutp, int H, in
 extern "C" int gt_wgrad_fast_splits(int KH, int KW, int Cinp, int Coutp, int H, int W, int prec) {
   (void)KH; (void)KW; (void)Cinp; (void)Coutp; (void)H;
   if (prec == 1) {
-    const char* e = getenv("GENTUN_F32_SPLITS16");     // A/B: splits of the 16-wide stage
     // 8-wide (deep stage 3): 4 splits x 4 column slices per group
-    return W >= 32 ? 32 : W <= 8 ? 4 : (e ? atoi(e) : 8);
+    return W >= 32 ? 32 : W <= 8 ? 4 : 8;
   }
   return W >= 32 ? 16 : 3;
 }

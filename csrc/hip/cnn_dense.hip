@@ -1226,19 +1226,19 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// streaming dense fwd / dgrad (default) vs the round-2 kernels: A/B switch
-// GENTUN_DENSE_STREAM=0 / gt_dense_set_stream (bit-identical either way)
+// streaming dense fwd / dgrad (default) vs the round-2 kernels: gt_dense_set_stream (tests: bit-identical
+// either way)
 static int g_dense_stream = -1;
 static bool dense_stream_on() {
   if (g_dense_stream < 0)
-    g_dense_stream = std::getenv("GENTUN_DENSE_STREAM") ? std::atoi(std::getenv("GENTUN_DENSE_STREAM")) : 1;
+    g_dense_stream = 1;
   return g_dense_stream != 0;
 }
 
-// A/B: GENTUN_DENSE_DGRAD2=0 keeps the v1 streaming data gradient even when the dH planes exist
+// gt_dense_set_dgrad2(0) (tests) keeps the v1 streaming data gradient even when the dH planes exist
 static int g_dgrad2 = -1;
 static bool dgrad2_on() {
-  if (g_dgrad2 < 0) g_dgrad2 = std::getenv("GENTUN_DENSE_DGRAD2") ? std::atoi(std::getenv("GENTUN_DENSE_DGRAD2")) : 1;
+  if (g_dgrad2 < 0) g_dgrad2 = 1;
   return g_dgrad2 != 0;
 }
 
@@ -1263,10 +1263,10 @@ int gt_step_begin(StepState* s, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-// split-K forward from the W1 master (default; GENTUN_DENSE_SK=0: the streaming kernel on the transposed copy)
+// split-K forward from the W1 master (gt_dense_set_sk(0), tests: the streaming kernel on the transposed copy)
 static int g_dense_sk = -1;
 static bool dense_sk_on() {
-  if (g_dense_sk < 0) g_dense_sk = std::getenv("GENTUN_DENSE_SK") ? std::atoi(std::getenv("GENTUN_DENSE_SK")) : 1;
+  if (g_dense_sk < 0) g_dense_sk = 1;
   return g_dense_sk != 0;
 }
 
@@ -1298,8 +1298,8 @@ int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
     return (int)hipGetLastError();
   }
   if (dense_stream_on()) {
-    // unit tiles per workgroup (A/B: GENTUN_DENSE_UT = 1 / 2 / 4; 4: 53 vs 67 us at 25 groups, W1 in MALL)
-    static const int ut = std::getenv("GENTUN_DENSE_UT") ? std::atoi(std::getenv("GENTUN_DENSE_UT")) : 4;
+    // unit tiles per workgroup (4: 53 vs 67 us for 1 at 25 groups, W1 in MALL)
+    constexpr int ut = 4;
     dim3 grid(a->Up / (16 * ut), (a->B + 31) / 32, a->G);
 #define DENSE_FWD_UT(UT_)                                                                                 \
   if (ut == UT_) {                                                                                        \
@@ -1307,8 +1307,6 @@ int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
     else hipLaunchKernelGGL((dense_fwd_stream_kernel<0, UT_>), grid, dim3(256), 0, stream, *a);           \
     return (int)hipGetLastError();                                                                        \
   }
-    DENSE_FWD_UT(1)
-    DENSE_FWD_UT(2)
     DENSE_FWD_UT(4)
 #undef DENSE_FWD_UT
   }

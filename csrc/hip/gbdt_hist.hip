@@ -117,7 +117,7 @@ struct Geo {
   int maxch;     // chunk records per fold
   int maxslot;   // partial histogram slots per fold
   int lg_n;
-  int rch;       // rows per histogram chunk (GB_R unless GENTUN_GBDT_CHUNK overrides)
+  int rch;       // rows per histogram chunk (GB_R)
 };
 
 // ---- G2: gradients of every fold (all rows; only indexed rows are read) ----
@@ -278,24 +278,54 @@ __global__ void level0_kernel(Geo geo, const int* __restrict__ nroot, LNode* __r
 // fixed-point value every row carries -- the same integer the 64-bit sum would
 // reach, so histograms stay exact and bitwise identical. The LDS image is
 // 49 KB instead of 66 KB (3 workgroups per CU instead of 2).
+// Packed (GT_HIST_PACK): the count rides in the low 17 bits of the gradient's own 64-bit word --
+// one LDS atomic of (qg << 17) + 1 per row and feature instead of a 64-bit plus a 32-bit one. Exact:
+// a chunk has at most GB_R = 2^16 rows, so the count never carries into the gradient bits, and with
+// |qg| < 2^29 per row (geo.lg_n >= 32 on this path) the chunk's gradient sum stays below 2^45,
+// shifted 2^62. Decode: count = word & (2^17 - 1), sum qg = word >> 17 (arithmetic).
 #define HB_GSTRIDE 258   // int64 per feature in the gradient-only image (256 bins + pad)
+#ifndef GT_HIST_PACK
+#define GT_HIST_PACK 1
+#endif
+#define HB_CBITS 17
+static_assert(GB_R < (1 << HB_CBITS), "packed counts must not carry into the gradient bits");
 template <bool HC>
 __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __restrict__ bins,
                                                     const int* __restrict__ rows, const float2* __restrict__ gh,
                                                     const Chunk* __restrict__ chunks, const int* __restrict__ counts,
                                                     i64* __restrict__ hist, i64* __restrict__ part,
                                                     const unsigned int* __restrict__ mx) {
-  const int k = blockIdx.z;
-  if ((int)blockIdx.x >= counts[2 * k]) return;
+  // XCD-aware order: the hardware deals consecutive workgroups to the 8 XCDs round-robin; remap so
+  // that the feature blocks of one row chunk are CONSECUTIVE workgroups of ONE XCD. They gather the
+  // same rows (row ids, gradients, and 16-byte slices of the same 256-byte bin rows), so all but the
+  // first of them hit that XCD's L2 instead of each XCD fetching every line from HBM (round-4 PMC:
+  // 24 % L2 hits, the kernel waited on memory half of its cycles)
+  int cx = blockIdx.x, cy = blockIdx.y, cz = blockIdx.z;
+  {
+    const int gx = gridDim.x, gy = gridDim.y;
+    const int total = gx * gy * gridDim.z;
+    int t = cx + gx * (cy + gy * cz);
+#ifndef GT_HIST_XCD
+#define GT_HIST_XCD 1
+#endif
+    if (GT_HIST_XCD && (total & 7) == 0) t = (t & 7) * (total >> 3) + (t >> 3);
+    cy = t % gy;
+    t /= gy;
+    cx = t % gx;
+    cz = t / gx;
+  }
+  const int k = cz;
+  if (cx >= counts[2 * k]) return;
   constexpr int LHN = HC ? HB_F * HB_GSTRIDE : HB_F * HB_STRIDE;
   __shared__ u64 lh[LHN];
-  __shared__ unsigned int lc[HC ? HB_F * GB_BINS : 1];
-  const Chunk c = chunks[(size_t)k * geo.maxch + blockIdx.x];
+  constexpr bool PK = HC && GT_HIST_PACK;
+  __shared__ unsigned int lc[HC && !PK ? HB_F * GB_BINS : 1];
+  const Chunk c = chunks[(size_t)k * geo.maxch + cx];
   const int F = geo.F, Fs = geo.Fs;
-  const int fb = blockIdx.y * HB_F, tid = threadIdx.x;
+  const int fb = cy * HB_F, tid = threadIdx.x;
   constexpr int RL = HB_T / 4;                  // row lanes
   for (int i = tid; i < LHN; i += HB_T) lh[i] = 0ull;
-  if (HC)
+  if (HC && !PK)
     for (int i = tid; i < HB_F * GB_BINS; i += HB_T) lc[i] = 0u;
   const float sg = ldexpf(1.f, fx_exp(mx[2 * k], geo.lg_n)), sh = ldexpf(1.f, fx_exp(mx[2 * k + 1], geo.lg_n));
   __syncthreads();
@@ -303,7 +333,12 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __re
   const int f4 = fb + wl * 4;
   const float2* gk = gh + (size_t)k * geo.n;
   auto add = [&](uint32_t w, u64 qg, u64 qh) {
-    if constexpr (HC) {
+    if constexpr (PK) {
+      u64* my = lh + wl * 4 * HB_GSTRIDE;
+      const u64 v = (qg << HB_CBITS) + 1ull;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) atomicAdd(my + q * HB_GSTRIDE + ((w >> (8 * q)) & 255u), v);
+    } else if constexpr (HC) {
       u64* my = lh + wl * 4 * HB_GSTRIDE;
       unsigned int* myc = lc + wl * 4 * GB_BINS;
 #pragma unroll
@@ -354,7 +389,10 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __re
   const i64 qh1 = (i64)llrintf(1.0f * sh);     // every row's hessian (h = 1) in fixed point
   for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
     const int fl = i >> 9, j = i & 511;
-    if constexpr (HC)
+    if constexpr (PK) {
+      const i64 v = (i64)lh[fl * HB_GSTRIDE + (j >> 1)];
+      dst[(size_t)fl * 2 * GB_BINS + j] = (j & 1) ? (v & ((1ll << HB_CBITS) - 1)) * qh1 : v >> HB_CBITS;
+    } else if constexpr (HC)
       dst[(size_t)fl * 2 * GB_BINS + j] = (j & 1) ? (i64)lc[fl * GB_BINS + (j >> 1)] * qh1
                                                   : (i64)lh[fl * HB_GSTRIDE + (j >> 1)];
     else
@@ -815,10 +853,8 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   const bool multi = objective >= 4;
   const int K = multi ? std::max(2, num_class) : 1;
   const int obj = multi ? 3 : (objective == 0 ? 0 : (objective == 1 ? 1 : 2));
-  // squared error: h = 1 for every row -> count histograms for the hessian (hist_kernel<true>);
-  // GENTUN_GBDT_HCONST=0 keeps the two 64-bit sums (A/B)
-  static const bool hc_on = !std::getenv("GENTUN_GBDT_HCONST") || std::atoi(std::getenv("GENTUN_GBDT_HCONST")) != 0;
-  const bool hconst = obj == 0 && hc_on;
+  // squared error: h = 1 for every row -> count histograms for the hessian (hist_kernel<true>)
+  const bool hconst = obj == 0;
   const int D = std::max(0, std::min((int)P[2], GB_MAXD));
   std::lock_guard<std::mutex> lock(gbdt_cache::mu);   // one GBDT call at a time per process (bins cache)
   int rc = 0;
@@ -827,13 +863,13 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   geo.Lmax = 1 << D;
   geo.Lh = 1 << std::max(0, D - 1);
   // rows per histogram chunk: fewer, longer chunks = fewer partial slots for the reduce to sum
-  static const int rch_env = std::getenv("GENTUN_GBDT_CHUNK") ? std::atoi(std::getenv("GENTUN_GBDT_CHUNK")) : 0;
-  geo.rch = rch_env >= 1024 ? rch_env : GB_R;
+  geo.rch = GB_R;
   const int rchunks = (n + geo.rch - 1) / geo.rch;
   geo.maxch = rchunks + geo.Lh + 2;
   geo.maxslot = 2 * rchunks + 2;
   geo.lg_n = 0;
   while ((1ll << geo.lg_n) < (long long)n + 1) ++geo.lg_n;
+  if (hconst && GT_HIST_PACK) geo.lg_n = std::max(geo.lg_n, 32);   // |qg| < 2^29 per row (packed counts)
   const int tsz = (2 << D) - 1;
   const size_t per_node = (size_t)F * 2 * GB_BINS;      // int64 per histogram node
   DevParams dp{P[1], P[8], P[9], P[4], P[0], P[3]};

@@ -85,3 +85,41 @@ class RunConfig(object):
 
     def to_json(self):
         return json.dumps(self.to_dict(), sort_keys=True)
+
+
+# Every GENTUN_* environment variable the framework reads, in one place (verdict r4: no A/B switches in
+# the hot path). Performance variants are not switchable by environment any more: rejected variants were
+# deleted (their measurements stay in profiles/), and the few variant pairs tests compare are module
+# constants or native setters the tests call. tests/test_config.py checks that the code reads no other
+# GENTUN_* variable.
+ENV_VARS = {
+    # run configuration (RunConfig.ENV)
+    "GENTUN_SEED": "run seed (GA stream, fold split, keyed weight init / dropout)",
+    "GENTUN_CHECKPOINT_DIR": "per-generation JSON checkpoints",
+    "GENTUN_EVENTS": "JSONL event log path",
+    "GENTUN_COLLECTIVE_TIMEOUT_S": "RCCL / gloo collective timeout",
+    "GENTUN_DTYPE": "CNN compute precision: fp32 (exact split MFMA) or bf16",
+    "GENTUN_LOSS": "bce_compat (reference) or ce",
+    "GENTUN_PAIRING": "RussianRouletteGA pairs: reference or disjoint",
+    "GENTUN_STREAMS": "concurrent population jobs per GPU",
+    "GENTUN_POP_BATCH": "Genetic-CNN candidates sharing each kernel launch",
+    "GENTUN_SCHEDULE": "distributed unit schedule: auto, lpt or dynamic",
+    "GENTUN_DIST_BACKEND": "torch.distributed backend (nccl = RCCL, gloo)",
+    # failure handling (parallel/fault.py)
+    "GENTUN_WATCHDOG": "per-generation deadline first_s[:factor[:min_s]] of a rank",
+    "GENTUN_FAULT": "fault injection rank:generation:{raise,exit,hang} (tests)",
+    "GENTUN_FAULT_ATTEMPT": "inject the fault only in this restart attempt (tests)",
+    # native libraries (ops/_lib.py, tools/build_native.py)
+    "GENTUN_HIP_LIB": "load this kernel library instead of the in-tree one (A/B builds, tools/build_ab.sh)",
+    "GENTUN_GBDT_LIB": "load this GBDT engine library (the sanitizer builds of tests/test_sanitizers.py)",
+    "GENTUN_NO_AUTOBUILD": "1: never rebuild a stale in-tree library on import (GPU boxes, CI)",
+    "GENTUN_HIP_ARCH": "offload architecture of the build (default gfx950)",
+    # GBDT diagnostics (csrc/hip/gbdt_hist.hip)
+    "GENTUN_GBDT_TIMING": "print per-phase device times of a GPU GBDT run",
+    "GENTUN_GBDT_PROGRESS": "print every N boosting rounds",
+    # data / examples
+    "GENTUN_WINE_CSV": "path of winequality-white.csv",
+    "GENTUN_EXAMPLE_SMALL": "1: examples run a CI-sized configuration (tests/test_examples.py)",
+    "GENTUN_DP_RECORD": "tests/test_hip_dp.py appends its measured drifts to this file",
+}
+

@@ -359,12 +359,12 @@ class FoldJob(object):
     # -- driver --------------------------------------------------------------
     def graph_steps(self):
         """Train steps per graph replay: the largest divisor of the epoch's
-        step count up to ``GENTUN_GRAPH_STEPS`` (default 1). One replay of a
+        step count up to ``cfg.graph_steps`` (default 1). One replay of a
         k-step graph is one host launch for k steps, so at small population
         sizes the host no longer paces the GPU (every step reads its batch
         through the device-side step counter, so k consecutive steps capture
         as k copies of the same launches)."""
-        kmax = max(1, int(os.environ.get("GENTUN_GRAPH_STEPS", getattr(self.cfg, "graph_steps", 1) or 1)))
+        kmax = max(1, int(getattr(self.cfg, "graph_steps", 1) or 1))
         n = self.steps_per_epoch
         return max(d for d in range(1, min(kmax, n) + 1) if n % d == 0)
 
@@ -398,13 +398,11 @@ class FoldJob(object):
             self.train_step()
 
     def launch(self):
-        # use_graph None (default): the captured step graph unless GENTUN_GRAPH=0 (eager
+        # use_graph None (default): the captured step graph (cfg.use_graph=False: eager
         # launches, through the native step program: -2..+12 % in a bare population
         # step depending on the box, 2.5 % slower in bench.py on two boxes --
         # profiles/graph_vs_eager_ab_r4.txt)
-        ug = self.cfg.use_graph
-        if ug is None:
-            ug = os.environ.get("GENTUN_GRAPH", "1") != "0"
+        ug = True if self.cfg.use_graph is None else bool(self.cfg.use_graph)
         use_graph = ug and self.device.type == "cuda" and getattr(self, "capture_ok", True)
         ctx = torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
         timed = self.device.type == "cuda"
@@ -479,6 +477,10 @@ class FoldJob(object):
         return self.result
 
 
+# sequential folds of the HIP executor reuse one job (module constant; tests compare both ways)
+FOLD_REUSE = True
+
+
 class SequentialFoldJob(object):
     """The reference's fold protocol (keras_models.py:127-143): the folds of
     the job's candidates train ONE AFTER ANOTHER; fold k+1 re-draws only the
@@ -492,14 +494,14 @@ class SequentialFoldJob(object):
     executor that can rebind (the HIP one) trains every fold on ONE job: the
     buffers, argument tables and captured step graph of fold 0 are reused,
     only the index tables and fold-keyed seeds change, and the biases are
-    carried in place (``GENTUN_FOLD_REUSE=0``: a new job per fold; results are
+    carried in place (``FOLD_REUSE = False``: a new job per fold; results are
     bit-identical either way, tests/test_hip_train.py)."""
 
     def __init__(self, make, nfolds, multi, spec=None):
         self.make = make
         self.nfolds = nfolds
         self.multi = multi
-        self.spec = spec if os.environ.get("GENTUN_FOLD_REUSE", "1") != "0" else None
+        self.spec = spec if FOLD_REUSE else None
         self.jobs = []
         self.phase_ms = None
 
@@ -614,9 +616,8 @@ class TorchFoldJob(FoldJob):
         self.lr = torch.zeros((), device=self.device)
         self.flat.grad = torch.zeros_like(self.flat)
         # MIOpen's algorithm search is not graph-capture safe: the stock-ops
-        # comparator runs eagerly unless explicitly asked to capture.
-        import os
-        self.capture_ok = os.environ.get("GENTUN_TORCH_GRAPH") == "1"
+        # comparator runs eagerly
+        self.capture_ok = False
         self.amp = (self.cfg.dtype == "bf16") and self.device.type == "cuda"
         self.drop_gen = None
         # BatchNorm running statistics per conv: [2 (mean, var)][G][C]

@@ -43,7 +43,6 @@ fold-minor.
 """
 
 import math
-import os
 
 import numpy as np
 import torch
@@ -53,20 +52,19 @@ from ..utils import rng as _rng
 from .cnn_engine import FoldJob
 from .pop_schedule import PopulationSchedule
 
-_SIDE_STREAMS = {}
-
-
-def _side_streams(dev, prio, n, main):
-    """The side streams of every job issued on stream ``main``, created once
-    per process: a stream gets its hardware queue (4 per process) when it is
-    created, so fresh per-job streams from torch's pool can land on the main
-    stream's queue in some jobs and not in others (profiles/stream_cache_ab_r4.txt).
-    GENTUN_STREAM_CACHE=1 (A/B, not yet measured on the GPU; default: fresh streams per job)."""
-    key = (str(dev), prio, n, main.cuda_stream if main is not None else 0)
-    if key not in _SIDE_STREAMS:
-        _SIDE_STREAMS[key] = [torch.cuda.Stream(dev, priority=prio) for _ in range(n)]
-    return _SIDE_STREAMS[key]
-
+# conv weight-gradient streams of a job (the dense W1 optimizer gets one more): the wgrads of
+# different layers are independent (own dz, own partial buffers), so they alternate over these
+# streams and a small launch (few groups: 64 workgroups) does not serialise the backward tail behind
+# one wgrad at a time (profiles/smallq_tiles_wgrad_streams_ab_r4.txt; 3 streams or a shared W1 stream
+# were slower, stream_layout_ab_r4.txt). Module constants, not switches: tests vary them to check that
+# results do not depend on the stream layout / issue path.
+WGRAD_STREAMS = 2
+# K4: fuse the 2x2 max-pool into the epilogue of the conv each group pools (and its backward into the
+# producer of the pool's gradient) wherever a shape-specialised kernel runs the launch
+POOL_FUSE = True
+# eager training issues a whole epoch of steps from C++ (csrc/hip/step_prog.hip) in one host call;
+# False: the Python issue path per step (what a captured step graph records)
+NATIVE_STEPS = True
 
 # bytes of forward-only activation twins an evaluation may allocate for all groups of a job
 EVAL_TWIN_BUDGET = 1 << 30
@@ -135,41 +133,11 @@ class HipPopJob(FoldJob):
         seeds = [_rng.stable_hash(self.member_seeds[self.gmember[q]], "dropout") & 0xFFFFFFFF for q in range(Q)]
         self.drop_seeds_t = torch.tensor(np.asarray(seeds, np.uint32).view(np.int32), device=dev)
         self._keep = []          # device group tables referenced by argument structs
-        # weight-gradient side stream: every conv wgrad and the dense W1
-        # optimizer run concurrently with the data-gradient chain (fork / join
-        # edges inside the captured step graph)
-        # GENTUN_SIDE_PRIO: priority of the side streams (A/B; HIP: lower = higher priority)
-        sprio = int(os.environ.get("GENTUN_SIDE_PRIO", "0"))
-        # the conv wgrads of different layers are independent (own dz, own
-        # partial buffers): round-robin over GENTUN_WGRAD_STREAMS streams so a
-        # small launch (few groups: 64 workgroups) does not serialise the
-        # backward tail behind one wgrad at a time; the dense W1 optimizer (the
-        # largest single launch) on a stream of its own, so it does not sit in
-        # front of the first conv wgrads
-        nws = max(1, int(os.environ.get("GENTUN_WGRAD_STREAMS", "2")))
-        if os.environ.get("GENTUN_STREAM_CACHE", "0") == "1":
-            ss = _side_streams(dev, sprio, nws + 1, getattr(self, "stream", None))
-        else:
-            ss = [torch.cuda.Stream(dev, priority=sprio) for _ in range(nws + 1)]
-        self.side = ss[0]
-        self.wg_streams = list(ss[:nws])
-        self.side2 = ss[nws]
-        # GENTUN_OVERLAP=0: one stream (A/B of the fork / join edges at small launches)
-        self.overlap = os.environ.get("GENTUN_OVERLAP", "1") != "0"
-        self.w1_stream = os.environ.get("GENTUN_W1_STREAM", "1") != "0"
-        # GENTUN_ADAM_OVERLAP=1: each conv layer's optimizer update runs on the
-        # W1 optimizer stream as soon as its wgrad and its last data-gradient op
-        # are done, instead of in one launch after the backward (A/B switch, off:
-        # 7-45 % slower, profiles/adam_overlap_w1stream_ab_r4.txt -- the
-        # two-parent update nodes serialise the captured graph's streams; a
-        # third-stream variant lost 5 %, stream_priority_adam_overlap_ab_r4.txt)
-        self.adam_overlap = os.environ.get("GENTUN_ADAM_OVERLAP", "0") == "1" and self.w1_stream
-        self.adam_split = os.environ.get("GENTUN_ADAM_SPLIT", "0") == "1" and self.w1_stream and not self.adam_overlap
-        if self.dp is not None:
-            self.adam_split = False
-            # X5: every update must see the all-reduced gradient; an in-backward conv
-            # update would run before _dp_allreduce and the ranks would diverge
-            self.adam_overlap = False
+        # side streams: every conv wgrad (alternating over WGRAD_STREAMS) and the dense W1 optimizer run
+        # concurrently with the data-gradient chain (fork / join edges inside the captured step graph)
+        ss = [torch.cuda.Stream(dev) for _ in range(WGRAD_STREAMS + 1)]
+        self.wg_streams = ss[:WGRAD_STREAMS]
+        self.side2 = ss[WGRAD_STREAMS]
         self._build_adam_table()
         self._build_args()
 
@@ -252,8 +220,8 @@ class HipPopJob(FoldJob):
             L.pps, L.S = K.wgrad_split(self.B * L.H * L.W, L.Kdim, L.coutp, band=band)
             # split-K partials summed by a reduce launch right after the layer's wgrad, on the
             # weight-gradient stream (off the data-gradient chain); the optimizer then reads one gradient
-            L.wred = L.S > 1 and (L.coutp * L.Kdim) % 4 == 0 and (
-                os.environ.get("GENTUN_WGRAD_REDUCE", "1") != "0" or self.dp is not None)
+            # (fused into the optimizer instead: 2-3 % slower, profiles/wgrad_reduce_fused_ab_r4.txt)
+            L.wred = L.S > 1 and (L.coutp * L.Kdim) % 4 == 0
         self.last = self.sched.last
         hs, ws = h0 >> len(p0.kernels_per_layer), w0 >> len(p0.kernels_per_layer)
         if hs < 1 or ws < 1:
@@ -376,11 +344,8 @@ class HipPopJob(FoldJob):
                 for o in range(0, p.numel(), 256):
                     blocks.append((idx, o))
 
-        # conv layers: one segment per (layer, group that has the layer); the
-        # layer's blocks are contiguous (L.adam_range) so its update can run as
-        # soon as its wgrad and dgrad are done (train_step)
+        # conv layers: one segment per (layer, group that has the layer)
         for L in self.layers:
-            b0 = len(blocks)
             for q, _ in L.rows:
                 p, m, v = (t[q] for t in L.w)
                 S = 1 if L.wred else L.S            # reduced into split 0 by gt_wgrad_reduce
@@ -392,8 +357,6 @@ class HipPopJob(FoldJob):
                     for t, g in ((L.gamma, L.g_gamma), (L.beta, L.g_beta)):
                         p, m, v = (x[q] for x in t)
                         add(p, m, v, g[q], 1, g[q].numel())
-            L.adam_range = (b0, len(blocks))
-        self.adam_head_range = (len(blocks), None)
         for name, g in (("b1", self.gb1), ("W2", self.gW2), ("b2", self.gb2)):
             p, m, v = self.views[name]
             add(p, m, v, g, 1, g.numel())
@@ -402,7 +365,6 @@ class HipPopJob(FoldJob):
         self.adam_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
         self.adam_blocks = torch.tensor(np.asarray(blocks, np.int32).reshape(-1, 2), device=self.device)
         self.adam_nblocks = len(blocks)
-        self.adam_head_range = (self.adam_head_range[0], len(blocks))
 
     def _dense_sk_buffers(self, df, rows):
         """Range partials and arrival counters of a split-K dense forward at
@@ -509,7 +471,7 @@ class HipPopJob(FoldJob):
         L_ = self.L
         fast_on = L_.gt_conv_set_fast(1)
         L_.gt_conv_set_fast(fast_on)
-        fuse_env = os.environ.get("GENTUN_POOL_FUSE", "1") != "0"
+        fuse_env = POOL_FUSE
         self.pool_fused = []
         for st in self.stages:
             hh, ww, cc = self.shapes[st.inp]
@@ -543,10 +505,8 @@ class HipPopJob(FoldJob):
         df.prec, df.wps = prec, self.w1t.numel()
         # split-K forward straight from the fp32 W1 master (csrc/hip/cnn_dense.hip dense_fwd_sk_kernel);
         # with the streaming data gradient also on the master, nothing reads the transposed copy and
-        # the W1 optimizer stops writing it (GENTUN_DENSE_SK=0: the copy and the streaming forward)
-        self.dense_sk = (os.environ.get("GENTUN_DENSE_SK", "1") != "0" and
-                         os.environ.get("GENTUN_DENSE_STREAM", "1") != "0" and
-                         os.environ.get("GENTUN_DENSE_DGRAD2", "1") != "0" and self.Up % 64 == 0)
+        # the W1 optimizer stops writing it (Up is a multiple of 64 by construction)
+        self.dense_sk = self.Up % 64 == 0
         if self.dense_sk:
             df.w1 = self.views["W1"][0].data_ptr()
             df.ks = int(self.L.gt_dense_fwd_splits(self.Fp))
@@ -599,7 +559,7 @@ class HipPopJob(FoldJob):
         # K4 backward: the gradient of a pool is un-pooled by its producer (the
         # dense data gradient for the last stage, the next stage's input-conv
         # data gradient otherwise) straight into the pool source's gradient
-        fuse_bwd = fast_on and os.environ.get("GENTUN_POOL_FUSE", "1") != "0"
+        fuse_bwd = fast_on and POOL_FUSE
         pool_stage = {st.pool: st for st in self.stages}
         self.unpool_fused = set()
         if fuse_bwd:
@@ -675,32 +635,6 @@ class HipPopJob(FoldJob):
         aa = K.AdamArgs()
         aa.segs, aa.blocks, aa.st = self.adam_segs.data_ptr(), self.adam_blocks.data_ptr(), self.state.data_ptr()
         self.adam_args = aa
-
-        def adam_part(rng):
-            b = K.AdamArgs.from_buffer_copy(aa)
-            b.blocks = self.adam_blocks.data_ptr() + rng[0] * self.adam_blocks.stride(0) * 4
-            return b, rng[1] - rng[0]
-        for L in self.layers:
-            L.adam_part = adam_part(L.adam_range)
-        self.adam_head = adam_part(self.adam_head_range)
-        # index of the last backward op of every layer: its optimizer update
-        # may start once that op (and the layer's wgrad) has run
-        self.bwd_last = {}
-        for i, (kind, a, Lr) in enumerate(self.bwd_ops):
-            if Lr is not None:
-                self.bwd_last[Lr.name] = i
-        # GENTUN_ADAM_SPLIT=1: the last stage's conv updates and the head's run on
-        # side2 once that stage's backward (dgrads, BN backward, wgrads) is done,
-        # the earlier stages' after the join (A/B switch)
-        self.adam_split_at = None
-        last = max(Ly.stage for Ly in self.layers)
-        late = [Ly for Ly in self.layers if Ly.stage == last]
-        b0 = min(Ly.adam_range[0] for Ly in late)
-        if (all((Ly.stage == last) == (Ly.adam_range[0] >= b0) for Ly in self.layers)
-                and all(Ly.name in self.bwd_last for Ly in late)):
-            self.adam_late = adam_part((b0, self.adam_head_range[1]))
-            self.adam_early = adam_part((0, b0))
-            self.adam_split_at = max(self.bwd_last[Ly.name] for Ly in late)
 
     # -------------------------------------------------------------- protocol
     def _build_init_table(self):
@@ -880,8 +814,7 @@ class HipPopJob(FoldJob):
         plan += [("k", "gt_dense_fwd", (self.dense_fwd_args,), main, "dense_fwd"),
                  ("k", "gt_head", (self.head_args,), main, "head"),
                  ("k", "gt_dense_dgrad", (self.dense_dgrad_args,), main, "dense_dgrad")]   # reads W1 before its update
-        side = self.side if self.overlap else main
-        side2 = (self.side2 if self.w1_stream else side) if self.overlap else main
+        side2 = self.side2
         nev = [0]
 
         def edge(src, dst):
@@ -893,23 +826,18 @@ class HipPopJob(FoldJob):
         # W1 gradient + Adam only needs dH and the pooled features: it overlaps
         # the whole conv backward. Each layer's wgrad reads its final dz and its
         # (unchanged) inputs: it overlaps the layer's dgrad and everything after.
+        # (Per-layer conv updates inside the backward, on the W1 stream, were 7-45 % slower:
+        # profiles/adam_overlap_w1stream_ab_r4.txt; the last stage's update on its own: neutral,
+        # adam_split_ab_r4.txt.)
         edge(main, side2)
         plan.append(("k", "gt_dense_wgrad_adam", (self.dense_wgrad_args,), side2, "dense_wgrad_adam"))
-        # per-layer optimizer updates on side2 (off the dgrad chain, behind the
-        # W1 update): layer L's update waits for its wgrad (+ reduce) stream and
-        # for its last main-stream op (the dgrad reading its flipped weights /
-        # its BN backward)
-        ovl = self.overlap and self.adam_overlap
-        split = self.overlap and self.adam_split and self.adam_split_at is not None
-        wgs = self.wg_streams if self.overlap else [side]
-        wg_of = {}
+        wgs = self.wg_streams
         nwg = 0
-        for i, (kind, a, Lr) in enumerate(self.bwd_ops):
+        for kind, a, Lr in self.bwd_ops:
             if kind == "wgrad":
                 ws = wgs[nwg % len(wgs)]
                 nwg += 1
                 edge(main, ws)
-                wg_of[Lr.name] = ws
                 plan.append(("k", "gt_conv_wgrad", (a,), ws, "conv_wgrad"))
                 if Lr.wred:
                     plan.append(("k", "gt_wgrad_reduce", (a,), ws, "wgrad_reduce"))
@@ -919,25 +847,11 @@ class HipPopJob(FoldJob):
                 plan.append(("k", "gt_bn_bwd", (a,), main, "bn_bwd"))
             else:
                 plan.append(("k", "gt_pool_bwd_mask", tuple(a), main, "pool_bwd"))
-            if split and i == self.adam_split_at:
-                edge(main, side2)
-                for ws in wgs[:min(nwg, len(wgs))]:
-                    edge(ws, side2)
-                plan.append(("k", "gt_adam_segments", self.adam_late, side2, "adam"))
-            if ovl and Lr is not None and self.bwd_last.get(Lr.name) == i and Lr.adam_part[1] > 0:
-                edge(main, side2)
-                if wg_of.get(Lr.name) is not None:
-                    edge(wg_of[Lr.name], side2)
-                plan.append(("k", "gt_adam_segments", Lr.adam_part, side2, "adam"))
         for stream in [side2] + list(wgs):
             edge(stream, main)
         return plan
 
     def _adam_plan(self):
-        if self.overlap and self.adam_split and self.adam_split_at is not None:
-            return [("k", "gt_adam_segments", self.adam_early, None, "adam")] if self.adam_early[1] > 0 else []
-        if self.overlap and self.adam_overlap:
-            return [("k", "gt_adam_segments", self.adam_head, None, "adam")]
         return [("k", "gt_adam_segments", (self.adam_args, self.adam_nblocks), None, "adam")]
 
     def _exec_plan(self, plan):
@@ -965,9 +879,9 @@ class HipPopJob(FoldJob):
 
     def train_steps(self, n):
         """``n`` training steps issued eagerly: through the native step program
-        (one host call; GENTUN_NATIVE_STEPS=0 or X5 data parallelism: the
+        (one host call; NATIVE_STEPS False or X5 data parallelism: the
         Python issue path per step)."""
-        if self.dp is None and os.environ.get("GENTUN_NATIVE_STEPS", "1") != "0":
+        if self.dp is None and NATIVE_STEPS:
             prog = getattr(self, "_prog", None)
             if prog is None:
                 prog = self._prog = K.StepProgram(self._step_plan() + self._adam_plan())

@@ -181,12 +181,8 @@ def lib():
         L.gt_conv_set_smallq.restype = I
         L.gt_conv_set_s2in_ct1.argtypes = [I]
         L.gt_conv_set_nwv.restype = I
-        if os.environ.get("GENTUN_CONV_NWV"):
-            L.gt_conv_set_nwv(int(os.environ["GENTUN_CONV_NWV"]))
         L.gt_conv_set_imgs.argtypes = [I]
         L.gt_conv_set_imgs.restype = I
-        if os.environ.get("GENTUN_CONV_IMGS"):
-            L.gt_conv_set_imgs(int(os.environ["GENTUN_CONV_IMGS"]))
         L.gt_glorot_init.argtypes = [C.POINTER(InitArgs), I, P]
         L.gt_glorot_init.restype = I
         L.gt_glorot_ref.argtypes = [C.c_uint64, C.c_uint64, I, C.c_float]
@@ -327,10 +323,8 @@ def wgrad_blocks(kdim, with_bias=True):
     return -(-(kdim + (8 if with_bias else 0)) // 64)
 
 
-WGRAD_TARGET_BLOCKS = int(__import__("os").environ.get("GENTUN_WGRAD_TARGET", "50"))
-WGRAD_FAST_SPLITS = int(__import__("os").environ.get("GENTUN_WGRAD_SPLITS", "0"))   # 0: per-shape default
-WGRAD_SPLITS_BY_WIDTH = {int(k): int(v) for k, v in (kv.split(":") for kv in
-                         __import__("os").environ.get("GENTUN_WGRAD_SPLITS_W", "").split(",") if kv)}
+WGRAD_TARGET_BLOCKS = 50     # generic wgrad: ~workgroups per fold
+WGRAD_FAST_SPLITS = 0        # shape-specialised wgrad splits: 0 = the per-shape default (tests override it)
 
 
 def wgrad_band(KH, KW, cinp, coutp, H, W, prec=0):
@@ -342,8 +336,6 @@ def wgrad_band(KH, KW, cinp, coutp, H, W, prec=0):
         return 0, 0
     band = int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W, prec))
     splits = int(L.gt_wgrad_fast_splits(KH, KW, cinp, coutp, H, W, prec)) if band else 0
-    if band and W in WGRAD_SPLITS_BY_WIDTH:
-        splits = WGRAD_SPLITS_BY_WIDTH[W]      # tuning override (GENTUN_WGRAD_SPLITS_W="16:8,32:16")
     return band, splits
 
 

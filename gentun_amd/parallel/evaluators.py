@@ -74,10 +74,8 @@ class LocalBatchEvaluator(SequentialEvaluator):
 
     def __init__(self, device=None, streams=2, cache=False, event_log=None, pop_batch=16, torch_pop=None):
         super(LocalBatchEvaluator, self).__init__(cache=cache, event_log=event_log)
-        # population-batch the torch executor too (TorchPopJob, comparator (a)): off unless
-        # GENTUN_TORCH_POP=1 (or torch_pop=True); otherwise the torch oracle trains one candidate per job
-        if torch_pop is None:
-            torch_pop = os.environ.get("GENTUN_TORCH_POP", "0") == "1"
+        # population-batch the torch executor too (torch_pop=True: TorchPopJob, comparator (a));
+        # otherwise the torch oracle trains one candidate per job
         self.torch_pop = bool(torch_pop)
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() \

@@ -43,11 +43,18 @@ def test_example_runs_small(script, expect):
         assert expect in r.stdout, r.stdout[-2000:]
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def test_distributed_cnn_example_gloo():
     """torchrun with 2 ranks on gloo: the Genetic-CNN master/worker pair."""
     env = dict(os.environ, **SMALL)
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29519",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                         os.path.join(ROOT, "examples", "distributed_cnn.py")],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -58,7 +65,7 @@ def test_distributed_xgb_example_gloo():
     """torchrun with 2 ranks on gloo: rank 0 runs the GA, rank 1 is a worker."""
     env = dict(os.environ, GENTUN_EXAMPLE_SMALL="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29517",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                         os.path.join(ROOT, "examples", "distributed_xgb.py")],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]

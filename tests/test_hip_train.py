@@ -153,8 +153,9 @@ def test_fused_pool_matches_separate_pool_kernel(dtype, bn, monkeypatch):
     cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-3,), batch_size=32, dtype=dtype, reset="all", use_graph=False,
                         batch_norm=bn)
     out = {}
+    from gentun_amd.models import cnn_hip
     for fuse in ("1", "0"):
-        monkeypatch.setenv("GENTUN_POOL_FUSE", fuse)
+        monkeypatch.setattr(cnn_hip, "POOL_FUSE", fuse == "1")
         job = HipPopJob(None, x, y, None, cfg, torch.device("cuda", 0), members=members)
         assert all(job.pool_fused) == (fuse == "1"), job.pool_fused
         # backward: every stage's pool gradient un-pooled by its producer
@@ -193,7 +194,7 @@ def test_sequential_folds_job_reuse_bit_identical(dtype, bn, monkeypatch):
                         batch_norm=bn)
     out = {}
     for reuse in ("1", "0"):
-        monkeypatch.setenv("GENTUN_FOLD_REUSE", reuse)
+        monkeypatch.setattr(E, "FOLD_REUSE", reuse == "1")
         job = E.make_population_job("hip", [(p, folds, [0, 1, 2]) for p in plans], x, y, cfg,
                                     torch.device("cuda", 0))
         out[reuse] = job.launch().finish()
@@ -211,6 +212,7 @@ def test_small_launch_tiles_bit_identical(bn, monkeypatch):
     order; the wgrads of different layers are independent)."""
     import numpy as np
     from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models import cnn_hip
     from gentun_amd.models.cnn_hip import HipPopJob
     from gentun_amd.models.genome import make_plan
     from gentun_amd.ops import cnn_kernels as Km
@@ -227,7 +229,7 @@ def test_small_launch_tiles_bit_identical(bn, monkeypatch):
     try:
         for small in (1, 0):
             lib.gt_conv_set_smallq(small)
-            monkeypatch.setenv("GENTUN_WGRAD_STREAMS", "3" if small else "1")
+            monkeypatch.setattr(cnn_hip, "WGRAD_STREAMS", 3 if small else 1)
             job = HipPopJob(None, x, y, None, cfg, torch.device("cuda", 0), members=members)
             job.init_params()
             job.reset_optimizer(1e-3)
@@ -258,11 +260,12 @@ def test_native_step_program_bit_identical(bn, monkeypatch):
     folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
     genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '111', 'S_2': '1000000001'}]
     plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
-    cfg = E.TrainConfig(epochs=(1, 1), learning_rate=(1e-3, 5e-4), batch_size=32, dtype="fp32", batch_norm=bn)
+    from gentun_amd.models import cnn_hip
     out = {}
     for mode in ("native", "python", "graph"):
-        monkeypatch.setenv("GENTUN_GRAPH", "1" if mode == "graph" else "0")
-        monkeypatch.setenv("GENTUN_NATIVE_STEPS", "1" if mode == "native" else "0")
+        cfg = E.TrainConfig(epochs=(1, 1), learning_rate=(1e-3, 5e-4), batch_size=32, dtype="fp32", batch_norm=bn,
+                            use_graph=mode == "graph")
+        monkeypatch.setattr(cnn_hip, "NATIVE_STEPS", mode == "native")
         job = E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg,
                                     torch.device("cuda", 0))
         out[mode] = job.launch().finish()
@@ -270,34 +273,6 @@ def test_native_step_program_bit_identical(bn, monkeypatch):
             assert all(getattr(j, "_prog", None) is not None for j in job.jobs)
     assert out["native"] == out["python"]
     assert out["native"] == out["graph"]
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("bn", [False, True])
-@pytest.mark.parametrize("switch", ["GENTUN_ADAM_OVERLAP", "GENTUN_ADAM_SPLIT"])
-def test_per_layer_adam_overlap_bit_identical(bn, switch, monkeypatch):
-    """GENTUN_ADAM_OVERLAP=1 runs each conv layer's optimizer update on the W1
-    optimizer stream inside the backward (after its wgrad and its last
-    data-gradient op); GENTUN_ADAM_SPLIT=1 updates the last stage and the head
-    there once that stage's backward is done. Both give the results of the one
-    update launch after the backward (captured step graph of a population job)."""
-    import numpy as np
-    from gentun_amd.models import cnn_engine as E
-    from gentun_amd.models.genome import make_plan
-    from gentun_amd.utils.data import make_cifar_like, stratified_kfold
-    x, y = make_cifar_like(n=400, seed=3)
-    folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)
-    genes = [{'S_1': '101', 'S_2': '0101110011'}, {'S_1': '111', 'S_2': '0000000001'}]
-    plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10) for g in genes]
-    cfg = E.TrainConfig(epochs=(1, 1), learning_rate=(1e-3, 5e-4), batch_size=32, dtype="fp32", reset="all",
-                        batch_norm=bn)
-    out = {}
-    for ovl in ("1", "0"):
-        monkeypatch.setenv(switch, ovl)
-        job = E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg,
-                                    torch.device("cuda", 0))
-        out[ovl] = job.launch().finish()
-    assert out["1"] == out["0"]
 
 
 @pytest.mark.gpu
