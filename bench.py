@@ -112,9 +112,7 @@ def main():
 def _teardown(comm):
     """Every rank leaves the RCCL / gloo group explicitly (after the STOP
     broadcast): no communicator is left for interpreter shutdown to tear down."""
-    if hasattr(comm, "destroy"):
-        comm.barrier()
-        comm.destroy()
+    comm.finish()
 
 
 def run(args):

@@ -59,12 +59,24 @@
 #include "gbdt_cache.h"
 
 #define GB_BINS 256
-#define HB_F 16          // features per histogram workgroup
+// features per histogram workgroup: gradient-only packed image (constant hessian) / (g, h) pairs
+#ifndef HB_FC
+#define HB_FC 32
+#endif
+#define HB_FG 16
 #define HB_STRIDE 514    // int64 per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
+#ifndef HB_T
 #define HB_T 512
-#define HB_U 4
-#define GB_R 65536       // rows per histogram chunk: 4x fewer partial slots to reduce than 16K (reduce 231 -> 144 us
-                         // per call at 1M x 256, depth 10; same tree time: profiles/gbdt_chunk_ab_r3.txt)
+#endif
+#ifndef HB_U
+#define HB_U 8           // rows in flight per thread
+#endif
+// rows per histogram chunk. 16K since round 5: with the reduce grid bounded by the nodes that can have
+// partial slots, more chunks (= more histogram workgroups at the shallow levels) won: depth-6 level time
+// -7.5 %, depth 10 even (r5/gbdt_chunk_ab_r5.txt; 64K had been chosen in round 3 against the old reduce)
+#ifndef GB_R
+#define GB_R 16384
+#endif
 #define GB_MAXD 12       // deepest supported tree
 
 namespace {
@@ -300,6 +312,7 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __re
   // same rows (row ids, gradients, and 16-byte slices of the same 256-byte bin rows), so all but the
   // first of them hit that XCD's L2 instead of each XCD fetching every line from HBM (round-4 PMC:
   // 24 % L2 hits, the kernel waited on memory half of its cycles)
+  constexpr int NF = HC ? HB_FC : HB_FG;
   int cx = blockIdx.x, cy = blockIdx.y, cz = blockIdx.z;
   {
     const int gx = gridDim.x, gy = gridDim.y;
@@ -316,20 +329,21 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __re
   }
   const int k = cz;
   if (cx >= counts[2 * k]) return;
-  constexpr int LHN = HC ? HB_F * HB_GSTRIDE : HB_F * HB_STRIDE;
+  constexpr int LHN = HC ? NF * HB_GSTRIDE : NF * HB_STRIDE;
   __shared__ u64 lh[LHN];
   constexpr bool PK = HC && GT_HIST_PACK;
-  __shared__ unsigned int lc[HC && !PK ? HB_F * GB_BINS : 1];
+  __shared__ unsigned int lc[HC && !PK ? NF * GB_BINS : 1];
   const Chunk c = chunks[(size_t)k * geo.maxch + cx];
   const int F = geo.F, Fs = geo.Fs;
-  const int fb = cy * HB_F, tid = threadIdx.x;
-  constexpr int RL = HB_T / 4;                  // row lanes
+  const int fb = cy * NF, tid = threadIdx.x;
+  constexpr int LPR = NF / 4;                 // lanes per row (4 features each)
+  constexpr int RL = HB_T / LPR;                // row lanes
   for (int i = tid; i < LHN; i += HB_T) lh[i] = 0ull;
   if (HC && !PK)
-    for (int i = tid; i < HB_F * GB_BINS; i += HB_T) lc[i] = 0u;
+    for (int i = tid; i < NF * GB_BINS; i += HB_T) lc[i] = 0u;
   const float sg = ldexpf(1.f, fx_exp(mx[2 * k], geo.lg_n)), sh = ldexpf(1.f, fx_exp(mx[2 * k + 1], geo.lg_n));
   __syncthreads();
-  const int wl = tid & 3, rl = tid >> 2;
+  const int wl = tid % LPR, rl = tid / LPR;
   const int f4 = fb + wl * 4;
   const float2* gk = gh + (size_t)k * geo.n;
   auto add = [&](uint32_t w, u64 qg, u64 qh) {
@@ -383,7 +397,7 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __re
   }
   __syncthreads();
   // exact integer sums: in place for a one-chunk node, else partial slot c.slot
-  const int nf = min(HB_F, F - fb);
+  const int nf = min(NF, F - fb);
   i64* dst = c.slot < 0 ? hist + (((size_t)k * geo.Lh + c.node) * F + fb) * 2 * GB_BINS
                         : part + (((size_t)k * geo.maxslot + c.slot) * F + fb) * 2 * GB_BINS;
   const i64 qh1 = (i64)llrintf(1.0f * sh);     // every row's hessian (h = 1) in fixed point
@@ -461,7 +475,10 @@ __device__ __forceinline__ bool later_wins(double g_early, bool early_ok, double
 // ---- G4: best split per (node, feature): one wave each (grid F x L x folds) --
 // order[(k * (D+1) + depth) * F + f] = position of f in the level's feature
 // scan (colsample_bytree / _bylevel), 0 = not sampled
+// prev != null (the last histogram level): the histograms of the non-built nodes were not materialised
+// (no later level subtracts from them) -- read as parent (prev) - built sibling, the same exact integers
 __global__ void __launch_bounds__(64) split_kernel(Geo geo, int depth, const i64* __restrict__ hist,
+                                                   const i64* __restrict__ prev,
                                                    const int* __restrict__ nbins, const int* __restrict__ order,
                                                    const LNode* __restrict__ cur, const unsigned int* __restrict__ mx,
                                                    SplitOut* __restrict__ out, DevParams p) {
@@ -473,10 +490,27 @@ __global__ void __launch_bounds__(64) split_kernel(Geo geo, int depth, const i64
   i64 bGL = 0, bHL = 0;
   if (nd.exists && nd.count >= 2 && ord >= 0) {
     const double ig = ldexp(1.0, -fx_exp(mx[2 * k], geo.lg_n)), ih = ldexp(1.0, -fx_exp(mx[2 * k + 1], geo.lg_n));
-    const i64* h = hist + (((size_t)k * geo.Lh + j) * F + f) * 2 * GB_BINS;
+    const bool virt = prev != nullptr && !nd.built;
+    const i64* h = hist + (((size_t)k * geo.Lh + (virt ? (j ^ 1) : j)) * F + f) * 2 * GB_BINS;
+    const i64* hp = virt ? prev + (((size_t)k * geo.Lh + nd.parent) * F + f) * 2 * GB_BINS : nullptr;
     i64 vg[4], vh[4], sg = 0, sh = 0;
+    {
+      const longlong2* h2 = reinterpret_cast<const longlong2*>(h) + lane * 4;
+      longlong2 v[4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) { vg[q] = h[2 * (lane * 4 + q)]; vh[q] = h[2 * (lane * 4 + q) + 1]; sg += vg[q]; sh += vh[q]; }
+      for (int q = 0; q < 4; ++q) v[q] = h2[q];
+      if (virt) {
+        const longlong2* p2 = reinterpret_cast<const longlong2*>(hp) + lane * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const longlong2 pv = p2[q];
+          v[q].x = pv.x - v[q].x;
+          v[q].y = pv.y - v[q].y;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { vg[q] = v[q].x; vh[q] = v[q].y; sg += vg[q]; sh += vh[q]; }
+    }
     i64 pg = sg, ph = sh;                       // inclusive scan across lanes (exact)
     for (int o = 1; o < 64; o <<= 1) {
       const i64 tg = __shfl_up(pg, o), th = __shfl_up(ph, o);
@@ -744,18 +778,61 @@ __global__ void __launch_bounds__(256) plan_next_kernel(Geo geo, int depth, cons
 }
 
 // ---- G6: prediction update by tree traversal (all rows of every fold) ------
-__global__ void predict_kernel(Geo geo, const uint8_t* __restrict__ bins, const int2* __restrict__ tree,
-                               const float* __restrict__ leaf, float* __restrict__ margin, int c) {
-  const int k = blockIdx.y, tsz = (2 << geo.max_depth) - 1;
-  const int2* tk = tree + (size_t)k * tsz;
-  const float* lk = leaf + (size_t)k * tsz;
-  float* mk = margin + (size_t)k * geo.n * geo.K;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < geo.n; i += gridDim.x * blockDim.x) {
-    const uint8_t* row = bins + (size_t)i * geo.Fs;
+// A workgroup stages R consecutive bin rows in LDS (coalesced 4-byte loads, row stride Fs + 4 bytes:
+// the lookups of R threads at one feature fall on distinct banks) and the trees of nk folds (split
+// table + leaf values, 2^(D+1) - 1 nodes each); each staged row is then walked through every staged
+// fold's tree from LDS. A row's bins leave HBM once per round for all folds, and the D dependent
+// lookups per row and tree are LDS reads: the walk with the tree in global memory and one byte load
+// per lookup moved a 128-byte line from L2 per lookup (0.65 ms per round at 1M rows x 5 folds,
+// depth 10). R = 0 (rows wider than the LDS budget): lookups straight from global memory.
+__global__ void __launch_bounds__(256) predict_kernel(Geo geo, const uint8_t* __restrict__ bins,
+                                                      const int2* __restrict__ tree, const float* __restrict__ leaf,
+                                                      float* __restrict__ margin, int c, int nk, int R) {
+  extern __shared__ uint32_t psm[];
+  const int k0 = blockIdx.y * nk, tsz = (2 << geo.max_depth) - 1, tid = threadIdx.x;
+  const int Fs = geo.Fs, rs = Fs / 4 + 1;           // LDS row stride in dwords
+  nk = min(nk, geo.nfold - k0);
+  uint32_t* prow = psm;
+  int2* ptree = reinterpret_cast<int2*>(psm + (size_t)R * rs + ((R * rs) & 1));
+  float* pleaf = reinterpret_cast<float*>(ptree + (size_t)nk * tsz);
+  for (int i = tid; i < nk * tsz; i += 256) {
+    ptree[i] = tree[(size_t)k0 * tsz + i];
+    pleaf[i] = leaf[(size_t)k0 * tsz + i];
+  }
+  auto walk = [&](const uint8_t* row, int rstride, int kk) {   // leaf of one row in fold k0 + kk's tree
+    const int2* tk = ptree + (size_t)kk * tsz;
     int id = 0;
     int2 t = tk[0];
-    while (t.x >= 0) { id = (row[t.x] <= t.y) ? 2 * id + 1 : 2 * id + 2; t = tk[id]; }
-    mk[(size_t)i * geo.K + c] += lk[id];
+    while (t.x >= 0) {
+      id = (row[(size_t)t.x * rstride] <= t.y) ? 2 * id + 1 : 2 * id + 2;
+      t = tk[id];
+    }
+    return pleaf[(size_t)kk * tsz + id];
+  };
+  if (R == 0) {
+    __syncthreads();
+    for (int i = blockIdx.x * 256 + tid; i < geo.n; i += gridDim.x * 256)
+      for (int kk = 0; kk < nk; ++kk)
+        margin[((size_t)(k0 + kk) * geo.n + i) * geo.K + c] += walk(bins + (size_t)i * Fs, 1, kk);
+    return;
+  }
+  const int tpr = 256 / R;                           // threads per row (folds split among them)
+  const int fd = Fs / 4;
+  for (long i0 = (long)blockIdx.x * R; i0 < geo.n; i0 += (long)gridDim.x * R) {
+    __syncthreads();                                 // the previous rows (and, first, the trees) are ready
+    const int rows = (int)min((long)R, geo.n - i0);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(bins + (size_t)i0 * Fs);
+    for (int v = tid; v < rows * fd; v += 256) {
+      const int r = v / fd;
+      prow[r * rs + (v - r * fd)] = src[v];
+    }
+    __syncthreads();
+    const int r = tid % R;
+    if (r < rows) {
+      const uint8_t* row = reinterpret_cast<const uint8_t*>(prow + r * rs);
+      for (int kk = tid / R; kk < nk; kk += tpr)
+        margin[((size_t)(k0 + kk) * geo.n + i0 + r) * geo.K + c] += walk(row, 1, kk);
+    }
   }
 }
 
@@ -876,7 +953,18 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   const int blocks = std::min(2048, (n + 255) / 256);
   const int pblocks = (n + 256 * PT_PER - 1) / (256 * PT_PER);
   const int mblocks = std::min(blocks, 256);
-  const int nfb = (F + HB_F - 1) / HB_F;
+  // predict: R staged rows (a power of two, 32 KB of LDS) + as many folds' trees as fit 96 KB more
+  int pr_rows = 0;
+  if (Fs + 4 <= 32768 / 4) {
+    pr_rows = 256;
+    while (pr_rows > 4 && (size_t)pr_rows * (Fs + 4) > 32768) pr_rows >>= 1;
+  }
+  const int pk = (int)std::max<size_t>(1, std::min<size_t>(nfold, (96u << 10) / ((size_t)tsz * 12)));
+  const size_t pred_lds = (size_t)pr_rows * (Fs + 4) + 8 + (size_t)pk * tsz * 12;
+  if (pred_lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(predict_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)pred_lds);
+  const int nfb = hconst ? (F + HB_FC - 1) / HB_FC : (F + HB_FG - 1) / HB_FG;
   const int ylen = std::max(1, (int)(per_node / 4096));
   const int rlen = std::max(1, (int)(per_node / 512));       // reduce: 2 elements per thread, ~256 workgroups per node
   // device buffers
@@ -1031,17 +1119,21 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
           else
             hipLaunchKernelGGL(hist_kernel<false>, dim3(geo.maxch, nfb, nfold), dim3(HB_T), 0, 0, geo, d_bins,
                                d_rows[d & 1], d_gh, d_chunks, d_counts, hcur, d_part, d_mx);
-          hipLaunchKernelGGL(reduce_kernel, dim3(geo.maxch, rlen, nfold), dim3(256), 0, 0, geo, d_part, hcur, d_reds,
-                             d_counts);
-          if (d > 0)
+          // a reduced node has more than rch rows: at most n / (rch + 1) of them per fold
+          hipLaunchKernelGGL(reduce_kernel, dim3(std::max(1, n / (geo.rch + 1)), rlen, nfold), dim3(256), 0, 0, geo,
+                             d_part, hcur, d_reds, d_counts);
+          // siblings = parent - built child, materialised only where a later level subtracts from them
+          // (the last histogram level's split reads them as the difference)
+          if (d == 0)
+            hipLaunchKernelGGL(root_totals_kernel, dim3(nfold), dim3(64), 0, 0, geo, hcur, cur);
+          else if (d + 1 < D)
             hipLaunchKernelGGL(subtract_kernel, dim3(L, ylen, nfold), dim3(256), 0, 0, geo, cur, d_hist[(d - 1) & 1],
                                hcur);
-          else
-            hipLaunchKernelGGL(root_totals_kernel, dim3(nfold), dim3(64), 0, 0, geo, hcur, cur);
         }
         if (d < D) {
-          hipLaunchKernelGGL(split_kernel, dim3(F, L, nfold), dim3(64), 0, 0, geo, d, hcur, d_nb, order_c, cur, d_mx,
-                             d_cand, dp);
+          hipLaunchKernelGGL(split_kernel, dim3(F, L, nfold), dim3(64), 0, 0, geo, d, hcur,
+                             (d > 0 && d + 1 == D) ? d_hist[(d - 1) & 1] : nullptr, d_nb, order_c, cur, d_mx, d_cand,
+                             dp);
           hipLaunchKernelGGL(best_kernel, dim3(L, nfold), dim3(256), 0, 0, geo, d_cand, d_best);
         }
         hipLaunchKernelGGL(plan_split_kernel, dim3(nfold), dim3(256), 0, 0, geo, d, cur, d_best, d_mx, d_tree, d_leaf,
@@ -1053,8 +1145,8 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
                              d_chunks, d_reds, d_counts);
         }
       }
-      hipLaunchKernelGGL(predict_kernel, dim3(blocks, nfold), dim3(256), 0, 0, geo, d_bins, d_tree, d_leaf, d_margin,
-                         c);
+      hipLaunchKernelGGL(predict_kernel, dim3(std::min(blocks, 512), (nfold + pk - 1) / pk), dim3(256), pred_lds, 0,
+                         geo, d_bins, d_tree, d_leaf, d_margin, c, pk, pr_rows);
     }
     for (int mi = 0; mi < n_metrics; ++mi)
       hipLaunchKernelGGL(metric_kernel, dim3(mblocks, nfold), dim3(256), 0, 0, geo, d_margin, d_y, d_fold,

@@ -33,3 +33,4 @@ if __name__ == "__main__":
         pop.shutdown()
     else:
         GentunWorker(GeneticCnnIndividual, x_train, y_train, comm=comm, evaluator=evaluator).work()
+    comm.finish()

@@ -30,3 +30,4 @@ if __name__ == "__main__":
         gw = GentunWorker(XgboostIndividual, x_train, y_train, host='localhost', user='guest', password='guest',
                           comm=comm)
         gw.work()
+    comm.finish()

@@ -98,6 +98,7 @@ def _run_search(args, species, x, y, extra, maximize):
     evaluator = LocalBatchEvaluator(device=device, streams=cfg.streams, pop_batch=cfg.pop_batch)
     if comm.rank != 0:
         GentunWorker(species, x, y, comm=comm, evaluator=evaluator).work()
+        comm.finish()
         return None
     roulette = args.algorithm == "roulette"
     cls = RussianRouletteGA if roulette else GeneticAlgorithm
@@ -130,10 +131,12 @@ def _run_search(args, species, x, y, extra, maximize):
         # error) propagates: a non-zero exit the supervisor restarts from the last checkpoint.
         try:
             ga.population.shutdown()
+            comm.finish()
         finally:
             sys.stderr.write("[gentun] search failed; evaluators released\n")
         raise SearchFailed()
     ga.population.shutdown()
+    comm.finish()
     out = {"best_fitness": best.get_fitness(), "best_genes": best.get_genes(),
            "history": [{k: h[k] for k in ("generation", "best_fitness", "evals", "wall_s", "candidates_per_hour")}
                        for h in ga.history]}

@@ -52,6 +52,22 @@ ADAM_B1, ADAM_B2, ADAM_EPS = 0.9, 0.999, 1e-7
 CLIP_EPS = 1e-7
 
 
+
+def check_hw_queues(nstreams, env=None):
+    """Refuse to capture a step graph over more streams than the process has hardware queues.
+
+    With ``GPU_MAX_HW_QUEUES=3`` the replay of a graph captured over 4 streams segfaults inside
+    HIP's graph launch -- reproduced with torch alone (tools/probe_hwq.py: 1 and 2 side streams
+    replay, 3 crash; profiles/r5/hwq3_graph_crash_r5.log), so it is the runtime's, not this
+    engine's; the population step graph forks onto 1 + WGRAD_STREAMS side streams. A clear error
+    instead of the crash (verdict r4 item 6a)."""
+    v = (os.environ if env is None else env).get("GPU_MAX_HW_QUEUES", "")
+    if v.strip().isdigit() and int(v) < nstreams:
+        raise RuntimeError(
+            "GPU_MAX_HW_QUEUES={} is below the {} streams of the captured step graph: HIP's graph launch "
+            "segfaults there (torch-only repro: tools/probe_hwq.py). Use GPU_MAX_HW_QUEUES >= {} (HIP's "
+            "default is 4) or eager steps (TrainConfig use_graph=False)".format(int(v), nstreams, nstreams))
+
 class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
                  dtype="fp32", seed=0, use_graph=None, eval_batch=1000, optimizer="adam", momentum=0.9,
@@ -369,6 +385,7 @@ class FoldJob(object):
         return max(d for d in range(1, min(kmax, n) + 1) if n % d == 0)
 
     def _capture(self):
+        check_hw_queues(getattr(self, "graph_streams", 1))
         snap = self.snapshot()
         # warm-up steps read the (still all-zero, i.e. valid) batch table; the
         # shuffle streams are NOT advanced so graph and eager runs are identical

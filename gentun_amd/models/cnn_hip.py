@@ -138,6 +138,7 @@ class HipPopJob(FoldJob):
         ss = [torch.cuda.Stream(dev) for _ in range(WGRAD_STREAMS + 1)]
         self.wg_streams = ss[:WGRAD_STREAMS]
         self.side2 = ss[WGRAD_STREAMS]
+        self.graph_streams = 2 + WGRAD_STREAMS     # capture stream + wgrad streams + W1 stream
         self._build_adam_table()
         self._build_args()
 

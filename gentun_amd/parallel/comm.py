@@ -47,6 +47,13 @@ class Communicator(object):
     def barrier(self):
         raise NotImplementedError
 
+    def finish(self):
+        """End of a job, on EVERY rank (after ``shutdown()`` on rank 0 and ``work()`` returning on the
+        others): leave the process group together, so no communicator is left for interpreter
+        shutdown to tear down (a gloo group destroyed there, with its store's client threads still
+        running, aborted a rank with ``terminate called without an active exception``). Idempotent."""
+        return None
+
     def ticket(self, key):
         """Atomic fetch-and-increment of a job-wide counter named ``key``
         (0, 1, 2, ... across all ranks): the work-stealing queue of dynamic
@@ -253,6 +260,12 @@ class DistComm(Communicator):
     def destroy(self):
         if self.dist.is_initialized():
             self.dist.destroy_process_group()
+
+    def finish(self):
+        if self.dist.is_initialized():
+            self.barrier()
+            self.dist.destroy_process_group()
+        self.store = None
 
 
 class _ThreadHub(object):

@@ -91,3 +91,15 @@ def test_every_env_variable_is_registered():
         found |= set(pat.findall((root / f).read_text()))
     assert set(RunConfig.ENV) <= set(ENV_VARS)
     assert found <= set(ENV_VARS), sorted(found - set(ENV_VARS))
+
+
+def test_graph_capture_refuses_fewer_hw_queues_than_streams():
+    """GPU_MAX_HW_QUEUES below the captured step graph's stream count segfaults in HIP's graph
+    launch (torch-only repro, tools/probe_hwq.py): the engine raises a clear error instead."""
+    import pytest
+    from gentun_amd.models import cnn_engine, cnn_hip
+    n = 2 + cnn_hip.WGRAD_STREAMS
+    with pytest.raises(RuntimeError, match="GPU_MAX_HW_QUEUES=3"):
+        cnn_engine.check_hw_queues(n, env={"GPU_MAX_HW_QUEUES": "3"})
+    cnn_engine.check_hw_queues(n, env={"GPU_MAX_HW_QUEUES": "4"})
+    cnn_engine.check_hw_queues(n, env={})

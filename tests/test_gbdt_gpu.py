@@ -43,10 +43,12 @@ def test_hip_binary_logistic_and_early_stopping():
     assert gpu['test-logloss-mean'][-1] == min(gpu['test-logloss-mean'])
 
 
-@pytest.mark.parametrize("f,depth", [(10, 9), (7, 1), (33, 6)])
+@pytest.mark.parametrize("f,depth", [(10, 9), (7, 1), (33, 6), (5, 2), (9, 12)])
 def test_hip_deep_trees_odd_feature_counts(f, depth):
-    """Row-segment partition + subtraction over many levels, feature counts
-    that are not multiples of the 4-byte row word / 32-feature block."""
+    """Row-segment partition + subtraction over many levels (the last histogram
+    level reads its siblings as parent - built child), feature counts that are
+    not multiples of the 4-byte row word / 32-feature block; depth 12 = the
+    deepest supported tree (its 8191-node predict table needs > 64 KB of LDS)."""
     x, y = make_regression(n=30000, f=f, seed=7)
     p = {'objective': 'reg:linear', 'eta': 0.3, 'max_depth': depth, 'min_child_weight': 0}
     cpu = gbdt.cv(p, x, y, num_boost_round=15, nfold=3, seed=1)
