@@ -30,15 +30,10 @@
 #define ADAM_B2 0.999f
 #define ADAM_EPS 1e-7f
 #define CLIP_EPS 1e-7f
-#ifndef GT_DGRAD_BUF
 #define GT_DGRAD_BUF 2     // dense_dgrad_stream2_kernel: k-steps in flight per wave (4: 3 % slower, profiles/dense_dgrad_buf_ab_r4.txt)
-#endif
-#ifndef GT_ADAM_UNROLL
 #define GT_ADAM_UNROLL 1   // adam_segments_kernel tiled path: elements per thread whose loads issue together (4: neutral, profiles/adam_unroll_ab_r4.txt)
-#endif
-#ifndef GT_WADAM_HOIST
-#define GT_WADAM_HOIST 0   // dense_wgrad_adam_kernel: 1 = optimizer-state loads hoisted above the row branches (A/B build)
-#endif
+// (dense_wgrad_adam_kernel with the optimizer-state loads hoisted above the row branches was 1.67x slower:
+// profiles/dense_wadam_hoist_ab_r3.txt; removed)
 
 __global__ void step_begin_kernel(StepState* s) {
   s->cur_step = s->step_ctr;
@@ -1016,47 +1011,6 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
       }
       continue;
     }
-#if GT_WADAM_HOIST
-    // all 24 optimizer-state loads issue before the first update: a branch around each row's loads made the
-    // compiler wait for them row by row (8 dependent HBM round trips per thread). Rows past Fp or on padded
-    // channels load row f0 (always real) and discard it.
-    float4 pp[8], mm[8], vv[8];
-    bool ok[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int f = f0 + fr + 2 * r;
-      ok[r] = f < a.Fp && !(a.Cp > 0 && f % a.Cp >= a.Cr);
-      const long off = ((long)g * a.Fp + (ok[r] ? f : f0)) * a.Up + u0;
-      pp[r] = *reinterpret_cast<const float4*>(a.p + off);
-      mm[r] = *reinterpret_cast<const float4*>(a.m + off);
-      vv[r] = *reinterpret_cast<const float4*>(a.v + off);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int f = f0 + fr + 2 * r;
-      if (f >= a.Fp) continue;
-      if (!ok[r]) {                            // padded channel: weights stay 0, only the copy tile
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (cp) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
-        continue;
-      }
-      const long off = ((long)g * a.Fp + f) * a.Up + u0;
-      float* P = &pp[r].x; float* M = &mm[r].x; float* V = &vv[r].x;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        P[i] = opt_update(a.st, P[i], acc[r][i], M[i], V[i], lr_t);
-        if (cp) {
-          if constexpr (PREC != 0) tt[(u0 + i) * 16 + fr + 2 * r] = P[i];
-          else tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
-        }
-      }
-      *reinterpret_cast<float4*>(a.p + off) = pp[r];
-      *reinterpret_cast<float4*>(a.m + off) = mm[r];
-      *reinterpret_cast<float4*>(a.v + off) = vv[r];
-    }
-#else
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int f = f0 + fr + 2 * r;
@@ -1084,7 +1038,6 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
       *reinterpret_cast<float4*>(a.m + off) = mm;
       *reinterpret_cast<float4*>(a.v + off) = vv;
     }
-#endif
   }
   // (uniform) no update, or no transposed copy: every W1 reader takes the master (split-K dense_fwd,
   // streaming dense_dgrad)

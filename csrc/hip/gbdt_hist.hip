@@ -10,12 +10,14 @@
 // Device-resident level loop: the level structure of a depth-D tree is static
 // (level d has at most 2^d nodes, heap-indexed), so every grid is a host-known
 // upper bound and the device decides which nodes exist. Per level:
-//   hist      : histograms of the "built" nodes (the root; then the smaller
+//   hist      : (XCD-grouped workgroups) histograms of the "built" nodes (the root; then the smaller
 //               child of every split) over their row segments, chunk lists
 //               written by the previous level's plan kernel (blocks past the
 //               fold's chunk count exit at once);
 //   reduce    : multi-chunk nodes: exact sum of their partial slots;
-//   subtract  : the sibling of every built node = parent - built (exact);
+//   subtract  : the sibling of every built node = parent - built (exact; on the
+//               last histogram level the split search reads the difference
+//               directly instead);
 //   split     : one wave per (node, feature): 256-bin prefix scan, xgboost's
 //               CalcGain (lambda, alpha L1 soft threshold, max_delta_step,
 //               min_child_weight) in fp64; best: per-node argmax;
@@ -60,23 +62,15 @@
 
 #define GB_BINS 256
 // features per histogram workgroup: gradient-only packed image (constant hessian) / (g, h) pairs
-#ifndef HB_FC
 #define HB_FC 32
-#endif
 #define HB_FG 16
 #define HB_STRIDE 514    // int64 per feature in the LDS histogram (256 (G,H) pairs + 1 pad pair)
-#ifndef HB_T
 #define HB_T 512
-#endif
-#ifndef HB_U
 #define HB_U 8           // rows in flight per thread
-#endif
 // rows per histogram chunk. 16K since round 5: with the reduce grid bounded by the nodes that can have
 // partial slots, more chunks (= more histogram workgroups at the shallow levels) won: depth-6 level time
 // -7.5 %, depth 10 even (r5/gbdt_chunk_ab_r5.txt; 64K had been chosen in round 3 against the old reduce)
-#ifndef GB_R
 #define GB_R 16384
-#endif
 #define GB_MAXD 12       // deepest supported tree
 
 namespace {
@@ -284,21 +278,15 @@ __global__ void level0_kernel(Geo geo, const int* __restrict__ nroot, LNode* __r
 }
 
 // ---- G3: histograms (grid: chunks x feature blocks x folds) -----------------
-// HC (constant hessian: squared error, h = 1 for every row): only the gradient
-// goes through 64-bit LDS atomics; the hessian sum of a bin is its row count
-// (32-bit LDS atomics, half the bank traffic of a 64-bit add) times the one
-// fixed-point value every row carries -- the same integer the 64-bit sum would
-// reach, so histograms stay exact and bitwise identical. The LDS image is
-// 49 KB instead of 66 KB (3 workgroups per CU instead of 2).
-// Packed (GT_HIST_PACK): the count rides in the low 17 bits of the gradient's own 64-bit word --
-// one LDS atomic of (qg << 17) + 1 per row and feature instead of a 64-bit plus a 32-bit one. Exact:
-// a chunk has at most GB_R = 2^16 rows, so the count never carries into the gradient bits, and with
-// |qg| < 2^29 per row (geo.lg_n >= 32 on this path) the chunk's gradient sum stays below 2^45,
-// shifted 2^62. Decode: count = word & (2^17 - 1), sum qg = word >> 17 (arithmetic).
+// HC (constant hessian: squared error, h = 1 for every row): the hessian sum of a bin is its row
+// count times the one fixed-point value every row carries, and the count rides in the low 17 bits of
+// the gradient's own 64-bit LDS word: ONE atomic of (qg << 17) + 1 per row and feature. Exact: a
+// chunk has at most GB_R = 2^14 rows, so the count never carries into the gradient bits, and with
+// |qg| < 2^29 per row (geo.lg_n >= 32 on this path) the chunk's gradient sum stays below 2^43,
+// shifted 2^60. Decode: count = word & (2^17 - 1), sum qg = word >> 17 (arithmetic). The image is
+// 32 features x 258 words = 66 KB (2 workgroups per CU): twice the features per workgroup of the
+// (g, h) image halves the row-id / gradient gathers per bin row (round 5: 590 -> 380 us per level).
 #define HB_GSTRIDE 258   // int64 per feature in the gradient-only image (256 bins + pad)
-#ifndef GT_HIST_PACK
-#define GT_HIST_PACK 1
-#endif
 #define HB_CBITS 17
 static_assert(GB_R < (1 << HB_CBITS), "packed counts must not carry into the gradient bits");
 template <bool HC>
@@ -318,10 +306,7 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __re
     const int gx = gridDim.x, gy = gridDim.y;
     const int total = gx * gy * gridDim.z;
     int t = cx + gx * (cy + gy * cz);
-#ifndef GT_HIST_XCD
-#define GT_HIST_XCD 1
-#endif
-    if (GT_HIST_XCD && (total & 7) == 0) t = (t & 7) * (total >> 3) + (t >> 3);
+    if ((total & 7) == 0) t = (t & 7) * (total >> 3) + (t >> 3);
     cy = t % gy;
     t /= gy;
     cx = t % gx;
@@ -331,36 +316,23 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __re
   if (cx >= counts[2 * k]) return;
   constexpr int LHN = HC ? NF * HB_GSTRIDE : NF * HB_STRIDE;
   __shared__ u64 lh[LHN];
-  constexpr bool PK = HC && GT_HIST_PACK;
-  __shared__ unsigned int lc[HC && !PK ? NF * GB_BINS : 1];
   const Chunk c = chunks[(size_t)k * geo.maxch + cx];
   const int F = geo.F, Fs = geo.Fs;
   const int fb = cy * NF, tid = threadIdx.x;
   constexpr int LPR = NF / 4;                 // lanes per row (4 features each)
   constexpr int RL = HB_T / LPR;                // row lanes
   for (int i = tid; i < LHN; i += HB_T) lh[i] = 0ull;
-  if (HC && !PK)
-    for (int i = tid; i < NF * GB_BINS; i += HB_T) lc[i] = 0u;
   const float sg = ldexpf(1.f, fx_exp(mx[2 * k], geo.lg_n)), sh = ldexpf(1.f, fx_exp(mx[2 * k + 1], geo.lg_n));
   __syncthreads();
   const int wl = tid % LPR, rl = tid / LPR;
   const int f4 = fb + wl * 4;
   const float2* gk = gh + (size_t)k * geo.n;
   auto add = [&](uint32_t w, u64 qg, u64 qh) {
-    if constexpr (PK) {
+    if constexpr (HC) {
       u64* my = lh + wl * 4 * HB_GSTRIDE;
       const u64 v = (qg << HB_CBITS) + 1ull;
 #pragma unroll
       for (int q = 0; q < 4; ++q) atomicAdd(my + q * HB_GSTRIDE + ((w >> (8 * q)) & 255u), v);
-    } else if constexpr (HC) {
-      u64* my = lh + wl * 4 * HB_GSTRIDE;
-      unsigned int* myc = lc + wl * 4 * GB_BINS;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t b = (w >> (8 * q)) & 255u;
-        atomicAdd(my + q * HB_GSTRIDE + b, qg);
-        atomicAdd(myc + q * GB_BINS + b, 1u);
-      }
     } else {
       u64* my = lh + wl * 4 * HB_STRIDE;
 #pragma unroll
@@ -403,13 +375,10 @@ __global__ void __launch_bounds__(HB_T) hist_kernel(Geo geo, const uint8_t* __re
   const i64 qh1 = (i64)llrintf(1.0f * sh);     // every row's hessian (h = 1) in fixed point
   for (int i = tid; i < nf * 2 * GB_BINS; i += HB_T) {
     const int fl = i >> 9, j = i & 511;
-    if constexpr (PK) {
+    if constexpr (HC) {
       const i64 v = (i64)lh[fl * HB_GSTRIDE + (j >> 1)];
       dst[(size_t)fl * 2 * GB_BINS + j] = (j & 1) ? (v & ((1ll << HB_CBITS) - 1)) * qh1 : v >> HB_CBITS;
-    } else if constexpr (HC)
-      dst[(size_t)fl * 2 * GB_BINS + j] = (j & 1) ? (i64)lc[fl * GB_BINS + (j >> 1)] * qh1
-                                                  : (i64)lh[fl * HB_GSTRIDE + (j >> 1)];
-    else
+    } else
       dst[(size_t)fl * 2 * GB_BINS + j] = (i64)lh[fl * HB_STRIDE + j];
   }
 }
@@ -946,7 +915,7 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   geo.maxslot = 2 * rchunks + 2;
   geo.lg_n = 0;
   while ((1ll << geo.lg_n) < (long long)n + 1) ++geo.lg_n;
-  if (hconst && GT_HIST_PACK) geo.lg_n = std::max(geo.lg_n, 32);   // |qg| < 2^29 per row (packed counts)
+  if (hconst) geo.lg_n = std::max(geo.lg_n, 32);   // |qg| < 2^29 per row (packed counts)
   const int tsz = (2 << D) - 1;
   const size_t per_node = (size_t)F * 2 * GB_BINS;      // int64 per histogram node
   DevParams dp{P[1], P[8], P[9], P[4], P[0], P[3]};
