@@ -936,6 +936,80 @@ __global__ void __launch_bounds__(256) dense_dgrad_stream2_kernel(DenseDgradArgs
   for (int m = 0; m < 2; ++m) dense_dgrad_epilogue<PREC>(a, g, f_t + 16 * m, b0, acc[m], lane);
 }
 
+
+// ---------------------------------------------------------------------------
+// fp32 data gradient on the fp32-input MFMA (v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulate;
+// 1/16 of the bf16 rate, which at batch 32 is about the HBM rate of streaming W1). W1 is read once from
+// the fp32 master with coalesced 16-byte loads -- no bf16 planes, no split VALU: 67.5-68.9 vs 73-74 us
+// for dense_dgrad_stream2 at 25 groups, and exact products. (The same scheme for the forward -- A = 4
+// unit tiles per 16-byte W1 load, split-K ranges reduced in order -- ran 72-92 us against the split-K
+// bf16x6 kernel's 59-63 at any prefetch depth, and was dropped: profiles/r5/dense_f32_mfma_ab_r5.txt.)
+// Operand maps of 16x16x4 f32: A[i][k], B[k][j] with lane l -> i or j = l & 15, k = l >> 4; C lane l
+// holds rows 4 (l >> 4) + r of column l & 15.
+__device__ __forceinline__ f32x4_t mfma4f(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// Data gradient: grid (Fp/128, ceil(B/32), G), XCD-grouped; wave = two 16-feature tiles x 32 rows over all
+// Up units. Per 32-unit block a lane loads 8 consecutive units of its W1 row (tile m: feature f_t + 16 m + l16)
+// and of its dH row (b0 + 16 h + l16), two 16-byte loads each; k-step s multiplies unit u0 + 8 k + s.
+// C layout = dense_dgrad_epilogue's (rows = features 4 kq + r, column = batch row).
+__global__ void __launch_bounds__(256) dense_dgrad_f32_kernel(DenseDgradArgs a) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
+  int bx, g;
+  xcd_tile(bx, g);
+  const int f_t = bx * 128 + wave * 32;
+  const int b0 = blockIdx.y * 32;
+  const float* wrow[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) wrow[m] = a.w1 + ((long)g * a.Fp + min(f_t + 16 * m + l16, a.Fp - 1)) * a.Up + 8 * kq;
+  const float* hrow[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) hrow[h] = a.dH + ((long)g * a.B + min(b0 + 16 * h + l16, a.B - 1)) * a.Up + 8 * kq;
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) acc[m][0] = acc[m][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  constexpr int NB = 2;                                     // 32-unit blocks in flight per wave (3, 4: slower)
+  float4 wv[NB][2][2], hv[NB][2][2];                        // [buf][m or h][half]
+  const int nblk = a.Up >> 5;
+  auto load = [&](int j, int buf) {
+    const int jj = min(j, nblk - 1);                        // past the end: re-read the last block, unused
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      wv[buf][m][0] = *reinterpret_cast<const float4*>(wrow[m] + 32 * jj);
+      wv[buf][m][1] = *reinterpret_cast<const float4*>(wrow[m] + 32 * jj + 4);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      hv[buf][h][0] = *reinterpret_cast<const float4*>(hrow[h] + 32 * jj);
+      hv[buf][h][1] = *reinterpret_cast<const float4*>(hrow[h] + 32 * jj + 4);
+    }
+  };
+  auto step = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float w0 = (&wv[buf][0][q >> 2].x)[q & 3], w1 = (&wv[buf][1][q >> 2].x)[q & 3];
+      const float h0 = (&hv[buf][0][q >> 2].x)[q & 3], h1 = (&hv[buf][1][q >> 2].x)[q & 3];
+      acc[0][0] = mfma4f(w0, h0, acc[0][0]);
+      acc[0][1] = mfma4f(w0, h1, acc[0][1]);
+      acc[1][0] = mfma4f(w1, h0, acc[1][0]);
+      acc[1][1] = mfma4f(w1, h1, acc[1][1]);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < NB - 1; ++i) load(i, i);
+  for (int j = 0; j < nblk; j += NB) {
+#pragma unroll
+    for (int q = 0; q < NB; ++q) {
+      if (j + q >= nblk) break;
+      load(j + q + NB - 1, (q + NB - 1) % NB);
+      step(q);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m) dense_dgrad_epilogue<1>(a, g, f_t + 16 * m, b0, acc[m], lane);
+}
+
 // ---------------------------------------------------------------------------
 struct DenseWgradAdamArgs {
   const void* x;       // [G][B][Fp] bf16 or fp32 (prec)
@@ -1216,6 +1290,15 @@ int gt_step_begin(StepState* s, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// fp32 data gradient on the f32-input MFMA (gt_dense_set_f32mma(0), tests: the bf16x6 kernels)
+static int g_dense_f32mma = 1;
+
+int gt_dense_set_f32mma(int on) {
+  const int old = g_dense_f32mma;
+  g_dense_f32mma = on;
+  return old;
+}
+
 // split-K forward from the W1 master (gt_dense_set_sk(0), tests: the streaming kernel on the transposed copy)
 static int g_dense_sk = -1;
 static bool dense_sk_on() {
@@ -1250,6 +1333,9 @@ int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
     }
     return (int)hipGetLastError();
   }
+  // the kernels below read the transposed W1 copy; a job that does not maintain it passes none (the
+  // split-K switch turned off after such a job was built must fail, not train on a stale copy)
+  if (a->wt == nullptr) return -3;
   if (dense_stream_on()) {
     // unit tiles per workgroup (4: 53 vs 67 us for 1 at 25 groups, W1 in MALL)
     constexpr int ut = 4;
@@ -1283,6 +1369,11 @@ int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
     return -1;
   if (a->Up % 8) return -1;
   if (a->prec != 0 && a->prec != 1) return -1;
+  if (a->prec == 1 && a->w1 && a->Up % 32 == 0 && g_dense_f32mma) {
+    dim3 grid((a->Fp + 127) / 128, (a->B + 31) / 32, a->G);
+    hipLaunchKernelGGL(dense_dgrad_f32_kernel, grid, dim3(256), 0, stream, *a);
+    return (int)hipGetLastError();
+  }
   if (a->w1 && a->dHp && dense_stream_on() && dgrad2_on()) {
     dim3 grid2((a->Fp + 127) / 128, (a->B + 31) / 32, a->G);
     if (a->prec) hipLaunchKernelGGL(dense_dgrad_stream2_kernel<1>, grid2, dim3(256), 0, stream, *a);
@@ -1291,10 +1382,12 @@ int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
   }
   dim3 grid((a->Fp + 63) / 64, (a->B + 31) / 32, a->G);
   if (a->w1 && dense_stream_on()) {
+    // (streaming v1 reads the master)
     if (a->prec) hipLaunchKernelGGL(dense_dgrad_stream_kernel<1>, grid, dim3(256), 0, stream, *a);
     else hipLaunchKernelGGL(dense_dgrad_stream_kernel<0>, grid, dim3(256), 0, stream, *a);
     return (int)hipGetLastError();
   }
+  if (a->wt == nullptr) return -3;                   // the round-2 kernel reads the transposed copy
   if (a->prec) hipLaunchKernelGGL(dense_dgrad_kernel<1>, grid, dim3(256), 0, stream, *a);
   else hipLaunchKernelGGL(dense_dgrad_kernel<0>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();

@@ -104,10 +104,15 @@ class GeneticCnnModel(GentunModel):
         return n
 
     def _live_jobs(self):
-        out = []
+        """The distinct models behind the last training: a SequentialFoldJob holds one job per fold, but
+        with fold reuse (the HIP default) those are shallow copies sharing ONE set of device buffers --
+        counted once (the last fold's job: its seeds are the ones the buffers were last re-pointed to)."""
+        seen = {}
         for job in self.jobs:
-            out.extend(getattr(job, "jobs", None) or [job])     # SequentialFoldJob: one job per fold
-        return out
+            for j in (getattr(job, "jobs", None) or [job]):     # SequentialFoldJob: one job per fold
+                flat = getattr(j, "flat", None)
+                seen[flat.data_ptr() if flat is not None else id(j)] = j
+        return list(seen.values())
 
     def plot(self, path=None):
         """Draw the decoded network to validate gene-to-DAG (keras_models.py:

@@ -512,6 +512,9 @@ class HipPopJob(FoldJob):
             df.w1 = self.views["W1"][0].data_ptr()
             df.ks = int(self.L.gt_dense_fwd_splits(self.Fp))
             self._dense_sk_buffers(df, B)
+            # the transposed copy is not maintained on this path: no launcher may read it (the copy-based
+            # kernels refuse a null copy instead of training on a stale one, cnn_dense.hip)
+            df.wt = 0
         self.dense_fwd_args = df
         hd = K.HeadArgs()
         hd.h, hd.w2, hd.b2 = self.hdrop.data_ptr(), self.views["W2"][0].data_ptr(), self.views["b2"][0].data_ptr()
@@ -534,6 +537,8 @@ class HipPopJob(FoldJob):
         dd.G, dd.B, dd.Fp, dd.Up = Q, B, self.Fp, self.Up
         dd.prec, dd.wps = prec, self.w1t.numel()
         dd.w1 = self.views["W1"][0].data_ptr()      # the fp32 master (updated after dgrad): streaming kernel
+        if self.dense_sk:
+            dd.wt = 0
         self.dense_dgrad_args = dd
         dw = K.DenseWgradAdamArgs()
         p, m, v = self.views["W1"]

@@ -146,3 +146,18 @@ def test_reset_weights_redraws_kernels_keeps_biases():
         else:
             assert torch.equal(before[name], after[name]), name
     assert any(before[n].abs().sum() > 0 for n, k in kinds.items() if k == "zero")    # trained biases kept
+
+
+def test_reset_weights_counts_shared_fold_models_once():
+    """Sequential folds (reset='kernels'): the per-fold jobs of one SequentialFoldJob may share one set of
+    buffers (fold reuse); reset_weights re-draws each distinct model once and reports how many it reset."""
+    import torch
+    from gentun_amd.utils.data import make_cifar_like
+    x, y = make_cifar_like(n=48, seed=1)
+    m = GeneticCnnModel(x, y, {'S_1': '1', 'S_2': '1'}, (2, 2), x.shape[1:], (4, 4), ((3, 3), (3, 3)), 8, 0.5, 10,
+                        nfold=2, epochs=(1,), learning_rate=(1e-2,), batch_size=16, backend="torch",
+                        device=torch.device("cpu"), reset="kernels")
+    m.cross_validate()
+    folds = [j for job in m.jobs for j in (getattr(job, "jobs", None) or [job])]
+    distinct = {j.flat.data_ptr() for j in folds}
+    assert m.reset_weights() == len(distinct) == len(m._live_jobs())

@@ -344,3 +344,22 @@ def test_eval_batch_does_not_change_metrics(bn):
         assert (job.eval_batch() == 32) if eb == 32 else (job.eval_batch() >= 128)   # 300-sample folds
         res.append(job.launch().finish())
     assert res[0] == res[1]
+
+
+@pytest.mark.gpu
+def test_hip_reset_weights_sequential_folds_once():
+    """HIP backend, reference folds (reset='kernels', fold reuse): the per-fold jobs share one set of
+    device buffers, so reset_weights re-draws that model once (it used to re-initialise the
+    same buffers nfold times with different folds' seeds)."""
+    import torch
+    from gentun_amd.models.cnn import GeneticCnnModel
+    from gentun_amd.utils.data import make_cifar_like
+    x, y = make_cifar_like(n=96, seed=1)
+    m = GeneticCnnModel(x, y, {'S_1': '1', 'S_2': '1'}, (2, 2), x.shape[1:], (4, 4), ((3, 3), (3, 3)), 8, 0.5, 10,
+                        nfold=3, epochs=(1,), learning_rate=(1e-2,), batch_size=16, backend="hip",
+                        device=torch.device("cuda:0"), reset="kernels", dtype="fp32")
+    m.cross_validate()
+    folds = [j for job in m.jobs for j in (getattr(job, "jobs", None) or [job])]
+    assert len(folds) == 3
+    distinct = {j.flat.data_ptr() for j in folds}
+    assert m.reset_weights() == len(distinct)
