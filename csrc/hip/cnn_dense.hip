@@ -2,19 +2,20 @@
 //
 // step_begin   : advances the captured step's device state (batch row, Adam t,
 //                bias-corrected lr_t) -- keeps the whole step graph-replayable.
-// dense_fwd    : K7  h = dropout(relu(x W1 + b1)) on v_mfma_f32_16x16x32_bf16,
-//                A = W1^T bf16 copy [u][f], B = x [b][f]; 4 consecutive units per
-//                lane in the epilogue -> 8-byte stores; dropout keyed by
+// dense_fwd    : K7  h = dropout(relu(x W1 + b1)): split-K over feature ranges
+//                straight from the fp32 master W1 (exact bf16 planes staged in
+//                LDS, v_mfma_f32_16x16x32_bf16), the ranges summed in order by
+//                a second launch that runs the epilogue; dropout keyed by
 //                hash(seed, fold, global step, row, unit) (deterministic).
 // head         : K9  logits = h W2 + b2, softmax, loss gradient (bce_compat =
 //                Keras softmax + binary_crossentropy with eps clipping, or ce),
 //                dh -> dH = dh * scale * (h > 0), dW2, db2, db1 -- one
 //                workgroup per fold, everything through LDS.
-// dense_dgrad  : K8  dX = dH W1^T on MFMA (A = W1 rows fp32->bf16, B = dH).
+// dense_dgrad  : K8  dX = dH W1^T from the master W1: fp32 on the f32-input
+//                MFMA (exact products), bf16 mode on the bf16 MFMA.
 // dense_wgrad_adam : K8+K10 fused: dW1 = X^T dH (K = batch, VALU) immediately
-//                applied by Adam to the fp32 master/m/v, plus the transposed
-//                bf16 copy for the next forward -- the gradient of the largest
-//                tensor (90 % of all parameters) never touches HBM.
+//                applied by Adam to the fp32 master/m/v -- the gradient of the
+//                largest tensor (90 % of all parameters) never touches HBM.
 // adam_segments: K10 multi-tensor Adam over every other parameter; reduces
 //                the conv wgrad split-K partials in fixed order, writes bf16
 //                copies (and the flipped/transposed dgrad copy of conv weights).
@@ -70,32 +71,6 @@ struct DenseFwdArgs {
   int* cnt;                // unused (reserved)
   int ks;
 };
-
-// an MFMA A operand of 8 consecutive weights of the transposed W1 copy: bf16
-// as is, fp32 split into the three exact planes in registers (4 bytes per
-// weight from HBM instead of 3 stored bf16 planes = 6)
-template <int PREC>
-__device__ __forceinline__ void w1_frag(const void* base, long off, bool ok, uint4* f) {
-  if (PREC) {
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (ok) load8f(static_cast<const float*>(base) + off, v);
-    split8(v, f[0], f[1], f[2]);
-  } else {
-    f[0] = ok ? *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(base) + off) : make_uint4(0, 0, 0, 0);
-  }
-}
-
-// an MFMA B operand of 8 consecutive activations: bf16 as is, fp32 split into planes
-template <int PREC>
-__device__ __forceinline__ void act_frag(const void* base, long off, bool ok, uint4* f) {
-  if (PREC) {
-    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (ok) load8f(static_cast<const float*>(base) + off, v);
-    split8(v, f[0], f[1], f[2]);
-  } else {
-    f[0] = ok ? *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(base) + off) : make_uint4(0, 0, 0, 0);
-  }
-}
 
 // bias + ReLU + dropout of one 16-unit x 32-row tile (D[row = unit][col =
 // batch row], two 16-row MFMA tiles), the activation store and the tile's
@@ -164,54 +139,7 @@ __device__ __forceinline__ void dense_fwd_epilogue(const DenseFwdArgs& a, int g,
   }
 }
 
-// grid (Up/16, ceil(B/32), G): one 16-unit x 32-row tile per workgroup, the
-// K (feature) loop split over the 4 waves and reduced through LDS.
-template <int PREC>
-__global__ void __launch_bounds__(256) dense_fwd_kernel(DenseFwdArgs a) {
-  typedef typename ActT<PREC>::T AT;
-  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
-  __shared__ f32x4_t red[3][2][64];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
-  const int g = blockIdx.z;
-  const int u_t = blockIdx.x * 16;
-  const int b0 = blockIdx.y * 32;
-  const int nchunks = a.Fp >> 3;
-  const long wg = (long)g * a.Up * a.Fp;
-  const long xg = (long)g * a.B * a.Fp;
-  f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  const int urow = u_t + l16;
-  const int br0 = b0 + l16, br1 = b0 + 16 + l16;
-  const long pa = wg + (long)urow * a.Fp;
-  const bool ua = urow < a.Up, b0ok = br0 < a.B, b1ok = br1 < a.B;
-  for (int ks = wave * 4; ks < nchunks; ks += 16) {
-    const int c = ks + kq;
-    uint4 af[NPL], bf0[NPL], bf1[NPL];
-    w1_frag<PREC>(a.wt, pa + c * 8, c < nchunks && ua, af);
-    act_frag<PREC>(a.x, xg + (long)br0 * a.Fp + c * 8, c < nchunks && b0ok, bf0);
-    act_frag<PREC>(a.x, xg + (long)br1 * a.Fp + c * 8, c < nchunks && b1ok, bf1);
-    acc[0] = mfma_np<NPL>(af, bf0, acc[0]);
-    acc[1] = mfma_np<NPL>(af, bf1, acc[1]);
-  }
-  if (wave > 0) {
-    red[wave - 1][0][lane] = acc[0];
-    red[wave - 1][1][lane] = acc[1];
-  }
-  __syncthreads();
-  if (wave > 0) return;
-#pragma unroll
-  for (int w = 0; w < 3; ++w) { acc[0] += red[w][0][lane]; acc[1] += red[w][1][lane]; }
-  dense_fwd_epilogue<PREC>(a, g, u_t, b0, acc, lane, blockIdx.x);
-}
-
-// Streaming forward (the default): one workgroup = UT 16-unit tiles x 32 rows,
-// the same per-wave k-step assignment as dense_fwd_kernel (wave w: k-steps
-// w, w+4, ...; 4 chunks of 8 features each) and the same fixed-order
-// reduction over the 4 waves, so the result is bit-identical -- but every wave
-// carries UT unit tiles (the activation fragments are loaded and split once
-// per UT tiles: UT x less x traffic), the raw W1 / x values of the next k-step
-// are loaded while the current one multiplies (two register sets, loads with
-// selected addresses instead of branches), and the workgroups of one group
-// are placed on one XCD (its x stays in that L2).
+// raw loads of 8 consecutive values (zero chunk when !ok: no branch around a load)
 template <typename T>
 __device__ __forceinline__ void ld8_raw(const T* p, bool ok, float* f) {
   if constexpr (sizeof(T) == 4) {
@@ -237,95 +165,6 @@ __device__ __forceinline__ void xcd_tile(int& bx, int& bz) {
   if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
   bz = lin / nbx;
   bx = lin - bz * nbx;
-}
-
-template <int PREC, int UT>
-__global__ void __launch_bounds__(256) dense_fwd_stream_kernel(DenseFwdArgs a) {
-  typedef typename ActT<PREC>::T AT;
-  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
-  __shared__ f32x4_t red[4][UT][2][64];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
-  int bx, g;
-  xcd_tile(bx, g);
-  const int u_t = bx * 16 * UT;
-  const int b0 = blockIdx.y * 32;
-  const int nchunks = a.Fp >> 3;
-  const int nks = (nchunks + 3) >> 2;                        // k-steps (4 chunks each)
-  const AT* wt = static_cast<const AT*>(a.wt) + (long)g * a.Up * a.Fp;
-  const AT* xg = static_cast<const AT*>(a.x) + (long)g * a.B * a.Fp;
-  const int br0 = b0 + l16, br1 = b0 + 16 + l16;
-  const AT* xr0 = xg + (long)min(br0, a.B - 1) * a.Fp;
-  const AT* xr1 = xg + (long)min(br1, a.B - 1) * a.Fp;
-  const AT* wr[UT];
-  bool uok[UT];
-#pragma unroll
-  for (int t = 0; t < UT; ++t) {
-    const int u = u_t + t * 16 + l16;
-    uok[t] = u < a.Up;
-    wr[t] = wt + (long)(uok[t] ? u : 0) * a.Fp;
-  }
-  f32x4_t acc[UT][2];
-#pragma unroll
-  for (int t = 0; t < UT; ++t) acc[t][0] = acc[t][1] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float rw[2][UT][8], rx[2][2][8];
-  auto load = [&](int j, int buf) {                          // k-step j = wave + 4 i
-    const int c = 4 * j + kq;
-    const bool cok = c < nchunks;
-#pragma unroll
-    for (int t = 0; t < UT; ++t) ld8_raw(wr[t] + c * 8, cok && uok[t], rw[buf][t]);
-    ld8_raw(xr0 + c * 8, cok && br0 < a.B, rx[buf][0]);
-    ld8_raw(xr1 + c * 8, cok && br1 < a.B, rx[buf][1]);
-  };
-  auto step = [&](int buf) {
-    uint4 b0f[NPL], b1f[NPL];
-    planes8<PREC>(rx[buf][0], b0f);
-    planes8<PREC>(rx[buf][1], b1f);
-#pragma unroll
-    for (int t = 0; t < UT; ++t) {
-      uint4 af[NPL];
-      planes8<PREC>(rw[buf][t], af);
-      acc[t][0] = mfma_np<NPL>(af, b0f, acc[t][0]);
-      acc[t][1] = mfma_np<NPL>(af, b1f, acc[t][1]);
-    }
-  };
-  // no branch around a load (hipcc would wait vmcnt(0) at each): k-steps past
-  // the end load the zero chunk and add exact zeros
-  // (sched barriers: keep each refill where it is -- the scheduler otherwise
-  // sinks it next to its use and the wait becomes vmcnt(0))
-  int j = wave;
-  load(j, 0);
-  __builtin_amdgcn_sched_barrier(0);      // the same load order as the loop body (exact vmcnt at its top)
-  load(j + 4, 1);
-  __builtin_amdgcn_sched_barrier(0);
-  for (; j < nks; j += 8) {
-    step(0);
-    __builtin_amdgcn_sched_barrier(0);
-    load(j + 8, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    step(1);
-    __builtin_amdgcn_sched_barrier(0);
-    load(j + 12, 1);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int t = 0; t < UT; ++t) {
-    red[wave][t][0][lane] = acc[t][0];
-    red[wave][t][1][lane] = acc[t][1];
-  }
-  __syncthreads();
-  // one unit tile per wave; partials summed in wave order (dense_fwd_kernel's)
-  for (int t = wave; t < UT; t += 4) {
-    f32x4_t r2[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      f32x4_t v = red[0][t][h][lane];
-      v += red[1][t][h][lane];
-      v += red[2][t][h][lane];
-      v += red[3][t][h][lane];
-      r2[h] = v;
-    }
-    dense_fwd_epilogue<PREC>(a, g, u_t + t * 16, b0, r2, lane, u_t / 16 + t);
-  }
 }
 
 // plane q (0..2) of the exact split of p (q = 0: the bf16 rounding)
@@ -719,147 +558,11 @@ __device__ __forceinline__ void dense_dgrad_epilogue(const DenseDgradArgs& a, in
   }
 }
 
-// grid (Fp/64, ceil(B/32), G): D[row = f][col = b], K = units.
-// W1 is read from the bf16 transposed copy (half the bytes of the fp32 master
-// this kernel used to read, on the critical path): each 32-unit x 64-feature
-// tile is one coalesced 16-byte load per thread, transposed through LDS so every
-// lane gets its 8 consecutive units as one 16-byte LDS read. The bf16 values are
-// the RNE roundings the old pack8(fp32) produced, so dx is bit-identical.
-template <int PREC>
-__global__ void __launch_bounds__(256) dense_dgrad_kernel(DenseDgradArgs a) {
-  typedef typename ActT<PREC>::T AT;
-  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
-  __shared__ __attribute__((aligned(16))) uint16_t tl[NPL][64][40];    // [plane][feature][unit], 80-byte rows
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
-  const int g = blockIdx.z;
-  const int fb = blockIdx.x * 64;
-  const int f_t = fb + wave * 16;
-  const int b0 = blockIdx.y * 32;
-  const long wg = (long)g * a.Up * a.Fp;
-  const float* dH = a.dH + (long)g * a.B * a.Up;
-  const int lu = tid >> 3, lf = (tid & 7) * 8;       // staging: unit row lu, features lf .. lf+7
-  const bool fok = fb + lf < a.Fp;                   // Fp % 8 == 0: all 8 or none
-  const int br0 = b0 + l16, br1 = b0 + 16 + l16;
-  f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  const int nchunks = a.Up >> 3;
-  for (int ks = 0; ks < nchunks; ks += 4) {
-    const int u = ks * 8 + lu;
-    uint4 qv[NPL];
-    w1_frag<PREC>(a.wt, wg + (long)u * a.Fp + fb + lf, fok && u < a.Up, qv);
-    const int c = ks + kq;
-    float f0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, f1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (c < nchunks) {
-      if (br0 < a.B) {
-        const float4* p = reinterpret_cast<const float4*>(dH + (long)br0 * a.Up + c * 8);
-        const float4 q0 = p[0], q1 = p[1];
-        f0[0] = q0.x; f0[1] = q0.y; f0[2] = q0.z; f0[3] = q0.w; f0[4] = q1.x; f0[5] = q1.y; f0[6] = q1.z; f0[7] = q1.w;
-      }
-      if (br1 < a.B) {
-        const float4* p = reinterpret_cast<const float4*>(dH + (long)br1 * a.Up + c * 8);
-        const float4 q0 = p[0], q1 = p[1];
-        f1[0] = q0.x; f1[1] = q0.y; f1[2] = q0.z; f1[3] = q0.w; f1[4] = q1.x; f1[5] = q1.y; f1[6] = q1.z; f1[7] = q1.w;
-      }
-    }
-    __syncthreads();                                 // previous tile fully read
-#pragma unroll
-    for (int pl = 0; pl < NPL; ++pl) {
-      const uint32_t w[4] = {qv[pl].x, qv[pl].y, qv[pl].z, qv[pl].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        tl[pl][lf + 2 * j][lu] = (uint16_t)(w[j] & 0xffffu);
-        tl[pl][lf + 2 * j + 1][lu] = (uint16_t)(w[j] >> 16);
-      }
-    }
-    __syncthreads();
-    uint4 af[NPL], b0f[NPL], b1f[NPL];
-#pragma unroll
-    for (int pl = 0; pl < NPL; ++pl) af[pl] = *reinterpret_cast<const uint4*>(&tl[pl][wave * 16 + l16][kq * 8]);
-    if constexpr (PREC != 0) {
-      split8(f0, b0f[0], b0f[1], b0f[2]);
-      split8(f1, b1f[0], b1f[1], b1f[2]);
-    } else {
-      b0f[0] = pack8(f0);
-      b1f[0] = pack8(f1);
-    }
-    acc[0] = mfma_np<NPL>(af, b0f, acc[0]);
-    acc[1] = mfma_np<NPL>(af, b1f, acc[1]);
-  }
-  dense_dgrad_epilogue<PREC>(a, g, f_t, b0, acc, lane);
-}
-
-// Streaming data gradient (the default when the fp32 master is given):
-// dX[b][f] = sum_u dH[b][u] W1[f][u] with A = the fp32 master W1 [G][Fp][Up]
-// itself -- 8 consecutive units of a feature row are one contiguous 32-byte
-// load, so there is no LDS transpose and no barrier in the k loop. The master
-// equals the copy dense_fwd multiplied by (the W1 update runs after this
-// kernel; prec 0 rounds it to bf16 exactly as the copy was rounded), and the
-// k-steps run in dense_dgrad_kernel's order: bit-identical. The next k-step's
-// raw values are loaded during the current one's MFMAs; XCD-grouped
-// workgroups (a group's dH stays in one L2).
-template <int PREC>
-__global__ void __launch_bounds__(256) dense_dgrad_stream_kernel(DenseDgradArgs a) {
-  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, kq = lane >> 4, l16 = lane & 15;
-  int bx, g;
-  xcd_tile(bx, g);
-  const int f_t = bx * 64 + wave * 16;
-  const int b0 = blockIdx.y * 32;
-  const int fa = f_t + l16;
-  const bool fok = fa < a.Fp;
-  const float* wrow = a.w1 + ((long)g * a.Fp + (fok ? fa : 0)) * a.Up;
-  const float* dH = a.dH + (long)g * a.B * a.Up;
-  const int br0 = b0 + l16, br1 = b0 + 16 + l16;
-  const float* h0 = dH + (long)min(br0, a.B - 1) * a.Up;
-  const float* h1 = dH + (long)min(br1, a.B - 1) * a.Up;
-  const int nchunks = a.Up >> 3;
-  const int nks = (nchunks + 3) >> 2;
-  f32x4_t acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-  float rw[2][8], rh[2][2][8];
-  auto load = [&](int j, int buf) {
-    const int c = 4 * j + kq;
-    const bool cok = c < nchunks;
-    ld8_raw(wrow + c * 8, cok && fok, rw[buf]);
-    ld8_raw(h0 + c * 8, cok && br0 < a.B, rh[buf][0]);
-    ld8_raw(h1 + c * 8, cok && br1 < a.B, rh[buf][1]);
-  };
-  auto step = [&](int buf) {
-    uint4 af[NPL], b0f[NPL], b1f[NPL];
-    planes8<PREC>(rw[buf], af);
-    if constexpr (PREC != 0) {
-      split8(rh[buf][0], b0f[0], b0f[1], b0f[2]);
-      split8(rh[buf][1], b1f[0], b1f[1], b1f[2]);
-    } else {
-      b0f[0] = pack8(rh[buf][0]);
-      b1f[0] = pack8(rh[buf][1]);
-    }
-    acc[0] = mfma_np<NPL>(af, b0f, acc[0]);
-    acc[1] = mfma_np<NPL>(af, b1f, acc[1]);
-  };
-  load(0, 0);                              // (unconditional loads, ordered: see dense_fwd_stream_kernel)
-  __builtin_amdgcn_sched_barrier(0);
-  load(1, 1);
-  __builtin_amdgcn_sched_barrier(0);
-  for (int j = 0; j < nks; j += 2) {
-    step(0);
-    __builtin_amdgcn_sched_barrier(0);
-    load(j + 2, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    step(1);
-    __builtin_amdgcn_sched_barrier(0);
-    load(j + 3, 1);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  dense_dgrad_epilogue<PREC>(a, g, f_t, b0, acc, lane);
-}
-
-// Data gradient v2 (the default when head_bwd wrote the dH planes): every
-// wave carries TWO 16-feature tiles (32 features) and takes dH as the
-// pre-split bf16 planes head_bwd stored once, instead of loading fp32 dH and
-// splitting it again in every wave of every workgroup (the v1 kernel spent 2/3
-// of its vector instructions on that). Per k-step a wave issues two W1 row
-// loads (split in registers) and 2 x NPL plane loads for 2 x 2 x 6 MFMAs. Same
-// k-step order and the same split values as dense_dgrad_stream_kernel: dx is
-// bit-identical. Grid (Fp/128, ceil(B/32), G), XCD-grouped.
+// Data gradient, bf16 mode (fp32: dense_dgrad_f32_kernel below): dX = dH W1^T with A = the fp32 master
+// W1 [G][Fp][Up] itself (8 consecutive units of a feature row = one 32-byte load, rounded to bf16 in
+// registers -- no transposed copy, no LDS, no barrier in the k loop); every wave carries TWO 16-feature
+// tiles and takes dH as the bf16 plane head_bwd stored once. Grid (Fp/128, ceil(B/32), G), XCD-grouped.
+// (The round-2 copy-based kernels and the streaming v1 kernel were removed in round 5.)
 template <int PREC>
 __global__ void __launch_bounds__(256) dense_dgrad_stream2_kernel(DenseDgradArgs a) {
   constexpr int NPL = PREC ? GT_NPL_F32 : 1;
@@ -1015,7 +718,7 @@ struct DenseWgradAdamArgs {
   const void* x;       // [G][B][Fp] bf16 or fp32 (prec)
   const float* dH;     // [G][B][Up]
   float* p; float* m; float* v;   // [G][Fp][Up]
-  void* wt;            // transposed copy [G][Up][Fp] for dense_fwd / dense_dgrad: bf16 (prec 0) or fp32 (prec 1)
+  void* wt;            // unused (kept for the ABI: the transposed W1 copy of rounds 2-4)
   const StepState* st;
   int G, B, Fp, Up;
   int Cp, Cr, Ur;      // feature = pixel * Cp + channel; channels >= Cr and units >= Ur are padding
@@ -1024,17 +727,15 @@ struct DenseWgradAdamArgs {
   long wps;            // unused (kept for the ABI)
   float* gbuf;         // X5 data parallelism: [G][Fp][Up] gradient buffer
   int mode;            // 0: fused gradient + update; 1: gradient -> gbuf only (all-reduced next);
-                       // 2: update (and transposed copy) from gbuf
+                       // 2: update from gbuf
 };
 
 // grid (Fp/16, G), 256 threads. Thread: unit quad q (4 units), rows fr, fr+2, ..., fr+14.
 template <int PREC>
 __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArgs a) {
   typedef typename ActT<PREC>::T AT;
-  constexpr int NPL = PREC ? GT_NPL_F32 : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* xs = reinterpret_cast<float*>(smem);                       // [B][16]
-  AT* tt = reinterpret_cast<AT*>(xs + a.B * 16);                    // [Up][16] transposed copy (bf16 / fp32)
   const int g = blockIdx.y, f0 = blockIdx.x * 16, tid = threadIdx.x;
   const AT* x = static_cast<const AT*>(a.x) + (long)g * a.B * a.Fp;
   for (int i = tid; i < a.B * 16; i += 256) {
@@ -1048,7 +749,6 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
   }
   __syncthreads();
   const float lr_t = a.st->lr_t;
-  const bool cp = a.wt != nullptr;                      // (uniform) transposed copy wanted: stage its tile
   const float* dH = a.dH + (long)g * a.B * a.Up;
   const int nq = a.Ur > 0 ? (a.Ur + 3) >> 2 : a.Up >> 2;
   const int fr = tid >> 7;
@@ -1089,46 +789,17 @@ __global__ void __launch_bounds__(256) dense_wgrad_adam_kernel(DenseWgradAdamArg
     for (int r = 0; r < 8; ++r) {
       const int f = f0 + fr + 2 * r;
       if (f >= a.Fp) continue;
-      if (a.Cp > 0 && f % a.Cp >= a.Cr) {      // padded channel: weights stay 0, only the copy tile
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (cp) tt[(u0 + i) * 16 + fr + 2 * r] = 0;
-        continue;
-      }
+      if (a.Cp > 0 && f % a.Cp >= a.Cr) continue;     // padded channel: weights stay 0
       const long off = ((long)g * a.Fp + f) * a.Up + u0;
       float4 pp = *reinterpret_cast<float4*>(a.p + off);
       float4 mm = *reinterpret_cast<float4*>(a.m + off);
       float4 vv = *reinterpret_cast<float4*>(a.v + off);
       float* P = &pp.x; float* M = &mm.x; float* V = &vv.x;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        P[i] = opt_update(a.st, P[i], acc[r][i], M[i], V[i], lr_t);
-        if (cp) {
-          if constexpr (PREC != 0) tt[(u0 + i) * 16 + fr + 2 * r] = P[i];
-          else tt[(u0 + i) * 16 + fr + 2 * r] = f2bf(P[i]);
-        }
-      }
+      for (int i = 0; i < 4; ++i) P[i] = opt_update(a.st, P[i], acc[r][i], M[i], V[i], lr_t);
       *reinterpret_cast<float4*>(a.p + off) = pp;
       *reinterpret_cast<float4*>(a.m + off) = mm;
       *reinterpret_cast<float4*>(a.v + off) = vv;
-    }
-  }
-  // (uniform) no update, or no transposed copy: every W1 reader takes the master (split-K dense_fwd,
-  // streaming dense_dgrad)
-  if (a.mode == 1 || a.wt == nullptr) return;
-  __syncthreads();
-  // transposed copy: wt[u][f0 .. f0+15] (32 / 64 contiguous bytes per unit), 8 values per store
-  const int nu = a.Ur > 0 ? ((a.Ur + 3) >> 2) << 2 : a.Up;
-  AT* wt = static_cast<AT*>(a.wt) + (long)g * a.Up * a.Fp;
-  for (int i = tid; i < nu * 2; i += 256) {
-    const int u = i >> 1, half = i & 1;
-    if (f0 + half * 8 + 8 <= a.Fp) {
-      float v[8];
-      ld_chunk(&tt[u * 16 + half * 8], v);
-      st_chunk(wt + (long)u * a.Fp + f0 + half * 8, v);
-    } else {
-      for (int j = 0; j < 8; ++j)
-        if (f0 + half * 8 + j < a.Fp) wt[(long)u * a.Fp + f0 + half * 8 + j] = tt[u * 16 + half * 8 + j];
     }
   }
 }
@@ -1252,65 +923,11 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// streaming dense fwd / dgrad (default) vs the round-2 kernels: gt_dense_set_stream (tests: bit-identical
-// either way)
-static int g_dense_stream = -1;
-static bool dense_stream_on() {
-  if (g_dense_stream < 0)
-    g_dense_stream = 1;
-  return g_dense_stream != 0;
-}
-
-// gt_dense_set_dgrad2(0) (tests) keeps the v1 streaming data gradient even when the dH planes exist
-static int g_dgrad2 = -1;
-static bool dgrad2_on() {
-  if (g_dgrad2 < 0) g_dgrad2 = 1;
-  return g_dgrad2 != 0;
-}
-
 extern "C" {
-
-int gt_dense_set_dgrad2(int on) {
-  dgrad2_on();
-  const int old = g_dgrad2;
-  g_dgrad2 = on;
-  return old;
-}
-
-int gt_dense_set_stream(int on) {
-  dense_stream_on();
-  const int old = g_dense_stream;
-  g_dense_stream = on;
-  return old;
-}
 
 int gt_step_begin(StepState* s, hipStream_t stream) {
   hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, stream, s);
   return (int)hipGetLastError();
-}
-
-// fp32 data gradient on the f32-input MFMA (gt_dense_set_f32mma(0), tests: the bf16x6 kernels)
-static int g_dense_f32mma = 1;
-
-int gt_dense_set_f32mma(int on) {
-  const int old = g_dense_f32mma;
-  g_dense_f32mma = on;
-  return old;
-}
-
-// split-K forward from the W1 master (gt_dense_set_sk(0), tests: the streaming kernel on the transposed copy)
-static int g_dense_sk = -1;
-static bool dense_sk_on() {
-  if (g_dense_sk < 0) g_dense_sk = 1;
-  return g_dense_sk != 0;
-}
-
-int gt_dense_set_sk(int on) {
-  dense_sk_on();
-  const int old = g_dense_sk;
-  g_dense_sk = on;
-  return old;
 }
 
 // feature ranges per output tile of the split-K forward: a per-shape constant (~12 k-steps of
@@ -1322,36 +939,16 @@ int gt_dense_fwd_splits(int Fp) {
 
 int gt_dense_fwd(const DenseFwdArgs* a, hipStream_t stream) {
   if (a->Fp % 8 || a->Up % 64 || a->C > HEAD_MAXC_FWD || (a->prec != 0 && a->prec != 1)) return -1;
-  if (a->w1 && a->ks >= 1 && (a->ks == 1 || a->part) && dense_sk_on()) {
-    dim3 grid(a->Up / 64 * a->ks, (a->B + 31) / 32, a->G);
-    if (a->prec) hipLaunchKernelGGL(dense_fwd_sk_kernel<1>, grid, dim3(256), 0, stream, *a);
-    else hipLaunchKernelGGL(dense_fwd_sk_kernel<0>, grid, dim3(256), 0, stream, *a);
-    if (a->ks > 1) {
-      dim3 rgrid(a->Up / 64, (a->B + 31) / 32, a->G);
-      if (a->prec) hipLaunchKernelGGL(dense_fwd_skred_kernel<1>, rgrid, dim3(256), 0, stream, *a);
-      else hipLaunchKernelGGL(dense_fwd_skred_kernel<0>, rgrid, dim3(256), 0, stream, *a);
-    }
-    return (int)hipGetLastError();
+  // W1 comes from the fp32 master only (the transposed copy of earlier rounds is gone)
+  if (!a->w1 || a->ks < 1 || (a->ks > 1 && !a->part)) return -3;
+  dim3 grid(a->Up / 64 * a->ks, (a->B + 31) / 32, a->G);
+  if (a->prec) hipLaunchKernelGGL(dense_fwd_sk_kernel<1>, grid, dim3(256), 0, stream, *a);
+  else hipLaunchKernelGGL(dense_fwd_sk_kernel<0>, grid, dim3(256), 0, stream, *a);
+  if (a->ks > 1) {
+    dim3 rgrid(a->Up / 64, (a->B + 31) / 32, a->G);
+    if (a->prec) hipLaunchKernelGGL(dense_fwd_skred_kernel<1>, rgrid, dim3(256), 0, stream, *a);
+    else hipLaunchKernelGGL(dense_fwd_skred_kernel<0>, rgrid, dim3(256), 0, stream, *a);
   }
-  // the kernels below read the transposed W1 copy; a job that does not maintain it passes none (the
-  // split-K switch turned off after such a job was built must fail, not train on a stale copy)
-  if (a->wt == nullptr) return -3;
-  if (dense_stream_on()) {
-    // unit tiles per workgroup (4: 53 vs 67 us for 1 at 25 groups, W1 in MALL)
-    constexpr int ut = 4;
-    dim3 grid(a->Up / (16 * ut), (a->B + 31) / 32, a->G);
-#define DENSE_FWD_UT(UT_)                                                                                 \
-  if (ut == UT_) {                                                                                        \
-    if (a->prec) hipLaunchKernelGGL((dense_fwd_stream_kernel<1, UT_>), grid, dim3(256), 0, stream, *a);   \
-    else hipLaunchKernelGGL((dense_fwd_stream_kernel<0, UT_>), grid, dim3(256), 0, stream, *a);           \
-    return (int)hipGetLastError();                                                                        \
-  }
-    DENSE_FWD_UT(4)
-#undef DENSE_FWD_UT
-  }
-  dim3 grid(a->Up / 16, (a->B + 31) / 32, a->G);
-  if (a->prec) hipLaunchKernelGGL(dense_fwd_kernel<1>, grid, dim3(256), 0, stream, *a);
-  else hipLaunchKernelGGL(dense_fwd_kernel<0>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 
@@ -1369,33 +966,21 @@ int gt_dense_dgrad(const DenseDgradArgs* a, hipStream_t stream) {
     return -1;
   if (a->Up % 8) return -1;
   if (a->prec != 0 && a->prec != 1) return -1;
-  if (a->prec == 1 && a->w1 && a->Up % 32 == 0 && g_dense_f32mma) {
-    dim3 grid((a->Fp + 127) / 128, (a->B + 31) / 32, a->G);
+  if (!a->w1) return -3;                               // the fp32 master W1 (no transposed copy)
+  dim3 grid((a->Fp + 127) / 128, (a->B + 31) / 32, a->G);
+  if (a->prec == 1) {
+    if (a->Up % 32) return -1;
     hipLaunchKernelGGL(dense_dgrad_f32_kernel, grid, dim3(256), 0, stream, *a);
-    return (int)hipGetLastError();
+  } else {
+    if (!a->dHp) return -3;                            // head_bwd's bf16 dH
+    hipLaunchKernelGGL(dense_dgrad_stream2_kernel<0>, grid, dim3(256), 0, stream, *a);
   }
-  if (a->w1 && a->dHp && dense_stream_on() && dgrad2_on()) {
-    dim3 grid2((a->Fp + 127) / 128, (a->B + 31) / 32, a->G);
-    if (a->prec) hipLaunchKernelGGL(dense_dgrad_stream2_kernel<1>, grid2, dim3(256), 0, stream, *a);
-    else hipLaunchKernelGGL(dense_dgrad_stream2_kernel<0>, grid2, dim3(256), 0, stream, *a);
-    return (int)hipGetLastError();
-  }
-  dim3 grid((a->Fp + 63) / 64, (a->B + 31) / 32, a->G);
-  if (a->w1 && dense_stream_on()) {
-    // (streaming v1 reads the master)
-    if (a->prec) hipLaunchKernelGGL(dense_dgrad_stream_kernel<1>, grid, dim3(256), 0, stream, *a);
-    else hipLaunchKernelGGL(dense_dgrad_stream_kernel<0>, grid, dim3(256), 0, stream, *a);
-    return (int)hipGetLastError();
-  }
-  if (a->wt == nullptr) return -3;                   // the round-2 kernel reads the transposed copy
-  if (a->prec) hipLaunchKernelGGL(dense_dgrad_kernel<1>, grid, dim3(256), 0, stream, *a);
-  else hipLaunchKernelGGL(dense_dgrad_kernel<0>, grid, dim3(256), 0, stream, *a);
   return (int)hipGetLastError();
 }
 
 int gt_dense_wgrad_adam(const DenseWgradAdamArgs* a, hipStream_t stream) {
   if (a->Up % 4 || (a->prec != 0 && a->prec != 1)) return -1;
-  const size_t lds = sizeof(float) * (size_t)a->B * 16 + (a->prec ? 4 : 2) * (size_t)a->Up * 16;
+  const size_t lds = sizeof(float) * (size_t)a->B * 16;
   if (lds > 160 * 1024) return -2;
   dim3 grid((a->Fp + 15) / 16, a->G);
   if (a->prec) {

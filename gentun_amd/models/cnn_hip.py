@@ -302,9 +302,6 @@ class HipPopJob(FoldJob):
             L.wT_bf = torch.zeros((npl, Q, L.cinp, L.KH, L.KW, L.coutp), dtype=torch.bfloat16, device=dev)
             L.part_w = torch.zeros((L.S, Q, L.coutp, L.Kdim), dtype=torch.float32, device=dev)   # split-K partials
             L.part_b = torch.zeros((L.S, Q, L.coutp), dtype=torch.float32, device=dev)
-        # transposed copy of W1 for dense_fwd / dense_dgrad (written by the W1
-        # optimizer): bf16, or fp32 split into planes in registers by the kernels
-        self.w1t = torch.zeros((Q, self.Up, self.Fp), dtype=self.adt, device=dev)
         self.gW2 = torch.zeros((Q, self.Up, self.classes), dtype=torch.float32, device=dev)
         self.gb2 = torch.zeros((Q, self.classes), dtype=torch.float32, device=dev)
         self.gb1 = torch.zeros((Q, self.Up), dtype=torch.float32, device=dev)
@@ -497,24 +494,18 @@ class HipPopJob(FoldJob):
         prec = self.prec
         # ---- head
         df = K.DenseFwdArgs()
-        df.x, df.wt, df.bias, df.out = (self.act[self.last].data_ptr(), self.w1t.data_ptr(),
-                                        self.views["b1"][0].data_ptr(), self.hdrop.data_ptr())
+        df.x, df.wt, df.bias, df.out = (self.act[self.last].data_ptr(), 0, self.views["b1"][0].data_ptr(),
+                                        self.hdrop.data_ptr())
         df.st, df.fold_ids, df.seeds = self.state.data_ptr(), self.fold_ids_t.data_ptr(), self.drop_seeds_t.data_ptr()
         df.G, df.B, df.Fp, df.Up = Q, B, self.Fp, self.Up
         df.drop_p, df.train, df.seed = self.cfg.dropout, 1, 0
         df.w2, df.plog, df.C = self.views["W2"][0].data_ptr(), self.plog.data_ptr(), self.classes
-        df.prec, df.wps = prec, self.w1t.numel()
-        # split-K forward straight from the fp32 W1 master (csrc/hip/cnn_dense.hip dense_fwd_sk_kernel);
-        # with the streaming data gradient also on the master, nothing reads the transposed copy and
-        # the W1 optimizer stops writing it (Up is a multiple of 64 by construction)
-        self.dense_sk = self.Up % 64 == 0
-        if self.dense_sk:
-            df.w1 = self.views["W1"][0].data_ptr()
-            df.ks = int(self.L.gt_dense_fwd_splits(self.Fp))
-            self._dense_sk_buffers(df, B)
-            # the transposed copy is not maintained on this path: no launcher may read it (the copy-based
-            # kernels refuse a null copy instead of training on a stale one, cnn_dense.hip)
-            df.wt = 0
+        df.prec, df.wps = prec, 0
+        # split-K forward straight from the fp32 W1 master (csrc/hip/cnn_dense.hip dense_fwd_sk_kernel; Up is
+        # a multiple of 64 by construction); the data gradient reads the master too: there is no W1 copy
+        df.w1 = self.views["W1"][0].data_ptr()
+        df.ks = int(self.L.gt_dense_fwd_splits(self.Fp))
+        self._dense_sk_buffers(df, B)
         self.dense_fwd_args = df
         hd = K.HeadArgs()
         hd.h, hd.w2, hd.b2 = self.hdrop.data_ptr(), self.views["W2"][0].data_ptr(), self.views["b2"][0].data_ptr()
@@ -532,22 +523,20 @@ class HipPopJob(FoldJob):
         hd.dHp = self.dHp.data_ptr()
         self.head_args = hd
         dd = K.DenseDgradArgs()
-        dd.dH, dd.wt, dd.dx = self.dH.data_ptr(), self.w1t.data_ptr(), self.grad[self.last].data_ptr()
+        dd.dH, dd.wt, dd.dx = self.dH.data_ptr(), 0, self.grad[self.last].data_ptr()
         dd.dHp = self.dHp.data_ptr()
         dd.G, dd.B, dd.Fp, dd.Up = Q, B, self.Fp, self.Up
-        dd.prec, dd.wps = prec, self.w1t.numel()
-        dd.w1 = self.views["W1"][0].data_ptr()      # the fp32 master (updated after dgrad): streaming kernel
-        if self.dense_sk:
-            dd.wt = 0
+        dd.prec, dd.wps = prec, 0
+        dd.w1 = self.views["W1"][0].data_ptr()      # the fp32 master (updated after dgrad)
         self.dense_dgrad_args = dd
         dw = K.DenseWgradAdamArgs()
         p, m, v = self.views["W1"]
         dw.x, dw.dH, dw.p, dw.m, dw.v = self.act[self.last].data_ptr(), self.dH.data_ptr(), p.data_ptr(), \
             m.data_ptr(), v.data_ptr()
-        dw.wt, dw.st = (0 if self.dense_sk else self.w1t.data_ptr()), self.state.data_ptr()
+        dw.wt, dw.st = 0, self.state.data_ptr()
         dw.G, dw.B, dw.Fp, dw.Up = Q, B, self.Fp, self.Up
         dw.Cp, dw.Cr, dw.Ur = self.final_cp, self.plan.kernels_per_layer[-1], self.plan.dense_units
-        dw.prec, dw.wps = prec, self.w1t.numel()
+        dw.prec, dw.wps = prec, 0
         self.dense_wgrad_args = dw
         if self.dp is not None:
             # X5: dW1 to a buffer (mode 1), all-reduced, then the update from it (mode 2)
@@ -710,7 +699,6 @@ class HipPopJob(FoldJob):
             w = L.w[0]
             L.w_bf.copy_(split_planes(w, self.npl))
             L.wT_bf.copy_(split_planes(w.flip(2, 3).permute(0, 4, 2, 3, 1), self.npl))
-        self.w1t.copy_(self.views["W1"][0].transpose(1, 2))
 
     def reset_optimizer(self, lr):
         self.m.zero_()
@@ -967,8 +955,7 @@ class HipPopJob(FoldJob):
         df = K.DenseFwdArgs.from_buffer_copy(self.dense_fwd_args)
         df.x, df.out, df.plog = rp(df.x), hdrop.data_ptr(), plog.data_ptr()
         df.B, df.train = EB, 0
-        if self.dense_sk:
-            self._dense_sk_buffers(df, EB)
+        self._dense_sk_buffers(df, EB)
         hd = K.HeadArgs.from_buffer_copy(self.head_args)
         hd.h, hd.plog = hdrop.data_ptr(), plog.data_ptr()
         hd.B, hd.eval, hd.st = EB, 1, self.eval_state.data_ptr()

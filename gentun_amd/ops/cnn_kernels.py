@@ -175,8 +175,6 @@ def lib():
         L.gt_conv_set_s2in_ct1.restype = I
         L.gt_dense_fwd_splits.argtypes = [I]
         L.gt_dense_fwd_splits.restype = I
-        L.gt_dense_set_sk.argtypes = [I]
-        L.gt_dense_set_sk.restype = I
         L.gt_conv_set_smallq.argtypes = [I]
         L.gt_conv_set_smallq.restype = I
         L.gt_conv_set_s2in_ct1.argtypes = [I]

@@ -3,7 +3,7 @@ population-launch size: G groups x batch 32, Fp = 3584 (8x8x56 pooled
 features of S=(3,5) kernels (20,50)), Up = 512. HIP-graph replay of `reps`
 launches; GB/s counts the fp32 W1 bytes (the roofline term).
 
-usage: GENTUN_DENSE_STREAM=0|1 GENTUN_DENSE_UT=1|2|4 python tools/bench_dense.py [G] [reps]
+usage: python tools/bench_dense.py [G] [reps]
 """
 import ctypes
 import json
@@ -35,6 +35,9 @@ a = Km.DenseFwdArgs()
 a.x, a.wt, a.bias, a.out, a.st = x.data_ptr(), wt.data_ptr(), b1.data_ptr(), out.data_ptr(), st.data_ptr()
 a.G, a.B, a.Fp, a.Up, a.drop_p, a.train, a.seed = G, B, Fp, Up, 0.5, 1, 1
 a.w2, a.plog, a.C, a.prec = w2.data_ptr(), plog.data_ptr(), C, 1
+ks = L.gt_dense_fwd_splits(Fp)
+part = torch.empty(G * (Up // 64) * ks * 4 * 2 * 64 * 4, device=dev)
+a.w1, a.part, a.ks = w1.data_ptr(), part.data_ptr(), ks
 d = Km.DenseDgradArgs()
 d.dH, d.wt, d.dx, d.G, d.B, d.Fp, d.Up, d.prec = dH.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Fp, Up, 1
 d.w1 = w1.data_ptr()
@@ -69,5 +72,4 @@ for name, fn in (("dense_fwd", lambda s: Km.check(L.gt_dense_fwd(a, ctypes.c_voi
         us = timeit(fn, cold)
         print(json.dumps({"kernel": name, "G": G, "cold": cold, "us": round(us, 1),
                           "w1_GBps": round(wbytes / us / 1e3, 1),
-                          "stream": os.environ.get("GENTUN_DENSE_STREAM", "1"),
-                          "ut": os.environ.get("GENTUN_DENSE_UT", "2")}), flush=True)
+                          }), flush=True)
