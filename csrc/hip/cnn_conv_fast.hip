@@ -1019,6 +1019,7 @@ extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
     if (s2in_ct1_on() && CONV_FAST_MATCH(5, 5, 7, 16, 8, 2, 3) && smallq_th(a, 8, 4) == 4)   // s2 input dgrad
       CONV_FAST_LAUNCH_CT1(5, 5, 7, 16, 4, 2, 3, 4)
     // Genetic-CNN CIFAR-shaped S=(3,5) space, kernels (20, 50), 5x5 stage convs
+    // (8-wave workgroups for these fp32 tiles: 35-40 % slower per launch, r5/conv_f32_nwv8_ab_r5.txt)
     CONV_FAST_CASE_F32_PK(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
     CONV_FAST_CASE_F32_PK(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
     CONV_FAST_CASE_F32(5, 5, 3, 16, 8, 4, 7, 4)   // s2 input conv (20 -> 50)
