@@ -877,12 +877,14 @@ static int g_probe = 0;
   CONV_FAST_LAUNCH_PK(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, PREC_, 0)
 
 // one co tile per wave (CTX 1), fp32, register-direct epilogue
-#define CONV_FAST_LAUNCH_CT1(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_)                                   \
+#define CONV_FAST_LAUNCH_CT1(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_) \
+  CONV_FAST_LAUNCH_CT1S(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1)
+#define CONV_FAST_LAUNCH_CT1S(KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, SCH_)                            \
   {                                                                                                     \
     if (g_probe) return 1000 + TH_;                                                                     \
     dim3 grid(a->B * (a->H / TH_), a->ngroups);                                                         \
     const size_t lds = FastCfg<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, 1>::lds(a->epi_bf16 != 0);          \
-    auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 0, 1, 1, 1>;              \
+    auto* fn = conv_fast_kernel<KH_, KW_, NCBI_, W_, TH_, NT_, NCO_, NWV_, 1, 0, 1, 1, SCH_>;           \
     lds_limit(fn, lds);                                                                                 \
     hipLaunchKernelGGL(fn, grid, dim3(NWV_ * 64), lds, stream, *a);                                     \
     return (int)hipGetLastError();                                                                      \
@@ -1022,10 +1024,14 @@ extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
     // (8-wave workgroups for these fp32 tiles: 35-40 % slower per launch, r5/conv_f32_nwv8_ab_r5.txt)
     CONV_FAST_CASE_F32_PK(5, 5, 1, 32, 8, 2, 3, 4)   // s1 input conv (3 -> 20)
     CONV_FAST_CASE_F32_PK(3, 3, 3, 32, 8, 2, 3, 4)   // s1 nodes / output conv, and their dgrad (20 -> 20)
-    CONV_FAST_CASE_F32(5, 5, 3, 16, 8, 4, 7, 4)   // s2 input conv (20 -> 50)
+    // s2 input conv (20 -> 50): one co tile per wave as well (fwd 84-85 vs 86-90 us, r5/conv_s2n_ct1_ab_r5.txt)
+    if (CONV_FAST_MATCH(5, 5, 3, 16, 8, 4, 7)) CONV_FAST_LAUNCH_CT1S(5, 5, 3, 16, 8, 4, 7, 4, 0)
     // (a packed tile here needs every wave to own all 4 co tiles: 2x the weight traffic per MFMA,
     // measured 20 % slower than the 2 + 2 split -- profiles/conv_f32_packed_tile_ab_r2.txt)
-    CONV_FAST_CASE_F32(3, 3, 7, 16, 8, 4, 7, 4)   // s2 nodes / output conv, and their dgrad (50 -> 50)
+    // s2 nodes / output conv, and their dgrad (50 -> 50): one co tile per wave, all 8 pixel groups (170 VGPRs
+    // at 2 waves/SIMD): half the weight-fragment loads per MFMA of the 2 co x 4 group split, -1 % per
+    // population step at 25 and 80 groups (r5/conv_s2n_ct1_ab_r5.txt; the enforced-pipeline build spills here)
+    if (CONV_FAST_MATCH(3, 3, 7, 16, 8, 4, 7)) CONV_FAST_LAUNCH_CT1S(3, 3, 7, 16, 8, 4, 7, 4, 0)
     if (s2in_ct1_on() && CONV_FAST_MATCH(5, 5, 7, 16, 8, 2, 3)) CONV_FAST_LAUNCH_CT1(5, 5, 7, 16, 8, 2, 3, 4)
     CONV_FAST_CASE_F32_PK(5, 5, 7, 16, 8, 2, 3, 4)   // s2 input conv dgrad (50 -> 20)
     // deep S=(3,4,5) space, kernels (20, 50, 100): stage 3 at 8x8, one image per workgroup
