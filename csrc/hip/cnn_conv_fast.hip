@@ -1041,7 +1041,8 @@ extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
     // wide deep space S=(3,4,5), kernels (64, 128, 256): the whole Cin patch in LDS (up to 154 KB: one
     // workgroup of 8 waves per CU for stages 2-3), 2 co tiles x 4 pixel groups per wave
     CONV_FAST_CASE_F32_NARROW(5, 5, 1, 32, 8, 4, 8, 4)     // s1 input conv (3 -> 64)
-    CONV_FAST_CASE_F32_NARROW(3, 3, 8, 32, 4, 4, 8, 4)     // s1 nodes / output conv, and their dgrad (64 -> 64)
+    // s1 nodes / output conv, and their dgrad (64 -> 64): one co tile per wave (-0.7 % per wide step)
+    if (CONV_FAST_MATCH(3, 3, 8, 32, 4, 4, 8)) CONV_FAST_LAUNCH_CT1S(3, 3, 8, 32, 4, 4, 8, 4, 0)
     // stage 2 (s2 input conv 64 -> 128; nodes / output conv and their dgrad 128 -> 128): one co tile per wave
     // over all 8 pixel groups (-4.3 % per wide population step, r5/conv_s2n_ct1_ab_r5.txt)
     if (CONV_FAST_MATCH(5, 5, 8, 16, 8, 8, 16)) CONV_FAST_LAUNCH_CT1S(5, 5, 8, 16, 8, 8, 16, 8, 0)
