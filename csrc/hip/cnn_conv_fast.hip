@@ -204,7 +204,10 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int WC = NT / CT;                       // waves along co
   constexpr int WP = NWV / WC;                        // waves along pixels
   constexpr int PG = NPG / WP;                      // pixel groups per wave
-  constexpr int PFM = PREC ? 2 : 4;                 // weight prefetch depth (k-steps; 3 planes each in prec 1)
+  // weight prefetch depth (k-steps; 3 planes each in prec 1). The S=(3,5) stage-2 tiles with one co tile per
+  // wave hold 3 k-steps of weights (12 VGPRs each): -0.6 % per population step, 2 and 4 neither
+  // (r5/conv_s2n_ct1_ab_r5.txt)
+  constexpr int PFM = PREC ? ((CTX == 1 && !SCH && NWV == 4 && NCBI <= 7) ? 3 : 2) : 4;
   constexpr int PF = NKS < PFM ? NKS : PFM;
   // fp32 enforced pipeline (SCH): the weights of k-step s+PF load into the ring slot k-step s-1 used, so
   // no load waits for an MFMA still reading its registers
