@@ -65,10 +65,10 @@ struct DenseFwdArgs {
   long wps;                // unused (kept for the ABI)
   int row_off;             // data parallelism (X5): this rank's first row of the full batch (dropout keys)
   // split-K forward (dense_fwd_sk_kernel): W1 read from the fp32 master [G][Fp][Up] itself, KS
-  // feature splits per output tile, partial tiles in `part`, per-tile arrival counters in `cnt`
+  // feature splits per output tile, partial tiles in `part` (summed in range order by dense_fwd_skred_kernel)
   const float* w1;
   float* part;             // [G][ceil(B/32)][Up/64][KS][4][2][64] f32x4 range partials
-  int* cnt;                // unused (reserved)
+  int* cnt;                // unused, 0 (ABI: the round-4 last-workgroup reduction's arrival counters)
   int ks;
 };
 

@@ -286,6 +286,12 @@ __global__ void level0_kernel(Geo geo, const int* __restrict__ nroot, LNode* __r
 // shifted 2^60. Decode: count = word & (2^17 - 1), sum qg = word >> 17 (arithmetic). The image is
 // 32 features x 258 words = 66 KB (2 workgroups per CU): twice the features per workgroup of the
 // (g, h) image halves the row-id / gradient gathers per bin row (round 5: 590 -> 380 us per level).
+// Resolution: lg_n >= 32 puts each row's gradient on a grid of 2^-29 * 2^ceil(log2 max|g|) (fx_exp),
+// instead of 2^-(61 - lg_n) at the real row count -- 2^12 coarser at 1M rows. A gradient 10^6 times
+// smaller than the largest one still keeps ~9 significant bits; rounding is to nearest, so the
+// per-bin error is unbiased and at most n_bin / 2 grid steps. Histograms stay exact integer sums of
+// those values (bitwise-reproducible). tests/test_gbdt_gpu.py::test_hip_outlier_gradients_match_cpu
+// pins a target whose gradients span 5 orders of magnitude against the CPU engine's fp64 sums.
 #define HB_GSTRIDE 258   // int64 per feature in the gradient-only image (256 bins + pad)
 #define HB_CBITS 17
 static_assert(GB_R < (1 << HB_CBITS), "packed counts must not carry into the gradient bits");

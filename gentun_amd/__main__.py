@@ -77,6 +77,27 @@ def _device():
     return torch.device("cpu")
 
 
+def _release_evaluators(population, timeout_s):
+    """Best-effort CMD_STOP to the evaluator ranks from a daemon thread, waited for at most
+    ``timeout_s`` (returns whether it completed)."""
+    import threading
+    done = []
+
+    def stop():
+        try:
+            population.shutdown()
+            done.append(True)
+        except Exception:  # noqa: BLE001 -- the original error is what gets reported
+            pass
+
+    t = threading.Thread(target=stop, daemon=True)
+    t.start()
+    t.join(timeout_s)
+    if done:
+        sys.stderr.write("[gentun] search aborted; evaluators released\n")
+    return bool(done)
+
+
 def _run_search(args, species, x, y, extra, maximize):
     from . import GeneticAlgorithm, RussianRouletteGA
     from .metrics import EventLog
@@ -135,6 +156,13 @@ def _run_search(args, species, x, y, extra, maximize):
         finally:
             sys.stderr.write("[gentun] search failed; evaluators released\n")
         raise SearchFailed()
+    except Exception:
+        # Under torchrun the agent tears the group down. A plain MASTER_ADDR / RANK launch has no
+        # agent: the evaluator ranks would wait in the next dispatch broadcast until the collective
+        # timeout, so try to release them (bounded: a dead peer can make the broadcast hang too).
+        if not os.environ.get("TORCHELASTIC_USE_AGENT_STORE"):
+            _release_evaluators(ga.population, timeout_s=30.0)
+        raise
     ga.population.shutdown()
     comm.finish()
     out = {"best_fitness": best.get_fitness(), "best_genes": best.get_genes(),

@@ -61,12 +61,37 @@ def check_hw_queues(nstreams, env=None):
     replay, 3 crash; profiles/r5/hwq3_graph_crash_r5.log), so it is the runtime's, not this
     engine's; the population step graph forks onto 1 + WGRAD_STREAMS side streams. A clear error
     instead of the crash (verdict r4 item 6a)."""
-    v = (os.environ if env is None else env).get("GPU_MAX_HW_QUEUES", "")
-    if v.strip().isdigit() and int(v) < nstreams:
+    if not hw_queues_ok(nstreams, env):
+        v = (os.environ if env is None else env).get("GPU_MAX_HW_QUEUES", "")
         raise RuntimeError(
             "GPU_MAX_HW_QUEUES={} is below the {} streams of the captured step graph: HIP's graph launch "
             "segfaults there (torch-only repro: tools/probe_hwq.py). Use GPU_MAX_HW_QUEUES >= {} (HIP's "
             "default is 4) or eager steps (TrainConfig use_graph=False)".format(int(v), nstreams, nstreams))
+
+def hw_queues_ok(nstreams, env=None):
+    """False when ``GPU_MAX_HW_QUEUES`` is set below ``nstreams`` (see :func:`check_hw_queues`)."""
+    v = (os.environ if env is None else env).get("GPU_MAX_HW_QUEUES", "")
+    return not (v.strip().isdigit() and int(v) < nstreams)
+
+
+_HWQ_WARNED = []
+
+
+def graph_or_eager(nstreams, env=None):
+    """Whether a job may capture its step graph: with too few hardware queues it trains with eager
+    steps instead (same launches, bit-identical results) and says so once per process -- a queue
+    setting must not fail every candidate of a search."""
+    if hw_queues_ok(nstreams, env):
+        return True
+    if not _HWQ_WARNED:
+        _HWQ_WARNED.append(1)
+        import warnings
+        v = (os.environ if env is None else env).get("GPU_MAX_HW_QUEUES", "")
+        warnings.warn("GPU_MAX_HW_QUEUES={} is below the {} streams of the captured step graph (HIP's graph "
+                      "launch segfaults there): training with eager steps instead".format(v.strip(), nstreams),
+                      RuntimeWarning, stacklevel=3)
+    return False
+
 
 class TrainConfig(object):
     def __init__(self, epochs=(3,), learning_rate=(1e-3,), batch_size=32, dropout=0.5, loss="bce_compat",
@@ -421,6 +446,7 @@ class FoldJob(object):
         # profiles/graph_vs_eager_ab_r4.txt)
         ug = True if self.cfg.use_graph is None else bool(self.cfg.use_graph)
         use_graph = ug and self.device.type == "cuda" and getattr(self, "capture_ok", True)
+        use_graph = use_graph and graph_or_eager(getattr(self, "graph_streams", 1))
         ctx = torch.cuda.stream(self.stream) if self.stream is not None else _nullctx()
         timed = self.device.type == "cuda"
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None

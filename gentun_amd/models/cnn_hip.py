@@ -365,14 +365,14 @@ class HipPopJob(FoldJob):
         self.adam_nblocks = len(blocks)
 
     def _dense_sk_buffers(self, df, rows):
-        """Range partials and arrival counters of a split-K dense forward at
-        ``rows`` batch rows (training and evaluation launches get their own)."""
+        """Range partials of a split-K dense forward at ``rows`` batch rows (training and evaluation
+        launches get their own); a separate reduce launch sums them, so ``cnt`` (the arrival
+        counters of the round-4 last-workgroup reduction) stays in the ABI, unused and 0."""
         nby, nut = -(-rows // 32), self.Up // 64
         part = torch.empty((self.Q * nby * nut * max(1, df.ks) * 4 * 2 * 64 * 4,), dtype=torch.float32,
                            device=self.device)
-        cnt = torch.zeros((self.Q * nby * nut,), dtype=torch.int32, device=self.device)
-        self._keep += [part, cnt]
-        df.part, df.cnt = part.data_ptr(), cnt.data_ptr()
+        self._keep.append(part)
+        df.part, df.cnt = part.data_ptr(), 0
 
     def _conv_args(self, L, in_ptrs, out_ptrs, mask_ptrs, w, bias, relu, rows, gather=None, Cinp=None, Coutp=None):
         a = K.ConvArgs()

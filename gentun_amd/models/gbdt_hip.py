@@ -3,9 +3,11 @@ predict kernels on the GPU (csrc/hip/gbdt_hist.hip: row-major bins, per-node
 row segments, smaller-child histograms + subtraction). Used by
 :func:`gentun_amd.models.gbdt.cv` when ``device`` is a CUDA/HIP device;
 every objective (regression, logistic, binary, multi-class) and every metric
-but auc run on the GPU; auc falls back to the CPU engine."""
+but auc run on the GPU; an auc run falls back to the CPU engine with a one-time
+``RuntimeWarning`` (never silently)."""
 
 import ctypes
+import warnings
 
 import numpy as np
 
@@ -112,8 +114,24 @@ def device_bins(x, key, fs):
     return out
 
 
+_WARNED = set()
+
+
+def _warn_fallback(obj, marr):
+    key = (int(obj), tuple(int(m) for m in marr))
+    if key in _WARNED:
+        return
+    _WARNED.add(key)
+    from .gbdt import METRICS
+    names = sorted(n for n, v in METRICS.items() if v in key[1] and v not in GPU_METRICS)
+    warnings.warn("gbdt.cv(device='cuda'): eval_metric {} has no GPU implementation; this cross-validation "
+                  "runs on the CPU engine (csrc/gbdt/engine.cpp)".format(", ".join(names) or key[1]),
+                  RuntimeWarning, stacklevel=3)
+
+
 def cv(x, y, fold_of, nfold, parr, obj, num_class, marr, nrounds, esr, seed, hist, x_key=None):
     if not supported(obj, marr):
+        _warn_fallback(obj, marr)
         return None
     xk = x if x_key is None else x_key
     fold_of = np.ascontiguousarray(fold_of.astype(np.int32))

@@ -70,8 +70,14 @@ def test_cli_maps_only_all_failed_to_the_final_exit(monkeypatch, tmp_path, exc, 
             cli.main(argv)
         assert e.value.code == EXIT_SEARCH_FAILED
     else:
+        # without a torchrun agent the evaluator ranks are released before the error propagates
+        from gentun_amd.parallel.distributed import DistributedPopulation
+        calls = []
+        monkeypatch.delenv("TORCHELASTIC_USE_AGENT_STORE", raising=False)
+        monkeypatch.setattr(DistributedPopulation, "shutdown", lambda self: calls.append(1))
         with pytest.raises(OSError):
             cli.main(argv)
+        assert calls == [1]
 
 
 def test_every_env_variable_is_registered():
@@ -103,3 +109,19 @@ def test_graph_capture_refuses_fewer_hw_queues_than_streams():
         cnn_engine.check_hw_queues(n, env={"GPU_MAX_HW_QUEUES": "3"})
     cnn_engine.check_hw_queues(n, env={"GPU_MAX_HW_QUEUES": "4"})
     cnn_engine.check_hw_queues(n, env={})
+
+
+def test_too_few_hw_queues_trains_eagerly_with_one_warning():
+    """A job's launch() does not capture with too few hardware queues: it warns once and runs eager
+    steps (a queue setting must not fail every candidate of a search)."""
+    import warnings
+    import pytest
+    from gentun_amd.models import cnn_engine, cnn_hip
+    n = 2 + cnn_hip.WGRAD_STREAMS
+    del cnn_engine._HWQ_WARNED[:]
+    assert cnn_engine.graph_or_eager(n, env={"GPU_MAX_HW_QUEUES": "8"})
+    with pytest.warns(RuntimeWarning, match="eager steps"):
+        assert not cnn_engine.graph_or_eager(n, env={"GPU_MAX_HW_QUEUES": "2"})
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert not cnn_engine.graph_or_eager(n, env={"GPU_MAX_HW_QUEUES": "2"})

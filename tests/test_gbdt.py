@@ -136,3 +136,22 @@ def test_unsupported_booster_and_unknown_params_raise():
     with pytest.raises(ValueError, match="unsupported GBDT parameter"):
         gbdt.cv({"max_leaves": 8}, x, y, num_boost_round=2, nfold=2)
     gbdt.cv({"booster": "gbtree", "silent": 1, "eval_metric": "rmse"}, x, y, num_boost_round=2, nfold=2)
+
+
+def test_gpu_auc_falls_back_loudly():
+    """eval_metric auc has no GPU implementation: device='cuda' must say (once) that the CV runs on
+    the CPU engine instead of silently changing device. The check in
+    gbdt_hip.cv happens before any device call, so it runs on CPU-only hosts too."""
+    import warnings
+    from gentun_amd.models import gbdt_hip
+    x, y = load_iris_xy()
+    yb = (y == 2).astype(np.float64)
+    gbdt_hip._WARNED.clear()
+    p = {'objective': 'binary:logistic', 'eval_metric': 'auc'}
+    with pytest.warns(RuntimeWarning, match="auc has no GPU implementation"):
+        h = gbdt.cv(dict(p), x, yb, num_boost_round=5, nfold=3, device='cuda')
+    ref = gbdt.cv(dict(p), x, yb, num_boost_round=5, nfold=3)
+    assert h['test-auc-mean'] == ref['test-auc-mean']          # the CPU engine's result
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")                         # once per (objective, metrics)
+        gbdt.cv(dict(p), x, yb, num_boost_round=5, nfold=3, device='cuda')

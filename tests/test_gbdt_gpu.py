@@ -137,3 +137,22 @@ def test_hip_subsample_colsample_multiclass_streams_match_cpu():
     gpu = gbdt.cv(p, x, y, num_boost_round=30, nfold=3, seed=3, device="cuda:0")
     a, b = np.array(cpu['test-mlogloss-mean']), np.array(gpu['test-mlogloss-mean'])
     assert np.max(np.abs(a - b) / a) < 0.01, (a[-3:], b[-3:])
+
+
+def test_hip_outlier_gradients_match_cpu():
+    """Squared error packs the row count into the gradient word, which coarsens each row's
+    fixed-point gradient to 2^-29 of the largest (csrc/hip/gbdt_hist.hip, HC block):
+    a target whose gradients span ~5 orders of magnitude (a few rows 10^5 x the rest) must still
+    give the CPU engine's trees, i.e. the same error history on the bulk of the rows."""
+    rs = np.random.RandomState(7)
+    x = rs.rand(20000, 8).astype(np.float32)
+    y = (np.sin(6 * x[:, 0]) + x[:, 1] ** 2 + 0.05 * rs.randn(20000)).astype(np.float32)
+    out = rs.choice(20000, 20, replace=False)
+    y[out] += (1e5 * np.sign(rs.randn(20))).astype(np.float32)
+    p = {'objective': 'reg:linear', 'eta': 0.3, 'max_depth': 6, 'eval_metric': 'mae'}
+    cpu = gbdt.cv(dict(p), x, y, num_boost_round=30, nfold=3, seed=0)
+    gpu = gbdt.cv(dict(p), x, y, num_boost_round=30, nfold=3, seed=0, device="cuda:0")
+    for k in ('train-mae-mean', 'test-mae-mean'):
+        a, b = np.array(cpu[k]), np.array(gpu[k])
+        assert len(a) == len(b)
+        assert np.max(np.abs(a - b) / a) < 0.01, (k, a[-5:], b[-5:])

@@ -37,13 +37,14 @@ DP_ORDER_FACTOR = 8.0
 DP_MAX_DRIFT = 5e-4
 
 
-def _job(dp_group=None):
+def _job(dp_group=None, hw=32):
+    # hw 28: MNIST-sized images, stored zero-padded to 32 x 32 (the padded fast path)
     from gentun_amd.models import cnn_engine as E
     from gentun_amd.models.genome import make_plan
     from gentun_amd.utils.data import make_image_classification, stratified_kfold
-    x, y = make_image_classification(n=520, shape=(32, 32, 3), classes=10, seed=3, noise=0.35, shift=3)
+    x, y = make_image_classification(n=520, shape=(hw, hw, 3), classes=10, seed=3, noise=0.35, shift=3)
     folds = stratified_kfold(np.argmax(y, 1), 2, seed=0)     # 260 training rows: a short last batch
-    plans = [make_plan(g, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10)
+    plans = [make_plan(g, (3, 5), (hw, hw, 3), (20, 50), ((5, 5), (5, 5)), 500, 10)
              for g in ({'S_1': '101', 'S_2': '0101110011'}, {'S_1': '000', 'S_2': '1000000001'})]
     # SGD: Adam turns the summation-order noise of near-zero gradients into +-lr steps (sign flips), which
     # would hide a real mismatch; with SGD-momentum the two trajectories must agree to fp32 rounding
@@ -52,13 +53,13 @@ def _job(dp_group=None):
     return E.make_population_job("hip", [(p, folds, [0, 1]) for p in plans], x, y, cfg, torch.device("cuda", 0))
 
 
-def _reordered_single():
+def _reordered_single(hw):
     """The single-process run with every specialised conv wgrad summed in another split order."""
     from gentun_amd.ops import cnn_kernels as K
     old = K.WGRAD_FAST_SPLITS
     K.WGRAD_FAST_SPLITS = 4
     try:
-        return _train(_job())
+        return _train(_job(hw=hw))
     finally:
         K.WGRAD_FAST_SPLITS = old
 
@@ -70,49 +71,50 @@ def _train(job):
     return job.flat.detach().cpu().clone(), res
 
 
-def _worker(rank, port, out, ct1):
+def _worker(rank, port, out, ct1, hw):
     import torch.distributed as dist
     from gentun_amd.ops import cnn_kernels as K
     torch.cuda.set_device(0)
     K.lib().gt_conv_set_s2in_ct1(int(ct1))
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:{}".format(port), rank=rank, world_size=2)
     try:
-        flat, res = _train(_job(dp_group=dist.group.WORLD))
+        flat, res = _train(_job(dp_group=dist.group.WORLD, hw=hw))
         torch.save({"flat": flat, "cat": [r["categorical_accuracy"] for r in res]},
                    os.path.join(out, "rank{}.pt".format(rank)))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ct1", ["1", "0"])
-def test_two_rank_hip_data_parallel_matches_single_process(ct1):
-    # ct1: the stage-2 input-conv dgrad with one co tile per wave (the default) or the packed tile
+@pytest.mark.parametrize("ct1,hw", [("1", 32), ("0", 32), ("1", 28)])
+def test_two_rank_hip_data_parallel_matches_single_process(ct1, hw):
+    # ct1: the stage-2 input-conv dgrad with one co tile per wave (the default) or the packed tile;
+    # hw 28: the zero-padded MNIST geometry on two ranks
     from gentun_amd.ops import cnn_kernels as K
     old = K.lib().gt_conv_set_s2in_ct1(int(ct1))
     try:
-        _compare(ct1)
+        _compare(ct1, hw)
     finally:
         K.lib().gt_conv_set_s2in_ct1(old)
 
 
-def _compare(ct1):
-    single, sres = _train(_job())
-    again, _ = _train(_job())
+def _compare(ct1, hw):
+    single, sres = _train(_job(hw=hw))
+    again, _ = _train(_job(hw=hw))
     assert torch.equal(single, again)                       # the executor itself is deterministic
-    reorder, _ = _reordered_single()
+    reorder, _ = _reordered_single(hw)
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(port, d, ct1), nprocs=2, join=True)
+        mp.spawn(_worker, args=(port, d, ct1, hw), nprocs=2, join=True)
         r0 = torch.load(os.path.join(d, "rank0.pt"), weights_only=True)
         r1 = torch.load(os.path.join(d, "rank1.pt"), weights_only=True)
     assert torch.equal(r0["flat"], r1["flat"])              # identical optimizer steps on every rank
     scale = single.abs().max().item()
     d_dp = (r0["flat"] - single).abs().max().item() / scale
     d_order = (reorder - single).abs().max().item() / scale
-    line = "[dp] ct1={} relative drift: data-parallel {:.3e}, single-process split reorder {:.3e}, ratio {:.2f}".format(
-        ct1, d_dp, d_order, d_dp / max(d_order, 1e-30))
+    line = "[dp] ct1={} hw={} relative drift: data-parallel {:.3e}, single-process split reorder {:.3e}, ratio {:.2f}".format(
+        ct1, hw, d_dp, d_order, d_dp / max(d_order, 1e-30))
     print(line)
     if os.environ.get("GENTUN_DP_RECORD"):
         with open(os.environ["GENTUN_DP_RECORD"], "a") as f:

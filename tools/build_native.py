@@ -110,6 +110,31 @@ def hipcc():
     return None
 
 
+class _BuildLock(object):
+    """Exclusive ``fcntl.flock`` on ``<OUT>/.<name>.lock`` around one target's
+    staleness check + build: under ``torchrun`` every rank loads the library
+    at start-up, and on a cold or stale tree they would otherwise run hipcc
+    concurrently into the same object files. The first rank builds, the others
+    block, then find the library fresh and load it."""
+
+    def __init__(self, name):
+        os.makedirs(OUT, exist_ok=True)
+        self.path = os.path.join(OUT, "." + name + ".lock")
+        self.fd = None
+
+    def __enter__(self):
+        import fcntl
+        self.fd = os.open(self.path, os.O_RDWR | os.O_CREAT, 0o666)
+        fcntl.flock(self.fd, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+        fcntl.flock(self.fd, fcntl.LOCK_UN)
+        os.close(self.fd)
+        return False
+
+
 def build_target(name, verbose=False, force=False):
     spec = TARGETS[name]
     srcs = [_abs(s) for s in spec["sources"]]
@@ -118,7 +143,14 @@ def build_target(name, verbose=False, force=False):
     lib = os.path.join(OUT, name)
     if not force and not _stale(name, lib):
         return lib
-    os.makedirs(OUT, exist_ok=True)
+    with _BuildLock(name):
+        # re-checked under the lock: another process may have built it while this one waited
+        if not force and not _stale(name, lib):
+            return lib
+        return _build_locked(name, spec, srcs, lib, verbose)
+
+
+def _build_locked(name, spec, srcs, lib, verbose):
     tmp = lib + ".tmp.{}".format(os.getpid())
     want = source_hash(name)
     hflag = ['-DGT_SRC_HASH="{}"'.format(want)]
@@ -128,8 +160,9 @@ def build_target(name, verbose=False, force=False):
         cc = hipcc()
         if cc is None:
             raise RuntimeError("hipcc not found; cannot build {}".format(name))
-        # one object per translation unit, compiled in parallel, then linked
-        objdir = os.path.join(ROOT, "build", "obj_" + name.split(".")[0])
+        # one object per translation unit, compiled in parallel, then linked (per-pid object
+        # directory: nothing outside the lock ever sees a half-written object)
+        objdir = os.path.join(ROOT, "build", "obj_{}_{}".format(name.split(".")[0], os.getpid()))
         os.makedirs(objdir, exist_ok=True)
         comp = [cc] + [f for f in _flags("hip") if f != "-shared"] + hflag + ["-I", os.path.join(ROOT, "csrc", "hip")]
         objs, cmds = [], []
@@ -148,9 +181,16 @@ def build_target(name, verbose=False, force=False):
     if verbose:
         print("[build]", " ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=ROOT)
-    os.replace(tmp, lib)
-    with open(_stamp(lib), "w") as f:
+    if spec["kind"] == "hip":
+        shutil.rmtree(objdir, ignore_errors=True)
+    # the stamp goes first, atomically, then the library: a reader that sees the new library also
+    # sees its stamp (a stamp newer than the library only triggers a rebuild check, which the
+    # embedded hash then settles)
+    stmp = _stamp(lib) + ".tmp.{}".format(os.getpid())
+    with open(stmp, "w") as f:
         f.write(want + "\n")
+    os.replace(stmp, _stamp(lib))
+    os.replace(tmp, lib)
     return lib
 
 
