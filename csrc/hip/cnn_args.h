@@ -62,6 +62,9 @@ struct ConvArgs {
   // FORWARD epilogue; every other kernel then sees zeros there (the data gradient's ReLU / pool masks
   // zero the gradient, the dense W1 rows of padded pixels stay 0), so results equal the unpadded network
   int Hr, Wr;
+  // 1: a 3x3 fp32 layer on the Winograd F(2x2, 3x3) kernels (cnn_conv_wino.hip); `w` then holds the
+  // transformed weight planes [3][Q][16][R][K] written by gt_wino_wtrans, never the direct planes
+  int wino;
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

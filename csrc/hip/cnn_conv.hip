@@ -717,7 +717,10 @@ int gt_conv_set_fast(int on) {
   return old;
 }
 
+int gt_conv_wino(const ConvArgs* a, hipStream_t stream, int probe);
+
 int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
+  if (a->wino) return gt_conv_wino(a, stream, 0);   // transformed weight planes: Winograd kernels only
   if (a->Cinp % 8 || a->Coutp % 8) return -1;
   if (a->prec != 0 && a->prec != 1) return -1;
   if (g_conv_fast && a->ngroups >= 1) {

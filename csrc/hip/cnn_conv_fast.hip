@@ -998,8 +998,11 @@ static int smallq_th(const ConvArgs* a, int TH, int THMIN) {
 }
 
 #ifndef GT_KERNELS_ONLY   // (tools/isa_one.sh: one explicit instantiation, no dispatch tables)
+extern "C" int gt_conv_wino(const ConvArgs* a, hipStream_t stream, int probe);
+
 extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
   const ConvArgs* a = a_in;
+  if (a->wino) return gt_conv_wino(a, stream, g_probe);   // Winograd 3x3 layers (cnn_conv_wino.hip)
   if (a->mask) return -100;                  // staged ReLU mask: generic kernel only
   if (a->prec == 1) {
     // small launches: shorter tiles of the S=(3,5) shapes (see smallq_th)

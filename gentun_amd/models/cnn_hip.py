@@ -66,6 +66,12 @@ POOL_FUSE = True
 # False: the Python issue path per step (what a captured step graph records)
 NATIVE_STEPS = True
 
+# fp32 3x3 layers with a Winograd F(2x2, 3x3) instantiation (csrc/hip/cnn_conv_wino.hip: the stage-2 node /
+# output convs of the S=(3,5) space) run their forward and data gradient on it, with the transformed
+# weights re-derived from the fp32 masters after every optimizer step. Module constant, not a switch: tests
+# flip it to compare against the direct kernels.
+WINOGRAD = True
+
 # bytes of forward-only activation twins an evaluation may allocate for all groups of a job
 EVAL_TWIN_BUDGET = 1 << 30
 
@@ -297,11 +303,23 @@ class HipPopJob(FoldJob):
                 self.views[kind] = view
             off += n
         npl = self.npl
+        wsegs = []
         for L in self.layers:
             L.w_bf = torch.zeros((npl, Q, L.coutp, L.KH, L.KW, L.cinp), dtype=torch.bfloat16, device=dev)
             L.wT_bf = torch.zeros((npl, Q, L.cinp, L.KH, L.KW, L.coutp), dtype=torch.bfloat16, device=dev)
+            # Winograd layers: transformed weight planes of the forward and of the data gradient
+            L.wino = bool(WINOGRAD and self.prec == 1 and (L.KH, L.KW) == (3, 3) and
+                          self.L.gt_conv_wino_supported(L.cinp, L.coutp, L.H, L.W) and
+                          self.L.gt_conv_wino_supported(L.coutp, L.cinp, L.H, L.W))
+            if L.wino:
+                R, Kc = K.wino_dims(L.cinp, L.coutp)
+                L.wU = torch.zeros((3, Q, 16, R, Kc), dtype=torch.bfloat16, device=dev)
+                R, Kc = K.wino_dims(L.coutp, L.cinp)
+                L.wUT = torch.zeros((3, Q, 16, R, Kc), dtype=torch.bfloat16, device=dev)
+                wsegs += [K.wino_segment(L.w[0], L.wU, False), K.wino_segment(L.w[0], L.wUT, True)]
             L.part_w = torch.zeros((L.S, Q, L.coutp, L.Kdim), dtype=torch.float32, device=dev)   # split-K partials
             L.part_b = torch.zeros((L.S, Q, L.coutp), dtype=torch.float32, device=dev)
+        self.wino_tr = K.WinoTransform(wsegs, dev) if wsegs else None
         self.gW2 = torch.zeros((Q, self.Up, self.classes), dtype=torch.float32, device=dev)
         self.gb2 = torch.zeros((Q, self.classes), dtype=torch.float32, device=dev)
         self.gb1 = torch.zeros((Q, self.Up), dtype=torch.float32, device=dev)
@@ -432,9 +450,10 @@ class HipPopJob(FoldJob):
             pools = pool_of.get(L.name, set())
             cpools = set() if self.bn else pools
             a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [out.data_ptr()], [],
-                                L.w_bf, L.b[0], 0 if self.bn else 1,
+                                L.wU if L.wino else L.w_bf, L.b[0], 0 if self.bn else 1,
                                 [(q, im, 1 | ((1 << 24) if q in cpools else 0)) for q, im in L.rows],
                                 gather=gather_train if first else None)
+            a.wino = 1 if L.wino else 0
             if L.xin is not None:
                 a.xsum = self.act[L.xin].data_ptr()
             if self.pad_hw is not None:
@@ -608,9 +627,10 @@ class HipPopJob(FoldJob):
                 def dgrad_args(unpool):
                     a = self._conv_args(L, [self.grad[L.name].data_ptr()],
                                         [self._slot_ptr(n, grad=True) for n in L.slots],
-                                        [self._slot_ptr(n) for n in L.slots], L.wT_bf, None, 0,
-                                        [(q, 1, of | ((1 << 25) if unpool else 0)) for q, of in rows],
+                                        [self._slot_ptr(n) for n in L.slots], L.wUT if L.wino else L.wT_bf,
+                                        None, 0, [(q, 1, of | ((1 << 25) if unpool else 0)) for q, of in rows],
                                         Cinp=L.coutp, Coutp=L.cinp)
+                    a.wino = 1 if L.wino else 0
                     if unpool:
                         st = pool_stage[L.slots[0]]
                         a.pool_y, a.pool_mask = self.grad[st.inp].data_ptr(), st.pmask.data_ptr()
@@ -699,6 +719,8 @@ class HipPopJob(FoldJob):
             w = L.w[0]
             L.w_bf.copy_(split_planes(w, self.npl))
             L.wT_bf.copy_(split_planes(w.flip(2, 3).permute(0, 4, 2, 3, 1), self.npl))
+        if self.wino_tr is not None:
+            self.wino_tr.run(self._stream())
 
     def reset_optimizer(self, lr):
         self.m.zero_()
@@ -846,7 +868,12 @@ class HipPopJob(FoldJob):
         return plan
 
     def _adam_plan(self):
-        return [("k", "gt_adam_segments", (self.adam_args, self.adam_nblocks), None, "adam")]
+        plan = [("k", "gt_adam_segments", (self.adam_args, self.adam_nblocks), None, "adam")]
+        if self.wino_tr is not None:
+            # the next step's Winograd layers convolve with the transform of the updated masters
+            plan.append(("k", "gt_wino_wtrans", (K.C.addressof(self.wino_tr.args), self.wino_tr.nblocks), None,
+                         "wino_wtrans"))
+        return plan
 
     def _exec_plan(self, plan):
         L = self.L

@@ -37,7 +37,24 @@ class ConvArgs(C.Structure):
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
                 ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long),
                 ("cbb", I), ("pool_y", P), ("pool_mask", P), ("unpool_x1", P), ("unpool_sel", P),
-                ("cout_real", I), ("Hr", I), ("Wr", I)]
+                ("cout_real", I), ("Hr", I), ("Wr", I), ("wino", I)]
+
+
+class WinoWSeg(C.Structure):
+    """csrc/hip/cnn_conv_wino.hip WinoWSeg: one layer's Winograd weight transform (forward or the
+    data gradient's flipped / transposed kernel)."""
+    _fields_ = [("w", P), ("u", P), ("ups", C.c_long), ("Q", I), ("Cop", I), ("Cip", I), ("R", I), ("K", I),
+                ("dgrad", I), ("pad", I)]
+
+
+class WinoWArgs(C.Structure):
+    _fields_ = [("segs", P), ("blocks", P)]
+
+
+def wino_dims(cinp, coutp):
+    """(rows, columns) of a layer's transformed weight planes [3][Q][16][rows][columns]: output
+    channels padded to 16 (one MFMA row tile), input channels to 32 (one k-step)."""
+    return -(-coutp // 16) * 16, -(-cinp // 32) * 32
 
 
 class WgradArgs(C.Structure):
@@ -116,7 +133,7 @@ class ProgOp(C.Structure):
 PROG_OPS = {"record": 0, "wait": 1, "gt_step_begin": 2, "gt_conv_fwd": 3, "gt_conv_wgrad": 4,
             "gt_wgrad_reduce": 5, "gt_bn_fwd": 6, "gt_bn_bwd": 7, "gt_dense_fwd": 8, "gt_head": 9,
             "gt_dense_dgrad": 10, "gt_dense_wgrad_adam": 11, "gt_adam_segments": 12, "gt_pool_fwd": 13,
-            "gt_pool_fwd_mask": 14, "gt_pool_bwd_mask": 15}
+            "gt_pool_fwd_mask": 14, "gt_pool_bwd_mask": 15, "gt_wino_wtrans": 16}
 
 
 class InitSeg(C.Structure):
@@ -169,6 +186,12 @@ def lib():
         L.gt_conv_fast_probe_any.restype = I
         L.gt_wgrad_reduce.argtypes = [C.POINTER(WgradArgs), P]
         L.gt_wgrad_reduce.restype = I
+        L.gt_conv_wino_supported.argtypes = [I, I, I, I]
+        L.gt_conv_wino_supported.restype = I
+        L.gt_wino_wtrans.argtypes = [P, I, P]
+        L.gt_wino_wtrans.restype = I
+        L.gt_sizeof_wino_wseg.restype = C.c_size_t
+        assert L.gt_sizeof_wino_wseg() == C.sizeof(WinoWSeg), "WinoWSeg ABI mismatch"
         L.gt_conv_set_fast.argtypes = [I]
         L.gt_conv_set_fast.restype = I
         L.gt_conv_set_nwv.argtypes = [I]
@@ -293,6 +316,64 @@ def conv_tile_rows(H, W, tile_pixels=None):
     if W > tp:
         raise ValueError("image width > {} not supported by conv_fwd tiles".format(tp))
     return max(1, min(H, tp // W))
+
+
+def wino_segment(master, planes, dgrad):
+    """WinoWSeg of one layer: fp32 master weights ``[Q][Cop][3][3][Cip]`` -> transformed bf16 planes
+    ``[3][Q][16][R][K]`` (R, K = :func:`wino_dims` of the forward, swapped for the data gradient)."""
+    Q, cop, kh, kw, cip = master.shape
+    assert (kh, kw) == (3, 3) and master.dtype.is_floating_point and master.is_contiguous()
+    R, Kc = (wino_dims(cop, cip) if dgrad else wino_dims(cip, cop))
+    assert tuple(planes.shape) == (3, Q, 16, R, Kc) and planes.is_contiguous(), (planes.shape, (3, Q, 16, R, Kc))
+    sg = WinoWSeg()
+    sg.w, sg.u, sg.ups = master.data_ptr(), planes.data_ptr(), planes[0].numel()
+    sg.Q, sg.Cop, sg.Cip, sg.R, sg.K, sg.dgrad = Q, cop, cip, R, Kc, 1 if dgrad else 0
+    return sg
+
+
+class WinoTransform(object):
+    """One launch that re-transforms the Winograd weights of several layers (both directions) from
+    their fp32 masters -- after every optimizer step and after initialisation."""
+
+    def __init__(self, segs, device):
+        import numpy as np
+        import torch
+        self.nseg = len(segs)
+        blocks = []
+        for i, sg in enumerate(segs):
+            n = sg.Q * sg.R * sg.K
+            blocks.extend((i, o) for o in range(0, n, 256))
+        arr = (WinoWSeg * max(1, len(segs)))(*segs)
+        self.segs_t = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8).to(device)
+        self.blocks_t = torch.tensor(np.asarray(blocks, np.int32).reshape(-1, 2), device=device)
+        self.args = WinoWArgs()
+        self.args.segs, self.args.blocks = self.segs_t.data_ptr(), self.blocks_t.data_ptr()
+        self.nblocks = len(blocks)
+
+    def run(self, stream):
+        if self.nblocks:
+            check(lib().gt_wino_wtrans(C.addressof(self.args), self.nblocks, stream), "wino_wtrans")
+
+
+def wino_unpack(planes):
+    """Logical ``[3][Q][16][R][K]`` view of fragment-major transformed planes (the layout
+    gt_wino_wtrans writes: per (xi, 16-row tile, 32-column k-step) one 64-lane x 8-value fragment,
+    lane = (column % 32) // 8 * 16 + row % 16)."""
+    npl, Q, nxi, R, Kc = planes.shape
+    f = planes.reshape(npl, Q, nxi, R // 16, Kc // 32, 4, 16, 8)     # [.., rt, ks, kq, l16, e]
+    return f.permute(0, 1, 2, 3, 6, 4, 5, 7).reshape(npl, Q, nxi, R, Kc)
+
+
+def wino_weights(master, dgrad=False, stream=None):
+    """Transformed planes of ``master`` (tests / one-off use; jobs keep a :class:`WinoTransform`)."""
+    import torch
+    Q, cop, _, _, cip = master.shape
+    R, Kc = wino_dims(cop, cip) if dgrad else wino_dims(cip, cop)
+    planes = torch.zeros((3, Q, 16, R, Kc), dtype=torch.bfloat16, device=master.device)
+    tr = WinoTransform([wino_segment(master.contiguous(), planes, dgrad)], master.device)
+    tr.run(torch.cuda.current_stream(master.device).cuda_stream if stream is None else stream)
+    tr.keep = planes
+    return planes
 
 
 def padded_hw(h, w, nstages, batch_norm=False):

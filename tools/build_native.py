@@ -182,7 +182,10 @@ def _build_locked(name, spec, srcs, lib, verbose):
         print("[build]", " ".join(cmd), flush=True)
     subprocess.check_call(cmd, cwd=ROOT)
     if spec["kind"] == "hip":
-        shutil.rmtree(objdir, ignore_errors=True)
+        # the objects of the library now in place (tools/build_ab.sh ONLY= links against them)
+        final = os.path.join(ROOT, "build", "obj_" + name.split(".")[0])
+        shutil.rmtree(final, ignore_errors=True)
+        os.replace(objdir, final)
     # the stamp goes first, atomically, then the library: a reader that sees the new library also
     # sees its stamp (a stamp newer than the library only triggers a rebuild check, which the
     # embedded hash then settles)
