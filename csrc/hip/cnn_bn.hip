@@ -19,7 +19,8 @@
 //                              output gradient g (the consumers' dgrad applied the mask)
 //              bn_bwd_apply -> dgamma / dbeta (chunk 0) and, in place,
 //                              dz = gamma rstd (g - sum g / N - xhat sum(g xhat) / N)
-//                              (0 on padding rows of a short batch)
+//                              (0 on padding rows of a short batch and on the padded pixels of a
+//                              zero-padded image: BnArgs::Hr / Wr)
 // The shift k = z at pixel 0 of the group keeps S2 / N - (S1 / N)^2 free of
 // cancellation when |mean| >> std.
 #include "common.h"
@@ -48,7 +49,22 @@ struct BnArgs {
   void* pool_y;
   uint8_t* pool_mask;
   int W;
+  // real extent of a zero-padded image (ConvArgs::Hr / Wr; 0: not padded): statistics count the real
+  // pixels only, and y / dz are exact zeros outside them (the padded network IS the unpadded one)
+  int Hr, Wr;
 };
+
+// pixel p (flat over the group's images) lies outside the real extent of a zero-padded image
+__device__ __forceinline__ bool bn_pad_px(const BnArgs& a, long p) {
+  if (a.Hr <= 0) return false;
+  const int pi = (int)(p % a.HW);
+  return pi / a.W >= a.Hr || pi % a.W >= a.Wr;
+}
+
+// real pixels per image (the statistics' count)
+__device__ __forceinline__ long bn_real_hw(const BnArgs& a) {
+  return a.Hr > 0 ? (long)a.Hr * a.Wr : (long)a.HW;
+}
 
 #define BN_THREADS 256
 
@@ -102,6 +118,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_stats_kernel(BnArgs a) {
     float k[8], v[8];
     ld_chunk(z + c8 * 8, k);                       // shift: the group's pixel 0
     for (long p = p0 + t / nc8; p < p1; p += nact / nc8) {
+      if (bn_pad_px(a, p)) continue;
       ld_chunk(z + p * Cp + c8 * 8, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -135,7 +152,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(BnArgs a) {
         s1 += part[(long)c * 2 * Cp + t];
         s2 += part[(long)c * 2 * Cp + Cp + t];
       }
-      const float n = npx > 0 ? (float)npx : 1.f;
+      const long nreal = (long)bn_rows(a, g) * bn_real_hw(a);
+      const float n = nreal > 0 ? (float)nreal : 1.f;
       const float m1 = s1 / n;
       const float var = fmaxf(s2 / n - m1 * m1, 0.f);
       float k;                                     // the shift of bn_stats: the group's pixel 0
@@ -147,7 +165,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(BnArgs a) {
         a.stat[(long)g * 2 * Cp + Cp + t] = rstd;
         float* rm = a.run + (long)g * Cp + t;
         float* rv = a.run + (long)a.G * Cp + (long)g * Cp + t;
-        const float unb = npx > 1 ? var * n / (n - 1.f) : var;
+        const float unb = nreal > 1 ? var * n / (n - 1.f) : var;
         *rm = a.momentum * *rm + (1.f - a.momentum) * mean;
         *rv = a.momentum * *rv + (1.f - a.momentum) * unb;
       }
@@ -168,8 +186,9 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(BnArgs a) {
     const int c8 = (int)(i % nc8);
     float v[8];
     ld_chunk(z + p * Cp + c8 * 8, v);
+    const bool pad = bn_pad_px(a, p);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[c8 * 8 + e] + sh[c8 * 8 + e], 0.f);
+    for (int e = 0; e < 8; ++e) v[e] = pad ? 0.f : fmaxf(v[e] * sc[c8 * 8 + e] + sh[c8 * 8 + e], 0.f);
     st_chunk(y + p * Cp + c8 * 8, v);
   }
   if (!a.pool_y || !((r.out_mask >> 24) & 1)) return;
@@ -192,9 +211,10 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(BnArgs a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       ld_chunk(z + (ptl + offs[q]) * Cp + c8 * 8, v);
+      const bool pad = bn_pad_px(a, ptl + offs[q]);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float o = fmaxf(v[e] * sc[c8 * 8 + e] + sh[c8 * 8 + e], 0.f);
+        float o = pad ? 0.f : fmaxf(v[e] * sc[c8 * 8 + e] + sh[c8 * 8 + e], 0.f);
         if constexpr (!PREC) o = bf2f(f2bf(o));
         if (q == 0) m[e] = o;
         else if (o > m[e]) { m[e] = o; arg[e] = q; }
@@ -238,6 +258,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_stats_kernel(BnArgs a) {
       rstd[e] = stat[Cp + c8 * 8 + e];
     }
     for (long p = p0 + t / nc8; p < p1; p += nact / nc8) {
+      if (bn_pad_px(a, p)) continue;
       ld_chunk(z + p * Cp + c8 * 8, v);
       ld_chunk(gy + p * Cp + c8 * 8, d);
 #pragma unroll
@@ -272,7 +293,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(BnArgs a) {
       a.gbeta[(long)g * Cp + t] = sg;
       a.ggamma[(long)g * Cp + t] = sgx;
     }
-    const float inv_n = nvpx > 0 ? 1.f / (float)nvpx : 0.f;
+    const long nreal = (long)bn_rows(a, g) * bn_real_hw(a);
+    const float inv_n = nreal > 0 ? 1.f / (float)nreal : 0.f;
     const float rstd = a.stat[(long)g * 2 * Cp + Cp + t];
     cg[t] = a.gamma[(long)g * Cp + t] * rstd;
     cm[t] = sg * inv_n;
@@ -289,7 +311,7 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(BnArgs a) {
     const long p = p0 + i / nc8;
     const int c8 = (int)(i % nc8);
     float v[8], d[8];
-    if (p < nvpx) {
+    if (p < nvpx && !bn_pad_px(a, p)) {
       ld_chunk(z + p * Cp + c8 * 8, v);
       ld_chunk(gy + p * Cp + c8 * 8, d);
 #pragma unroll

@@ -1057,6 +1057,30 @@ extern "C" int gt_conv_fast(const ConvArgs* a_in, hipStream_t stream) {
     CONV_FAST_CASE_F32_NARROW(5, 5, 16, 8, 8, 16, 32, 8)   // s3 input conv (128 -> 256)
     CONV_FAST_CASE_F32_NARROW(3, 3, 32, 8, 8, 16, 32, 8)   // s3 nodes / output conv, and their dgrad (256 -> 256)
     CONV_FAST_CASE_F32_NARROW(5, 5, 32, 8, 4, 8, 16, 4)    // s3 input conv dgrad (256 -> 128)
+    // 3x3 stage-input kernels (kernel_sizes ((3, 3), ...): a user choice, gentun/individuals.py:223), tiled
+    // like their 5x5 counterparts above; the 3x3 node shapes are the same kernels already
+    if (CONV_FAST_MATCH(3, 3, 1, 32, 8, 2, 3) && smallq_th(a, 8, 4) == 4) {      // s1 input conv 3x3
+      if (pk_ok(a, 2)) CONV_FAST_LAUNCH_PK(3, 3, 1, 32, 4, 2, 3, 2, 1, 1)
+      CONV_FAST_LAUNCH(3, 3, 1, 32, 4, 2, 3, 2, 1)
+    }
+    CONV_FAST_CASE_F32_PK(3, 3, 1, 32, 8, 2, 3, 4)      // s1 input conv 3x3 (3 -> 20)
+    if (CONV_FAST_MATCH(3, 3, 3, 16, 8, 4, 7)) {       // s2 input conv 3x3 (20 -> 50)
+      const int th = smallq_th(a, 8, 2);
+      if (th == 4) CONV_FAST_LAUNCH(3, 3, 3, 16, 4, 4, 7, 4, 1)
+      if (th == 2) CONV_FAST_LAUNCH_CT1(3, 3, 3, 16, 2, 4, 7, 4)
+      CONV_FAST_LAUNCH_CT1S(3, 3, 3, 16, 8, 4, 7, 4, 0)
+    }
+    if (CONV_FAST_MATCH(3, 3, 7, 16, 8, 2, 3)) {       // s2 input conv 3x3 dgrad (50 -> 20)
+      if (smallq_th(a, 8, 4) == 4) CONV_FAST_LAUNCH_CT1(3, 3, 7, 16, 4, 2, 3, 4)
+      CONV_FAST_LAUNCH_CT1(3, 3, 7, 16, 8, 2, 3, 4)
+    }
+    CONV_FAST_CASE_F32_NARROW(3, 3, 7, 8, 8, 7, 13, 7)     // deep s3 input conv 3x3 (50 -> 100)
+    CONV_FAST_CASE_F32_NARROW(3, 3, 13, 8, 8, 4, 7, 4)     // deep s3 input conv 3x3 dgrad (100 -> 50)
+    CONV_FAST_CASE_F32_NARROW(3, 3, 1, 32, 8, 4, 8, 4)     // wide s1 input conv 3x3 (3 -> 64)
+    if (CONV_FAST_MATCH(3, 3, 8, 16, 8, 8, 16)) CONV_FAST_LAUNCH_CT1S(3, 3, 8, 16, 8, 8, 16, 8, 0)   // wide s2 in 3x3
+    CONV_FAST_CASE_F32_NARROW(3, 3, 16, 16, 4, 4, 8, 4)    // wide s2 input conv 3x3 dgrad (128 -> 64)
+    CONV_FAST_CASE_F32_NARROW(3, 3, 16, 8, 8, 16, 32, 8)   // wide s3 input conv 3x3 (128 -> 256)
+    CONV_FAST_CASE_F32_NARROW(3, 3, 32, 8, 4, 8, 16, 4)    // wide s3 input conv 3x3 dgrad (256 -> 128)
     return -100;
   }
   if (a->prec != 0) return -1;
@@ -1751,6 +1775,13 @@ static int wgrad_rows(int KH, int KW, int Cinp, int Coutp, int H, int W, int pre
     if (KH == 3 && KW == 3 && Cinp == 128 && Coutp == 128 && W == 16 && H % 2 == 0) return 2;
     if (KH == 5 && KW == 5 && Cinp == 128 && Coutp == 256 && W == 8 && H % 4 == 0) return 4;
     if (KH == 3 && KW == 3 && Cinp == 256 && Coutp == 256 && W == 8 && H % 4 == 0) return 4;
+    // 3x3 stage-input kernels (bands as their 5x5 counterparts)
+    if (KH == 3 && KW == 3 && Cinp == 8 && Coutp == 24 && W == 32 && H % 8 == 0) return 8;
+    if (KH == 3 && KW == 3 && Cinp == 24 && Coutp == 56 && W == 16 && H % 4 == 0) return 4;
+    if (KH == 3 && KW == 3 && Cinp == 56 && Coutp == 104 && W == 8 && H % 4 == 0) return 4;
+    if (KH == 3 && KW == 3 && Cinp == 8 && Coutp == 64 && W == 32 && H % 4 == 0) return 4;
+    if (KH == 3 && KW == 3 && Cinp == 64 && Coutp == 128 && W == 16 && H % 2 == 0) return 2;
+    if (KH == 3 && KW == 3 && Cinp == 128 && Coutp == 256 && W == 8 && H % 4 == 0) return 4;
     return 0;
   }
   if (KH == 5 && KW == 5 && Cinp == 8 && Coutp == 24 && W == 32 && H % 8 == 0) return 8;
@@ -1806,6 +1837,13 @@ extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
     WGRAD_FAST_CASE_F32Z(3, 3, 16, 16, 16, 2, 8, 4)   // s2 nodes / output conv (128 -> 128)
     WGRAD_FAST_CASE_F32Z(5, 5, 16, 32, 8, 4, 8, 13)   // s3 input conv (128 -> 256)
     WGRAD_FAST_CASE_F32Z(3, 3, 32, 32, 8, 4, 8, 10)   // s3 nodes / output conv (256 -> 256)
+    // 3x3 stage-input kernels
+    WGRAD_FAST_CASE_F32(3, 3, 1, 3, 32, 8, 4, 1)      // s1 input conv 3x3 (3 -> 20)
+    WGRAD_FAST_CASE_F32(3, 3, 3, 7, 16, 4, 8, 1)      // s2 input conv 3x3 (20 -> 50)
+    WGRAD_FAST_CASE_F32Z(3, 3, 7, 13, 8, 4, 8, 4)     // deep s3 input conv 3x3 (50 -> 100)
+    WGRAD_FAST_CASE_F32(3, 3, 1, 8, 32, 4, 4, 1)      // wide s1 input conv 3x3 (3 -> 64)
+    WGRAD_FAST_CASE_F32Z(3, 3, 8, 16, 16, 2, 8, 4)    // wide s2 input conv 3x3 (64 -> 128)
+    WGRAD_FAST_CASE_F32Z(3, 3, 16, 32, 8, 4, 8, 5)    // wide s3 input conv 3x3 (128 -> 256)
     return -100;
   }
   if (a->prec != 0) return -1;

@@ -66,11 +66,13 @@ POOL_FUSE = True
 # False: the Python issue path per step (what a captured step graph records)
 NATIVE_STEPS = True
 
-# fp32 3x3 layers with a Winograd F(2x2, 3x3) instantiation (csrc/hip/cnn_conv_wino.hip: the stage-2 node /
-# output convs of the S=(3,5) space) run their forward and data gradient on it, with the transformed
-# weights re-derived from the fp32 masters after every optimizer step. Module constant, not a switch: tests
-# flip it to compare against the direct kernels.
-WINOGRAD = True
+# True: fp32 3x3 layers with a Winograd F(2x2, 3x3) instantiation (csrc/hip/cnn_conv_wino.hip: the stage-2
+# node / output convs of the S=(3,5) space) run their forward and data gradient on it, with the transformed
+# weights re-derived from the fp32 masters after every optimizer step. 7-18 % faster than the direct kernel
+# alone but 3.5 % slower in the population step, where its 256-VGPR / 68 KB workgroups share the CUs with
+# the weight-gradient kernels (profiles/r6/wino_bench_r6.txt): off. Module constant, not a switch; tests
+# flip it to check the executor path.
+WINOGRAD = False
 
 # bytes of forward-only activation twins an evaluation may allocate for all groups of a job
 EVAL_TWIN_BUDGET = 1 << 30
@@ -93,6 +95,41 @@ def split_planes(w, npl):
         out[q] = r.to(torch.bfloat16)
         r = r - out[q].float()
     return out
+
+
+def fast_path_report(plan, dtype="fp32", ngroups=25, B=32, pad_images=True, batch_norm=False):
+    """Which kernels a population step of this search space runs, probed without a GPU: the stored image
+    size and per-stage channel padding the executor picks (cnn_kernels.padded_hw / stage_channel_pads),
+    and per superset launch (every stage's input conv, node and output convs: forward, data gradient,
+    weight gradient) whether a shape-specialised kernel runs it. ``generic_launches`` counts the
+    launches of a superset step (all nodes present) left on the generic kernels."""
+    prec = K.PREC[dtype]
+    h0r, w0r, c0 = plan.input_shape
+    kernels, nodes = list(plan.kernels_per_layer), list(plan.nodes)
+    ks = [tuple(k) for k in plan.kernel_sizes]
+    hw = K.padded_hw(h0r, w0r, len(kernels), batch_norm)
+    h0, w0 = hw if pad_images else (h0r, w0r)
+    pads = K.stage_channel_pads(c0, kernels, ks, h0, w0, prec, ngroups=ngroups, B=B)
+    lib = K.lib()
+    layers, generic, fast = [], 0, 0
+    cin, cinr = pad8(c0), c0
+    for s, (cp, k) in enumerate(zip(pads, ks)):
+        H, W = h0 >> s, w0 >> s
+        for kind, (KH, KW), ci, cir, n in (("in", k, cin, cinr, 1), ("node/out", (3, 3), cp, kernels[s], nodes[s] + 1)):
+            first = s == 0 and kind == "in"
+            f = K.layer_fast(KH, KW, ci, cp, H, W, prec, ngroups, B, cir, kernels[s], first)
+            wino = bool(WINOGRAD and prec == 1 and (KH, KW) == (3, 3) and lib.gt_conv_wino_supported(ci, cp, H, W)
+                        and lib.gt_conv_wino_supported(cp, ci, H, W))
+            nl = n * (2 if first else 3)
+            bad = n * sum(1 for x in (f if not first else f[::2]) if not x)
+            generic += bad
+            fast += nl - bad
+            layers.append({"stage": s, "layer": kind, "k": KH, "hw": H, "cin_p": ci, "cout_p": cp,
+                           "fwd_fast": f[0], "dgrad_fast": None if first else f[1], "wgrad_fast": f[2],
+                           "winograd": wino})
+        cin, cinr = cp, kernels[s]
+    return {"stored_hw": [h0, w0], "stage_channels_padded": pads, "fast_launches": fast,
+            "generic_launches": generic, "layers": layers}
 
 
 class HipPopJob(FoldJob):
@@ -219,8 +256,14 @@ class HipPopJob(FoldJob):
         h0, w0 = self.pad_hw or (h0r, w0r)
         self.sched = PopulationSchedule([self.members[self.gmember[q]][0] for q in range(Q)], hw=self.pad_hw)
         self.stages, self.layers = self.sched.stages, self.sched.layers
+        # per-stage channel padding: every layer on the shape-specialised kernels where padding up allows
+        ks = [tuple(k) for k in p0.kernel_sizes]
+        self.stage_cp = K.stage_channel_pads(p0.input_shape[2], list(p0.kernels_per_layer), ks, h0, w0,
+                                             self.prec, ngroups=Q, B=self.B)
         for L in self.layers:
-            L.cinp, L.coutp = pad8(L.cin), pad8(L.cout)
+            L.coutp = self.stage_cp[L.stage]
+            L.cinp = pad8(L.cin) if L.kind == "in" and L.stage == 0 else \
+                self.stage_cp[L.stage - 1] if L.kind == "in" else L.coutp
             L.Kdim = L.KH * L.KW * L.cinp
             L.TH = K.conv_tile_rows(L.H, L.W)
             band = K.wgrad_band(L.KH, L.KW, L.cinp, L.coutp, L.H, L.W, self.prec)
@@ -235,7 +278,7 @@ class HipPopJob(FoldJob):
             raise ValueError("input too small for the pooling stages")
         self.final_hw = (hs, ws)
         self.final_hw_real = (h0r >> len(p0.kernels_per_layer), w0r >> len(p0.kernels_per_layer))
-        self.final_cp = pad8(p0.kernels_per_layer[-1])
+        self.final_cp = self.stage_cp[-1]
 
     # ------------------------------------------------------------ buffers
     def _allocate(self):
@@ -244,7 +287,7 @@ class HipPopJob(FoldJob):
         for st in self.stages:
             for L in st.layers:
                 self.shapes[L.name] = (L.H, L.W, L.coutp)
-            self.shapes[st.pool] = (st.H // 2, st.W // 2, pad8(p0.kernels_per_layer[st.s]))
+            self.shapes[st.pool] = (st.H // 2, st.W // 2, self.stage_cp[st.s])
         self.act, self.grad = {}, {}
         for name, (hh, ww, cc) in self.shapes.items():
             self.act[name] = torch.zeros((Q, B, hh, ww, cc), dtype=self.adt, device=dev)
@@ -431,6 +474,8 @@ class HipPopJob(FoldJob):
         a.nchunk, a.chunk_px = L.bn_nchunk, L.bn_chunk
         a.momentum, a.eps = self.cfg.bn_momentum, self.cfg.bn_eps
         a.train, a.prec = train, self.prec
+        if self.pad_hw is not None:
+            a.Hr, a.Wr = L.Hr, L.Wr          # statistics over the real pixels, zeros outside them
         return a
 
     def _stage_fwd_ops(self, st, gather_train, fuse):

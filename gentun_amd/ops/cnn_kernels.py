@@ -113,7 +113,7 @@ class BnArgs(C.Structure):
                 ("ggamma", P), ("gbeta", P), ("gtab", P), ("valid", P), ("st", P),
                 ("ngroups", I), ("G", I), ("B", I), ("HW", I), ("Cp", I), ("nchunk", I), ("chunk_px", I),
                 ("momentum", C.c_float), ("eps", C.c_float), ("train", I), ("prec", I),
-                ("pool_y", P), ("pool_mask", P), ("W", I)]
+                ("pool_y", P), ("pool_mask", P), ("W", I), ("Hr", I), ("Wr", I)]
 
 
 BN_CHUNK_PX = 512     # pixels per BatchNorm workgroup (fixed per shape: batch-invariant sums)
@@ -389,12 +389,76 @@ def padded_hw(h, w, nstages, batch_norm=False):
     are initialised to 0 and receive zero gradient, so the padded network IS
     the unpadded one (tests/test_hip_train.py::test_padded_mnist_geometry).
     Conditions: square, every stage's real size even (no floor pooling inside
-    the padding), at most 25 % wider, no BatchNorm (its batch statistics would
-    count the padding)."""
+    the padding), at most 25 % wider. With BatchNorm the statistics count the
+    real pixels only and BN writes zeros outside them (cnn_bn.hip BnArgs::Hr /
+    Wr); ``batch_norm`` is kept for callers."""
+    del batch_norm
     p = 1 << max(0, int(w) - 1).bit_length()
-    if (h != w or p == w or batch_norm or p > 1.25 * w or w % (1 << nstages) or p >> nstages < 8):
+    if (h != w or p == w or p > 1.25 * w or w % (1 << nstages) or p >> nstages < 8):
         return h, w
     return p, p
+
+
+# channel paddings the shape-specialised conv / wgrad kernels are instantiated for (the narrow (20, 50, 100) and
+# wide (64, 128, 256) search spaces' stage widths, padded to 8); other channel counts are padded UP to one of
+# these when that puts every layer of the network on the fast kernels (stage_channel_pads)
+FAST_PADS = (24, 56, 64, 104, 128, 256)
+
+
+def _probe_conv(L, KH, KW, cinp, coutp, H, W, prec, ngroups, B, cout_real, fwd):
+    a = ConvArgs()
+    a.KH, a.KW, a.Cinp, a.Coutp, a.H, a.W = KH, KW, cinp, coutp, H, W
+    a.G = a.ngroups = max(1, ngroups)
+    a.B, a.prec, a.cout_real = B, prec, cout_real
+    a.epi_bf16 = 1 if fwd else 0
+    a.TH = conv_tile_rows(H, W)
+    return bool(L.gt_conv_fast_probe_any(a))
+
+
+def layer_fast(KH, KW, cinp, coutp, H, W, prec, ngroups, B, cin_real, cout_real, first):
+    """(forward, data gradient, weight gradient) of one layer geometry run on shape-specialised kernels
+    (gt_conv_fast / gt_wgrad_fast) -- each probed without launching anything (no GPU needed)."""
+    L = lib()
+    fwd = _probe_conv(L, KH, KW, cinp, coutp, H, W, prec, ngroups, B, cout_real, True)
+    dgr = True if first else _probe_conv(L, KH, KW, coutp, cinp, H, W, prec, ngroups, B, cin_real, False)
+    wgr = int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W, prec)) > 0
+    return fwd, dgr, wgr
+
+
+def stage_channel_pads(c0, kernels, kernel_sizes, h0, w0, prec, ngroups=25, B=32, max_factor=2.0):
+    """Channel padding of every stage's tensors (input conv output, node outputs, output conv, pool).
+
+    The reference lets the user choose ``kernels_per_layer`` / ``kernel_sizes`` freely
+    (gentun/individuals.py:221-223). The fast kernels exist for a set of padded channel counts
+    (FAST_PADS): each stage's count is padded up to one of them -- at most ``max_factor`` x its own
+    8-padding -- choosing the cheapest combination (padded multiply-adds) under which EVERY conv
+    launch (forward, data gradient, weight gradient) runs a shape-specialised kernel; when no
+    combination does, the plain 8-padding (some layers on the generic kernels). Padded channels have
+    zero weights, zero bias and zero gradient (they stay exactly 0: the network computes the
+    unpadded one)."""
+    import itertools
+    c0p = (c0 + 7) // 8 * 8
+    base = [(c + 7) // 8 * 8 for c in kernels]
+    cands = [sorted({b} | {v for v in FAST_PADS if b <= v <= max_factor * b}) for b in base]
+    best = None
+    for combo in itertools.product(*cands):
+        cost, ok = 0.0, True
+        cin, cinr = c0p, c0
+        for s, (cp, k) in enumerate(zip(combo, kernel_sizes)):
+            H, W = h0 >> s, w0 >> s
+            kh, kw = tuple(k)
+            for (KH, KW, ci, cir, first) in ((kh, kw, cin, cinr, s == 0), (3, 3, cp, kernels[s], False)):
+                f = layer_fast(KH, KW, ci, cp, H, W, prec, ngroups, B, cir, kernels[s], first)
+                if not all(f):
+                    ok = False
+                    break
+                cost += H * W * KH * KW * ci * cp
+            if not ok:
+                break
+            cin, cinr = cp, kernels[s]
+        if ok and (best is None or cost < best[0]):
+            best = (cost, combo)
+    return list(best[1]) if best is not None else base
 
 
 def wgrad_blocks(kdim, with_bias=True):

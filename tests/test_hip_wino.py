@@ -288,3 +288,31 @@ def test_wino_refuses_unsupported_shapes():
     assert Km.lib().gt_conv_wino_supported(104, 104, 8, 8) == 0
     assert Km.lib().gt_conv_wino_supported(56, 56, 16, 16) == 1
     assert Km.lib().gt_conv_wino_supported(24, 24, 32, 32) == 0      # stage 1: the direct kernel is faster
+
+
+def test_winograd_executor_matches_direct():
+    """cnn_hip.WINOGRAD = True (off by default: slower in the step, profiles/r6/wino_bench_r6.txt) trains
+    the same network: the stage-2 3x3 layers on the Winograd kernels with weights re-transformed after every
+    optimizer step give the direct kernels' validation losses to fp32 summation-order rounding."""
+    import numpy as np
+    from gentun_amd.models import cnn_engine as E
+    from gentun_amd.models import cnn_hip
+    from gentun_amd.models.genome import make_plan
+    from gentun_amd.utils.data import make_image_classification, stratified_kfold
+    x, y = make_image_classification(n=640, shape=(32, 32, 3), classes=10, seed=5, noise=0.35, shift=2)
+    folds = stratified_kfold(np.argmax(y, 1), 3, seed=0)
+    plan = make_plan({'S_1': '101', 'S_2': '0101110011'}, (3, 5), (32, 32, 3), (20, 50), ((5, 5), (5, 5)), 500, 10)
+    res, old = {}, cnn_hip.WINOGRAD
+    try:
+        for wino in (False, True):
+            cnn_hip.WINOGRAD = wino
+            cfg = E.TrainConfig(epochs=(1,), learning_rate=(1e-2,), batch_size=32, dtype="fp32", loss="ce",
+                                reset="all", optimizer="sgd")
+            job = E.make_job("hip", plan, x, y, folds, cfg, DEV)
+            assert any(L.wino for L in job.layers) == wino
+            job.launch()
+            res[wino] = job.finish()
+    finally:
+        cnn_hip.WINOGRAD = old
+    a, b = np.array(res[True]["val_loss"]), np.array(res[False]["val_loss"])
+    assert np.all(np.isfinite(a)) and np.max(np.abs(a - b) / np.abs(b)) < 2e-4, (a, b)
