@@ -96,6 +96,11 @@ def parse():
     ap.add_argument("--input-shape", default="32,32,3",
                     help="H,W,C of the synthetic images; 28,28,1 is the reference's MNIST default "
                          "(gentun/individuals.py:221, tests/test_mnist.py)")
+    ap.add_argument("--kernel-size", type=int, default=5,
+                    help="stage-input conv kernel size of every stage (the reference's kernel_sizes; nodes are 3x3)")
+    ap.add_argument("--generic-kernels", action="store_true",
+                    help="HIP backend on its generic conv / wgrad kernels only (the comparison figure for the "
+                         "shape-specialised fast path)")
     ap.add_argument("--pad-images", type=int, default=1,
                     help="1: a 28x28 image is stored zero-padded to 32x32 so every stage runs the "
                          "shape-specialised kernels (ops/cnn_kernels.padded_hw); 0: the generic kernels")
@@ -169,8 +174,25 @@ def run(args):
     if args.kernels:
         kernels = tuple(int(k) for k in args.kernels.split(","))
     space = "S=({}) kernels ({})".format(",".join(map(str, nodes)), ",".join(map(str, kernels)))
+    if args.kernel_size != 5:
+        space += " {}x{} stage-input convs".format(args.kernel_size, args.kernel_size)
+    ksz = (args.kernel_size, args.kernel_size)
+    if args.generic_kernels:
+        from gentun_amd.ops import cnn_kernels as _K
+        _K.lib().gt_conv_set_fast(0)            # every conv / wgrad on the generic kernels
+    fast_path = None
+    if device.type == "cuda" and (args.backend or "hip") == "hip":
+        # which kernels a superset step of this space runs (probed: cnn_hip.fast_path_report)
+        from gentun_amd.models.cnn_hip import fast_path_report
+        from gentun_amd.models.genome import make_plan as _mk
+        genes_all = {"S_{}".format(i + 1): "1" * (k * (k - 1) // 2) for i, k in enumerate(nodes)}
+        rep = fast_path_report(_mk(genes_all, nodes, shape, kernels, (ksz,) * len(nodes), 500, 10), args.dtype,
+                               ngroups=per_gpu * args.nfold, B=32, pad_images=bool(args.pad_images),
+                               batch_norm=args.batch_norm)
+        fast_path = {k: rep[k] for k in ("stored_hw", "stage_channels_padded", "fast_launches", "generic_launches")}
+        fast_path["note"] = "launches of a superset step (every node present): fwd + dgrad + wgrad per conv layer"
     extra = dict(nodes=nodes, input_shape=shape, kernels_per_layer=kernels,
-                 kernel_sizes=((5, 5),) * len(nodes), dense_units=500, dropout_probability=0.5, classes=10,
+                 kernel_sizes=(ksz,) * len(nodes), dense_units=500, dropout_probability=0.5, classes=10,
                  nfold=args.nfold, epochs=epochs, learning_rate=lrs, batch_size=32, dtype=args.dtype,
                  loss=args.loss, seed=args.seed, backend=args.backend, reset=args.fold_reset, batching="keras",
                  batch_norm=args.batch_norm, pad_images=bool(args.pad_images))
@@ -285,7 +307,9 @@ def run(args):
                                  if device.type == "cuda" and (args.backend or "hip") == "hip"
                                  else "stock PyTorch fp32 ops (MIOpen / hipBLASLt)") if args.dtype == "fp32" else None,
                    "torch_population_batched": (not args.torch_unbatched) if args.backend == "torch" else None,
-                   "streams_per_gpu": args.streams, "pop_batch": args.pop_batch},
+                   "streams_per_gpu": args.streams, "pop_batch": args.pop_batch,
+                   "kernels": "generic only" if args.generic_kernels else "shape-specialised where available",
+                   "fast_path": fast_path},
         "generations": len(completed),
         "evals": total_evals,
         "timed_candidates": timed_evals,

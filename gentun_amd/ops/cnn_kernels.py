@@ -402,7 +402,7 @@ def padded_hw(h, w, nstages, batch_norm=False):
 # channel paddings the shape-specialised conv / wgrad kernels are instantiated for (the narrow (20, 50, 100) and
 # wide (64, 128, 256) search spaces' stage widths, padded to 8); other channel counts are padded UP to one of
 # these when that puts every layer of the network on the fast kernels (stage_channel_pads)
-FAST_PADS = (24, 56, 64, 104, 128, 256)
+FAST_PADS = (24, 32, 56, 64, 104, 128, 256)
 
 
 def _probe_conv(L, KH, KW, cinp, coutp, H, W, prec, ngroups, B, cout_real, fwd):
@@ -419,6 +419,10 @@ def layer_fast(KH, KW, cinp, coutp, H, W, prec, ngroups, B, cin_real, cout_real,
     """(forward, data gradient, weight gradient) of one layer geometry run on shape-specialised kernels
     (gt_conv_fast / gt_wgrad_fast) -- each probed without launching anything (no GPU needed)."""
     L = lib()
+    on = L.gt_conv_set_fast(1)               # the fast path switched off (generic-kernel comparisons): none
+    L.gt_conv_set_fast(on)
+    if not on:
+        return False, False, False
     fwd = _probe_conv(L, KH, KW, cinp, coutp, H, W, prec, ngroups, B, cout_real, True)
     dgr = True if first else _probe_conv(L, KH, KW, coutp, cinp, H, W, prec, ngroups, B, cin_real, False)
     wgr = int(L.gt_wgrad_fast_band(KH, KW, cinp, coutp, H, W, prec)) > 0

@@ -80,7 +80,15 @@ CONV_SHAPES = [(32, 32, 3, 20, 5, 1), (32, 32, 20, 20, 3, 3), (16, 16, 20, 50, 5
                (8, 8, 256, 256, 5, 1), (8, 8, 256, 100, 5, 2), (16, 16, 128, 128, 5, 3), (32, 32, 64, 64, 5, 2),
                # ... and their shape-specialised tile kernels (round 3): every conv / dgrad shape of the space
                (32, 32, 3, 64, 5, 1), (32, 32, 64, 64, 3, 2), (16, 16, 64, 128, 5, 1), (16, 16, 128, 128, 3, 2),
-               (16, 16, 128, 64, 5, 1), (8, 8, 128, 256, 5, 1), (8, 8, 256, 256, 3, 3), (8, 8, 256, 128, 5, 1)]
+               (16, 16, 128, 64, 5, 1), (8, 8, 128, 256, 5, 1), (8, 8, 256, 256, 3, 3), (8, 8, 256, 128, 5, 1),
+               # round 6, user-chosen architectures (cnn_conv_fast_ext.hip): 32 / 64-channel stages ...
+               (32, 32, 3, 32, 5, 1), (32, 32, 32, 32, 3, 2), (16, 16, 32, 64, 5, 1), (16, 16, 64, 64, 3, 2),
+               (16, 16, 64, 32, 5, 1),
+               # ... and 3x3 stage-input convs (forward and, as the transposed shape, data gradient)
+               (32, 32, 3, 20, 3, 1), (16, 16, 20, 50, 3, 1), (16, 16, 50, 20, 3, 1), (8, 8, 50, 100, 3, 1),
+               (8, 8, 100, 50, 3, 1), (32, 32, 3, 64, 3, 1), (16, 16, 64, 128, 3, 1), (16, 16, 128, 64, 3, 1),
+               (8, 8, 128, 256, 3, 1), (8, 8, 256, 128, 3, 1), (32, 32, 3, 32, 3, 1), (16, 16, 32, 64, 3, 1),
+               (16, 16, 64, 32, 3, 1)]
 
 
 @pytest.mark.gpu
@@ -192,7 +200,14 @@ def test_conv_dgrad_fanout_fp32(k, H):
                                                       # wide deep space, shape-specialised (round 3)
                                                       (32, 32, 3, 64, 5, 1, True), (32, 32, 64, 64, 3, 2, False),
                                                       (16, 16, 64, 128, 5, 1, False), (16, 16, 128, 128, 3, 1, False),
-                                                      (8, 8, 128, 256, 5, 1, False), (8, 8, 256, 256, 3, 2, False)])
+                                                      (8, 8, 128, 256, 5, 1, False), (8, 8, 256, 256, 3, 2, False),
+                                                      # round 6: 32 / 64-channel stages, 3x3 stage-input convs
+                                                      (32, 32, 3, 32, 5, 1, True), (32, 32, 32, 32, 3, 2, False),
+                                                      (16, 16, 32, 64, 5, 1, False), (16, 16, 64, 64, 3, 1, False),
+                                                      (32, 32, 3, 20, 3, 1, True), (16, 16, 20, 50, 3, 1, False),
+                                                      (32, 32, 3, 64, 3, 1, True), (16, 16, 64, 128, 3, 1, False),
+                                                      (8, 8, 50, 100, 3, 1, False), (8, 8, 128, 256, 3, 1, False),
+                                                      (32, 32, 3, 32, 3, 1, True), (16, 16, 32, 64, 3, 1, False)])
 @pytest.mark.parametrize("pk", [0, 1])
 def test_conv_wgrad_fp32(H, W, cin, cout, k, nin, first, pk):
     """Weight + bias gradient (specialised register-staged kernel and the
