@@ -13,8 +13,8 @@ run() {   # name, extra args
     > gpurun_out/r6/gen_$name.json 2> gpurun_out/r6/gen_$name.err || { tail -3 gpurun_out/r6/gen_$name.err; return 1; }
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read()); print(sys.argv[2], d['value'], d['config']['model'], d['config']['fast_path'])" gpurun_out/r6/gen_$name.json $name
 }
-for cfg in "k16_32:--kernels 16,32" "ks3:--kernel-size 3" "k32_64:--kernels 32,64" "mnist_bn:--input-shape 28,28,1 --batch-norm"; do
-  name=${cfg%%:*}; args=${cfg#*:}
+for cfg in ${CFGS:-"k16_32:--kernels 16,32" "ks3:--kernel-size 3" "k32_64:--kernels 32,64" "mnist_bn:--input-shape 28,28,1 --batch-norm"}; do
+  name=${cfg%%:*}; args=${cfg#*:}; args=${args//_/ }
   run ${name}_fast $args || exit 1
   run ${name}_generic $args --generic-kernels || exit 1
 done
