@@ -65,6 +65,9 @@ struct ConvArgs {
   // 1: a 3x3 fp32 layer on the Winograd F(2x2, 3x3) kernels (cnn_conv_wino.hip); `w` then holds the
   // transformed weight planes [3][Q][16][R][K] written by gt_wino_wtrans, never the direct planes
   int wino;
+  // 1: `w` holds FRAGMENT-MAJOR planes [planes][Q][NT][NKS][64][8] of the shape-specialised fp32 kernels
+  // (gt_conv_wfrag, conv_fast_impl.h): each MFMA A fragment one contiguous KB in lane order
+  int wfrag;
 };
 
 __device__ __forceinline__ GroupRec group_rec(const GroupRec* gtab, int y, int n_in, int n_out, int acc,

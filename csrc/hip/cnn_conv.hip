@@ -727,6 +727,7 @@ int gt_conv_fwd(const ConvArgs* a, hipStream_t stream) {
     const int rc = gt_conv_fast(a, stream);
     if (rc != -100) return rc;
   }
+  if (a->wfrag) return -102;                 // fragment-major planes: shape-specialised kernels only
   if (a->pool_y) return -60;                 // fused pool / un-pool: shape-specialised kernels only (gt_conv_fast_probe)
   if (!a->gtab && (a->n_in < 1 || a->n_in > GT_MAXSLOT || a->n_out < 1 || a->n_out > GT_MAXSLOT)) return -1;
   if (a->TH * a->W > 256 || a->TH < 1 || a->TH > a->H) return -2;

@@ -364,3 +364,92 @@ extern "C" int gt_wgrad_fast(const WgradArgs* a, hipStream_t stream) {
   return -100;
 }
 #endif  // GT_KERNELS_ONLY
+
+// ===========================================================================
+// Fragment-major weight planes of the shape-specialised convs (ConvArgs::wfrag)
+// ===========================================================================
+// Entry e of a conv's reduction list -> its row-major chunk (kk * NCBI + cb), as the kernels order it
+// (part-major for the stage-2 3x3 fp32 shape, S2Parts; kk-major otherwise); -1 past the list.
+extern "C" int gt_conv_frag_order(int KH, int KW, int NCBI, int W, int prec, int* out, int n) {
+  const int NCH = KH * KW * NCBI;
+  const bool parts = prec == 1 && NCBI == 7 && W == 16 && KH == 3 && KW == 3;
+  for (int e = 0; e < n; ++e) {
+    int kk, cb;
+    if (e >= NCH) { out[e] = -1; continue; }
+    if (parts) {
+      const int E0 = KH * KW * 4;
+      if (e < E0) { kk = e >> 2; cb = e & 3; }
+      else { const int e1 = e - E0; kk = e1 / 3; cb = 4 + e1 - kk * 3; }
+    } else {
+      kk = e / NCBI; cb = e - kk * NCBI;
+    }
+    out[e] = kk * NCBI + cb;
+  }
+  return (NCH + 3) / 4;
+}
+
+struct FragSeg {
+  const float* w;        // fp32 master [Q][Cop][KH][KW][Cip] of the layer
+  uint16_t* dst;         // [npl][Q][NT][NKS][64][8] bf16 planes
+  const int* order;      // [NKS * 4]: row-major chunk of each entry in the conv's view, -1 = zero
+  long ps;               // plane stride (elements)
+  int Q, Cop, Cip, KH, KW;
+  int NT, NKS, NCBIc;    // the conv's co tiles, k-steps, input chunks (layer Cip / 8, or Cop / 8 for dgrad)
+  int dgrad;             // 1: the flipped / transposed kernel of the data gradient
+  int npl;               // 3 (fp32: exact split) or 1 (bf16)
+};
+
+struct FragArgs {
+  const FragSeg* segs;
+  const int2* blocks;    // per block: (segment, first lane-item of Q x NT x NKS x 64)
+};
+
+__global__ void __launch_bounds__(256) conv_wfrag_kernel(FragArgs a) {
+  const int2 blk = a.blocks[blockIdx.x];
+  const FragSeg s = a.segs[blk.x];
+  const long item = (long)blk.y + threadIdx.x;
+  if (item >= (long)s.Q * s.NT * s.NKS * 64) return;
+  const int lane = (int)(item & 63);
+  long r = item >> 6;
+  const int ks = (int)(r % s.NKS); r /= s.NKS;
+  const int t = (int)(r % s.NT);
+  const int q = (int)(r / s.NT);
+  const int row = t * 16 + (lane & 15), e = ks * 4 + (lane >> 4);
+  const int nat = s.order[e];
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 0.f;
+  if (nat >= 0) {
+    const int kk = nat / s.NCBIc, cb = nat - kk * s.NCBIc;
+    const int kh = kk / s.KW, kw = kk - kh * s.KW;
+    if (!s.dgrad && row < s.Cop) {
+      const float* src = s.w + ((((long)q * s.Cop + row) * s.KH + kh) * s.KW + kw) * s.Cip + cb * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[j];
+    } else if (s.dgrad && row < s.Cip) {
+      // the data gradient's row = layer input channel, its chunk cb = layer output channels cb*8.., flipped taps
+      const int khl = s.KH - 1 - kh, kwl = s.KW - 1 - kw;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        v[j] = s.w[((((long)q * s.Cop + cb * 8 + j) * s.KH + khl) * s.KW + kwl) * s.Cip + row];
+    }
+  }
+  uint16_t* d = s.dst + item * 8;
+  if (s.npl == 1) {
+    *reinterpret_cast<uint4*>(d) = pack8(v);
+    return;
+  }
+  uint4 p0, p1, p2;
+  split8(v, p0, p1, p2);
+  *reinterpret_cast<uint4*>(d) = p0;
+  *reinterpret_cast<uint4*>(d + s.ps) = p1;
+  *reinterpret_cast<uint4*>(d + 2 * s.ps) = p2;
+}
+
+extern "C" int gt_conv_wfrag(const void* av, int nblocks, hipStream_t stream) {
+  if (nblocks < 1) return 0;
+  hipLaunchKernelGGL(conv_wfrag_kernel, dim3(nblocks), dim3(256), 0, stream, *static_cast<const FragArgs*>(av));
+  return (int)hipGetLastError();
+}
+
+extern "C" size_t gt_sizeof_frag_seg() { return sizeof(FragSeg); }

@@ -246,6 +246,11 @@ conv_fast_kernel(ConvArgs a) {
   // ---- weights: first PF k-steps in flight before the patch ---------------
   const int wco = (wave % WC) * CT;                 // first co tile of this wave
   const int pgw = (wave / WC) * PG;                 // first pixel group of this wave
+  // weight planes: row-major [Q][Coutp][KH][KW][Cinp] (a.wfrag = 0), or FRAGMENT-MAJOR [Q][NT][NKS][64 lanes][8]
+  // (a.wfrag = 1, written by gt_conv_wfrag: the 16 rows x 32 k of one (co tile, k-step) are one contiguous KB
+  // in lane order, so a wave's 16-byte-per-lane load fills 8 whole 128-byte lines instead of touching 16 half
+  // used ones -- 6-16 % per launch, profiles/r6/conv_wfrag_r6.txt). wrow: the lane's row base; per k-step the
+  // offset is the entry's chunk (row-major) or s * 512 (fragment-major)
   const uint16_t* wrow[CT];
   bool wok[CT];
 #pragma unroll
@@ -253,12 +258,14 @@ conv_fast_kernel(ConvArgs a) {
     if (PK && t == CT - 1) {                        // packed tile: row l16 = (channel l16/4, plane l16%4)
       const int co = (wco + t) * 16 + (l16 >> 2), pl = l16 & 3;
       wok[t] = pl < 3 && co < a.cout_real;
-      wrow[t] = a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8) + (wok[t] ? pl : 0) * a.wps;
+      wrow[t] = a.wfrag ? a.w + (((long)g * NT + wco + t) * NKS * 64 + kq * 16 + (l16 >> 2)) * 8 + (wok[t] ? pl : 0) * a.wps
+                        : a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8) + (wok[t] ? pl : 0) * a.wps;
       continue;
     }
     const int co = (wco + t) * 16 + l16;
     wok[t] = co < NCO * 8;
-    wrow[t] = a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8);
+    wrow[t] = a.wfrag ? a.w + (((long)g * NT + wco + t) * NKS * 64 + lane) * 8
+                      : a.w + ((long)g * (NCO * 8) + (wok[t] ? co : 0)) * (NCH * 8);
   }
   uint4 areg[RA][CT][NPL];
   auto load_a = [&](int s, uint4 (*dst)[NPL]) {
@@ -270,12 +277,16 @@ conv_fast_kernel(ConvArgs a) {
       ent(e, kk, cb);
       c = kk * NCBI + cb;
     }
+    const bool fr = a.wfrag != 0;
 #pragma unroll
-    for (int t = 0; t < CT; ++t)
+    for (int t = 0; t < CT; ++t) {
+      // fragment-major planes hold exact zeros in padded rows and entries past the chunk list
+      const bool ok = fr ? (!(PK && t == CT - 1) || wok[t]) : (wok[t] && e < NCH);
+      const long off = fr ? (long)((a.dbg & 8) ? 0 : s) * 512 : (long)c * 8;
 #pragma unroll
       for (int p = 0; p < ((PK && t == CT - 1) ? 1 : NPL); ++p)
-        dst[t][p] = *reinterpret_cast<const uint4*>((wok[t] && e < NCH) ? (const void*)(wrow[t] + p * a.wps + c * 8)
-                                                                          : (const void*)gt_zero8);
+        dst[t][p] = *reinterpret_cast<const uint4*>(ok ? (const void*)(wrow[t] + p * a.wps + off) : (const void*)gt_zero8);
+    }
   };
   // one k-step of tile t: the six-term product, or the packed tile's three MFMAs
   auto mma = [&](int t, const uint4* af, const uint4* bf, f32x4_t c) {

@@ -39,6 +39,7 @@ int gt_pool_fwd_mask(const void* x0, const void* x1, const int* sel, void* y, in
 int gt_pool_bwd_mask(const uint8_t* mask, const int* sel, const void* dy, void* dx0, void* dx1, int NB, int B,
                      int H, int W, int Cp, int relu_mask, int prec, hipStream_t s);
 int gt_wino_wtrans(const void* a, int nblocks, hipStream_t s);
+int gt_conv_wfrag(const void* a, int nblocks, hipStream_t s);
 }
 
 namespace {
@@ -47,7 +48,7 @@ namespace {
 enum : int32_t {
   OP_RECORD = 0, OP_WAIT = 1, OP_STEP_BEGIN = 2, OP_CONV = 3, OP_WGRAD = 4, OP_WGRAD_REDUCE = 5,
   OP_BN_FWD = 6, OP_BN_BWD = 7, OP_DENSE_FWD = 8, OP_HEAD = 9, OP_DENSE_DGRAD = 10, OP_DENSE_WGRAD_ADAM = 11,
-  OP_ADAM = 12, OP_POOL_FWD = 13, OP_POOL_FWD_MASK = 14, OP_POOL_BWD_MASK = 15, OP_WINO_WTRANS = 16, OP_COUNT = 17
+  OP_ADAM = 12, OP_POOL_FWD = 13, OP_POOL_FWD_MASK = 14, OP_POOL_BWD_MASK = 15, OP_WINO_WTRANS = 16, OP_CONV_WFRAG = 17, OP_COUNT = 18
 };
 
 constexpr int kMaxV = 14;
@@ -89,6 +90,7 @@ static int run_op(const GtProg& p, const GtProgOp& o, const hipStream_t* streams
     case OP_DENSE_WGRAD_ADAM: return gt_dense_wgrad_adam(P(v[0]), s);
     case OP_ADAM: return gt_adam_segments(P(v[0]), I(v[1]), s);
     case OP_WINO_WTRANS: return gt_wino_wtrans(P(v[0]), I(v[1]), s);
+    case OP_CONV_WFRAG: return gt_conv_wfrag(P(v[0]), I(v[1]), s);
     case OP_POOL_FWD:
       return gt_pool_fwd(P(v[0]), P(v[1]), static_cast<const int*>(P(v[2])), P(v[3]), I(v[4]), I(v[5]), I(v[6]),
                          I(v[7]), I(v[8]), I(v[9]), s);

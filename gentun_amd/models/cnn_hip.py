@@ -74,6 +74,12 @@ NATIVE_STEPS = True
 # flip it to check the executor path.
 WINOGRAD = False
 
+# layers (and directions) whose launches run the shape-specialised kernels read FRAGMENT-MAJOR weight planes
+# (ConvArgs::wfrag: each MFMA A fragment one contiguous KB, 6-16 % per conv launch,
+# profiles/r6/conv_wfrag_r6.txt), rewritten from the fp32 masters after every optimizer step; the optimizer
+# then skips the row-major bf16 planes of those layers. Module constant; tests flip it.
+WFRAG = True
+
 # bytes of forward-only activation twins an evaluation may allocate for all groups of a job
 EVAL_TWIN_BUDGET = 1 << 30
 
@@ -363,6 +369,28 @@ class HipPopJob(FoldJob):
             L.part_w = torch.zeros((L.S, Q, L.coutp, L.Kdim), dtype=torch.float32, device=dev)   # split-K partials
             L.part_b = torch.zeros((L.S, Q, L.coutp), dtype=torch.float32, device=dev)
         self.wino_tr = K.WinoTransform(wsegs, dev) if wsegs else None
+        # fragment-major planes for every layer direction a shape-specialised kernel runs
+        fspecs = []
+        for L in self.layers:
+            first = L.slots == ["input"]
+            L.wfrag = L.wfragT = False
+            if not WFRAG or L.wino:
+                continue
+            nr = max(1, len(L.rows))
+            if K._probe_conv(self.L, L.KH, L.KW, L.cinp, L.coutp, L.H, L.W, self.prec, nr, B, L.cout, True):
+                _, nks = K.frag_order(L.KH, L.KW, L.cinp // 8, L.W, self.prec)
+                L.wF = torch.zeros((npl, Q, -(-L.coutp // 16) * nks * 512), dtype=torch.bfloat16, device=dev)
+                fspecs.append((L.w[0], L.wF, L.W, self.prec, False))
+                L.wfrag = True
+            if not first and K._probe_conv(self.L, L.KH, L.KW, L.coutp, L.cinp, L.H, L.W, self.prec, nr, B, L.cin,
+                                           False):
+                _, nks = K.frag_order(L.KH, L.KW, L.coutp // 8, L.W, self.prec)
+                L.wTF = torch.zeros((npl, Q, -(-L.cinp // 16) * nks * 512), dtype=torch.bfloat16, device=dev)
+                fspecs.append((L.w[0], L.wTF, L.W, self.prec, True))
+                L.wfragT = True
+            # the optimizer writes no row-major bf16 planes when nothing reads them
+            L.bf_needed = not (L.wfrag and (L.wfragT or first))
+        self.frag_tr = K.FragTransform(fspecs, dev) if fspecs else None
         self.gW2 = torch.zeros((Q, self.Up, self.classes), dtype=torch.float32, device=dev)
         self.gb2 = torch.zeros((Q, self.classes), dtype=torch.float32, device=dev)
         self.gb1 = torch.zeros((Q, self.Up), dtype=torch.float32, device=dev)
@@ -408,8 +436,11 @@ class HipPopJob(FoldJob):
             for q, _ in L.rows:
                 p, m, v = (t[q] for t in L.w)
                 S = 1 if L.wred else L.S            # reduced into split 0 by gt_wgrad_reduce
-                add(p, m, v, L.part_w[0, q], S, L.part_w[0].numel(), bf=L.w_bf[0, q], bfT=L.wT_bf[0, q],
-                    tdims=(1, L.coutp, L.KH, L.KW, L.cinp), pstrides=(L.w_bf[0].numel(), L.wT_bf[0].numel()))
+                if getattr(L, "bf_needed", True):
+                    add(p, m, v, L.part_w[0, q], S, L.part_w[0].numel(), bf=L.w_bf[0, q], bfT=L.wT_bf[0, q],
+                        tdims=(1, L.coutp, L.KH, L.KW, L.cinp), pstrides=(L.w_bf[0].numel(), L.wT_bf[0].numel()))
+                else:                               # fragment-major planes: rewritten by gt_conv_wfrag
+                    add(p, m, v, L.part_w[0, q], S, L.part_w[0].numel())
                 p, m, v = (t[q] for t in L.b)
                 add(p, m, v, L.part_b[0, q], S, L.part_b[0].numel())
                 if self.bn:
@@ -495,10 +526,11 @@ class HipPopJob(FoldJob):
             pools = pool_of.get(L.name, set())
             cpools = set() if self.bn else pools
             a = self._conv_args(L, [self._slot_ptr(n) for n in L.slots], [out.data_ptr()], [],
-                                L.wU if L.wino else L.w_bf, L.b[0], 0 if self.bn else 1,
+                                L.wU if L.wino else L.wF if L.wfrag else L.w_bf, L.b[0], 0 if self.bn else 1,
                                 [(q, im, 1 | ((1 << 24) if q in cpools else 0)) for q, im in L.rows],
                                 gather=gather_train if first else None)
             a.wino = 1 if L.wino else 0
+            a.wfrag = 1 if L.wfrag else 0
             if L.xin is not None:
                 a.xsum = self.act[L.xin].data_ptr()
             if self.pad_hw is not None:
@@ -672,10 +704,12 @@ class HipPopJob(FoldJob):
                 def dgrad_args(unpool):
                     a = self._conv_args(L, [self.grad[L.name].data_ptr()],
                                         [self._slot_ptr(n, grad=True) for n in L.slots],
-                                        [self._slot_ptr(n) for n in L.slots], L.wUT if L.wino else L.wT_bf,
+                                        [self._slot_ptr(n) for n in L.slots],
+                                        L.wUT if L.wino else L.wTF if L.wfragT else L.wT_bf,
                                         None, 0, [(q, 1, of | ((1 << 25) if unpool else 0)) for q, of in rows],
                                         Cinp=L.coutp, Coutp=L.cinp)
                     a.wino = 1 if L.wino else 0
+                    a.wfrag = 1 if L.wfragT else 0
                     if unpool:
                         st = pool_stage[L.slots[0]]
                         a.pool_y, a.pool_mask = self.grad[st.inp].data_ptr(), st.pmask.data_ptr()
@@ -764,6 +798,8 @@ class HipPopJob(FoldJob):
             w = L.w[0]
             L.w_bf.copy_(split_planes(w, self.npl))
             L.wT_bf.copy_(split_planes(w.flip(2, 3).permute(0, 4, 2, 3, 1), self.npl))
+        if self.frag_tr is not None:
+            self.frag_tr.run(self._stream())
         if self.wino_tr is not None:
             self.wino_tr.run(self._stream())
 
@@ -914,6 +950,10 @@ class HipPopJob(FoldJob):
 
     def _adam_plan(self):
         plan = [("k", "gt_adam_segments", (self.adam_args, self.adam_nblocks), None, "adam")]
+        if self.frag_tr is not None:
+            # the next step's convs read the fragment-major planes of the updated masters
+            plan.append(("k", "gt_conv_wfrag", (K.C.addressof(self.frag_tr.args), self.frag_tr.nblocks), None,
+                         "conv_wfrag"))
         if self.wino_tr is not None:
             # the next step's Winograd layers convolve with the transform of the updated masters
             plan.append(("k", "gt_wino_wtrans", (K.C.addressof(self.wino_tr.args), self.wino_tr.nblocks), None,

@@ -37,7 +37,7 @@ class ConvArgs(C.Structure):
                 ("G", I), ("B", I), ("H", I), ("W", I), ("Cinp", I), ("Coutp", I), ("KH", I), ("KW", I),
                 ("TH", I), ("ngroups", I), ("xsum", P), ("dbg", I), ("epi_bf16", I), ("prec", I), ("wps", C.c_long),
                 ("cbb", I), ("pool_y", P), ("pool_mask", P), ("unpool_x1", P), ("unpool_sel", P),
-                ("cout_real", I), ("Hr", I), ("Wr", I), ("wino", I)]
+                ("cout_real", I), ("Hr", I), ("Wr", I), ("wino", I), ("wfrag", I)]
 
 
 class WinoWSeg(C.Structure):
@@ -49,6 +49,73 @@ class WinoWSeg(C.Structure):
 
 class WinoWArgs(C.Structure):
     _fields_ = [("segs", P), ("blocks", P)]
+
+
+class FragSeg(C.Structure):
+    """csrc/hip/cnn_conv_fast.hip FragSeg: one layer direction's fragment-major weight planes."""
+    _fields_ = [("w", P), ("dst", P), ("order", P), ("ps", C.c_long), ("Q", I), ("Cop", I), ("Cip", I), ("KH", I),
+                ("KW", I), ("NT", I), ("NKS", I), ("NCBIc", I), ("dgrad", I), ("npl", I)]
+
+
+class FragArgs(C.Structure):
+    _fields_ = [("segs", P), ("blocks", P)]
+
+
+def frag_order(KH, KW, ncbi, W, prec):
+    """Row-major chunk (kk * NCBI + cb) of every entry of a shape-specialised conv's reduction list, in the
+    kernel's order (-1 past the list), and the k-step count."""
+    nks = (KH * KW * ncbi + 3) // 4
+    out = (C.c_int * (nks * 4))()
+    lib().gt_conv_frag_order(KH, KW, ncbi, W, prec, out, nks * 4)
+    return list(out), nks
+
+
+class FragTransform(object):
+    """One launch that rewrites the fragment-major weight planes (ConvArgs::wfrag) of several layers and
+    directions from their fp32 masters -- after every optimizer step and after initialisation."""
+
+    def __init__(self, specs, device):
+        """``specs``: (master [Q][Cop][KH][KW][Cip] fp32, planes [npl][Q][NT*NKS*512] bf16, W, prec, dgrad)."""
+        import numpy as np
+        import torch
+        segs, blocks, self._keep = [], [], []
+        for master, planes, W, prec, dgrad in specs:
+            Q, cop, KH, KW, cip = master.shape
+            ncbi = (cop if dgrad else cip) // 8
+            nt = -(-(cip if dgrad else cop) // 16)
+            order, nks = frag_order(KH, KW, ncbi, W, prec)
+            assert tuple(planes.shape) == (planes.shape[0], Q, nt * nks * 512) and planes.is_contiguous()
+            ot = torch.tensor(order, dtype=torch.int32, device=device)
+            self._keep.append(ot)
+            sg = FragSeg()
+            sg.w, sg.dst, sg.order, sg.ps = master.data_ptr(), planes.data_ptr(), ot.data_ptr(), planes[0].numel()
+            sg.Q, sg.Cop, sg.Cip, sg.KH, sg.KW = Q, cop, cip, KH, KW
+            sg.NT, sg.NKS, sg.NCBIc, sg.dgrad, sg.npl = nt, nks, ncbi, 1 if dgrad else 0, planes.shape[0]
+            n = Q * nt * nks * 64
+            blocks.extend((len(segs), o) for o in range(0, n, 256))
+            segs.append(sg)
+        arr = (FragSeg * max(1, len(segs)))(*segs)
+        self.segs_t = torch.frombuffer(bytearray(bytes(memoryview(arr).cast("B"))), dtype=torch.uint8).to(device)
+        self.blocks_t = torch.tensor(np.asarray(blocks, np.int32).reshape(-1, 2), device=device)
+        self.args = FragArgs()
+        self.args.segs, self.args.blocks = self.segs_t.data_ptr(), self.blocks_t.data_ptr()
+        self.nblocks = len(blocks)
+
+    def run(self, stream):
+        if self.nblocks:
+            check(lib().gt_conv_wfrag(C.addressof(self.args), self.nblocks, stream), "conv_wfrag")
+
+
+def frag_planes(master, W, prec=1, dgrad=False):
+    """Fragment-major planes of ``master`` (tests / one-off use): [npl][Q][NT * NKS * 512] bf16."""
+    import torch
+    Q, cop, KH, KW, cip = master.shape
+    nt = -(-(cip if dgrad else cop) // 16)
+    _, nks = frag_order(KH, KW, (cop if dgrad else cip) // 8, W, prec)
+    planes = torch.zeros((3 if prec else 1, Q, nt * nks * 512), dtype=torch.bfloat16, device=master.device)
+    tr = FragTransform([(master.contiguous(), planes, W, prec, dgrad)], master.device)
+    tr.run(torch.cuda.current_stream(master.device).cuda_stream)
+    return planes
 
 
 def wino_dims(cinp, coutp):
@@ -133,7 +200,8 @@ class ProgOp(C.Structure):
 PROG_OPS = {"record": 0, "wait": 1, "gt_step_begin": 2, "gt_conv_fwd": 3, "gt_conv_wgrad": 4,
             "gt_wgrad_reduce": 5, "gt_bn_fwd": 6, "gt_bn_bwd": 7, "gt_dense_fwd": 8, "gt_head": 9,
             "gt_dense_dgrad": 10, "gt_dense_wgrad_adam": 11, "gt_adam_segments": 12, "gt_pool_fwd": 13,
-            "gt_pool_fwd_mask": 14, "gt_pool_bwd_mask": 15, "gt_wino_wtrans": 16}
+            "gt_pool_fwd_mask": 14, "gt_pool_bwd_mask": 15, "gt_wino_wtrans": 16,
+            "gt_conv_wfrag": 17}
 
 
 class InitSeg(C.Structure):
@@ -186,6 +254,12 @@ def lib():
         L.gt_conv_fast_probe_any.restype = I
         L.gt_wgrad_reduce.argtypes = [C.POINTER(WgradArgs), P]
         L.gt_wgrad_reduce.restype = I
+        L.gt_conv_frag_order.argtypes = [I, I, I, I, I, C.POINTER(C.c_int), I]
+        L.gt_conv_frag_order.restype = I
+        L.gt_conv_wfrag.argtypes = [P, I, P]
+        L.gt_conv_wfrag.restype = I
+        L.gt_sizeof_frag_seg.restype = C.c_size_t
+        assert L.gt_sizeof_frag_seg() == C.sizeof(FragSeg), "FragSeg ABI mismatch"
         L.gt_conv_wino_supported.argtypes = [I, I, I, I]
         L.gt_conv_wino_supported.restype = I
         L.gt_wino_wtrans.argtypes = [P, I, P]

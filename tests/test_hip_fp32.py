@@ -93,8 +93,8 @@ CONV_SHAPES = [(32, 32, 3, 20, 5, 1), (32, 32, 20, 20, 3, 3), (16, 16, 20, 50, 5
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,cin,cout,k,nin", CONV_SHAPES)
-@pytest.mark.parametrize("pk", [0, 1])
-def test_conv_fwd_fp32(H, W, cin, cout, k, nin, pk):
+@pytest.mark.parametrize("pk,wfrag", [(0, 0), (1, 0), (1, 1)])
+def test_conv_fwd_fp32(H, W, cin, cout, k, nin, pk, wfrag):
     """Forward conv (shape-specialised and generic kernels): fused N-ary Add
     in fp32, split MFMA, bias + ReLU; the input sum written for the wgrad
     (``xsum``) is the exact fp32 sum. ``pk``: the real output channel count
@@ -109,7 +109,8 @@ def test_conv_fwd_fp32(H, W, cin, cout, k, nin, pk):
     b = torch.randn(G, cout) * 0.1
     x_in = [torch.stack([nhwc_pad(x[g], cinp) for g in range(G)]).to(DEV).contiguous() for x in xs]
     wp = torch.stack([pack_w(w[g], coutp, cinp) for g in range(G)]).to(DEV)
-    wpl = _split(wp).contiguous()
+    # wfrag: the fragment-major planes (ConvArgs::wfrag) of the shape-specialised kernels
+    wpl = Km.frag_planes(wp.contiguous(), W) if wfrag else _split(wp).contiguous()
     bp = torch.zeros(G, coutp, device=DEV)
     bp[:, :cout] = b.to(DEV)
     out = torch.full((G, B, H, W, coutp), 7.0, device=DEV)
@@ -127,6 +128,10 @@ def test_conv_fwd_fp32(H, W, cin, cout, k, nin, pk):
     a.TH = Km.conv_tile_rows(H, W)
     a.prec = 1
     a.cout_real = cout if pk else 0
+    a.wfrag = wfrag
+    if wfrag and not Km.lib().gt_conv_fast_probe_any(a):
+        assert Km.lib().gt_conv_fwd(a, stream()) == -102           # generic kernels refuse fragment planes
+        pytest.skip("generic-kernel shape: no fragment-major planes")
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "conv")
     torch.cuda.synchronize()
     worst = worst32 = 0.0
@@ -139,13 +144,14 @@ def test_conv_fwd_fp32(H, W, cin, cout, k, nin, pk):
         assert torch.all(out[g, ..., cout:] == 0)
         if nin > 1:
             assert torch.equal(xsum[g, ..., :cin].permute(0, 3, 1, 2).cpu(), x32)
-    report("conv_fwd {}x{} {}->{} k{} n{}".format(H, W, cin, cout, k, nin), worst, worst32)
+    report("conv_fwd {}x{} {}->{} k{} n{}{}".format(H, W, cin, cout, k, nin, " wfrag" if wfrag else ""), worst, worst32)
     assert worst < TOL
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,H", [(3, 16), (5, 16), (3, 32), (3, 8), (3, -16)])
-def test_conv_dgrad_fanout_fp32(k, H):
+@pytest.mark.parametrize("wfrag", [0, 1])
+def test_conv_dgrad_fanout_fp32(k, H, wfrag):
     """Data gradient = conv of dz with the flipped / transposed weight planes;
     DAG fan-out into two slots, one accumulating, one ReLU-masked."""
     Km = K()
@@ -161,7 +167,8 @@ def test_conv_dgrad_fanout_fp32(k, H):
                        for g in range(G)])
     r32 = torch.stack([torch.nn.grad.conv2d_input((B, cin, H, W), w[g], dz[g], padding=k // 2) for g in range(G)])
     wp = torch.stack([pack_w(w[g], coutp, cinp) for g in range(G)]).to(DEV)
-    wT = _split(wp.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous()).contiguous()
+    wT = Km.frag_planes(wp.contiguous(), W, dgrad=True) if wfrag else \
+        _split(wp.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous()).contiguous()
     dz_p = torch.stack([nhwc_pad(dz[g], coutp) for g in range(G)]).to(DEV).contiguous()
     out0 = torch.zeros(G, B, H, W, cinp, device=DEV)
     prev = torch.randn(G, B, H, W, cinp, device=DEV)
@@ -180,6 +187,10 @@ def test_conv_dgrad_fanout_fp32(k, H):
     a.TH = Km.conv_tile_rows(H, W)
     a.prec = 1
     a.cout_real = cin                      # packed last tile where the shape allows (20 = 16 + 4)
+    a.wfrag = wfrag
+    if wfrag and not Km.lib().gt_conv_fast_probe_any(a):
+        assert Km.lib().gt_conv_fwd(a, stream()) == -102           # generic kernels refuse fragment planes
+        pytest.skip("generic-kernel shape: no fragment-major planes")
     Km.check(Km.lib().gt_conv_fwd(a, stream()), "dgrad")
     torch.cuda.synchronize()
     got0 = out0[..., :cin].permute(0, 1, 4, 2, 3)

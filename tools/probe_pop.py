@@ -2,7 +2,7 @@
 split into jobs of ``pop_batch`` on ``streams`` streams, 1 epoch each.
 
 usage: python tools/probe_pop.py [P] [pop_batch] [streams] [epochs] [samples]
-Env: WINO=0/1 (Winograd stage-2 3x3 layers), SHAPE=28,28,1 (MNIST-shaped: the reference default, stored zero-padded to 32 x 32 unless PAD=0),
+Env: WINO=0/1 (Winograd stage-2 3x3 layers), WFRAG=0/1 (fragment-major conv weights), SHAPE=28,28,1 (MNIST-shaped: the reference default, stored zero-padded to 32 x 32 unless PAD=0),
 SPACE=deep, KERNELS=, BN=1, DTYPE=, RESET=, GRAPH=0, WARM=0.
 """
 import json
@@ -28,6 +28,9 @@ dev = torch.device("cuda", 0)
 if os.environ.get("WINO") is not None:                # A/B: Winograd stage-2 3x3 layers on (1) / off (0)
     from gentun_amd.models import cnn_hip
     cnn_hip.WINOGRAD = os.environ["WINO"] != "0"
+if os.environ.get("WFRAG") is not None:               # A/B: fragment-major conv weight planes on (1) / off (0)
+    from gentun_amd.models import cnn_hip as _ch
+    _ch.WFRAG = os.environ["WFRAG"] != "0"
 if os.environ.get("GENTUN_WGRAD_NB"):                 # A/B: force the wgrad band buffers
     from gentun_amd.ops import cnn_kernels as K
     K.lib().gt_wgrad_set_nb(int(os.environ["GENTUN_WGRAD_NB"]))

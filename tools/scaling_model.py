@@ -47,7 +47,9 @@ def generation_time(curve, pending, world, per_gpu=5, slack=1, nfold=5, overhead
     t, rounds = 0.0, []
     while pending > 0:
         n = balanced_round(pending, per_gpu * world, slack=slack * world)
-        units, _ = make_units([1.0] * n, nfold, world)
+        # the population-batched evaluator takes (candidate, fold) units (DistributedPopulation._dispatch:
+        # per_fold when pop_batch > 1 and the folds train concurrently); equal candidate costs here
+        units, _ = make_units([1.0] * n, nfold, world, True, per_fold=world > 1)
         folds_per_unit = [len(u[1]) for u in units]
         owner = lpt_assign([float(f) for f in folds_per_unit], world)
         groups = [0] * world
