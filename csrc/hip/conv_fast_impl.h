@@ -71,10 +71,34 @@ struct FastCfg {
   // the wide deep space -- put every lane of a ds_read_b128 pass on the same banks: 8-16 way
   // conflicts, PMC LDSbc 0.7-0.86 on those launches); the S=(3,5) / (20,50,100) strides are odd already
   static constexpr int NCBP = NCBI + ((NCBI & 1) ? 0 : 1);
-  static constexpr int NPP = (TH + KH - 1) * PW * NCBP;
+  // PAIR layout (fp32 shapes with >= 2 input chunks): chunk PAIRS (cb 2j, 2j+1) of every pixel side by side,
+  // pixel stride 2 chunks, one pair-plane of PP2 chunks per j. A ds_read_b128 lane group holds 8 pixels of k
+  // entry kq and 8 of kq+1; when those entries are chunks of opposite parity (cb, cb+1 of one tap: every
+  // k-step of the part-major stage-2 order, most of the kk-major ones) the 16 addresses fall on 16 different
+  // 16-byte bank quads (2 x pixel is even, the chunk parity adds 0 / 1). With the pixel-major odd stride
+  // NCBP, seven of the eight lane pairs met on one quad: every patch read took 2 LDS passes (PMC LDSbc
+  // 0.47 on the stage-2 conv, profiles/r5/pmc_step_fp32_p5_final_r5.txt). PP2 mod 8 is picked per chunk count
+  // for the fewest read, then write, conflicts (tools/lds_patch_sim.py models every lane group of the reads
+  // and the staging writes).
+  static constexpr int NPIX = (TH + KH - 1) * PW;
+  static constexpr int PPR = (S2Parts<KH, KW, NCBI, W, PREC>::on || NCBI == 3) ? 5 : (NCBI % 2 == 0) ? (NCBI == 4 ? 4 : 2) : 6;
+  static constexpr int PP2 = 2 * NPIX + ((PPR - (2 * NPIX) % 8) + 8) % 8;
   static constexpr int TP = TH * W;
   static constexpr int OROW = NT * 16 + 4;          // fp32 tile row (floats; conflict-free float4 writes)
   static constexpr int OROWB = NT * 16 + 8;         // bf16 tile row (elements; conflict-free 8-byte writes)
+  static constexpr int NPL_ = PREC ? GT_NPL_F32 : 1;
+  static constexpr long OTILE = (long)TP * OROW * 4;
+  static constexpr long LDS_PM = (long)NPIX * NCBP * 16 * NPL_ > OTILE ? (long)NPIX * NCBP * 16 * NPL_ : OTILE;
+  static constexpr long LDS_PR = (long)((NCBI + 1) / 2) * PP2 * 16 * NPL_ > OTILE ? (long)((NCBI + 1) / 2) * PP2 * 16 * NPL_ : OTILE;
+  static constexpr long LDS_CU = 160 * 1024;
+  // only where the patch's LDS does not cost a workgroup per CU: the s1 3x3 tile (3 -> 2 workgroups per CU by
+  // LDS) ran 7-14 % slower per launch in the pair layout, the stage-2 tiles 0.5-1.5 % faster, the population
+  // step -0.8 % with this rule (profiles/r6/conv_patch_pair_r6.txt)
+  static constexpr bool PAIR = PREC == 1 && NCBI >= 2 && LDS_CU / LDS_PR >= LDS_CU / LDS_PM;
+  static constexpr int PXS = PAIR ? 2 : NCBP;       // LDS pixel stride (chunks)
+  static constexpr int NPP = PAIR ? ((NCBI + 1) / 2) * PP2 : NPIX * NCBP;
+  // LDS chunk offset of chunk cb within a pixel
+  __host__ __device__ static constexpr int cbo(int cb) { return PAIR ? (cb >> 1) * PP2 + (cb & 1) : cb; }
   static size_t lds(bool fwd) {
     const size_t p = (size_t)NPP * 16 * NPL;
     const size_t o = (fwd && !PREC) ? (size_t)TP * OROWB * 2 : (size_t)TP * OROW * 4;
@@ -180,12 +204,14 @@ conv_fast_kernel(ConvArgs a) {
   constexpr int NTH = NWV * 64;                     // threads
   constexpr int PH = TH + KH - 1, PW = W + KW - 1;
   constexpr int NP = PH * PW * NCBI;                // patch chunks (8 channels) per plane
-  constexpr int NCBP = FastCfg<KH, KW, NCBI, W, TH, NT, NCO, PREC>::NCBP;   // LDS chunks per patch pixel
-  constexpr int NPP = PH * PW * NCBP;               // LDS plane stride (chunks)
+  using FCL = FastCfg<KH, KW, NCBI, W, TH, NT, NCO, PREC>;
+  constexpr int NCBP = FCL::NCBP;                   // LDS chunks per patch pixel (pixel-major layout)
+  constexpr int PXS = FCL::PXS;                     // LDS pixel stride (chunks)
+  constexpr int NPP = FCL::NPP;                     // LDS plane stride (chunks)
   // staged chunk i (pixel i / NCBI, chunk i % NCBI) -> its LDS slot
   auto pslot = [&](int i) {
-    if constexpr (NCBP == NCBI) return i;
-    else return (i / NCBI) * NCBP + i % NCBI;
+    if constexpr (NCBP == NCBI && !FCL::PAIR) return i;
+    else return (i / NCBI) * PXS + FCL::cbo(i % NCBI);
   };
   constexpr int NPT = (NP + NTH - 1) / NTH;             // patch chunks per thread
   constexpr int NCH = KH * KW * NCBI;               // reduction chunks
@@ -403,7 +429,7 @@ conv_fast_kernel(ConvArgs a) {
       const int cb = i % NCBI, pix = i / NCBI;
       const int r = pix / W, c = pix % W;
       if (h0 + r >= a.H) continue;
-      const int pi = ((r + KH / 2) * PW + c + KW / 2) * NCBP + cb;
+      const int pi = ((r + KH / 2) * PW + c + KW / 2) * PXS + FCL::cbo(cb);
       if (PREC) {
         float f[8];
         join8(patch[pi], patch[NPP + pi], patch[2 * NPP + pi], f);   // exact: the fp32 sum
@@ -417,7 +443,7 @@ conv_fast_kernel(ConvArgs a) {
   for (int c = tid; c < NKS * 4; c += NTH) {
     int kk, cb;
     ent(c, kk, cb);
-    coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBP + cb : 0;
+    coff[c] = c < NCH ? ((kk / KW) * PW + (kk % KW)) * PXS + FCL::cbo(cb) : 0;
   }
   // first PF k-steps of weights in flight before the barrier (after the patch
   // staging: its registers are dead by now -- lower peak register pressure)
@@ -436,11 +462,11 @@ conv_fast_kernel(ConvArgs a) {
 
   // ---- MFMA main loop ------------------------------------------------------
   // lane's pixel within a group: (l16 / W) rows down, l16 % W across (W >= 16: same row)
-  const int lbase = ((l16 / W) * PW + (l16 % W)) * NCBP;
+  const int lbase = ((l16 / W) * PW + (l16 % W)) * PXS;
   int gbase;
   {
     const int p = pgw * 16;
-    gbase = ((p / W) * PW + (p % W)) * NCBP;
+    gbase = ((p / W) * PW + (p % W)) * PXS;
   }
   f32x4_t acc[CT][PG];
 #pragma unroll
@@ -453,7 +479,7 @@ conv_fast_kernel(ConvArgs a) {
     const int c = s * 4 + kq;
     int kk, cb;
     ent(c, kk, cb);
-    return c < NCH ? ((kk / KW) * PW + (kk % KW)) * NCBP + cb : 0;
+    return c < NCH ? ((kk / KW) * PW + (kk % KW)) * PXS + FCL::cbo(cb) : 0;
   };
   // the patch fragments of k-step s: the offset from the LDS table, or (pipelined loop) computed in
   // registers so no table read drains lgkmcnt in the middle of the MFMA stream
@@ -463,7 +489,7 @@ conv_fast_kernel(ConvArgs a) {
     for (int h = 0; h < PG; ++h) {
       const int p = h * 16;                        // relative to the wave's first group
 #pragma unroll
-      for (int q = 0; q < NPL; ++q) dst[h][q] = pb[q * NPP + ((p / W) * PW + (p % W)) * NCBP];
+      for (int q = 0; q < NPL; ++q) dst[h][q] = pb[q * NPP + ((p / W) * PW + (p % W)) * PXS];
     }
   };
   if (!(a.dbg & 1)) {

@@ -41,6 +41,15 @@ a.w1, a.part, a.ks = w1.data_ptr(), part.data_ptr(), ks
 d = Km.DenseDgradArgs()
 d.dH, d.wt, d.dx, d.G, d.B, d.Fp, d.Up, d.prec = dH.data_ptr(), wt.data_ptr(), dx.data_ptr(), G, B, Fp, Up, 1
 d.w1 = w1.data_ptr()
+# fused dW1 + Adam on the fp32 master / m / v (padded channels 50 of 56, units 500 of 512: the bench shapes)
+pm, vm = torch.zeros_like(w1), torch.ones_like(w1) * 1e-3
+st[:] = 0
+st.view(torch.float32)[3] = 1e-3
+L.gt_step_begin(st.data_ptr(), None)
+wa = Km.DenseWgradAdamArgs()
+wa.x, wa.dH, wa.p, wa.m, wa.v, wa.wt, wa.st = x.data_ptr(), dH.data_ptr(), w1.data_ptr(), pm.data_ptr(), \
+    vm.data_ptr(), 0, st.data_ptr()
+wa.G, wa.B, wa.Fp, wa.Up, wa.Cp, wa.Cr, wa.Ur, wa.prec = G, B, Fp, Up, 56, 50, 500, 1
 flush = torch.empty(512 * 1024 * 1024 // 4, device=dev)     # 512 MB: evicts the Infinity Cache
 
 
@@ -67,9 +76,12 @@ def timeit(fn, cold):
 
 wbytes = G * Fp * Up * 4
 for name, fn in (("dense_fwd", lambda s: Km.check(L.gt_dense_fwd(a, ctypes.c_void_p(s)), "fwd")),
-                 ("dense_dgrad", lambda s: Km.check(L.gt_dense_dgrad(d, ctypes.c_void_p(s)), "dgrad"))):
+                 ("dense_dgrad", lambda s: Km.check(L.gt_dense_dgrad(d, ctypes.c_void_p(s)), "dgrad")),
+                 ("dense_wgrad_adam", lambda s: Km.check(L.gt_dense_wgrad_adam(wa, ctypes.c_void_p(s)), "wadam"))):
     for cold in (True, False):
         us = timeit(fn, cold)
         print(json.dumps({"kernel": name, "G": G, "cold": cold, "us": round(us, 1),
                           "w1_GBps": round(wbytes / us / 1e3, 1),
+                          # p/m/v read + written over the real rows / units (the kernel's HBM floor)
+                          "pmv_GBps": round(6 * G * 3200 * 500 * 4 / us / 1e3, 1) if name == "dense_wgrad_adam" else None,
                           }), flush=True)
