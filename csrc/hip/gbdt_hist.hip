@@ -47,6 +47,7 @@
 // lane reads 4 features of a row as one 4-byte word.
 
 #include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -858,6 +859,55 @@ __global__ void __launch_bounds__(256) metric_kernel(Geo geo, const float* __res
   if (threadIdx.x < 4) out[((size_t)k * gridDim.x + blockIdx.x) * 4 + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// ---- G8 auc: tie-averaged rank sum of the positives per (fold, train / test) segment ----------
+// engine.cpp auc_score sorts every fold's margins and gives a tie group its average rank. Here one
+// radix sort orders all nfold * n rows at once by key = seg << 33 | ordered(margin) << 1 | positive
+// (seg = 2 k + [row in fold k's test set]); a positive then finds its tie group [a, b] and its
+// segment's start by binary search in the sorted keys (negatives of the group sort first, which does
+// not change its bounds). Each positive adds (a + b) / 2 + 1 - start, a multiple of 1/2 below 2^52,
+// so the fp64 sums are exact and independent of the atomic order: the result is deterministic.
+__global__ void __launch_bounds__(256) auc_keys_kernel(Geo geo, const float* __restrict__ margin,
+                                                       const float* __restrict__ y,
+                                                       const int* __restrict__ fold_of, u64* __restrict__ keys) {
+  const int k = blockIdx.y;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < geo.n; i += gridDim.x * blockDim.x) {
+    const unsigned int b = __float_as_uint(margin[((size_t)k * geo.n + i) * geo.K] + 0.f);   // -0 -> +0
+    const unsigned int ord = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    const u64 seg = 2u * (unsigned)k + (fold_of[i] == k ? 1u : 0u);
+    keys[(size_t)k * geo.n + i] = (seg << 33) | ((u64)ord << 1) | (y[i] > 0.5f ? 1u : 0u);
+  }
+}
+
+__device__ __forceinline__ size_t lower_bound_u64(const u64* __restrict__ a, size_t n, u64 x) {
+  size_t lo = 0;
+  while (n > 0) {
+    const size_t h = n >> 1;
+    if (a[lo + h] < x) { lo += h + 1; n -= h + 1; } else n = h;
+  }
+  return lo;
+}
+
+// acc[seg * 2 + {0: rank sum of the positives, 1: positives}], zeroed before the launch; nseg <= 64
+__global__ void __launch_bounds__(256) auc_rank_kernel(const u64* __restrict__ sorted, size_t N, int nseg,
+                                                       double* __restrict__ acc) {
+  __shared__ double s[128];
+  for (int t = threadIdx.x; t < 2 * nseg; t += blockDim.x) s[t] = 0.0;
+  __syncthreads();
+  for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (size_t)gridDim.x * blockDim.x) {
+    const u64 key = sorted[p];
+    if (!(key & 1u)) continue;
+    const u64 seg = key >> 33;
+    const size_t a = lower_bound_u64(sorted, N, key & ~1ull);
+    const size_t b = lower_bound_u64(sorted, N, key + 1) - 1;     // key | 1 == key: last of the group
+    const size_t st = lower_bound_u64(sorted, N, seg << 33);
+    atomicAdd(&s[2 * seg], 0.5 * (double)(a + b) + 1.0 - (double)st);
+    atomicAdd(&s[2 * seg + 1], 1.0);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < 2 * nseg; t += blockDim.x)
+    if (s[t] != 0.0) atomicAdd(&acc[t], s[t]);
+}
+
 uint64_t smix(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -887,8 +937,9 @@ extern "C" {
 
 // Same contract as gbdt_cv (csrc/gbdt/engine.cpp) for every objective
 // (reg:linear/squarederror, reg:logistic, binary:logistic/logitraw,
-// multi:softmax/softprob: one tree per class) and every metric but auc
-// (rmse, mae, logloss, error, merror, mlogloss; early stopping on the last).
+// multi:softmax/softprob: one tree per class) and every metric (rmse, mae,
+// logloss, error, auc, merror, mlogloss; early stopping on the last, auc
+// maximised). auc needs nfold <= 32 (64 sort segments).
 // bins_h may be null when gbdt_quantize_hip already left the dataset's bins
 // on the device under cache_key (returns -7 if they were evicted). bins:
 // ROW-major [n][Fs] uint8 (Fs >= F, Fs % 4 == 0). cache_key != 0 keeps the
@@ -900,8 +951,12 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
                 long long cache_key, double* out_hist) {
   if (objective < 0 || objective > 5 || n_metrics < 1 || Fs % 4 || Fs < F || n <= 0 || nfold <= 0 || F <= 0)
     return -1;
-  for (int mi = 0; mi < n_metrics; ++mi)
-    if (metrics[mi] < 0 || metrics[mi] > 6 || metrics[mi] == 4) return -1;   // auc: CPU engine
+  bool want_auc = false;
+  for (int mi = 0; mi < n_metrics; ++mi) {
+    if (metrics[mi] < 0 || metrics[mi] > 6) return -1;
+    want_auc = want_auc || metrics[mi] == 4;
+  }
+  if (want_auc && nfold > 32) return -1;
   const bool multi = objective >= 4;
   const int K = multi ? std::max(2, num_class) : 1;
   const int obj = multi ? 3 : (objective == 0 ? 0 : (objective == 1 ? 1 : 2));
@@ -965,8 +1020,19 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   const size_t met_elems = (size_t)n_metrics * nfold * mblocks * 4;
   const uint8_t* d_bins = nullptr;
   double base = P[11];
-  const bool lower_better = true;
-  double best_score = INFINITY;
+  const bool lower_better = metrics[n_metrics - 1] != 4;      // engine.cpp higher_better: auc
+  double best_score = lower_better ? INFINITY : -INFINITY;
+  // auc: sort keys (two buffers + rocprim scratch) and [2 nfold][2] rank sums; rows per test fold
+  u64 *d_akeys = nullptr, *d_asorted = nullptr;
+  void* d_atmp = nullptr;
+  size_t atmp_bytes = 0;
+  double* d_aacc = nullptr;
+  const size_t aN = (size_t)nfold * n;
+  const int aseg_bits = 33 + [](int s) { int b = 0; while ((1 << b) < s) ++b; return b; }(2 * nfold);
+  std::vector<double> h_aacc(4 * (size_t)nfold);
+  std::vector<double> ntest(nfold, 0.0);
+  for (int i = 0; i < n; ++i)
+    if (fold_h[i] >= 0 && fold_h[i] < nfold) ntest[fold_h[i]] += 1.0;
   int best_round = 0, rounds_done = 0;
   static const bool timing = std::getenv("GENTUN_GBDT_TIMING") != nullptr;
   static const int progress = std::getenv("GENTUN_GBDT_PROGRESS") ? std::atoi(std::getenv("GENTUN_GBDT_PROGRESS")) : 0;
@@ -1016,6 +1082,13 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
   HC(hipMalloc(&d_keys, keys_bytes));
   HC(hipMalloc(&d_order, sizeof(int) * K * order_elems));
   HC(hipMalloc(&d_met, sizeof(double) * met_elems));
+  if (want_auc) {
+    HC(hipMalloc(&d_akeys, sizeof(u64) * aN));
+    HC(hipMalloc(&d_asorted, sizeof(u64) * aN));
+    HC(hipMalloc(&d_aacc, sizeof(double) * 4 * nfold));
+    HC(rocprim::radix_sort_keys(nullptr, atmp_bytes, d_akeys, d_asorted, aN, 0u, (unsigned)aseg_bits));
+    HC(hipMalloc(&d_atmp, std::max<size_t>(atmp_bytes, 1)));
+  }
   HC(hipHostMalloc(&h_up, up_bytes, hipHostMallocDefault));
   HC(hipHostMalloc((void**)&h_met, sizeof(double) * met_elems, hipHostMallocDefault));
   HC(hipMemcpy(d_y, y_h, sizeof(float) * n, hipMemcpyHostToDevice));
@@ -1124,15 +1197,33 @@ int gbdt_cv_hip(const uint8_t* bins_h, int Fs, const int* nbins_h, int n, int F,
                          geo, d_bins, d_tree, d_leaf, d_margin, c, pk, pr_rows);
     }
     for (int mi = 0; mi < n_metrics; ++mi)
-      hipLaunchKernelGGL(metric_kernel, dim3(mblocks, nfold), dim3(256), 0, 0, geo, d_margin, d_y, d_fold,
-                         metrics[mi], objective, d_met + (size_t)mi * nfold * mblocks * 4);
+      if (metrics[mi] != 4)
+        hipLaunchKernelGGL(metric_kernel, dim3(mblocks, nfold), dim3(256), 0, 0, geo, d_margin, d_y, d_fold,
+                           metrics[mi], objective, d_met + (size_t)mi * nfold * mblocks * 4);
+    if (want_auc) {
+      hipLaunchKernelGGL(auc_keys_kernel, dim3(mblocks, nfold), dim3(256), 0, 0, geo, d_margin, d_y, d_fold, d_akeys);
+      HC(rocprim::radix_sort_keys(d_atmp, atmp_bytes, d_akeys, d_asorted, aN, 0u, (unsigned)aseg_bits));
+      HC(hipMemsetAsync(d_aacc, 0, sizeof(double) * 4 * nfold, 0));
+      hipLaunchKernelGGL(auc_rank_kernel, dim3((unsigned)std::min<size_t>(1024, (aN + 255) / 256)), dim3(256), 0, 0,
+                         d_asorted, aN, 2 * nfold, d_aacc);
+    }
     HC(hipGetLastError());
-    // the round's one blocking copy: early stopping needs the test metric
+    // the round's blocking copies: early stopping needs the test metric
     HC(hipMemcpy(h_met, d_met, sizeof(double) * met_elems, hipMemcpyDeviceToHost));
+    if (want_auc) HC(hipMemcpy(h_aacc.data(), d_aacc, sizeof(double) * 4 * nfold, hipMemcpyDeviceToHost));
     double tem_last = 0;
     for (int mi = 0; mi < n_metrics; ++mi) {
       std::vector<double> trv(nfold), tev(nfold);
       for (int k = 0; k < nfold; ++k) {
+        if (metrics[mi] == 4) {         // engine.cpp auc_score: (R+ - n+(n+ + 1)/2) / (n+ n-), 0.5 if one class
+          auto auc = [](double r, double np, double nn) {
+            return (np == 0 || nn <= 0) ? 0.5 : (r - np * (np + 1) / 2) / (np * nn);
+          };
+          const double* a = &h_aacc[4 * (size_t)k];
+          trv[k] = auc(a[0], a[1], (double)n - ntest[k] - a[1]);
+          tev[k] = auc(a[2], a[3], ntest[k] - a[3]);
+          continue;
+        }
         double met[4] = {0, 0, 0, 0};
         const double* pm = h_met + ((size_t)mi * nfold + k) * mblocks * 4;
         for (int b = 0; b < mblocks; ++b)
@@ -1169,7 +1260,7 @@ done:
                   (void*)d_gh, (void*)d_hist[0], (void*)d_hist[1], (void*)d_part, (void*)d_lvl[0], (void*)d_lvl[1],
                   (void*)d_chunks, (void*)d_reds, (void*)d_counts, (void*)d_nroot, (void*)d_cand, (void*)d_best,
                   (void*)d_tree, (void*)d_leaf, (void*)d_split, (void*)d_cur, (void*)d_mx, (void*)d_keys,
-                  (void*)d_order, (void*)d_met})
+                  (void*)d_order, (void*)d_met, (void*)d_akeys, (void*)d_asorted, (void*)d_atmp, (void*)d_aacc})
     if (p) (void)hipFree(p);
   if (h_up) (void)hipHostFree(h_up);
   if (h_met) (void)hipHostFree(h_met);

@@ -3,8 +3,10 @@ predict kernels on the GPU (csrc/hip/gbdt_hist.hip: row-major bins, per-node
 row segments, smaller-child histograms + subtraction). Used by
 :func:`gentun_amd.models.gbdt.cv` when ``device`` is a CUDA/HIP device;
 every objective (regression, logistic, binary, multi-class) and every metric
-but auc run on the GPU; an auc run falls back to the CPU engine with a one-time
-``RuntimeWarning`` (never silently)."""
+run on the GPU (auc: one radix sort of every fold's margins per round plus a
+binary-search rank kernel). The one unsupported case, auc with more than 32
+folds, falls back to the CPU engine with a one-time ``RuntimeWarning`` (never
+silently)."""
 
 import ctypes
 import warnings
@@ -14,11 +16,13 @@ import numpy as np
 from ..ops import _lib
 
 GPU_OBJECTIVES = (0, 1, 2, 3, 4, 5)      # every objective of models/gbdt.py OBJECTIVES
-GPU_METRICS = (0, 1, 2, 3, 5, 6)         # all but auc (a sort per fold: CPU engine)
+GPU_METRICS = (0, 1, 2, 3, 4, 5, 6)      # every metric of models/gbdt.py METRICS
+AUC, AUC_MAX_FOLDS = 4, 32                # auc sorts 2 segments per fold into a 6-bit segment id
 
 
-def supported(obj, metrics):
-    return obj in GPU_OBJECTIVES and len(metrics) >= 1 and all(int(m) in GPU_METRICS for m in metrics)
+def supported(obj, metrics, nfold=1):
+    return (obj in GPU_OBJECTIVES and len(metrics) >= 1 and all(int(m) in GPU_METRICS for m in metrics)
+            and not (nfold > AUC_MAX_FOLDS and any(int(m) == AUC for m in metrics)))
 
 
 def _fn():
@@ -117,21 +121,19 @@ def device_bins(x, key, fs):
 _WARNED = set()
 
 
-def _warn_fallback(obj, marr):
-    key = (int(obj), tuple(int(m) for m in marr))
+def _warn_fallback(obj, marr, nfold):
+    key = (int(obj), tuple(int(m) for m in marr), int(nfold))
     if key in _WARNED:
         return
     _WARNED.add(key)
-    from .gbdt import METRICS
-    names = sorted(n for n, v in METRICS.items() if v in key[1] and v not in GPU_METRICS)
-    warnings.warn("gbdt.cv(device='cuda'): eval_metric {} has no GPU implementation; this cross-validation "
-                  "runs on the CPU engine (csrc/gbdt/engine.cpp)".format(", ".join(names) or key[1]),
+    warnings.warn("gbdt.cv(device='cuda'): eval_metric auc with {} folds (GPU auc supports <= {}); this "
+                  "cross-validation runs on the CPU engine (csrc/gbdt/engine.cpp)".format(nfold, AUC_MAX_FOLDS),
                   RuntimeWarning, stacklevel=3)
 
 
 def cv(x, y, fold_of, nfold, parr, obj, num_class, marr, nrounds, esr, seed, hist, x_key=None):
-    if not supported(obj, marr):
-        _warn_fallback(obj, marr)
+    if not supported(obj, marr, nfold):
+        _warn_fallback(obj, marr, nfold)
         return None
     xk = x if x_key is None else x_key
     fold_of = np.ascontiguousarray(fold_of.astype(np.int32))

@@ -139,19 +139,21 @@ def test_unsupported_booster_and_unknown_params_raise():
 
 
 def test_gpu_auc_falls_back_loudly():
-    """eval_metric auc has no GPU implementation: device='cuda' must say (once) that the CV runs on
-    the CPU engine instead of silently changing device. The check in
-    gbdt_hip.cv happens before any device call, so it runs on CPU-only hosts too."""
+    """GPU auc sorts 2 segments per fold (<= 32 folds). Beyond that device='cuda' must say (once)
+    that the CV runs on the CPU engine instead of silently changing device.
+    The check in gbdt_hip.cv happens before any device call, so it runs on CPU-only hosts too."""
     import warnings
     from gentun_amd.models import gbdt_hip
     x, y = load_iris_xy()
     yb = (y == 2).astype(np.float64)
+    assert gbdt_hip.supported(1, [4], nfold=32) and not gbdt_hip.supported(1, [4], nfold=33)
+    assert gbdt_hip.supported(1, [2], nfold=40)
     gbdt_hip._WARNED.clear()
     p = {'objective': 'binary:logistic', 'eval_metric': 'auc'}
-    with pytest.warns(RuntimeWarning, match="auc has no GPU implementation"):
-        h = gbdt.cv(dict(p), x, yb, num_boost_round=5, nfold=3, device='cuda')
-    ref = gbdt.cv(dict(p), x, yb, num_boost_round=5, nfold=3)
+    with pytest.warns(RuntimeWarning, match="auc with 33 folds"):
+        h = gbdt.cv(dict(p), x, yb, num_boost_round=3, nfold=33, device='cuda')
+    ref = gbdt.cv(dict(p), x, yb, num_boost_round=3, nfold=33)
     assert h['test-auc-mean'] == ref['test-auc-mean']          # the CPU engine's result
     with warnings.catch_warnings():
-        warnings.simplefilter("error")                         # once per (objective, metrics)
-        gbdt.cv(dict(p), x, yb, num_boost_round=5, nfold=3, device='cuda')
+        warnings.simplefilter("error")                         # once per (objective, metrics, folds)
+        gbdt.cv(dict(p), x, yb, num_boost_round=3, nfold=33, device='cuda')

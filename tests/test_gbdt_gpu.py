@@ -103,6 +103,40 @@ def test_hip_logitraw_and_metric_semantics():
             assert np.max(np.abs(a - b)) < 0.02 + 0.02 * np.max(np.abs(a)), (p, k, a[-3:], b[-3:])
 
 
+@pytest.mark.parametrize("obj", ["binary:logistic", "binary:logitraw"])
+def test_hip_auc_matches_cpu(obj):
+    """GPU auc (one radix sort of every fold's train / test margins, tie groups found by binary search,
+    exact fp64 rank sums): same values as the CPU engine's tie-averaged auc_score up to the fp32 margins,
+    maximised by early stopping, bitwise reproducible."""
+    x, y = make_regression(n=20000, f=10, seed=5)
+    yb = (y > np.median(y)).astype(np.float64)
+    p = {'objective': obj, 'eval_metric': ['logloss', 'auc'] if obj == 'binary:logistic' else 'auc',
+         'max_depth': 3, 'eta': 0.3}
+    cpu = gbdt.cv(dict(p), x, yb, num_boost_round=40, nfold=4, early_stopping_rounds=5, seed=0)
+    gpu = gbdt.cv(dict(p), x, yb, num_boost_round=40, nfold=4, early_stopping_rounds=5, seed=0, device="cuda:0")
+    assert len(cpu['test-auc-mean']) == len(gpu['test-auc-mean'])
+    for k in ('train-auc-mean', 'test-auc-mean', 'test-auc-std'):
+        a, b = np.array(cpu[k]), np.array(gpu[k])
+        assert np.max(np.abs(a - b)) < 2e-3, (k, a[-3:], b[-3:])
+    assert 0.8 < gpu['test-auc-mean'][-1] <= 1.0
+    assert gpu['test-auc-mean'][-1] == max(gpu['test-auc-mean'])   # auc is maximised
+    again = gbdt.cv(dict(p), x, yb, num_boost_round=40, nfold=4, early_stopping_rounds=5, seed=0, device="cuda:0")
+    assert again == gpu
+
+
+def test_hip_auc_ties_and_one_class_fold():
+    """Heavy ties (depth-1 stumps: two margin values per tree) and a constant label (auc 0.5) on the GPU."""
+    x, y = load_iris_xy()
+    yb = (y == 2).astype(np.float64)
+    p = {'objective': 'binary:logistic', 'eval_metric': 'auc', 'max_depth': 1}
+    cpu = gbdt.cv(dict(p), x, yb, num_boost_round=3, nfold=5, seed=0)
+    gpu = gbdt.cv(dict(p), x, yb, num_boost_round=3, nfold=5, seed=0, device="cuda:0")
+    assert np.max(np.abs(np.array(cpu['test-auc-mean']) - np.array(gpu['test-auc-mean']))) < 5e-3
+    assert np.max(np.abs(np.array(cpu['train-auc-mean']) - np.array(gpu['train-auc-mean']))) < 5e-3
+    z = gbdt.cv(dict(p), x, np.zeros_like(yb), num_boost_round=2, nfold=3, seed=0, device="cuda:0")
+    assert z['test-auc-mean'] == [0.5, 0.5]
+
+
 def test_device_quantisation_bit_identical_to_cpu_engine():
     """G1 on the GPU (transpose + segmented radix sort + cuts + binning) gives
     exactly the CPU engine's bins: NaN -> lowest bin, few-valued columns,
