@@ -819,6 +819,7 @@ struct AdamSeg {
 
 
 #define ADAM_TK 64
+#define ADAM_BLK 1024   // elements per block of an element-wise (untiled) segment
 
 struct AdamArgs {
   const AdamSeg* segs;
@@ -897,29 +898,60 @@ __global__ void __launch_bounds__(256) adam_segments_kernel(AdamArgs a) {
     }
     return;
   }
-  const int i = blk.y + (int)threadIdx.x;          // segments are < 2^31 elements
-  if (i >= sg.n) return;
-  float gr = 0.f;
-  for (int s = 0; s < sg.S; ++s) gr += sg.g[(long)s * sg.gstride + i];
+  // element-wise segment: ADAM_BLK elements per block, 4 consecutive per thread with 16-byte loads and
+  // stores of p / m / v / gradient partials when aligned (one 4-byte element per thread kept too few
+  // bytes in flight: ~2 TB/s); the per-element arithmetic and the partial-sum order are unchanged
   const float lr_t = a.st->lr_t;
-  float m = sg.m[i], v = sg.v[i];
-  const float p = opt_update(a.st, sg.p[i], gr, m, v, lr_t);
-  sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
-  uint16_t h[3];
-  split3(p, h);
-  if (sg.bf)
-    for (int q = 0; q < npl; ++q) sg.bf[q * sg.pstride_bf + i] = h[q];
-  if (sg.bfT) {
-    // flipped / transposed dgrad copy: 32-bit index math (64-bit division is
-    // a long software sequence on the GPU)
-    uint32_t r = (uint32_t)i;
-    const uint32_t ci = r % (uint32_t)sg.tCi; r /= (uint32_t)sg.tCi;
-    const uint32_t kw = r % (uint32_t)sg.tKW; r /= (uint32_t)sg.tKW;
-    const uint32_t kh = r % (uint32_t)sg.tKH; r /= (uint32_t)sg.tKH;
-    const uint32_t co = r % (uint32_t)sg.tCo;
-    const uint32_t gg = r / (uint32_t)sg.tCo;
-    const long o = ((((long)gg * sg.tCi + ci) * sg.tKH + (sg.tKH - 1 - kh)) * sg.tKW + (sg.tKW - 1 - kw)) * sg.tCo + co;
-    for (int q = 0; q < npl; ++q) sg.bfT[q * sg.pstride_bfT + o] = h[q];
+  const int i0 = blk.y;                             // segments are < 2^31 elements
+  auto one = [&](int i, float gr, float p, float& m, float& v) {
+    p = opt_update(a.st, p, gr, m, v, lr_t);
+    uint16_t h[3];
+    split3(p, h);
+    if (sg.bf)
+      for (int q = 0; q < npl; ++q) sg.bf[q * sg.pstride_bf + i] = h[q];
+    if (sg.bfT) {
+      // flipped / transposed dgrad copy: 32-bit index math (64-bit division is
+      // a long software sequence on the GPU)
+      uint32_t r = (uint32_t)i;
+      const uint32_t ci = r % (uint32_t)sg.tCi; r /= (uint32_t)sg.tCi;
+      const uint32_t kw = r % (uint32_t)sg.tKW; r /= (uint32_t)sg.tKW;
+      const uint32_t kh = r % (uint32_t)sg.tKH; r /= (uint32_t)sg.tKH;
+      const uint32_t co = r % (uint32_t)sg.tCo;
+      const uint32_t gg = r / (uint32_t)sg.tCo;
+      const long o = ((((long)gg * sg.tCi + ci) * sg.tKH + (sg.tKH - 1 - kh)) * sg.tKW + (sg.tKW - 1 - kw)) * sg.tCo + co;
+      for (int q = 0; q < npl; ++q) sg.bfT[q * sg.pstride_bfT + o] = h[q];
+    }
+    return p;
+  };
+  const bool vec = ((reinterpret_cast<uintptr_t>(sg.p) | reinterpret_cast<uintptr_t>(sg.m) |
+                     reinterpret_cast<uintptr_t>(sg.v) | reinterpret_cast<uintptr_t>(sg.g)) & 15) == 0 &&
+                   (sg.gstride & 3) == 0 && (long)i0 + ADAM_BLK <= sg.n;
+  if (vec) {
+    const int i = i0 + 4 * (int)threadIdx.x;
+    float4 gr = make_float4(0.f, 0.f, 0.f, 0.f);     // 0 + partial 0 + ...: the scalar path's order
+    for (int s = 0; s < sg.S; ++s) {
+      const float4 t = *reinterpret_cast<const float4*>(sg.g + (long)s * sg.gstride + i);
+      gr.x += t.x; gr.y += t.y; gr.z += t.z; gr.w += t.w;
+    }
+    float4 m = *reinterpret_cast<const float4*>(sg.m + i), v = *reinterpret_cast<const float4*>(sg.v + i);
+    float4 p = *reinterpret_cast<const float4*>(sg.p + i);
+    p.x = one(i, gr.x, p.x, m.x, v.x);
+    p.y = one(i + 1, gr.y, p.y, m.y, v.y);
+    p.z = one(i + 2, gr.z, p.z, m.z, v.z);
+    p.w = one(i + 3, gr.w, p.w, m.w, v.w);
+    *reinterpret_cast<float4*>(sg.m + i) = m;
+    *reinterpret_cast<float4*>(sg.v + i) = v;
+    *reinterpret_cast<float4*>(sg.p + i) = p;
+    return;
+  }
+  for (int e = 0; e < ADAM_BLK / 256; ++e) {
+    const int i = i0 + e * 256 + (int)threadIdx.x;
+    if (i >= sg.n) return;
+    float gr = 0.f;
+    for (int s = 0; s < sg.S; ++s) gr += sg.g[(long)s * sg.gstride + i];
+    float m = sg.m[i], v = sg.v[i];
+    const float p = one(i, gr, sg.p[i], m, v);
+    sg.m[i] = m; sg.v[i] = v; sg.p[i] = p;
   }
 }
 
@@ -999,6 +1031,7 @@ int gt_adam_segments(const AdamArgs* a, int nblocks, hipStream_t stream) {
 }
 
 size_t gt_sizeof_adam_seg() { return sizeof(AdamSeg); }
+int gt_adam_block_elems() { return ADAM_BLK; }
 size_t gt_sizeof_dense_fwd_args() { return sizeof(DenseFwdArgs); }
 size_t gt_sizeof_head_args() { return sizeof(HeadArgs); }
 size_t gt_sizeof_dense_dgrad_args() { return sizeof(DenseDgradArgs); }

@@ -428,7 +428,7 @@ class HipPopJob(FoldJob):
             if ntiles:
                 blocks.extend((idx, t) for t in range(ntiles))
             else:
-                for o in range(0, p.numel(), 256):
+                for o in K.adam_blocks(p.numel()):
                     blocks.append((idx, o))
 
         # conv layers: one segment per (layer, group that has the layer)

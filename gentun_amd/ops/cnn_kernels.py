@@ -165,9 +165,17 @@ class AdamSeg(C.Structure):
 ADAM_TK = 64        # adam_segments transpose tiles: tCo rows x ADAM_TK reduction columns
 
 
+ADAM_BLK = 1024     # elements per block of an element-wise Adam segment (cnn_dense.hip ADAM_BLK)
+
+
+def adam_blocks(n):
+    """Block offsets of an element-wise (untiled) Adam segment of ``n`` elements."""
+    return range(0, n, ADAM_BLK)
+
+
 def adam_tiles(tG, tCo, tKH, tKW, tCi):
     """Blocks of a tiled conv-weight segment (csrc/hip/cnn_dense.hip, tiled
-    path), or 0 when the segment cannot be tiled (then: 256-element blocks)."""
+    path), or 0 when the segment cannot be tiled (then: ADAM_BLK-element blocks)."""
     if tCo % 8:
         return 0
     kd = tKH * tKW * tCi
@@ -298,6 +306,7 @@ def lib():
         assert L.gt_sizeof_init_seg() == C.sizeof(InitSeg), "InitSeg ABI mismatch"
         assert L.gt_sizeof_wgrad_args() == C.sizeof(WgradArgs), "WgradArgs ABI mismatch"
         assert L.gt_sizeof_adam_seg() == C.sizeof(AdamSeg), "AdamSeg ABI mismatch"
+        assert L.gt_adam_block_elems() == ADAM_BLK, "Adam block size mismatch"
         assert L.gt_sizeof_bn_args() == C.sizeof(BnArgs), "BnArgs ABI mismatch"
         for nm, st in (("dense_fwd_args", DenseFwdArgs), ("head_args", HeadArgs),
                        ("dense_dgrad_args", DenseDgradArgs), ("dense_wgrad_args", DenseWgradAdamArgs)):

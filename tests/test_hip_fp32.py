@@ -444,7 +444,7 @@ def test_adam_segments_fp32_planes(tiled):
     sg.npl, sg.pstride_bf, sg.pstride_bfT = 3, n, bfT[0].numel()
     nt = Km.adam_tiles(G, co, kh, kw, ci) if tiled else 0
     sg.tiled = 1 if nt else 0
-    blocks = [(0, t) for t in range(nt)] if nt else [(0, o) for o in range(0, n, 256)]
+    blocks = [(0, t) for t in range(nt)] if nt else [(0, o) for o in Km.adam_blocks(n)]
     segs = (Km.AdamSeg * 1)(sg)
     segs_t = torch.frombuffer(bytearray(bytes(memoryview(segs).cast("B"))), dtype=torch.uint8).to(DEV)
     blocks_t = torch.tensor(np.asarray(blocks, np.int32).reshape(-1, 2), device=DEV)

@@ -497,7 +497,7 @@ def test_adam_segments_with_partials_and_transpose(tiled, dims):
     sg.tiled = 1 if ntiles else 0
     raw = bytes(memoryview((Km.AdamSeg * 1)(sg)).cast("B"))
     segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(DEV)
-    blk = [[0, t] for t in range(ntiles)] if ntiles else [[0, o] for o in range(0, n, 256)]
+    blk = [[0, t] for t in range(ntiles)] if ntiles else [[0, o] for o in Km.adam_blocks(n)]
     blocks = torch.tensor(blk, dtype=torch.int32, device=DEV)
     st = torch.zeros(8, dtype=torch.int32, device=DEV)
     st.view(torch.float32)[3] = 1e-2
@@ -514,6 +514,48 @@ def test_adam_segments_with_partials_and_transpose(tiled, dims):
     W = p.view(G, co, kh, kw, ci)
     WT = W.flip(2, 3).permute(0, 4, 2, 3, 1).contiguous().to(torch.bfloat16).view(-1)
     assert torch.equal(bfT, WT)
+
+
+@pytest.mark.parametrize("n,S", [(5000, 2), (4096, 1), (1000, 3)])
+def test_adam_segments_vector_path_bit_identical(n, S):
+    """Element-wise segments run 4 elements per thread with 16-byte loads / stores when every pointer is
+    16-byte aligned, else one element per thread: the same arithmetic and partial-sum order, so a
+    misaligned copy of the same state (pointers one float in) must give bitwise the same p / m / v."""
+    Km = K()
+    import ctypes
+    torch.manual_seed(3)
+    base = [torch.randn(n, device=DEV) for _ in range(3)]
+    base[2] = base[2].abs()
+    parts = torch.randn(S, n + 4, device=DEV)
+    out = []
+    for off in (0, 1):
+        bufs = [torch.zeros(n + off, device=DEV) for _ in range(3)]
+        for b, t in zip(bufs, base):
+            b[off:] = t
+        p, m, v = (b[off:] for b in bufs)
+        gsrc = torch.zeros(S, n + 4, device=DEV)
+        gsrc[:, off:off + n] = parts[:, :n]
+        sg = Km.AdamSeg()
+        sg.p, sg.m, sg.v, sg.g = p.data_ptr(), m.data_ptr(), v.data_ptr(), gsrc.data_ptr() + 4 * off
+        sg.bf = sg.bfT = 0
+        sg.n, sg.gstride, sg.S, sg.npl, sg.tiled = n, n + 4, S, 1, 0
+        raw = bytes(memoryview((Km.AdamSeg * 1)(sg)).cast("B"))
+        segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(DEV)
+        blocks = torch.tensor([[0, o] for o in Km.adam_blocks(n)], dtype=torch.int32, device=DEV)
+        st = torch.zeros(8, dtype=torch.int32, device=DEV)
+        st.view(torch.float32)[3] = 1e-2
+        Km.check(Km.lib().gt_step_begin(st.data_ptr(), stream()), "sb")
+        a = Km.AdamArgs()
+        a.segs, a.blocks, a.st = segs.data_ptr(), blocks.data_ptr(), st.data_ptr()
+        Km.check(Km.lib().gt_adam_segments(ctypes.byref(a), blocks.shape[0], stream()), "adam")
+        torch.cuda.synchronize()
+        out.append((p.clone(), m.clone(), v.clone()))
+    for x, y in zip(*out):
+        assert torch.equal(x, y)
+    g = parts[:, :n].sum(0)
+    rp, rm, rv = _adam_ref(base[0].clone(), base[1].clone(), base[2].clone(), g, 1e-2, 1)
+    assert torch.allclose(out[0][0], rp, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(out[0][1], rm, rtol=1e-5, atol=1e-6)
 
 
 def test_glorot_init_kernel():
