@@ -22,7 +22,10 @@
 //                              (0 on padding rows of a short batch and on the padded pixels of a
 //                              zero-padded image: BnArgs::Hr / Wr)
 // The shift k = z at pixel 0 of the group keeps S2 / N - (S1 / N)^2 free of
-// cancellation when |mean| >> std.
+// cancellation when |mean| >> std. Pixels per chunk: cnn_kernels.bn_chunk_px (a function of the layer
+// shape; at most 16K values per chunk so wide stages launch enough workgroups).
+// Measured and not kept (round 6, profiles/r6/bn_chunk_r6.txt): 4 pixels' loads in flight per thread in
+// the statistics kernels and 4 chunks' loads before the stores in the apply kernels (no gain).
 #include "common.h"
 #include "cnn_args.h"
 
@@ -67,6 +70,28 @@ __device__ __forceinline__ long bn_real_hw(const BnArgs& a) {
 }
 
 #define BN_THREADS 256
+
+// sum over the nch chunk partials of channel t (stride 2 Cp), in chunk order, 8 loads in flight: the
+// apply kernels' prologue (a dependent load per chunk made it ~0.7 us per chunk on every workgroup)
+__device__ __forceinline__ void bn_sum_parts(const float* __restrict__ part, int nch, int Cp, int t, float& s1,
+                                             float& s2) {
+  s1 = 0.f; s2 = 0.f;
+  int c = 0;
+  for (; c + 8 <= nch; c += 8) {
+    float x1[8], x2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      x1[k] = part[(long)(c + k) * 2 * Cp + t];
+      x2[k] = part[(long)(c + k) * 2 * Cp + Cp + t];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s1 += x1[k]; s2 += x2[k]; }
+  }
+  for (; c < nch; ++c) {
+    s1 += part[(long)c * 2 * Cp + t];
+    s2 += part[(long)c * 2 * Cp + Cp + t];
+  }
+}
 
 __device__ __forceinline__ int bn_rows(const BnArgs& a, int g) {
   if (!a.train || !a.valid) return a.B;
@@ -147,11 +172,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_apply_kernel(BnArgs a) {
       const long npx = (long)bn_rows(a, g) * a.HW;
       const int nch = (int)((npx + a.chunk_px - 1) / a.chunk_px);
       const float* part = a.part + (long)g * a.nchunk * 2 * Cp;
-      float s1 = 0.f, s2 = 0.f;
-      for (int c = 0; c < nch; ++c) {
-        s1 += part[(long)c * 2 * Cp + t];
-        s2 += part[(long)c * 2 * Cp + Cp + t];
-      }
+      float s1, s2;
+      bn_sum_parts(part, nch, Cp, t, s1, s2);
       const long nreal = (long)bn_rows(a, g) * bn_real_hw(a);
       const float n = nreal > 0 ? (float)nreal : 1.f;
       const float m1 = s1 / n;
@@ -284,11 +306,8 @@ __global__ void __launch_bounds__(BN_THREADS) bn_bwd_apply_kernel(BnArgs a) {
   if (t < Cp) {
     const int nch = (int)((nvpx + a.chunk_px - 1) / a.chunk_px);
     const float* part = a.part + (long)g * a.nchunk * 2 * Cp;
-    float sg = 0.f, sgx = 0.f;
-    for (int c = 0; c < nch; ++c) {
-      sg += part[(long)c * 2 * Cp + t];
-      sgx += part[(long)c * 2 * Cp + Cp + t];
-    }
+    float sg, sgx;
+    bn_sum_parts(part, nch, Cp, t, sg, sgx);
     if (blockIdx.x == 0) {
       a.gbeta[(long)g * Cp + t] = sg;
       a.ggamma[(long)g * Cp + t] = sgx;

@@ -309,7 +309,7 @@ class HipPopJob(FoldJob):
         if self.bn:
             for L in self.layers:
                 self.zpre[L.name] = torch.zeros((Q, B, L.H, L.W, L.coutp), dtype=self.adt, device=dev)
-                L.bn_chunk = K.BN_CHUNK_PX
+                L.bn_chunk = K.bn_chunk_px(L.H, L.W, L.coutp)
                 L.bn_nchunk = -(-(B * L.H * L.W) // L.bn_chunk)
                 L.bn_stat = torch.zeros((Q, 2, L.coutp), dtype=torch.float32, device=dev)
                 L.bn_run = torch.zeros((2, Q, L.coutp), dtype=torch.float32, device=dev)
@@ -569,7 +569,8 @@ class HipPopJob(FoldJob):
         self.pool_fused = []
         for st in self.stages:
             hh, ww, cc = self.shapes[st.inp]
-            # with BatchNorm the pool runs in the BN-apply launch (its chunks hold whole row pairs)
+            # with BatchNorm the pool runs in the BN-apply launch (its chunks hold whole row pairs:
+            # bn_chunk_px only halves 512 while the halves stay multiples of 2W)
             fuse_ok = fuse_env and (K.BN_CHUNK_PX % (2 * ww) == 0 and hh % 2 == 0 if self.bn else fast_on)
             sel = torch.tensor(self.sched.pool_source(st), dtype=torch.int32, device=self.device)
             self._keep.append(sel)

@@ -191,7 +191,20 @@ class BnArgs(C.Structure):
                 ("pool_y", P), ("pool_mask", P), ("W", I), ("Hr", I), ("Wr", I)]
 
 
-BN_CHUNK_PX = 512     # pixels per BatchNorm workgroup (fixed per shape: batch-invariant sums)
+BN_CHUNK_PX = 512     # pixels per BatchNorm workgroup at most (fixed per shape: batch-invariant sums)
+BN_CHUNK_VALUES = 16384
+
+
+def bn_chunk_px(H, W, Cp):
+    """Pixels per BatchNorm workgroup of a layer: 512, halved while a chunk holds more than 16K values and
+    the halves still hold whole row pairs (the fused 2x2 pool). A function of the layer shape only, so a
+    group's sums do not depend on the other groups of the launch. At 512 pixels a 256-channel 8x8 stage
+    had 4 workgroups per group (100 per 25-group launch on 256 CUs: ~1.4 TB/s)."""
+    c = BN_CHUNK_PX
+    pooled = BN_CHUNK_PX % (2 * W) == 0            # else the pool runs as its own kernel (cnn_hip.py)
+    while c * Cp > BN_CHUNK_VALUES and (c // 2 >= 2 * W and (c // 2) % (2 * W) == 0 if pooled else c > 64):
+        c //= 2
+    return c
 
 
 class AdamArgs(C.Structure):

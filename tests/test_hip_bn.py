@@ -30,7 +30,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("prec", [1, 0])
-@pytest.mark.parametrize("shape", [(32, 16, 16, 24, 20), (32, 8, 8, 104, 100), (8, 32, 32, 8, 3)])
+@pytest.mark.parametrize("shape", [(32, 16, 16, 24, 20), (32, 8, 8, 104, 100), (8, 32, 32, 8, 3),
+                                   (32, 8, 8, 256, 250), (32, 16, 16, 128, 120)])
 def test_bn_kernels_match_batchnorm2d(prec, shape):
     from gentun_amd.ops import cnn_kernels as K
     L = K.lib()
@@ -50,7 +51,7 @@ def test_bn_kernels_match_batchnorm2d(prec, shape):
     gamma[:, :C] = torch.rand(Q, C) + 0.5
     beta[:, :C] = torch.randn(Q, C) * 0.5
     run = torch.stack([torch.randn(Q, Cp) * 0.1, torch.rand(Q, Cp) + 0.5])
-    chunk = K.BN_CHUNK_PX
+    chunk = K.bn_chunk_px(H, W, Cp)                  # the executor's per-shape chunk
     nchunk = -(-(B * HW) // chunk)
     y = torch.zeros_like(z)
     stat = torch.zeros(Q, 2, Cp, device=dev)

@@ -31,6 +31,9 @@ if os.environ.get("WINO") is not None:                # A/B: Winograd stage-2 3x
 if os.environ.get("WFRAG") is not None:               # A/B: fragment-major conv weight planes on (1) / off (0)
     from gentun_amd.models import cnn_hip as _ch
     _ch.WFRAG = os.environ["WFRAG"] != "0"
+if os.environ.get("BNCHUNK") == "old":             # A/B: BatchNorm chunks of 512 pixels for every shape (round 5)
+    from gentun_amd.ops import cnn_kernels as _K
+    _K.bn_chunk_px = lambda H, W, Cp: _K.BN_CHUNK_PX
 if os.environ.get("GENTUN_WGRAD_NB"):                 # A/B: force the wgrad band buffers
     from gentun_amd.ops import cnn_kernels as K
     K.lib().gt_wgrad_set_nb(int(os.environ["GENTUN_WGRAD_NB"]))
