@@ -11,7 +11,7 @@ per-round cost (evaluation, initialisation, dispatch; ``--round-overhead``). Col
 broadcast + one all_gather per round) are ignored: microseconds against seconds-long rounds.
 
 usage: python tools/scaling_model.py [--qcurve FILE] [--pending 14] [--round-overhead 0.3]
-FILE: lines "all P groups ms/step ..." as in profiles/r5/qcurve_fp32_r5.txt (default: that file)."""
+FILE: lines "all P groups ms/step ..." as in profiles/r6/qcurve_fp32_r6.txt (default: that file)."""
 
 import argparse
 import os
@@ -66,7 +66,7 @@ def generation_time(curve, pending, world, per_gpu=5, slack=1, nfold=5, overhead
 def main():
     ap = argparse.ArgumentParser()
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    ap.add_argument("--qcurve", default=os.path.join(root, "profiles", "r5", "qcurve_fp32_r5.txt"))
+    ap.add_argument("--qcurve", default=os.path.join(root, "profiles", "r6", "qcurve_fp32_r6.txt"))
     ap.add_argument("--pending", type=int, default=14, help="candidates re-evaluated per generation (RR-GA: ~14 of 32)")
     ap.add_argument("--round-overhead", type=float, default=0.3)
     args = ap.parse_args()
