@@ -1,3 +1,4 @@
+# (The LASTRED switch was removed after this A/B: profiles/r6/last_wred_r6.txt.)
 # Round 6: last weight gradient summed by Adam (LASTRED=1) vs a reduce launch (LASTRED=0): HIP training tests,
 # then alternating population steps (25 and 10 groups) on one box.
 export GENTUN_NO_AUTOBUILD=1
