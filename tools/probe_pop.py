@@ -31,6 +31,9 @@ if os.environ.get("WINO") is not None:                # A/B: Winograd stage-2 3x
 if os.environ.get("WFRAG") is not None:               # A/B: fragment-major conv weight planes on (1) / off (0)
     from gentun_amd.models import cnn_hip as _ch
     _ch.WFRAG = os.environ["WFRAG"] != "0"
+if os.environ.get("BNVALUES"):                      # A/B: BatchNorm values per workgroup budget (cnn_kernels)
+    from gentun_amd.ops import cnn_kernels as _K
+    _K.BN_CHUNK_VALUES = int(os.environ["BNVALUES"])
 if os.environ.get("BNCHUNK") == "old":             # A/B: BatchNorm chunks of 512 pixels for every shape (round 5)
     from gentun_amd.ops import cnn_kernels as _K
     _K.bn_chunk_px = lambda H, W, Cp: _K.BN_CHUNK_PX
