@@ -887,20 +887,26 @@ __device__ __forceinline__ size_t lower_bound_u64(const u64* __restrict__ a, siz
   return lo;
 }
 
-// acc[seg * 2 + {0: rank sum of the positives, 1: positives}], zeroed before the launch; nseg <= 64
+// acc[seg * 2 + {0: rank sum of the positives, 1: positives}], zeroed before the launch; nseg <= 64.
+// Segment starts: one binary search per segment per workgroup (LDS); tie-group bounds: a positive whose
+// neighbours carry other margins is its own group (the common case once trees separate the rows), else
+// binary search.
 __global__ void __launch_bounds__(256) auc_rank_kernel(const u64* __restrict__ sorted, size_t N, int nseg,
                                                        double* __restrict__ acc) {
   __shared__ double s[128];
+  __shared__ size_t st[64];
   for (int t = threadIdx.x; t < 2 * nseg; t += blockDim.x) s[t] = 0.0;
+  for (int t = threadIdx.x; t < nseg; t += blockDim.x) st[t] = lower_bound_u64(sorted, N, (u64)t << 33);
   __syncthreads();
   for (size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (size_t)gridDim.x * blockDim.x) {
     const u64 key = sorted[p];
     if (!(key & 1u)) continue;
-    const u64 seg = key >> 33;
-    const size_t a = lower_bound_u64(sorted, N, key & ~1ull);
-    const size_t b = lower_bound_u64(sorted, N, key + 1) - 1;     // key | 1 == key: last of the group
-    const size_t st = lower_bound_u64(sorted, N, seg << 33);
-    atomicAdd(&s[2 * seg], 0.5 * (double)(a + b) + 1.0 - (double)st);
+    const u64 seg = key >> 33, m = key >> 1;
+    const bool lo_tie = p > 0 && (sorted[p - 1] >> 1) == m;
+    const bool hi_tie = p + 1 < N && (sorted[p + 1] >> 1) == m;
+    const size_t a = lo_tie ? lower_bound_u64(sorted, N, key & ~1ull) : p;
+    const size_t b = hi_tie ? lower_bound_u64(sorted, N, key + 1) - 1 : p;     // key | 1 == key: last of the group
+    atomicAdd(&s[2 * seg], 0.5 * (double)(a + b) + 1.0 - (double)st[seg]);
     atomicAdd(&s[2 * seg + 1], 1.0);
   }
   __syncthreads();
